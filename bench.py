@@ -1,0 +1,215 @@
+"""Benchmark: rows/s of the filtered GROUP BY SUM segment query path on MI355X (BASELINE.json metric).
+
+One step = one query over every segment this GPU owns (30 x 2^25-doc segments = 1B rows per GPU by default,
+weak scaling: config 5 "AdAnalytics ... 8B rows sharded across 8xMI355X" at N=8), including the per-query plan
+packing, the query kernel, the RCCL all-reduce of the partial group-by tables (N>1) and rank 0's compaction to
+host results.  Segments are generated in HBM before timing (synthetic data, seeded; see pinot_amd/synth.py).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|range_in|groupby1m]
+  torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL over xGMI)
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (query_kernel: algorithmic bytes per
+launch / its HIP-event time) and the CPU baseline (oracle/pinot_cpu.c, Pinot's per-segment operators restated,
+timed on a bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="adanalytics")
+    ap.add_argument("--segments", type=int, default=30, help="segments per GPU")
+    ap.add_argument("--docs", type=int, default=1 << 25, help="docs per segment")
+    ap.add_argument("--cpu-sample-segments", type=int, default=4)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = Pinot default min(#seg, min(10, nproc/2))")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip the small GPU-vs-oracle check of this workload")
+    return ap.parse_args()
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from pinot_amd.combine import DistributedExecutor
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.query import parse_sql
+    from pinot_amd.segment import GpuContext
+    from pinot_amd.synth import WORKLOADS, build_segments_gpu
+
+    w = WORKLOADS[args.workload]
+    ctx = GpuContext(local)
+    seg_ids = list(range(rank * args.segments, (rank + 1) * args.segments))
+    t0 = time.time()
+    segs = build_segments_gpu(ctx, w, seg_ids, args.docs)
+    torch.cuda.synchronize()
+    gen_s = time.time() - t0
+    opts = dict(w.options)
+    q = parse_sql(w.sql)
+    pm = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000))
+    ex = DistributedExecutor(pm)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # algorithmic bytes of one launch (stats pass: dense tile bytes + touched 32-B sectors of sparse reads)
+    pm.collect_stats = True
+    r_stats = ex.execute(q, segs)
+    st = ex.last_stats
+    pm.collect_stats = False
+    n_value_cols = len(set(a.column for a in q.aggregations if a.column))
+    out_bytes = 8 * 1
+    algo_bytes = st.dense_bytes + st.sparse_sector_bytes + 32 * st.num_docs_scanned * n_value_cols + out_bytes
+
+    for _ in range(args.warmup):
+        ex.execute(q, segs)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t_start = time.perf_counter()
+    result = None
+    for _ in range(args.steps):
+        result = ex.execute(q, segs)
+        kernel_ms.append(ex.last_stats.kernel_ms)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    rows_per_gpu = args.segments * args.docs
+    total_rows = rows_per_gpu * world
+    value = total_rows / (elapsed / args.steps)
+
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+
+    # small parity check of the same workload against the oracle (2 x 2^18-doc segments)
+    check = None
+    if rank == 0 and not args.no_check:
+        check = parity_check(ctx, w, q, opts)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, q, args)
+
+    if rank == 0:
+        traffic = _pmc_traffic(args.workload)
+        line = {
+            "metric": "rows/sec for filtered GROUP BY SUM at 1/8 GPUs + achieved HBM GB/s vs peak",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (seeded dict ids generated in HBM; dictionaries per BASELINE.md section 3)",
+            "config": {"workload": args.workload, "description": w.description, "query": w.sql,
+                       "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
+                       "rows_per_gpu": rows_per_gpu, "total_rows": total_rows,
+                       "parallelism": f"segments sharded over {world} GPU(s); partial tables all-reduced over RCCL"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel_ms_avg": avg_kernel_ms,
+                         "bytes_breakdown": {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
+                                             "dictionary_sectors": 32 * st.num_docs_scanned * n_value_cols}},
+            "cpu_baseline": cpu,
+            "result": {"matched_docs_per_gpu": st.num_docs_scanned, "groups": (len(result.group_rows)
+                       if result and result.group_rows is not None else None),
+                       "rows": [list(r) for r in (result.rows[:3] if result else [])]},
+            "parity_check": check,
+            "setup_s": round(gen_s, 1),
+        }
+        print(json.dumps(line, default=float), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(workload):
+    """HBM bytes per launch measured by rocprofv3 PMC (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when a
+    committed measurement for this workload exists under profiles/."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if os.path.exists(p):
+        try:
+            with open(p) as f:
+                return json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def parity_check(ctx, w, q, opts):
+    from oracle import engine
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    from pinot_amd.synth import build_segment_cpu
+
+    segs = [build_segment_cpu(w, s, 1 << 18, pack_fixed_bit) for s in range(2)]
+    gs = [GpuSegment(ctx, s) for s in segs]
+    try:
+        res = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000)).execute(q, gs)
+        ref = engine.execute(q, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
+        if q.group_by:
+            ok = sorted(res.group_rows) == sorted(ref.group_rows)
+        else:
+            ok = list(res.aggregation_result) == list(ref.aggregation_result)
+        ok = ok and res.stats.num_docs_scanned == ref.num_docs_scanned
+        return {"docs": 2 * (1 << 18), "matched": ref.num_docs_scanned, "ok": bool(ok)}
+    finally:
+        for g in gs:
+            g.release()
+
+
+def cpu_baseline(w, q, args):
+    from oracle.cpu import CpuBaseline, synth_segment
+
+    nseg = args.cpu_sample_segments
+    segs = [synth_segment(w, s, args.docs) for s in range(nseg)]
+    nproc = os.cpu_count() or 1
+    threads = args.cpu_threads or max(1, min(nseg, min(10, nproc // 2)))
+    cb = CpuBaseline(q, segs)
+    dt, matched, _, _, _ = cb.run(threads)
+    return {"value": nseg * args.docs / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{nseg} segment(s) x {args.docs} docs of the same workload, oracle/pinot_cpu.c "
+                      f"(AndDocIdIterator over SVScanDocIdIterators, 10k-doc blocks, double SUM), "
+                      f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
+            "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,253 @@
+/*
+ * pinot_gpu.h — C ABI of libpinotgpu.so, the MI355X segment query path for Apache Pinot.
+ *
+ * This is the drop-in boundary.  A Pinot server binds these entry points (JNI stub in INTEGRATION.md) from
+ *   - an IndexingOverride (segspi/index/IndexingOverrides.java:82-92) that uploads the forward index, dictionary,
+ *     sorted index and bitmap inverted index bytes of every immutable segment to HBM once, at load time
+ *     (seglocal/indexsegment/immutable/ImmutableSegmentLoader.java:186-187), and
+ *   - a GpuPlanMaker (core/plan/maker/PlanMaker.java:36-59) whose per-query combine operator replaces
+ *     BaseCombineOperator + AggregationOperator / AggregationGroupByOrderByOperator for the segments it owns
+ *     (core/plan/CombinePlanNode.java:85-196, core/operator/combine/BaseCombineOperator.java:79-227).
+ *
+ * Rules of the ABI:
+ *   - plain C types, pointers and sizes only; no C++ exceptions cross it;
+ *   - every function returns PGPU_OK (0) or a negative PGPU_E* status; the message of the last failure on the
+ *     calling thread is available through pgpu_last_error (thread-local), mirroring the processing-exception
+ *     path of BaseCombineOperator.onException (core/operator/combine/BaseCombineOperator.java:177-179);
+ *   - segment handles are immutable after pgpu_segment_seal and may be shared by concurrent queries;
+ *   - pgpu_query_execute is re-entrant: each call takes its own workspace and HIP stream.
+ *
+ * Dictionary ids are segment-local, exactly as in the reference: the host evaluates predicates against each
+ * segment's dictionary (core/operator/filter/predicate/<X>PredicateEvaluatorFactory.java) and passes dict-id ranges /
+ * sets per segment.  Group-by keys are made global by per-segment remap tables (see pgpu_remap_upload).
+ */
+#ifndef PINOT_GPU_H
+#define PINOT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGPU_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------------------------- */
+#define PGPU_OK 0
+#define PGPU_E_INVALID (-1)     /* bad argument / malformed plan or index bytes */
+#define PGPU_E_HIP (-2)         /* HIP runtime failure (out of memory, launch failure, ...) */
+#define PGPU_E_UNSUPPORTED (-3) /* plan shape this build does not run on the GPU: caller keeps the CPU plan */
+#define PGPU_E_NOT_FOUND (-4)
+
+/* ---- stored data types (spi/data/FieldSpec.java DataType, stored type) -------------------------------------- */
+#define PGPU_INT 0
+#define PGPU_LONG 1
+#define PGPU_FLOAT 2
+#define PGPU_DOUBLE 3
+#define PGPU_STRING 4 /* dictionary values stay on the host; ids only on the device */
+
+/* ---- memory kinds for upload sources --------------------------------------------------------------------- */
+#define PGPU_MEM_HOST 0
+#define PGPU_MEM_DEVICE 1 /* source already in this device's HBM (e.g. a staged loader); copied D2D */
+
+typedef struct pgpu_context pgpu_context;
+typedef struct pgpu_segment pgpu_segment;
+typedef struct pgpu_buffer pgpu_buffer;
+
+/* ---- lifecycle ------------------------------------------------------------------------------------------- */
+int pgpu_abi_version(void);
+/* Open device `device_ordinal` (HIP ordinal, one process per GPU). */
+int pgpu_init(int device_ordinal, pgpu_context** out_ctx);
+int pgpu_shutdown(pgpu_context* ctx);
+/* Copies the calling thread's last error message (NUL-terminated, truncated to len). Returns its full length. */
+int pgpu_last_error(char* buf, size_t len);
+
+/* ---- segment upload (IndexingOverrides seam) -------------------------------------------------------------
+ * One pgpu_segment per immutable segment, one column slot per column the queries may touch.  All byte sources
+ * are in the reference's on-disk layouts and are COPIED (the caller may unmap after return):
+ *   forward index : FixedBitSVForwardIndexWriter layout — value i in bits [i*b, (i+1)*b) of an MSB-first,
+ *                   big-endian bit stream, ceil(numDocs*b/8) bytes
+ *                   (seglocal/io/writer/impl/FixedBitSVForwardIndexWriter.java:39-47,
+ *                    seglocal/io/util/PinotDataBitSet.java:78-165)
+ *   sorted index  : 2 big-endian int32 (startDocId, endDocId inclusive) per dict id; also the forward index of a
+ *                   sorted column (seglocal/segment/index/readers/sorted/SortedIndexReaderImpl.java:37-121)
+ *   dictionary    : sorted unique values, big-endian fixed width (4 B INT/FLOAT, 8 B LONG/DOUBLE)
+ *                   (seglocal/segment/index/readers/BaseImmutableDictionary.java:40-322,
+ *                    seglocal/io/util/FixedByteValueReaderWriter.java:37-53)
+ *   inverted index: (card+1) big-endian int32 offsets followed by one Roaring portable-format bitmap per dict id
+ *                   (seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:35-124,
+ *                    seglocal/segment/index/readers/BitmapInvertedIndexReader.java:45-61)
+ */
+int pgpu_segment_create(pgpu_context* ctx, int32_t num_docs, int32_t num_columns, pgpu_segment** out_seg);
+/* bits_per_value = PinotDataBitSet.getNumBitsPerValue(cardinality - 1) (PinotDataBitSet.java:59-71), 1..32 */
+int pgpu_segment_add_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                   int32_t bits_per_value, int32_t cardinality, int32_t mem_kind);
+int pgpu_segment_add_sorted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                  int32_t cardinality);
+/* data_type PGPU_STRING: pass bytes=NULL; only the cardinality is recorded. */
+int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_type, const void* bytes,
+                                uint64_t num_bytes, int32_t cardinality);
+int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                    int32_t cardinality);
+int pgpu_segment_seal(pgpu_segment* seg);
+/* HBM bytes held by the segment (all columns, including padding and container directories). */
+int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);
+int pgpu_segment_release(pgpu_segment* seg);
+
+/* ---- group-key remap tables ------------------------------------------------------------------------------
+ * Per-segment int32 table: local dict id -> global group id (global dictionary = sorted union of the group
+ * column's segment dictionaries).  Uploaded once and cached by the host; NULL in a plan means identity. */
+int pgpu_remap_upload(pgpu_context* ctx, const int32_t* map, int32_t length, pgpu_buffer** out_buf);
+int pgpu_buffer_release(pgpu_buffer* buf);
+
+/* ---- query plan ------------------------------------------------------------------------------------------
+ * The filter of each segment is a flat program in prefix order (the operator tree the reference builds in
+ * core/plan/FilterPlanNode.java:192-313 after FilterOperatorUtils leaf choice and AND re-ordering,
+ * core/operator/filter/FilterOperatorUtils.java:42-221):
+ *   AND_BEGIN  c1 .. cn  AND_END      (each child is followed by AND_CHILD_END)
+ *   OR_BEGIN   c1 .. cn  OR_END       (each child is followed by OR_CHILD_END)
+ *   NOT c
+ *   SCAN  leaf : ScanBasedFilterOperator over the forward index (ScanBasedFilterOperator.java:46-54)
+ *   INVERTED leaf: BitmapBasedFilterOperator, OR of the bitmaps of `ids` (BitmapBasedFilterOperator.java:66-110)
+ *   SORTED leaf: SortedIndexBasedFilterOperator, inclusive doc ranges (SortedIndexBasedFilterOperator.java:51-219)
+ *   MATCH_ALL / EMPTY: MatchAllFilterOperator / EmptyFilterOperator
+ * `negate` on a leaf complements it within [0, numDocs) — the NEQ / NOT IN / NOT BETWEEN forms
+ * (BitmapBasedFilterOperator.java:82-100).  SCAN predicates are dict-id forms of the reference evaluators:
+ *   PGPU_PRED_RANGE: lo <= dictId < hi   (SortedDictionaryBasedRangePredicateEvaluator.applySV,
+ *                    RangePredicateEvaluatorFactory.java:174-177; EQ is [id, id+1))
+ *   PGPU_PRED_SET  : dictId in ids[]     (DictionaryBasedInPredicateEvaluator, InPredicateEvaluatorFactory.java:142-182)
+ */
+#define PGPU_F_MATCH_ALL 0
+#define PGPU_F_EMPTY 1
+#define PGPU_F_SCAN 2
+#define PGPU_F_INVERTED 3
+#define PGPU_F_SORTED 4
+#define PGPU_F_AND_BEGIN 5
+#define PGPU_F_AND_CHILD_END 6
+#define PGPU_F_AND_END 7
+#define PGPU_F_OR_BEGIN 8
+#define PGPU_F_OR_CHILD_END 9
+#define PGPU_F_OR_END 10
+#define PGPU_F_NOT 11
+
+#define PGPU_PRED_RANGE 0
+#define PGPU_PRED_SET 1
+
+typedef struct {
+  int32_t op;         /* PGPU_F_* */
+  int32_t column;     /* query column index (leaf ops) */
+  int32_t pred;       /* PGPU_PRED_* (SCAN) */
+  int32_t negate;     /* leaf complement within [0, numDocs) */
+  int32_t lo, hi;     /* RANGE: [lo, hi) */
+  const int32_t* ids; /* SET / INVERTED: dict ids; SORTED: 2*num_ids ints (start, end inclusive) */
+  int32_t num_ids;
+  int32_t reserved;
+} pgpu_filter_node;
+
+/* aggregation functions (core/query/aggregation/function/<X>AggregationFunction.java) */
+#define PGPU_AGG_COUNT 0 /* CountAggregationFunction.java:74-141; column = -1 */
+#define PGPU_AGG_SUM 1   /* SumAggregationFunction.java:55-129 */
+#define PGPU_AGG_MIN 2   /* MinAggregationFunction.java:55-138, empty = +inf */
+#define PGPU_AGG_MAX 3   /* MaxAggregationFunction.java:55-138, empty = -inf */
+#define PGPU_AGG_AVG 4   /* AvgAggregationFunction.java:58-190 + AvgPair */
+
+typedef struct {
+  int32_t fn;
+  int32_t column; /* query column index, -1 for COUNT(*) */
+} pgpu_agg;
+
+typedef struct {
+  const pgpu_segment* segment;
+  const int32_t* column_map;          /* query column index -> segment column slot (num_columns entries) */
+  const pgpu_filter_node* filter;     /* prefix-order program; NULL or 0 nodes = match all */
+  int32_t num_filter_nodes;
+  int32_t reserved;
+  const pgpu_buffer* const* group_remap; /* per group-by column; NULL array or NULL entry = identity */
+} pgpu_segment_plan;
+
+typedef struct {
+  int32_t num_columns;                /* query columns referenced by filter / aggregations / group-by */
+  int32_t num_segments;
+  const pgpu_segment_plan* segments;
+  int32_t num_aggs;
+  int32_t num_group_columns;          /* 0 = aggregation only */
+  const pgpu_agg* aggs;
+  const int32_t* group_columns;       /* query column indexes, key = sum_j gid_j * prod_{k<j} card_k */
+  const int32_t* group_cardinalities; /* global cardinality per group column */
+  uint64_t flags;                     /* PGPU_Q_* */
+} pgpu_query_desc;
+
+#define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
+
+/* ---- partial-result table ----------------------------------------------------------------------------------
+ * A query produces a dense table over G = prod(group_cardinalities) keys (G = 1 for aggregation only), laid out
+ * as sections of G 8-byte cells so that RCCL can reduce each section with one op:
+ *   section 0                : count      int64, SUM   (docs per key; COUNT(*) and the AVG count)
+ *   one section per agg slot : SUM of INT/LONG column   -> int64   SUM (exact; == the reference's double sum
+ *                                                                    while |partial sums| < 2^53)
+ *                              SUM of FLOAT/DOUBLE      -> float64 SUM
+ *                              MIN / MAX                -> int64 MIN / MAX of an order-preserving key
+ *                              AVG                      -> as SUM (count comes from section 0)
+ *                              COUNT                    -> no section (section 0)
+ * pgpu_table_layout describes it; pgpu_decode_minmax_key turns MIN/MAX keys back into doubles.
+ */
+#define PGPU_RED_SUM_I64 0
+#define PGPU_RED_SUM_F64 1
+#define PGPU_RED_MIN_I64 2
+#define PGPU_RED_MAX_I64 3
+
+typedef struct {
+  uint64_t num_keys;       /* G */
+  int32_t num_sections;
+  int32_t section_op[17];  /* PGPU_RED_* per section (section 0 = count) */
+  int32_t agg_section[16]; /* section of agg i, or 0 for COUNT */
+  int32_t agg_value_type[16]; /* stored type of the agg column (PGPU_INT..), -1 for COUNT */
+} pgpu_table_layout;
+
+int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out);
+
+typedef struct {
+  int64_t num_docs_scanned;              /* docs matching the filter (AggregationOperator.java:82-87) */
+  int64_t num_entries_scanned_in_filter; /* forward-index entries the GPU filter evaluated */
+  int64_t num_total_docs;
+  int64_t num_segments_matched;          /* reserved (0): per-segment match counts are not tracked */
+  int64_t sparse_sector_bytes;           /* PGPU_Q_STATS: 32-B sectors touched by sparse reads * 32 */
+  int64_t dense_bytes;                   /* forward-index bytes streamed in dense (staged) mode */
+  double kernel_ms;                      /* main query kernel time (HIP events on the query stream) */
+} pgpu_query_stats;
+
+/* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the dense partial
+ * table in caller-provided device memory `dev_table` (table_bytes >= 8 * num_sections * G).  Does not
+ * synchronize.  Used for multi-GPU combine: the caller RCCL-reduces the sections, then calls
+ * pgpu_table_compact.  Stats become valid after pgpu_query_wait. */
+typedef struct pgpu_query pgpu_query;
+int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
+                      uint64_t table_bytes, pgpu_query** out_query);
+int pgpu_query_wait(pgpu_query* query, pgpu_query_stats* out_stats);
+int pgpu_query_release(pgpu_query* query);
+
+/* Compact a (reduced) dense table: copy every key with count > 0 to the host, ascending by key.
+ *   out_keys  : int64[capacity]               (global raw key)
+ *   out_cells : int64[capacity * num_sections] row-major (section 0 = count, then sections in layout order;
+ *               float64 sections are bit-cast into the int64 cells)
+ * *out_num_groups receives the number of non-empty keys; if it exceeds capacity nothing beyond is written
+ * and PGPU_E_INVALID is returned with the needed count. Synchronizes `stream`. */
+int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
+                       int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups);
+
+/* Convenience: launch + wait + compact, table kept in a context-owned workspace. */
+int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
+                       uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);
+
+/* MIN/MAX order-preserving key -> double (value_type = stored type of the aggregated column). */
+double pgpu_decode_minmax_key(int64_t key, int32_t value_type);
+
+/* ---- introspection --------------------------------------------------------------------------------------- */
+/* Number of workgroups the query kernel launches and the docs per tile (for roofline accounting). */
+int pgpu_kernel_geometry(pgpu_context* ctx, int32_t* out_grid, int32_t* out_tile_docs, int32_t* out_block);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINOT_GPU_H */

@@ -1,0 +1,635 @@
+"""Per-segment query execution and combine, restated on the CPU (test infrastructure; see oracle/__init__.py).
+
+Independent of pinot_amd's planner: predicates are evaluated on decoded VALUES with SQL comparison semantics
+(not on dict ids), the physical filter tree is rebuilt here from FilterOperatorUtils' rules, and the iterator
+model below reproduces numEntriesScannedInFilter.
+
+References (abbreviations as in SURVEY.md):
+  FilterPlanNode.constructPhysicalOperator ................ core/plan/FilterPlanNode.java:192-313
+  FilterOperatorUtils (leaf choice, AND/OR folding, order) . core/operator/filter/FilterOperatorUtils.java:42-221
+  AndDocIdSet.iterator / OrDocIdSet.iterator .............. core/operator/docidsets/AndDocIdSet.java:60-146,
+                                                             OrDocIdSet.java:58-110, NotDocIdSet.java:34-37
+  SVScanDocIdIterator.next/advance/applyAnd ............... core/operator/dociditerators/SVScanDocIdIterator.java:57-94
+  AndDocIdIterator / OrDocIdIterator / NotDocIdIterator ... core/operator/dociditerators/*.java
+  Sum/Count/Min/Max/AvgAggregationFunction ................ core/query/aggregation/function/*.java
+  DictionaryBasedGroupKeyGenerator (holders, limit) ........ core/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:100-1016
+  AggregationOperator / AggregationGroupByOrderByOperator stats core/operator/query/AggregationOperator.java:58-87
+  combine + broker reduce (merge, ORDER BY, LIMIT) ........ core/operator/combine/*.java, core/data/table/IndexedTable.java:103-156
+"""
+from __future__ import annotations
+
+import bisect
+import math
+from dataclasses import dataclass, field
+from fractions import Fraction
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING
+from pinot_amd.query import UNBOUNDED, FilterContext, Predicate, QueryContext
+from pinot_amd.segment import SegmentData
+
+from .segment_writer import NATIVE, read_inverted_bitmap, unpack_fixed_bit
+
+EOF = -(2 ** 31)  # Constants.EOF = Integer.MIN_VALUE
+
+
+# ---- decoded segment ------------------------------------------------------------------------------------------
+class DecodedSegment:
+    """Dict ids / values of a SegmentData decoded from its reference-format bytes."""
+
+    def __init__(self, seg: SegmentData):
+        self.seg = seg
+        self.name = seg.name
+        self.num_docs = seg.num_docs
+        self._ids: Dict[str, np.ndarray] = {}
+        self._dict: Dict[str, object] = {}
+
+    def dictionary(self, col: str):
+        d = self._dict.get(col)
+        if d is None:
+            c = self.seg.column(col)
+            if c.data_type == PGPU_STRING:
+                d = list(c.dictionary)
+            else:
+                be = {PGPU_INT: ">i4", PGPU_LONG: ">i8", PGPU_FLOAT: ">f4", PGPU_DOUBLE: ">f8"}[c.data_type]
+                d = np.frombuffer(c.dictionary, dtype=be).astype(NATIVE[c.data_type])
+            self._dict[col] = d
+        return d
+
+    def ids(self, col: str) -> np.ndarray:
+        a = self._ids.get(col)
+        if a is None:
+            c = self.seg.column(col)
+            if c.sorted_index is not None:
+                pairs = np.frombuffer(c.sorted_index, dtype=">i4").reshape(-1, 2)
+                a = np.repeat(np.arange(len(pairs)), pairs[:, 1] - pairs[:, 0] + 1)
+            else:
+                bits = 1 if c.cardinality - 1 <= 1 else int(c.cardinality - 1).bit_length()
+                a = unpack_fixed_bit(c.forward, bits, self.num_docs)
+            assert len(a) == self.num_docs
+            self._ids[col] = a
+        return a
+
+    def values(self, col: str):
+        d = self.dictionary(col)
+        ids = self.ids(col)
+        if isinstance(d, list):
+            return [d[i] for i in ids]
+        return d[ids]
+
+
+# ---- predicates on values (SQL semantics) -----------------------------------------------------------------------
+def _lit(v: str, dt: int):
+    if dt == PGPU_STRING:
+        return v
+    if dt in (PGPU_INT, PGPU_LONG):
+        return Fraction(v)
+    if dt == PGPU_FLOAT:
+        return float(np.float32(float(v)))
+    return float(v)
+
+
+def _truth_on_dictionary(d, dt: int, p: Predicate) -> np.ndarray:
+    """Predicate truth per dictionary value, with SQL comparison semantics on the value."""
+    if dt == PGPU_STRING:
+        vals = list(d)
+
+        def ok(v):
+            if p.type == "EQ":
+                return v == p.values[0]
+            if p.type == "NOT_EQ":
+                return v != p.values[0]
+            if p.type == "IN":
+                return v in p.values
+            if p.type == "NOT_IN":
+                return v not in p.values
+            r = True
+            if p.lower != UNBOUNDED:
+                r &= v >= p.lower if p.lower_inclusive else v > p.lower
+            if p.upper != UNBOUNDED:
+                r &= v <= p.upper if p.upper_inclusive else v < p.upper
+            return r
+
+        return np.fromiter((ok(v) for v in vals), dtype=bool, count=len(vals))
+    v = np.asarray(d)
+    if dt in (PGPU_INT, PGPU_LONG):
+        v = v.astype(np.int64)
+
+        def eq(lit):
+            f = Fraction(lit)
+            return (v == int(f)) if f.denominator == 1 else np.zeros(len(v), bool)
+
+        def ge(lit, inclusive):  # v >= lit  /  v > lit
+            f = Fraction(lit)
+            return v >= math.ceil(f) if inclusive else v > math.floor(f)
+
+        def le(lit, inclusive):  # v <= lit  /  v < lit
+            f = Fraction(lit)
+            return v <= math.floor(f) if inclusive else v < math.ceil(f)
+    else:
+        v = v.astype(np.float64)
+        cast = (lambda x: float(np.float32(float(x)))) if dt == PGPU_FLOAT else float
+
+        def eq(lit):
+            return v == cast(lit)
+
+        def ge(lit, inclusive):
+            return v >= cast(lit) if inclusive else v > cast(lit)
+
+        def le(lit, inclusive):
+            return v <= cast(lit) if inclusive else v < cast(lit)
+    if p.type == "EQ":
+        return eq(p.values[0])
+    if p.type == "NOT_EQ":
+        return ~eq(p.values[0])
+    if p.type in ("IN", "NOT_IN"):
+        m = np.zeros(len(v), dtype=bool)
+        for x in p.values:
+            m |= eq(x)
+        return m if p.type == "IN" else ~m
+    m = np.ones(len(v), dtype=bool)
+    if p.lower != UNBOUNDED:
+        m &= ge(p.lower, p.lower_inclusive)
+    if p.upper != UNBOUNDED:
+        m &= le(p.upper, p.upper_inclusive)
+    return m
+
+
+def predicate_mask(ds: DecodedSegment, p: Predicate) -> np.ndarray:
+    """Boolean per doc: does the doc's value satisfy the predicate (truth per dictionary value, gathered by the
+    doc's dict id — value semantics, since the dictionary holds the values)."""
+    c = ds.seg.column(p.column)
+    return _truth_on_dictionary(ds.dictionary(p.column), c.data_type, p)[ds.ids(p.column)]
+
+
+# ---- physical operator tree (restated FilterOperatorUtils) ------------------------------------------------------
+@dataclass
+class POp:
+    kind: str                 # EMPTY ALL SCAN BITMAP SORTED AND OR NOT
+    children: List["POp"] = field(default_factory=list)
+    mask: Optional[np.ndarray] = None   # leaf doc set
+
+    def priority(self) -> int:
+        return {"SORTED": 0, "BITMAP": 1, "AND": 3, "OR": 4, "SCAN": 5}.get(self.kind) if self.kind != "NOT" \
+            else self.children[0].priority()
+
+
+def build_physical(ds: DecodedSegment, f: Optional[FilterContext]) -> POp:
+    if f is None:
+        return POp("ALL")
+    if f.type in ("AND", "OR"):
+        kids = []
+        for ch in f.children:
+            op = build_physical(ds, ch)
+            if f.type == "AND":
+                if op.kind == "EMPTY":
+                    return POp("EMPTY")
+                if op.kind != "ALL":
+                    kids.append(op)
+            else:
+                if op.kind == "ALL":
+                    return POp("ALL")
+                if op.kind != "EMPTY":
+                    kids.append(op)
+        if not kids:
+            return POp("ALL" if f.type == "AND" else "EMPTY")
+        if len(kids) == 1:
+            return kids[0]
+        if f.type == "AND":
+            kids = sorted(kids, key=lambda o: o.priority())
+        return POp(f.type, kids)
+    if f.type == "NOT":
+        ch = build_physical(ds, f.children[0])
+        if ch.kind == "ALL":
+            return POp("EMPTY")
+        if ch.kind == "EMPTY":
+            return POp("ALL")
+        return POp("NOT", [ch])
+    p = f.predicate
+    m = predicate_mask(ds, p)
+    col = ds.seg.column(p.column)
+    # alwaysTrue / alwaysFalse are decided on the dictionary (every dict value matches / none does)
+    d = ds.dictionary(p.column)
+    truth_card = int(np.count_nonzero(_truth_on_dictionary(d, col.data_type, p)))
+    if truth_card == 0:
+        return POp("EMPTY")
+    if truth_card == len(d):
+        return POp("ALL")
+    if col.sorted_index is not None:
+        return POp("SORTED", mask=m)
+    if p.type != "RANGE" and col.inverted is not None:
+        # the inverted index is read through its own bytes: checks the Roaring writer too
+        ids = ds.ids(p.column)
+        inv_mask = np.zeros(ds.num_docs, dtype=bool)
+        matching = np.unique(ids[m]) if not p.is_exclusive else np.unique(ids[~m])
+        for i in matching:
+            inv_mask[read_inverted_bitmap(col.inverted, col.cardinality, int(i))] = True
+        if p.is_exclusive:
+            inv_mask = ~inv_mask
+        assert np.array_equal(inv_mask, m), "inverted index disagrees with forward index"
+        return POp("BITMAP", mask=m)
+    return POp("SCAN", mask=m)
+
+
+def eval_mask(op: POp, n: int) -> np.ndarray:
+    if op.kind == "ALL":
+        return np.ones(n, dtype=bool)
+    if op.kind == "EMPTY":
+        return np.zeros(n, dtype=bool)
+    if op.mask is not None:
+        return op.mask
+    if op.kind == "AND":
+        m = np.ones(n, dtype=bool)
+        for c in op.children:
+            m &= eval_mask(c, n)
+        return m
+    if op.kind == "OR":
+        m = np.zeros(n, dtype=bool)
+        for c in op.children:
+            m |= eval_mask(c, n)
+        return m
+    return ~eval_mask(op.children[0], n)
+
+
+# ---- iterator model (numEntriesScannedInFilter) ------------------------------------------------------------------
+class _Scan:
+    kind = "scan"
+
+    def __init__(self, mask: np.ndarray, counter: list):
+        self.n = len(mask)
+        self.hits = np.flatnonzero(mask)
+        self.mask = mask
+        self.nxt = 0
+        self.counter = counter
+
+    def next(self):
+        if self.nxt >= self.n:
+            return EOF
+        i = bisect.bisect_left(self.hits, self.nxt)
+        if i < len(self.hits):
+            d = int(self.hits[i])
+            self.counter[0] += d - self.nxt + 1
+            self.nxt = d + 1
+            return d
+        self.counter[0] += self.n - self.nxt
+        self.nxt = self.n
+        return EOF
+
+    def advance(self, t):
+        self.nxt = t
+        return self.next()
+
+    def apply_and(self, docs: np.ndarray) -> np.ndarray:
+        self.counter[0] += len(docs)
+        return docs[self.mask[docs]]
+
+
+class _Docs:
+    """BitmapDocIdIterator / RangelessBitmapDocIdIterator / SortedDocIdIterator over a doc array."""
+
+    def __init__(self, docs: np.ndarray, kind: str):
+        self.docs = docs
+        self.i = 0
+        self.kind = kind  # "bitmap" or "sorted"
+
+    def next(self):
+        if self.i < len(self.docs):
+            self.i += 1
+            return int(self.docs[self.i - 1])
+        return EOF
+
+    def advance(self, t):
+        self.i = bisect.bisect_left(self.docs, t, self.i)
+        return self.next()
+
+
+class _And:
+    kind = "other"
+
+    def __init__(self, its):
+        self.its = its
+        self.nxt = 0
+
+    def next(self):
+        mx, mi, i = self.nxt, -1, 0
+        while i < len(self.its):
+            if i == mi:
+                i += 1
+                continue
+            d = self.its[i].advance(mx)
+            if d == EOF:
+                return EOF
+            if d == mx:
+                i += 1
+            else:
+                mx, mi, i = d, i, 0
+        self.nxt = mx + 1
+        return mx
+
+    def advance(self, t):
+        self.nxt = t
+        return self.next()
+
+
+class _Or:
+    kind = "other"
+
+    def __init__(self, its):
+        self.its = list(its)
+        self.nd = [-1] * len(its)
+        self.k = len(its)
+        self.prev = -1
+
+    def _drop(self):
+        i = 0
+        while i < self.k:
+            if self.nd[i] == EOF:
+                self.k -= 1
+                self.its[i] = self.its[self.k]
+                self.nd[i] = self.nd[self.k]
+            else:
+                i += 1
+
+    def next(self):
+        best, ex = None, False
+        for i in range(self.k):
+            d = self.nd[i]
+            if d == self.prev:
+                d = self.its[i].next()
+                self.nd[i] = d
+                if d == EOF:
+                    ex = True
+                    continue
+            best = d if best is None else min(best, d)
+        if ex:
+            self._drop()
+        if best is None:
+            return EOF
+        self.prev = best
+        return best
+
+    def advance(self, t):
+        best, ex = None, False
+        for i in range(self.k):
+            d = self.nd[i]
+            if d < t:
+                d = self.its[i].advance(t)
+                self.nd[i] = d
+                if d == EOF:
+                    ex = True
+                    continue
+            best = d if best is None else min(best, d)
+        if ex:
+            self._drop()
+        if best is None:
+            return EOF
+        self.prev = best
+        return best
+
+
+class _Not:
+    kind = "other"
+
+    def __init__(self, child, n):
+        self.child = child
+        self.n = n
+        self.nxt = 0
+        d = child.next()
+        self.nnm = n if d == EOF else d
+
+    def next(self):
+        while self.nxt == self.nnm:
+            self.nxt += 1
+            d = self.child.next()
+            self.nnm = self.n if d == EOF else d
+        if self.nxt >= self.n:
+            return EOF
+        self.nxt += 1
+        return self.nxt - 1
+
+    def advance(self, t):
+        self.nxt = t
+        if t > self.nnm:
+            d = self.child.advance(t)
+            self.nnm = self.n if d == EOF else d
+        return self.next()
+
+
+def make_iterator(op: POp, n: int, counter: list):
+    """FilterBlockDocIdSet.iterator() of the physical operator `op`."""
+    if op.kind == "SCAN":
+        return _Scan(op.mask, counter)
+    if op.kind == "BITMAP":
+        return _Docs(np.flatnonzero(op.mask), "bitmap")
+    if op.kind == "SORTED":
+        return _Docs(np.flatnonzero(op.mask), "sorted")
+    if op.kind == "ALL":
+        return _Docs(np.arange(n), "other")
+    if op.kind == "EMPTY":
+        return _Docs(np.zeros(0, np.int64), "other")
+    if op.kind == "NOT":
+        return _Not(make_iterator(op.children[0], n, counter), n)
+    its = [make_iterator(c, n, counter) for c in op.children]
+    idx = [i for i in its if getattr(i, "kind", "") in ("sorted", "bitmap")]
+    scans = [i for i in its if getattr(i, "kind", "") == "scan"]
+    rest = [i for i in its if i not in idx and i not in scans]
+    if op.kind == "AND":
+        if (idx and scans) or len(idx) > 1:
+            docs = None
+            for it in idx:
+                docs = it.docs if docs is None else np.intersect1d(docs, it.docs, assume_unique=True)
+            for s in scans:
+                docs = s.apply_and(docs)
+            merged = _Docs(docs, "bitmap")  # RangelessBitmapDocIdIterator is bitmap-based
+            return merged if not rest else _And([merged] + rest)
+        return _And(its)
+    # OR
+    if len(idx) > 1:
+        docs = np.unique(np.concatenate([i.docs for i in idx]))
+        merged = _Docs(docs, "bitmap")
+        rest = [i for i in its if i not in idx]
+        return merged if not rest else _Or([merged] + rest)
+    return _Or(its)
+
+
+def entries_scanned_in_filter(op: POp, n: int) -> Tuple[int, np.ndarray]:
+    """Drain the iterator like DocIdSetOperator; returns (numEntriesScannedInFilter, matched doc ids)."""
+    counter = [0]
+    it = make_iterator(op, n, counter)
+    out = []
+    while True:
+        d = it.next()
+        if d == EOF:
+            break
+        out.append(d)
+    return counter[0], np.asarray(out, dtype=np.int64)
+
+
+# ---- aggregation -------------------------------------------------------------------------------------------------
+def _as_float_values(ds: DecodedSegment, col: str, docs: np.ndarray) -> np.ndarray:
+    d = ds.dictionary(col)
+    if isinstance(d, list):
+        raise ValueError(f"non-numeric column {col}")
+    return d[ds.ids(col)[docs]]
+
+
+def _sum_reference(vals: np.ndarray) -> float:
+    """`sum += values[i]` in doc order starting from 0.0 (SumAggregationFunction.aggregate)."""
+    if vals.size == 0:
+        return 0.0
+    if vals.dtype.kind in "iu":
+        exact = int(vals.astype(np.int64).sum(dtype=np.int64)) if vals.size < (1 << 31) else int(sum(map(int, vals)))
+        if abs(exact) < (1 << 53) and float(np.abs(vals).max()) * vals.size < 2.0 ** 53:
+            return float(exact)  # every partial sum is an exact double
+    return float(np.cumsum(vals.astype(np.float64))[-1])
+
+
+def aggregate(fn: str, vals: Optional[np.ndarray], count: int):
+    """Intermediate result of one aggregation over the matching docs of one segment."""
+    if fn == "COUNT":
+        return count
+    if fn == "SUM":
+        return _sum_reference(vals)
+    if fn == "MIN":
+        return float(vals.astype(np.float64).min()) if count else math.inf
+    if fn == "MAX":
+        return float(vals.astype(np.float64).max()) if count else -math.inf
+    if fn == "AVG":
+        return (_sum_reference(vals), count)
+    raise ValueError(fn)
+
+
+def merge(fn: str, a, b):
+    """AggregationFunction.merge."""
+    if fn in ("COUNT", "SUM"):
+        return a + b
+    if fn == "MIN":
+        return min(a, b)
+    if fn == "MAX":
+        return max(a, b)
+    return (a[0] + b[0], a[1] + b[1])
+
+
+def final(fn: str, v):
+    """AggregationFunction.extractFinalResult."""
+    if fn == "AVG":
+        return -math.inf if v[1] == 0 else v[0] / v[1]
+    if fn == "COUNT":
+        return int(v)
+    return float(v)
+
+
+@dataclass
+class SegmentResult:
+    aggregation: Optional[list] = None               # intermediate values (aggregation only)
+    groups: Optional[Dict[tuple, list]] = None       # group values -> intermediate values
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
+    num_total_docs: int = 0
+    matched: Optional[np.ndarray] = None
+
+
+def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int = 100_000,
+                    max_init_group_holder_capacity: int = 10_000, iterator_stats: bool = False) -> SegmentResult:
+    ds = seg if isinstance(seg, DecodedSegment) else DecodedSegment(seg)
+    n = ds.num_docs
+    op = build_physical(ds, query.filter)
+    mask = eval_mask(op, n)
+    docs = np.flatnonzero(mask)
+    res = SegmentResult(num_docs_scanned=len(docs), num_total_docs=n, matched=docs)
+    if iterator_stats:
+        res.num_entries_scanned_in_filter, it_docs = entries_scanned_in_filter(op, n)
+        assert np.array_equal(it_docs, docs), "iterator model disagrees with the mask algebra"
+    res.num_entries_scanned_post_filter = len(docs) * len(query.projected_columns)
+    if not query.group_by:
+        res.aggregation = [aggregate(a.function, None if a.column is None else _as_float_values(ds, a.column, docs),
+                                     len(docs)) for a in query.aggregations]
+        return res
+    # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long)
+    cards = [ds.seg.column(g).cardinality for g in query.group_by]
+    prod = 1
+    for c in cards:
+        prod *= c
+    idmat = np.stack([ds.ids(g)[docs].astype(np.int64) for g in query.group_by], axis=1) if len(docs) else \
+        np.zeros((0, len(cards)), dtype=np.int64)
+    uniq, first, inv = (np.unique(idmat, axis=0, return_index=True, return_inverse=True) if len(docs)
+                        else (np.zeros((0, len(cards)), np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)))
+    inv = np.asarray(inv).reshape(-1)
+    keep_groups = np.ones(len(uniq), dtype=bool)
+    if prod > max_init_group_holder_capacity and len(uniq) > num_groups_limit:
+        # map-based holder: only the first `limit` distinct keys (in doc order) get group ids
+        keep_groups[:] = False
+        keep_groups[np.argsort(first, kind="stable")[:num_groups_limit]] = True
+    order = np.argsort(inv, kind="stable")  # stable: docs stay in doc order inside each group
+    inv_s, docs_s = inv[order], docs[order]
+    bounds = np.flatnonzero(np.diff(inv_s)) + 1
+    groups: Dict[tuple, list] = {}
+    dicts = [ds.dictionary(g) for g in query.group_by]
+    for part_docs, part_g in zip(np.split(docs_s, bounds), np.split(inv_s, bounds)):
+        if part_docs.size == 0 or not keep_groups[part_g[0]]:
+            continue
+        vals = []
+        for j, d in enumerate(dicts):
+            v = d[int(uniq[part_g[0], j])]
+            vals.append(v.item() if hasattr(v, "item") else v)
+        groups[tuple(vals)] = [aggregate(a.function, None if a.column is None else
+                                         _as_float_values(ds, a.column, part_docs), len(part_docs))
+                               for a in query.aggregations]
+    res.groups = groups
+    return res
+
+
+@dataclass
+class OracleResult:
+    aggregation_result: Optional[list] = None
+    group_rows: Optional[List[tuple]] = None
+    rows: Optional[List[tuple]] = None
+    intermediate: Optional[dict] = None
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
+    num_total_docs: int = 0
+
+
+def execute(query: QueryContext, segments: Sequence[SegmentData], num_groups_limit: int = 100_000,
+            max_init_group_holder_capacity: int = 10_000, iterator_stats: bool = False) -> OracleResult:
+    """All segments of one server + the broker reduce (no group trimming)."""
+    fns = [a.function for a in query.aggregations]
+    out = OracleResult()
+    decoded: Dict[int, DecodedSegment] = {}
+    agg = None
+    groups: Dict[tuple, list] = {}
+    for s in segments:
+        ds = decoded.setdefault(id(s), DecodedSegment(s))
+        r = execute_segment(query, ds, num_groups_limit, max_init_group_holder_capacity, iterator_stats)
+        out.num_docs_scanned += r.num_docs_scanned
+        out.num_entries_scanned_in_filter += r.num_entries_scanned_in_filter
+        out.num_entries_scanned_post_filter += r.num_entries_scanned_post_filter
+        out.num_total_docs += r.num_total_docs
+        if r.aggregation is not None:
+            agg = r.aggregation if agg is None else [merge(f, a, b) for f, a, b in zip(fns, agg, r.aggregation)]
+        else:
+            for k, v in r.groups.items():
+                groups[k] = v if k not in groups else [merge(f, a, b) for f, a, b in zip(fns, groups[k], v)]
+    if not query.group_by:
+        out.intermediate = {(): agg}
+        out.aggregation_result = [final(f, v) for f, v in zip(fns, agg)]
+        out.rows = [tuple(out.aggregation_result)]
+        return out
+    out.intermediate = groups
+    rows = [k + tuple(final(f, v) for f, v in zip(fns, vs)) for k, vs in groups.items()]
+    out.group_rows = rows
+    names = list(query.group_by) + [a.result_name for a in query.aggregations]
+    ordered = rows
+    for ob in reversed(query.order_by):
+        i = names.index(ob.expression)
+        ordered = sorted(ordered, key=lambda r, i=i: r[i], reverse=not ob.ascending)
+    ordered = ordered[: query.limit]
+    sel = []
+    for r in ordered:
+        sel.append(tuple(r[names.index(s if isinstance(s, str) else s.result_name)] for s in query.select))
+    out.rows = sel
+    return out

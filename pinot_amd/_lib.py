@@ -1,0 +1,146 @@
+"""ctypes binding of libpinotgpu.so (include/pinot_gpu.h).
+
+This is the host-side view of the drop-in boundary: the same entry points a Pinot server binds through JNI
+(INTEGRATION.md).  The library is built in-tree by ``__graft_entry__.build()``; importing this module on a machine
+without the built library, or calling into it without a gfx950 device, raises — there is no CPU fallback on the
+product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpinotgpu.so")
+SYNTH_LIB_PATH = os.path.join(_HERE, "libpinotgpu_synth.so")
+
+# ---- constants (mirror include/pinot_gpu.h) ------------------------------------------------------------------
+PGPU_OK = 0
+PGPU_E_INVALID = -1
+PGPU_E_HIP = -2
+PGPU_E_UNSUPPORTED = -3
+
+PGPU_INT, PGPU_LONG, PGPU_FLOAT, PGPU_DOUBLE, PGPU_STRING = range(5)
+PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
+
+(PGPU_F_MATCH_ALL, PGPU_F_EMPTY, PGPU_F_SCAN, PGPU_F_INVERTED, PGPU_F_SORTED, PGPU_F_AND_BEGIN,
+ PGPU_F_AND_CHILD_END, PGPU_F_AND_END, PGPU_F_OR_BEGIN, PGPU_F_OR_CHILD_END, PGPU_F_OR_END, PGPU_F_NOT) = range(12)
+PGPU_PRED_RANGE, PGPU_PRED_SET = 0, 1
+PGPU_AGG_COUNT, PGPU_AGG_SUM, PGPU_AGG_MIN, PGPU_AGG_MAX, PGPU_AGG_AVG = range(5)
+PGPU_RED_SUM_I64, PGPU_RED_SUM_F64, PGPU_RED_MIN_I64, PGPU_RED_MAX_I64 = range(4)
+PGPU_Q_STATS = 1
+
+
+class PinotGpuError(RuntimeError):
+    """Non-zero status from libpinotgpu (the IntermediateResultsBlock(Exception) path of the reference)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libpinotgpu status {code}: {message}")
+        self.code = code
+
+
+class UnsupportedPlanError(PinotGpuError):
+    """PGPU_E_UNSUPPORTED: the server keeps the reference CPU plan for this query."""
+
+
+# ---- structs -------------------------------------------------------------------------------------------------
+class FilterNode(C.Structure):
+    _fields_ = [("op", C.c_int32), ("column", C.c_int32), ("pred", C.c_int32), ("negate", C.c_int32),
+                ("lo", C.c_int32), ("hi", C.c_int32), ("ids", C.POINTER(C.c_int32)), ("num_ids", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class Agg(C.Structure):
+    _fields_ = [("fn", C.c_int32), ("column", C.c_int32)]
+
+
+class SegmentPlan(C.Structure):
+    _fields_ = [("segment", C.c_void_p), ("column_map", C.POINTER(C.c_int32)), ("filter", C.POINTER(FilterNode)),
+                ("num_filter_nodes", C.c_int32), ("reserved", C.c_int32), ("group_remap", C.POINTER(C.c_void_p))]
+
+
+class QueryDesc(C.Structure):
+    _fields_ = [("num_columns", C.c_int32), ("num_segments", C.c_int32), ("segments", C.POINTER(SegmentPlan)),
+                ("num_aggs", C.c_int32), ("num_group_columns", C.c_int32), ("aggs", C.POINTER(Agg)),
+                ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
+                ("flags", C.c_uint64)]
+
+
+class TableLayout(C.Structure):
+    _fields_ = [("num_keys", C.c_uint64), ("num_sections", C.c_int32), ("section_op", C.c_int32 * 17),
+                ("agg_section", C.c_int32 * 16), ("agg_value_type", C.c_int32 * 16)]
+
+
+class QueryStats(C.Structure):
+    _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
+                ("num_total_docs", C.c_int64), ("num_segments_matched", C.c_int64),
+                ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double)]
+
+
+# exported symbols and their signatures: (name, restype, argtypes)
+_P = C.c_void_p
+SIGNATURES = [
+    ("pgpu_abi_version", C.c_int, []),
+    ("pgpu_init", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("pgpu_shutdown", C.c_int, [_P]),
+    ("pgpu_last_error", C.c_int, [C.c_char_p, C.c_size_t]),
+    ("pgpu_segment_create", C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    ("pgpu_segment_add_forward_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32, C.c_int32, C.c_int32]),
+    ("pgpu_segment_add_sorted_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32]),
+    ("pgpu_segment_add_dictionary", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_uint64, C.c_int32]),
+    ("pgpu_segment_add_inverted_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32]),
+    ("pgpu_segment_seal", C.c_int, [_P]),
+    ("pgpu_segment_device_bytes", C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    ("pgpu_segment_release", C.c_int, [_P]),
+    ("pgpu_remap_upload", C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),
+    ("pgpu_buffer_release", C.c_int, [_P]),
+    ("pgpu_table_layout_of", C.c_int, [C.POINTER(QueryDesc), C.POINTER(TableLayout)]),
+    ("pgpu_query_launch", C.c_int, [_P, C.POINTER(QueryDesc), _P, _P, C.c_uint64, C.POINTER(_P)]),
+    ("pgpu_query_wait", C.c_int, [_P, C.POINTER(QueryStats)]),
+    ("pgpu_query_release", C.c_int, [_P]),
+    ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                     C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
+    ("pgpu_decode_minmax_key", C.c_double, [C.c_int64, C.c_int32]),
+    ("pgpu_kernel_geometry", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+]
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libpinotgpu.so (fails loudly when it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    lib = C.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pgpu_abi_version() != 1:
+        raise ImportError("libpinotgpu ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    lib = load()
+    buf = C.create_string_buffer(2048)
+    lib.pgpu_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int) -> None:
+    if rc != PGPU_OK:
+        msg = last_error()
+        if rc == PGPU_E_UNSUPPORTED:
+            raise UnsupportedPlanError(rc, msg)
+        raise PinotGpuError(rc, msg)
+
+
+def decode_minmax_key(key: int, value_type: int) -> float:
+    return load().pgpu_decode_minmax_key(key, value_type)

@@ -1,0 +1,1070 @@
+// libpinotgpu.so host runtime: the C ABI of include/pinot_gpu.h.
+//
+// Responsibilities (reference counterparts in parentheses):
+//   * segment residency — copy each column's reference-format bytes to HBM once per segment and build the small
+//     device-side directories (ImmutableSegmentLoader.load / PhysicalColumnIndexContainer reader wiring,
+//     seglocal/indexsegment/immutable/ImmutableSegmentLoader.java:153-214,
+//     seglocal/segment/index/column/PhysicalColumnIndexContainer.java:76-170);
+//   * plan packing — turn the per-segment filter trees (already dict-id predicates, as produced by the
+//     reference's PredicateEvaluators) into one flat device program with statically assigned mask slots;
+//   * launch — one query kernel per query per GPU over all its segments, partial results in a dense HBM table
+//     (replaces the per-segment operators + BaseCombineOperator thread pool,
+//     core/operator/combine/BaseCombineOperator.java:79-227);
+//   * compaction — non-empty groups back to the host (IntermediateResultsBlock payload).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pinot_gpu.h"
+#include "pgpu_internal.h"
+
+// kernels (pgpu_kernels.hip)
+size_t pgpu_static_smem_bytes();
+hipError_t pgpu_occupancy(int mode, size_t dyn_smem, int* blocks_per_cu);
+hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
+hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
+hipError_t pgpu_launch_finalize(const DevParams& p, int nblocks, int64_t* stats_out, hipStream_t st);
+hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts, int64_t* total,
+                               int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(PGPU_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+inline uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+inline uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+inline uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t le32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+int type_width(int32_t t) { return (t == PGPU_INT || t == PGPU_FLOAT) ? 4 : 8; }
+
+// Device buffer that frees itself.
+struct DevMem {
+  void* p = nullptr;
+  size_t n = 0;
+  DevMem() = default;
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+  DevMem(DevMem&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  ~DevMem() { reset(); }
+  void reset() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t bytes) {
+    reset();
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) n = bytes;
+    else p = nullptr;
+    return e;
+  }
+  hipError_t ensure(size_t bytes) { return n >= bytes ? hipSuccess : alloc(std::max(bytes, n * 3 / 2)); }
+};
+
+struct PinnedMem {
+  void* p = nullptr;
+  size_t n = 0;
+  PinnedMem() = default;
+  PinnedMem(const PinnedMem&) = delete;
+  PinnedMem& operator=(const PinnedMem&) = delete;
+  ~PinnedMem() { reset(); }
+  void reset() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t bytes) {
+    if (n >= bytes) return hipSuccess;
+    reset();
+    bytes = std::max(bytes, (size_t)4096);
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) n = bytes;
+    else p = nullptr;
+    return e;
+  }
+};
+
+struct Workspace {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells;
+  PinnedMem h_arena, h_stats, h_total;
+  bool busy = false;
+  ~Workspace() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+}  // namespace
+
+struct pgpu_context {
+  int device = 0;
+  int num_cus = 256;
+  std::mutex mu;
+  std::vector<std::unique_ptr<Workspace>> pool;
+  int occ_cache[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};  // mode -> (dyn smem, blocks/CU)
+};
+
+struct pgpu_buffer {
+  pgpu_context* ctx;
+  DevMem mem;
+  int32_t length;
+};
+
+namespace {
+
+struct HostColumn {
+  int32_t kind = PGPU_COL_NONE;
+  int32_t bits = 0;
+  int32_t card = 0;
+  int32_t fwd_card = 0;
+  int32_t dict_type = -1;
+  int32_t dict_card = 0;
+  int32_t inv_card = 0;
+  DevMem fwd, sorted, dict, inv_dir, inv_ct, inv_data;
+  uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
+};
+
+}  // namespace
+
+struct pgpu_segment {
+  pgpu_context* ctx;
+  int32_t num_docs;
+  std::vector<HostColumn> cols;
+  std::vector<DevColumn> dev;
+  bool sealed = false;
+};
+
+struct pgpu_query {
+  pgpu_context* ctx;
+  Workspace* ws;
+  hipStream_t stream;
+  DevParams params;
+  int grid;
+  pgpu_query_stats stats;
+};
+
+namespace {
+
+Workspace* acquire_ws(pgpu_context* ctx, int* err) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (auto& w : ctx->pool)
+    if (!w->busy) {
+      w->busy = true;
+      return w.get();
+    }
+  std::unique_ptr<Workspace> w(new Workspace());
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&w->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&w->ev1);
+  if (e != hipSuccess) {
+    *err = fail(PGPU_E_HIP, "workspace creation failed: %s", hipGetErrorString(e));
+    return nullptr;
+  }
+  w->busy = true;
+  ctx->pool.push_back(std::move(w));
+  return ctx->pool.back().get();
+}
+
+void release_ws(pgpu_context* ctx, Workspace* w) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  w->busy = false;
+}
+
+// ---- Roaring portable format (RoaringBitmap 0.9.26 serialize / ImmutableRoaringBitmap) ----------------------
+// cookie 12346: int32 cookie, int32 size, (key, card-1) uint16 pairs, int32 offsets, containers.
+// cookie 12347: low 16 bits = 12347, high 16 bits = size-1, run-flag bitset ceil(size/8) bytes, (key, card-1)
+//               pairs, int32 offsets only when size >= 4, containers.  Container: run (flag set) = uint16 n +
+//               n (start, length-1) pairs; else card > 4096 = bitmap 1024 x uint64; else array card x uint16.
+struct ParsedContainer {
+  uint32_t key, type, card;
+  const uint8_t* payload;
+  size_t payload_bytes;
+};
+
+int parse_roaring(const uint8_t* p, size_t n, std::vector<ParsedContainer>* out) {
+  if (n < 4) return fail(PGPU_E_INVALID, "roaring bitmap truncated");
+  const uint32_t cookie = le32(p);
+  size_t pos;
+  uint32_t size;
+  bool has_run = false;
+  const uint8_t* runflags = nullptr;
+  if ((cookie & 0xFFFFu) == 12347u) {
+    has_run = true;
+    size = (cookie >> 16) + 1;
+    runflags = p + 4;
+    pos = 4 + (size + 7) / 8;
+  } else if (cookie == 12346u) {
+    if (n < 8) return fail(PGPU_E_INVALID, "roaring bitmap truncated");
+    size = le32(p + 4);
+    pos = 8;
+  } else {
+    return fail(PGPU_E_INVALID, "bad roaring cookie %u", cookie);
+  }
+  if (size > 65536u) return fail(PGPU_E_INVALID, "bad roaring container count %u", size);
+  if (pos + 4ull * size > n) return fail(PGPU_E_INVALID, "roaring header truncated");
+  const uint8_t* kc = p + pos;
+  pos += 4ull * size;
+  if (!has_run || size >= 4) pos += 4ull * size;  // offsets
+  for (uint32_t i = 0; i < size; ++i) {
+    ParsedContainer c;
+    c.key = le16(kc + 4 * i);
+    const uint32_t card = (uint32_t)le16(kc + 4 * i + 2) + 1;
+    const bool run = has_run && ((runflags[i / 8] >> (i % 8)) & 1);
+    if (run) {
+      if (pos + 2 > n) return fail(PGPU_E_INVALID, "roaring run container truncated");
+      const uint32_t nruns = le16(p + pos);
+      pos += 2;
+      c.type = PGPU_CT_RUN;
+      c.card = nruns;
+      c.payload = p + pos;
+      c.payload_bytes = 4ull * nruns;
+    } else if (card > 4096) {
+      c.type = PGPU_CT_BITMAP;
+      c.card = card;
+      c.payload = p + pos;
+      c.payload_bytes = 8192;
+    } else {
+      c.type = PGPU_CT_ARRAY;
+      c.card = card;
+      c.payload = p + pos;
+      c.payload_bytes = 2ull * card;
+    }
+    if (pos + c.payload_bytes > n) return fail(PGPU_E_INVALID, "roaring container %u truncated", i);
+    if (i > 0 && c.key <= out->back().key) return fail(PGPU_E_INVALID, "roaring keys not ascending");
+    pos += c.payload_bytes;
+    out->push_back(c);
+  }
+  return PGPU_OK;
+}
+
+int check_column(pgpu_segment* seg, int32_t column) {
+  if (!seg) return fail(PGPU_E_INVALID, "null segment");
+  if (seg->sealed) return fail(PGPU_E_INVALID, "segment already sealed");
+  if (column < 0 || column >= (int32_t)seg->cols.size()) return fail(PGPU_E_INVALID, "bad column %d", column);
+  return PGPU_OK;
+}
+
+hipError_t upload(DevMem& m, const void* src, size_t bytes, size_t alloc_bytes, int mem_kind) {
+  hipError_t e = m.alloc(alloc_bytes);
+  if (e != hipSuccess) return e;
+  if (alloc_bytes > bytes) e = hipMemset((char*)m.p + bytes, 0, alloc_bytes - bytes);
+  if (e != hipSuccess) return e;
+  if (bytes)
+    e = hipMemcpy(m.p, src, bytes, mem_kind == PGPU_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice);
+  return e;
+}
+
+}  // namespace
+
+// =============================================================================================================
+extern "C" {
+
+int pgpu_abi_version(void) { return PGPU_ABI_VERSION; }
+
+int pgpu_last_error(char* buf, size_t len) {
+  if (buf && len) {
+    size_t k = std::min(len - 1, g_last_error.size());
+    memcpy(buf, g_last_error.data(), k);
+    buf[k] = 0;
+  }
+  return (int)g_last_error.size();
+}
+
+int pgpu_init(int device_ordinal, pgpu_context** out_ctx) {
+  if (!out_ctx) return fail(PGPU_E_INVALID, "null out_ctx");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device_ordinal < 0 || device_ordinal >= n)
+    return fail(PGPU_E_INVALID, "device %d out of range (%d devices)", device_ordinal, n);
+  HIP_TRY(hipSetDevice(device_ordinal));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device_ordinal));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(PGPU_E_UNSUPPORTED, "libpinotgpu is built for gfx950 (MI355X); device is %s", prop.gcnArchName);
+  auto* ctx = new pgpu_context();
+  ctx->device = device_ordinal;
+  ctx->num_cus = prop.multiProcessorCount;
+  *out_ctx = ctx;
+  return PGPU_OK;
+}
+
+int pgpu_shutdown(pgpu_context* ctx) {
+  if (!ctx) return PGPU_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ctx;
+  return PGPU_OK;
+}
+
+int pgpu_segment_create(pgpu_context* ctx, int32_t num_docs, int32_t num_columns, pgpu_segment** out_seg) {
+  if (!ctx || !out_seg) return fail(PGPU_E_INVALID, "null argument");
+  if (num_docs < 0 || num_columns < 0 || num_columns > 4096)
+    return fail(PGPU_E_INVALID, "bad segment shape (%d docs, %d columns)", num_docs, num_columns);
+  auto* s = new pgpu_segment();
+  s->ctx = ctx;
+  s->num_docs = num_docs;
+  s->cols.resize(num_columns);
+  *out_seg = s;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                   int32_t bits_per_value, int32_t cardinality, int32_t mem_kind) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (bits_per_value < 1 || bits_per_value > 32) return fail(PGPU_E_INVALID, "bits_per_value %d", bits_per_value);
+  const uint64_t need = ((uint64_t)seg->num_docs * bits_per_value + 7) / 8;
+  if (num_bytes < need || (!bytes && need))
+    return fail(PGPU_E_INVALID, "forward index of column %d: %llu bytes < %llu needed", column,
+                (unsigned long long)num_bytes, (unsigned long long)need);
+  HostColumn& c = seg->cols[column];
+  if (c.kind == PGPU_COL_SORTED) return fail(PGPU_E_INVALID, "column %d already has a sorted index", column);
+  const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
+  const uint64_t alloc = std::max<uint64_t>(ntiles * PGPU_TILE / 8 * bits_per_value, need) + 16;
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.fwd, bytes, need, alloc, mem_kind));
+  c.kind = PGPU_COL_FIXED_BIT;
+  c.bits = bits_per_value;
+  c.fwd_card = cardinality;
+  c.fwd_bytes = need;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_sorted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                  int32_t cardinality) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (cardinality < 1 || num_bytes != 8ull * cardinality || !bytes)
+    return fail(PGPU_E_INVALID, "sorted index of column %d: %llu bytes for cardinality %d", column,
+                (unsigned long long)num_bytes, cardinality);
+  HostColumn& c = seg->cols[column];
+  if (c.kind == PGPU_COL_FIXED_BIT) return fail(PGPU_E_INVALID, "column %d already has a forward index", column);
+  std::vector<int32_t> pairs(2 * (size_t)cardinality);
+  const uint8_t* b = (const uint8_t*)bytes;
+  int32_t prev_end = -1;
+  for (int32_t i = 0; i < cardinality; ++i) {
+    pairs[2 * i] = (int32_t)be32(b + 8 * i);
+    pairs[2 * i + 1] = (int32_t)be32(b + 8 * i + 4);
+    if (pairs[2 * i] != prev_end + 1 || pairs[2 * i + 1] < pairs[2 * i] - 1)
+      return fail(PGPU_E_INVALID, "sorted index of column %d: ranges not contiguous at dict id %d", column, i);
+    prev_end = pairs[2 * i + 1];
+  }
+  if (prev_end != seg->num_docs - 1)
+    return fail(PGPU_E_INVALID, "sorted index of column %d ends at %d, numDocs %d", column, prev_end, seg->num_docs);
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.sorted, pairs.data(), pairs.size() * 4, pairs.size() * 4, PGPU_MEM_HOST));
+  c.kind = PGPU_COL_SORTED;
+  c.fwd_card = cardinality;
+  c.fwd_bytes = num_bytes;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_type, const void* bytes,
+                                uint64_t num_bytes, int32_t cardinality) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (data_type < PGPU_INT || data_type > PGPU_STRING || cardinality < 1)
+    return fail(PGPU_E_INVALID, "dictionary of column %d: bad type %d / cardinality %d", column, data_type,
+                cardinality);
+  HostColumn& c = seg->cols[column];
+  c.dict_type = data_type;
+  c.dict_card = cardinality;
+  if (data_type == PGPU_STRING) return PGPU_OK;
+  const int w = type_width(data_type);
+  if (!bytes || num_bytes != (uint64_t)w * cardinality)
+    return fail(PGPU_E_INVALID, "dictionary of column %d: %llu bytes, expected %llu", column,
+                (unsigned long long)num_bytes, (unsigned long long)w * cardinality);
+  std::vector<uint8_t> le(num_bytes);
+  const uint8_t* b = (const uint8_t*)bytes;
+  for (int32_t i = 0; i < cardinality; ++i) {
+    if (w == 4) {
+      uint32_t v = be32(b + 4 * i);
+      memcpy(&le[4 * i], &v, 4);
+    } else {
+      uint64_t v = be64(b + 8 * i);
+      memcpy(&le[8 * (size_t)i], &v, 8);
+    }
+  }
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
+  c.dict_bytes = num_bytes;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                    int32_t cardinality) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  const uint8_t* b = (const uint8_t*)bytes;
+  const uint64_t hdr = 4ull * ((uint64_t)cardinality + 1);
+  if (cardinality < 1 || !bytes || num_bytes < hdr)
+    return fail(PGPU_E_INVALID, "inverted index of column %d: %llu bytes for cardinality %d", column,
+                (unsigned long long)num_bytes, cardinality);
+  // BitmapInvertedIndexReader: offsets may be absolute (writer) or bitmap-relative; subtract the first one.
+  const uint32_t first = be32(b);
+  std::vector<uint32_t> dir(cardinality + 1);
+  std::vector<DevContainer> cts;
+  std::vector<uint8_t> data;
+  std::vector<ParsedContainer> parsed;
+  for (int32_t i = 0; i < cardinality; ++i) {
+    const uint32_t o0 = be32(b + 4ull * i), o1 = be32(b + 4ull * (i + 1));
+    if (o0 < first || o1 < o0 || hdr + (o1 - first) > num_bytes)
+      return fail(PGPU_E_INVALID, "inverted index of column %d: bad offsets at dict id %d", column, i);
+    parsed.clear();
+    rc = parse_roaring(b + hdr + (o0 - first), o1 - o0, &parsed);
+    if (rc) return rc;
+    dir[i] = (uint32_t)cts.size();
+    for (const ParsedContainer& pc : parsed) {
+      if ((uint64_t)pc.key << 16 >= (uint64_t)seg->num_docs + 65536)
+        return fail(PGPU_E_INVALID, "inverted index of column %d: container key %u beyond numDocs", column, pc.key);
+      size_t off = (data.size() + 7) & ~(size_t)7;
+      data.resize(off + pc.payload_bytes);
+      memcpy(&data[off], pc.payload, pc.payload_bytes);
+      cts.push_back(DevContainer{pc.key, pc.type, pc.card, (uint32_t)off});
+      if (data.size() > 0xFFFFFFF0ull) return fail(PGPU_E_INVALID, "inverted index too large");
+    }
+  }
+  dir[cardinality] = (uint32_t)cts.size();
+  HostColumn& c = seg->cols[column];
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.inv_dir, dir.data(), dir.size() * 4, dir.size() * 4, PGPU_MEM_HOST));
+  HIP_TRY(upload(c.inv_ct, cts.data(), cts.size() * sizeof(DevContainer), cts.size() * sizeof(DevContainer) + 16,
+                 PGPU_MEM_HOST));
+  HIP_TRY(upload(c.inv_data, data.data(), data.size(), data.size() + 16, PGPU_MEM_HOST));
+  c.inv_card = cardinality;
+  c.inv_bytes = num_bytes;
+  return PGPU_OK;
+}
+
+int pgpu_segment_seal(pgpu_segment* seg) {
+  if (!seg) return fail(PGPU_E_INVALID, "null segment");
+  seg->dev.resize(seg->cols.size());
+  for (size_t i = 0; i < seg->cols.size(); ++i) {
+    HostColumn& c = seg->cols[i];
+    DevColumn d{};
+    d.fwd = (const uint32_t*)c.fwd.p;
+    d.sorted = (const int32_t*)c.sorted.p;
+    d.dict = c.dict.p;
+    d.inv_dir = (const uint32_t*)c.inv_dir.p;
+    d.inv_ct = (const DevContainer*)c.inv_ct.p;
+    d.inv_data = (const uint8_t*)c.inv_data.p;
+    d.kind = c.kind;
+    d.bits = c.bits;
+    d.card = c.fwd_card ? c.fwd_card : (c.dict_card ? c.dict_card : c.inv_card);
+    d.dict_type = c.dict_type;
+    c.card = d.card;
+    if (c.dict_card && c.fwd_card && c.dict_card != c.fwd_card)
+      return fail(PGPU_E_INVALID, "column %zu: dictionary cardinality %d != index cardinality %d", i, c.dict_card,
+                  c.fwd_card);
+    seg->dev[i] = d;
+  }
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  seg->sealed = true;
+  return PGPU_OK;
+}
+
+int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes) {
+  if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
+  uint64_t t = 0;
+  for (const HostColumn& c : seg->cols)
+    t += c.fwd.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n;
+  *out_bytes = t;
+  return PGPU_OK;
+}
+
+int pgpu_segment_release(pgpu_segment* seg) {
+  if (!seg) return PGPU_OK;
+  (void)hipSetDevice(seg->ctx->device);
+  delete seg;
+  return PGPU_OK;
+}
+
+int pgpu_remap_upload(pgpu_context* ctx, const int32_t* map, int32_t length, pgpu_buffer** out_buf) {
+  if (!ctx || !out_buf || length < 0 || (!map && length)) return fail(PGPU_E_INVALID, "bad remap arguments");
+  auto* b = new pgpu_buffer();
+  b->ctx = ctx;
+  b->length = length;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e == hipSuccess) e = upload(b->mem, map, 4ull * length, 4ull * length + 16, PGPU_MEM_HOST);
+  if (e != hipSuccess) {
+    delete b;
+    return fail(PGPU_E_HIP, "remap upload: %s", hipGetErrorString(e));
+  }
+  *out_buf = b;
+  return PGPU_OK;
+}
+
+int pgpu_buffer_release(pgpu_buffer* buf) {
+  delete buf;
+  return PGPU_OK;
+}
+
+int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
+  if (!q || !out) return fail(PGPU_E_INVALID, "null argument");
+  if (q->num_aggs < 0 || q->num_aggs > PGPU_MAX_AGGS) return fail(PGPU_E_UNSUPPORTED, "%d aggregations", q->num_aggs);
+  if (q->num_group_columns < 0 || q->num_group_columns > PGPU_MAX_GCOLS)
+    return fail(PGPU_E_UNSUPPORTED, "%d group-by columns", q->num_group_columns);
+  if (q->num_segments < 1 || !q->segments) return fail(PGPU_E_INVALID, "no segments");
+  memset(out, 0, sizeof(*out));
+  uint64_t G = 1;
+  for (int i = 0; i < q->num_group_columns; ++i) {
+    const int32_t c = q->group_cardinalities ? q->group_cardinalities[i] : 0;
+    if (c < 1) return fail(PGPU_E_INVALID, "group column %d cardinality %d", i, c);
+    G *= (uint64_t)c;
+    if (G > (1ull << 31)) return fail(PGPU_E_UNSUPPORTED, "group key space %llu exceeds the dense-table limit", G);
+  }
+  out->num_keys = G;
+  out->num_sections = 1;
+  out->section_op[0] = PGPU_RED_SUM_I64;
+  const pgpu_segment* s0 = q->segments[0].segment;
+  for (int a = 0; a < q->num_aggs; ++a) {
+    const pgpu_agg& ag = q->aggs[a];
+    if (ag.fn < PGPU_AGG_COUNT || ag.fn > PGPU_AGG_AVG) return fail(PGPU_E_UNSUPPORTED, "aggregation fn %d", ag.fn);
+    if (ag.fn == PGPU_AGG_COUNT) {
+      out->agg_section[a] = 0;
+      out->agg_value_type[a] = -1;
+      continue;
+    }
+    if (ag.column < 0 || ag.column >= q->num_columns) return fail(PGPU_E_INVALID, "agg %d column %d", a, ag.column);
+    const int32_t slot = q->segments[0].column_map[ag.column];
+    if (!s0 || slot < 0 || slot >= (int32_t)s0->cols.size()) return fail(PGPU_E_INVALID, "agg %d column slot", a);
+    const int32_t vt = s0->cols[slot].dict_type;
+    if (vt < PGPU_INT || vt > PGPU_DOUBLE)
+      return fail(PGPU_E_UNSUPPORTED, "agg %d over a non-numeric or dictionary-less column", a);
+    int op;
+    if (ag.fn == PGPU_AGG_MIN) op = PGPU_RED_MIN_I64;
+    else if (ag.fn == PGPU_AGG_MAX) op = PGPU_RED_MAX_I64;
+    else op = (vt == PGPU_INT || vt == PGPU_LONG) ? PGPU_RED_SUM_I64 : PGPU_RED_SUM_F64;
+    out->agg_section[a] = out->num_sections;
+    out->agg_value_type[a] = vt;
+    out->section_op[out->num_sections++] = op;
+  }
+  return PGPU_OK;
+}
+
+double pgpu_decode_minmax_key(int64_t key, int32_t value_type) {
+  if (value_type == PGPU_INT || value_type == PGPU_LONG) return (double)key;
+  int64_t b = key >= 0 ? key : (key ^ 0x7FFFFFFFFFFFFFFFll);
+  double d;
+  memcpy(&d, &b, 8);
+  return d;
+}
+
+int pgpu_kernel_geometry(pgpu_context* ctx, int32_t* out_grid, int32_t* out_tile_docs, int32_t* out_block) {
+  if (!ctx) return fail(PGPU_E_INVALID, "null ctx");
+  if (out_tile_docs) *out_tile_docs = PGPU_TILE;
+  if (out_block) *out_block = PGPU_BLOCK;
+  if (out_grid) {
+    int bpc = 0;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(pgpu_occupancy(PGPU_MODE_AGG, 0, &bpc));
+    *out_grid = std::max(1, bpc) * ctx->num_cus;
+  }
+  return PGPU_OK;
+}
+
+}  // extern "C"
+
+// ---- plan packing ---------------------------------------------------------------------------------------------
+namespace {
+
+struct Packer {
+  std::vector<DevSeg> segs;
+  std::vector<DevInstr> instrs;
+  std::vector<DevColumn> cols;
+  std::vector<int32_t> pool;
+  std::vector<const int32_t*> remaps;
+};
+
+// Convert one segment's prefix-order filter program into slot-resolved device instructions.
+int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_segment* seg,
+                   Packer& pk) {
+  struct Frame {
+    int kind;  // 0 AND, 1 OR, 2 NOT
+    int slot;
+    int care;  // care slot of this frame's children
+    int outer_care;
+    std::vector<int> patch;  // AND_CHILD instructions to patch with the AND_END index
+  };
+  std::vector<Frame> st;
+  const int base = (int)pk.instrs.size();
+  int cur = 0;     // slot the next node writes
+  int care = -1;   // care slot of the next node
+  auto emit = [&](DevInstr in) { pk.instrs.push_back(in); return (int)pk.instrs.size() - 1 - base; };
+  auto close_nots = [&]() {
+    while (!st.empty() && st.back().kind == 2) {
+      DevInstr in{};
+      in.op = PGPU_I_NOT;
+      in.dst = in.src = st.back().slot;
+      in.care = st.back().outer_care;
+      emit(in);
+      cur = st.back().slot;
+      care = st.back().outer_care;
+      st.pop_back();
+    }
+  };
+  auto col_of = [&](int32_t qc, const DevColumn** out) -> int {
+    if (qc < 0 || qc >= q->num_columns) return fail(PGPU_E_INVALID, "filter column %d", qc);
+    const int32_t slot = sp.column_map[qc];
+    if (slot < 0 || slot >= (int32_t)seg->dev.size()) return fail(PGPU_E_INVALID, "filter column %d slot %d", qc, slot);
+    *out = &seg->dev[slot];
+    return PGPU_OK;
+  };
+  for (int i = 0; i < sp.num_filter_nodes; ++i) {
+    const pgpu_filter_node& nd = sp.filter[i];
+    if (cur >= PGPU_MAX_SLOTS) return fail(PGPU_E_UNSUPPORTED, "filter nesting deeper than %d", PGPU_MAX_SLOTS);
+    DevInstr in{};
+    in.col = nd.column;
+    in.negate = nd.negate ? 1 : 0;
+    in.dst = cur;
+    in.care = care;
+    switch (nd.op) {
+      case PGPU_F_MATCH_ALL:
+      case PGPU_F_EMPTY:
+        in.op = nd.op == PGPU_F_MATCH_ALL ? PGPU_I_ALL : PGPU_I_EMPTY;
+        emit(in);
+        close_nots();
+        break;
+      case PGPU_F_SCAN: {
+        const DevColumn* c;
+        int rc = col_of(nd.column, &c);
+        if (rc) return rc;
+        if (c->kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "SCAN on column %d without forward index", nd.column);
+        in.op = PGPU_I_SCAN;
+        in.pred = nd.pred;
+        if (nd.pred == PGPU_PRED_RANGE) {
+          in.lo = std::max(0, nd.lo);
+          in.hi = std::min(nd.hi, c->card);
+          if (in.hi < in.lo) in.hi = in.lo;
+        } else if (nd.pred == PGPU_PRED_SET) {
+          in.pool_off = (int32_t)pk.pool.size();
+          pk.pool.resize(pk.pool.size() + (c->card + 31) / 32 + 1, 0);
+          for (int k = 0; k < nd.num_ids; ++k) {
+            const int32_t id = nd.ids[k];
+            if (id < 0 || id >= c->card) return fail(PGPU_E_INVALID, "SET id %d out of range", id);
+            pk.pool[in.pool_off + (id >> 5)] |= (int32_t)(1u << (id & 31));
+          }
+        } else {
+          return fail(PGPU_E_INVALID, "predicate kind %d", nd.pred);
+        }
+        emit(in);
+        close_nots();
+        break;
+      }
+      case PGPU_F_INVERTED: {
+        const DevColumn* c;
+        int rc = col_of(nd.column, &c);
+        if (rc) return rc;
+        if (!c->inv_dir) return fail(PGPU_E_INVALID, "INVERTED on column %d without inverted index", nd.column);
+        in.op = PGPU_I_INV;
+        in.pool_off = (int32_t)pk.pool.size();
+        in.n = nd.num_ids;
+        for (int k = 0; k < nd.num_ids; ++k) {
+          if (nd.ids[k] < 0 || nd.ids[k] >= c->card) return fail(PGPU_E_INVALID, "bitmap id %d out of range", nd.ids[k]);
+          pk.pool.push_back(nd.ids[k]);
+        }
+        emit(in);
+        close_nots();
+        break;
+      }
+      case PGPU_F_SORTED: {
+        in.op = PGPU_I_SORTED;
+        std::vector<std::pair<int32_t, int32_t>> r;
+        for (int k = 0; k < nd.num_ids; ++k) {
+          int32_t s = std::max(0, nd.ids[2 * k]), e = std::min(nd.ids[2 * k + 1], seg->num_docs - 1);
+          if (s <= e) r.emplace_back(s, e);
+        }
+        std::sort(r.begin(), r.end());
+        in.pool_off = (int32_t)pk.pool.size();
+        int n = 0;
+        for (auto& x : r) {
+          if (n && x.first <= pk.pool.back() + 1) {
+            pk.pool.back() = std::max(pk.pool.back(), x.second);
+          } else {
+            pk.pool.push_back(x.first);
+            pk.pool.push_back(x.second);
+            ++n;
+          }
+        }
+        in.n = n;
+        emit(in);
+        close_nots();
+        break;
+      }
+      case PGPU_F_AND_BEGIN:
+      case PGPU_F_OR_BEGIN: {
+        const bool is_and = nd.op == PGPU_F_AND_BEGIN;
+        in.op = is_and ? PGPU_I_AND_BEGIN : PGPU_I_OR_BEGIN;
+        emit(in);
+        Frame f;
+        f.kind = is_and ? 0 : 1;
+        f.slot = cur;
+        f.outer_care = care;
+        f.care = is_and ? cur : care;
+        st.push_back(f);
+        cur = f.slot + 1;
+        care = f.care;
+        break;
+      }
+      case PGPU_F_AND_CHILD_END:
+      case PGPU_F_OR_CHILD_END: {
+        const bool is_and = nd.op == PGPU_F_AND_CHILD_END;
+        if (st.empty() || st.back().kind != (is_and ? 0 : 1)) return fail(PGPU_E_INVALID, "unbalanced filter at node %d", i);
+        in.op = is_and ? PGPU_I_AND_CHILD : PGPU_I_OR_CHILD;
+        in.dst = st.back().slot;
+        in.src = st.back().slot + 1;
+        in.care = st.back().outer_care;
+        const int idx = emit(in);
+        if (is_and) st.back().patch.push_back(idx);
+        cur = st.back().slot + 1;
+        care = st.back().care;
+        break;
+      }
+      case PGPU_F_AND_END:
+      case PGPU_F_OR_END: {
+        const bool is_and = nd.op == PGPU_F_AND_END;
+        if (st.empty() || st.back().kind != (is_and ? 0 : 1)) return fail(PGPU_E_INVALID, "unbalanced filter at node %d", i);
+        in.op = is_and ? PGPU_I_AND_END : PGPU_I_OR_END;
+        in.dst = st.back().slot;
+        const int idx = emit(in);
+        for (int p : st.back().patch) pk.instrs[base + p].jump = idx;
+        cur = st.back().slot;
+        care = st.back().outer_care;
+        st.pop_back();
+        close_nots();
+        break;
+      }
+      case PGPU_F_NOT: {
+        Frame f;
+        f.kind = 2;
+        f.slot = cur;
+        f.outer_care = care;
+        f.care = care;
+        st.push_back(f);
+        break;
+      }
+      default:
+        return fail(PGPU_E_INVALID, "filter op %d", nd.op);
+    }
+  }
+  if (!st.empty()) return fail(PGPU_E_INVALID, "unterminated filter program");
+  if (sp.num_filter_nodes > 0 && cur != 0) return fail(PGPU_E_INVALID, "filter program leaves slot %d", cur);
+  return PGPU_OK;
+}
+
+int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_layout& L, Packer& pk, DevParams& p) {
+  memset(&p, 0, sizeof(p));
+  p.ncols = q->num_columns;
+  p.nagg = q->num_aggs;
+  p.ngcols = q->num_group_columns;
+  p.nsec = L.num_sections;
+  p.G = L.num_keys;
+  p.flags = (q->flags & PGPU_Q_STATS) ? PGPU_FLAG_STATS : 0;
+  for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
+  uint32_t stride = 1;
+  for (int g = 0; g < q->num_group_columns; ++g) {
+    if (q->group_columns[g] < 0 || q->group_columns[g] >= q->num_columns)
+      return fail(PGPU_E_INVALID, "group column %d", q->group_columns[g]);
+    p.gcols[g] = q->group_columns[g];
+    p.gstride[g] = stride;
+    stride *= (uint32_t)q->group_cardinalities[g];
+  }
+  for (int a = 0; a < q->num_aggs; ++a) {
+    p.aggs[a].fn = q->aggs[a].fn;
+    p.aggs[a].col = q->aggs[a].column;
+    p.aggs[a].sec = L.agg_section[a];
+    p.aggs[a].op = L.section_op[L.agg_section[a]];
+    p.aggs[a].vtype = L.agg_value_type[a];
+  }
+  int tiles = 0;
+  for (int s = 0; s < q->num_segments; ++s) {
+    const pgpu_segment_plan& sp = q->segments[s];
+    const pgpu_segment* seg = sp.segment;
+    if (!seg || !seg->sealed) return fail(PGPU_E_INVALID, "segment %d missing or not sealed", s);
+    if (seg->ctx != ctx) return fail(PGPU_E_INVALID, "segment %d belongs to another context", s);
+    if (!sp.column_map && q->num_columns) return fail(PGPU_E_INVALID, "segment %d: no column map", s);
+    DevSeg ds{};
+    ds.num_docs = seg->num_docs;
+    ds.tile_begin = tiles;
+    ds.prog_begin = (int32_t)pk.instrs.size();
+    ds.col_begin = (int32_t)pk.cols.size();
+    ds.remap_begin = (int32_t)pk.remaps.size();
+    for (int c = 0; c < q->num_columns; ++c) {
+      const int32_t slot = sp.column_map[c];
+      if (slot < 0 || slot >= (int32_t)seg->dev.size())
+        return fail(PGPU_E_INVALID, "segment %d: column %d mapped to bad slot %d", s, c, slot);
+      pk.cols.push_back(seg->dev[slot]);
+    }
+    // group / aggregation column checks
+    for (int g = 0; g < q->num_group_columns; ++g) {
+      const DevColumn& c = pk.cols[ds.col_begin + p.gcols[g]];
+      if (c.kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "segment %d: group column without forward index", s);
+      const pgpu_buffer* rb = sp.group_remap ? sp.group_remap[g] : nullptr;
+      if (rb && rb->length < c.card) return fail(PGPU_E_INVALID, "segment %d: remap shorter than cardinality", s);
+      if (!rb && c.card > q->group_cardinalities[g])
+        return fail(PGPU_E_INVALID, "segment %d: identity group ids exceed the global cardinality", s);
+      pk.remaps.push_back(rb ? (const int32_t*)rb->mem.p : nullptr);
+    }
+    for (int a = 0; a < q->num_aggs; ++a) {
+      if (q->aggs[a].fn == PGPU_AGG_COUNT) continue;
+      const DevColumn& c = pk.cols[ds.col_begin + q->aggs[a].column];
+      if (c.kind == PGPU_COL_NONE || !c.dict) return fail(PGPU_E_INVALID, "segment %d: agg column not readable", s);
+      if (c.dict_type != L.agg_value_type[a]) return fail(PGPU_E_INVALID, "segment %d: agg column type differs", s);
+    }
+    if (sp.num_filter_nodes > 0) {
+      int rc = convert_filter(q, sp, seg, pk);
+      if (rc) return rc;
+    }
+    ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
+    pk.segs.push_back(ds);
+    tiles += (seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
+  }
+  p.nseg = q->num_segments;
+  p.total_tiles = tiles;
+  return PGPU_OK;
+}
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+}  // namespace
+
+extern "C" {
+
+int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
+                      uint64_t table_bytes, pgpu_query** out_query) {
+  if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
+  pgpu_table_layout L;
+  int rc = pgpu_table_layout_of(q, &L);
+  if (rc) return rc;
+  const uint64_t need = 8ull * L.num_sections * L.num_keys;
+  if (!dev_table || table_bytes < need)
+    return fail(PGPU_E_INVALID, "table buffer %llu bytes < %llu needed", (unsigned long long)table_bytes,
+                (unsigned long long)need);
+  Packer pk;
+  DevParams p;
+  rc = pack_query(ctx, q, L, pk, p);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+
+  // mode and launch geometry
+  size_t dyn = 0;
+  if (q->num_group_columns == 0) {
+    p.mode = PGPU_MODE_AGG;
+  } else if (8ull * L.num_sections * L.num_keys + PGPU_TILE * 4 <= PGPU_LDS_TABLE_BYTES) {
+    p.mode = PGPU_MODE_LDS;
+    dyn = PGPU_TILE * 4 + 8ull * L.num_sections * L.num_keys;
+  } else {
+    p.mode = PGPU_MODE_GLOBAL;
+    dyn = PGPU_TILE * 4;
+  }
+  int bpc = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->occ_cache[p.mode][0] == (int)dyn) bpc = ctx->occ_cache[p.mode][1];
+  }
+  if (bpc <= 0) {
+    HIP_TRY(pgpu_occupancy(p.mode, dyn, &bpc));
+    if (bpc < 1) return fail(PGPU_E_HIP, "query kernel does not fit a CU (dyn LDS %zu)", dyn);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->occ_cache[p.mode][0] = (int)dyn;
+    ctx->occ_cache[p.mode][1] = bpc;
+  }
+  const int grid = std::max(1, std::min(p.total_tiles, bpc * ctx->num_cus));
+
+  Workspace* ws = acquire_ws(ctx, &rc);
+  if (!ws) return rc;
+  auto bail = [&](int code) {
+    release_ws(ctx, ws);
+    return code;
+  };
+  hipStream_t st = stream ? (hipStream_t)stream : ws->stream;
+
+  // arena: segs | instrs | cols | pool | remaps
+  const size_t o_segs = 0;
+  const size_t o_ins = align16(o_segs + pk.segs.size() * sizeof(DevSeg));
+  const size_t o_cols = align16(o_ins + pk.instrs.size() * sizeof(DevInstr));
+  const size_t o_pool = align16(o_cols + pk.cols.size() * sizeof(DevColumn));
+  const size_t o_rem = align16(o_pool + pk.pool.size() * 4);
+  const size_t total = align16(o_rem + pk.remaps.size() * sizeof(void*)) + 16;
+  hipError_t e = ws->h_arena.ensure(total);
+  if (e == hipSuccess) e = ws->arena.ensure(total);
+  if (e == hipSuccess) e = ws->slab.ensure(8ull * grid * L.num_sections + 16);
+  if (e == hipSuccess) e = ws->stats.ensure(8ull * grid * PGPU_NSTATS + 16);
+  if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
+  if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS);
+  if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
+  char* h = (char*)ws->h_arena.p;
+  memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
+  memcpy(h + o_ins, pk.instrs.data(), pk.instrs.size() * sizeof(DevInstr));
+  memcpy(h + o_cols, pk.cols.data(), pk.cols.size() * sizeof(DevColumn));
+  memcpy(h + o_pool, pk.pool.data(), pk.pool.size() * 4);
+  memcpy(h + o_rem, pk.remaps.data(), pk.remaps.size() * sizeof(void*));
+  char* d = (char*)ws->arena.p;
+  p.segs = (const DevSeg*)(d + o_segs);
+  p.instrs = (const DevInstr*)(d + o_ins);
+  p.cols = (const DevColumn*)(d + o_cols);
+  p.pool = (const int32_t*)(d + o_pool);
+  p.remaps = (const int32_t* const*)(d + o_rem);
+  p.table = (int64_t*)dev_table;
+  p.slab = (int64_t*)ws->slab.p;
+  p.stats = (int64_t*)ws->stats.p;
+
+  e = hipMemcpyAsync(ws->arena.p, ws->h_arena.p, total, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && p.mode != PGPU_MODE_AGG) e = pgpu_launch_table_init(p, st);
+  if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
+  if (e == hipSuccess) e = pgpu_launch_query(p, grid, dyn, st);
+  if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
+  if (e == hipSuccess) e = pgpu_launch_finalize(p, grid, (int64_t*)ws->stats_out.p, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ws->h_stats.p, ws->stats_out.p, 8 * PGPU_NSTATS, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
+
+  auto* qq = new pgpu_query();
+  qq->ctx = ctx;
+  qq->ws = ws;
+  qq->stream = st;
+  qq->params = p;
+  qq->grid = grid;
+  memset(&qq->stats, 0, sizeof(qq->stats));
+  int64_t tot_docs = 0;
+  for (int s = 0; s < q->num_segments; ++s) tot_docs += q->segments[s].segment->num_docs;
+  qq->stats.num_total_docs = tot_docs;
+  *out_query = qq;
+  return PGPU_OK;
+}
+
+int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
+  if (!qq) return fail(PGPU_E_INVALID, "null query");
+  HIP_TRY(hipSetDevice(qq->ctx->device));
+  HIP_TRY(hipStreamSynchronize(qq->stream));
+  const int64_t* s = (const int64_t*)qq->ws->h_stats.p;
+  qq->stats.num_docs_scanned = s[PGPU_STAT_MATCHED];
+  qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED];
+  qq->stats.sparse_sector_bytes = s[PGPU_STAT_SECTOR_BYTES];
+  qq->stats.dense_bytes = s[PGPU_STAT_DENSE_BYTES];
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
+  qq->stats.kernel_ms = ms;
+  if (out_stats) *out_stats = qq->stats;
+  return PGPU_OK;
+}
+
+int pgpu_query_release(pgpu_query* qq) {
+  if (!qq) return PGPU_OK;
+  release_ws(qq->ctx, qq->ws);
+  delete qq;
+  return PGPU_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, const void* dev_table,
+                 hipStream_t st, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
+                 uint64_t* out_num_groups) {
+  const uint64_t G = L->num_keys;
+  const int nsec = L->num_sections;
+  const uint64_t nb = (G + 4095) / 4096;
+  HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16));
+  HIP_TRY(ws->cmp_total.ensure(16));
+  HIP_TRY(ws->h_total.ensure(16));
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, (int32_t*)ws->cmp_counts.p,
+                              (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st));
+  HIP_TRY(hipMemcpyAsync(ws->h_total.p, ws->cmp_total.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t n = (uint64_t)*(const int64_t*)ws->h_total.p;
+  *out_num_groups = n;
+  if (n > capacity)
+    return fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
+                (unsigned long long)capacity);
+  if (n == 0) return PGPU_OK;
+  HIP_TRY(ws->cmp_keys.ensure(8 * n));
+  HIP_TRY(ws->cmp_cells.ensure(8 * n * nsec));
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, (int32_t*)ws->cmp_counts.p, nullptr,
+                              (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st));
+  HIP_TRY(hipMemcpyAsync(out_keys, ws->cmp_keys.p, 8 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out_cells, ws->cmp_cells.p, 8 * n * nsec, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  (void)ctx;
+  return PGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
+                       int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups) {
+  if (!ctx || !layout || !dev_table || !out_num_groups) return fail(PGPU_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = 0;
+  Workspace* ws = acquire_ws(ctx, &rc);
+  if (!ws) return rc;
+  rc = compact_into(ctx, ws, layout, dev_table, stream ? (hipStream_t)stream : ws->stream, out_keys, out_cells,
+                    capacity, out_num_groups);
+  release_ws(ctx, ws);
+  return rc;
+}
+
+int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
+                       uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
+  if (!ctx || !q || !out_num_groups) return fail(PGPU_E_INVALID, "null argument");
+  pgpu_table_layout L;
+  int rc = pgpu_table_layout_of(q, &L);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  int err = 0;
+  Workspace* tws = acquire_ws(ctx, &err);  // owns the table buffer for this call
+  if (!tws) return err;
+  const uint64_t bytes = 8ull * L.num_sections * L.num_keys;
+  hipError_t e = tws->table.ensure(bytes);
+  if (e != hipSuccess) {
+    release_ws(ctx, tws);
+    return fail(PGPU_E_HIP, "table allocation: %s", hipGetErrorString(e));
+  }
+  pgpu_query* qq = nullptr;
+  rc = pgpu_query_launch(ctx, q, tws->stream, tws->table.p, tws->table.n, &qq);
+  if (rc == PGPU_OK) rc = pgpu_query_wait(qq, out_stats);
+  if (rc == PGPU_OK)
+    rc = compact_into(ctx, qq->ws, &L, tws->table.p, tws->stream, out_keys, out_cells, capacity, out_num_groups);
+  if (qq) pgpu_query_release(qq);
+  release_ws(ctx, tws);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,469 @@
+"""GpuPlanMaker: the host side of the drop-in boundary for aggregation / group-by queries.
+
+Mirrors the reference's per-segment planning and hands the whole query to libpinotgpu in one call per GPU:
+
+* filter tree -> physical operator tree, exactly as ``FilterPlanNode.constructPhysicalOperator``
+  (core/plan/FilterPlanNode.java:192-313) and ``FilterOperatorUtils`` (leaf choice sorted > inverted > scan,
+  empty/match-all folding, stable AND re-ordering by priority; core/operator/filter/FilterOperatorUtils.java:42-221);
+  the tree is then emitted as the flat prefix program of ``pgpu_filter_node``;
+* predicates -> dict-id ranges / sets per segment (``predicate.py``; SortedIndexBasedFilterOperator doc ranges,
+  core/operator/filter/SortedIndexBasedFilterOperator.java:60-135; BitmapBasedFilterOperator matching /
+  non-matching ids + flip, BitmapBasedFilterOperator.java:66-110);
+* group-by columns -> a global dictionary (sorted union of the segment dictionaries) and per-segment remap
+  tables, so that per-segment dict-id keys (DictionaryBasedGroupKeyGenerator raw keys, :275-322) merge across
+  segments in HBM instead of in ``GroupByOrderByCombineOperator``'s IndexedTable (:127-248);
+* results -> final aggregation values (``AggregationFunction.extractFinalResult``) and the execution statistics
+  (CombineOperatorUtils.setExecutionStatistics, core/operator/combine/CombineOperatorUtils.java:55-82).
+
+Group-count semantics: when a segment's key space can exceed ``numGroupsLimit`` in a map-based holder the
+reference keeps only the first-seen keys (DictionaryBasedGroupKeyGenerator.java:991-1016); that shape is
+reported as PGPU_E_UNSUPPORTED-equivalent (``UnsupportedPlanError``) so the server keeps its CPU plan.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import (PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX, PGPU_AGG_MIN, PGPU_AGG_SUM, PGPU_DOUBLE,
+                   PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64,
+                   PGPU_RED_SUM_I64, PGPU_STRING, Agg, FilterNode, QueryDesc, QueryStats, SegmentPlan, TableLayout,
+                   UnsupportedPlanError)
+from .predicate import DictPredicateEvaluator, SortedDictionary, get_predicate_evaluator
+from .query import FilterContext, QueryContext
+from .segment import GpuContext, GpuSegment
+
+AGG_FN = {"COUNT": PGPU_AGG_COUNT, "SUM": PGPU_AGG_SUM, "MIN": PGPU_AGG_MIN, "MAX": PGPU_AGG_MAX,
+          "AVG": PGPU_AGG_AVG}
+DEFAULT_NUM_GROUPS_LIMIT = 100_000          # InstancePlanMakerImplV2.java:73-74
+DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000
+
+
+# ---- physical filter operators (host-side tree) ---------------------------------------------------------------
+@dataclass
+class FilterOp:
+    kind: str                                 # EMPTY, ALL, SCAN, INV, SORTED, AND, OR, NOT
+    children: List["FilterOp"] = field(default_factory=list)
+    column: Optional[str] = None
+    evaluator: Optional[DictPredicateEvaluator] = None
+    doc_ranges: Optional[List[Tuple[int, int]]] = None
+    negate: bool = False
+
+    def priority(self) -> int:
+        """FilterOperatorUtils.reorderAndFilterChildOperators#getPriority (single-value columns)."""
+        if self.kind == "SORTED":
+            return 0
+        if self.kind == "INV":
+            return 1
+        if self.kind == "AND":
+            return 3
+        if self.kind == "OR":
+            return 4
+        if self.kind == "NOT":
+            return self.children[0].priority()
+        return 5  # SCAN
+
+
+EMPTY = FilterOp("EMPTY")
+ALL = FilterOp("ALL")
+
+
+class SegmentFilterPlanner:
+    """FilterPlanNode + FilterOperatorUtils for one segment."""
+
+    def __init__(self, seg: GpuSegment):
+        self.seg = seg
+        self._dicts: Dict[str, SortedDictionary] = {}
+
+    def dictionary(self, column: str) -> SortedDictionary:
+        d = self._dicts.get(column)
+        if d is None:
+            col = self.seg.column(column)
+            d = SortedDictionary(self.seg.dictionaries[column], col.data_type)
+            self._dicts[column] = d
+        return d
+
+    def build(self, f: Optional[FilterContext]) -> FilterOp:
+        return ALL if f is None else self._construct(f)
+
+    def _construct(self, f: FilterContext) -> FilterOp:
+        if f.type == "AND":
+            kids = []
+            for ch in f.children:
+                op = self._construct(ch)
+                if op.kind == "EMPTY":
+                    return EMPTY
+                if op.kind != "ALL":
+                    kids.append(op)
+            if not kids:
+                return ALL
+            if len(kids) == 1:
+                return kids[0]
+            kids.sort(key=lambda o: o.priority())  # stable, like List.sort with a Comparator
+            return FilterOp("AND", kids)
+        if f.type == "OR":
+            kids = []
+            for ch in f.children:
+                op = self._construct(ch)
+                if op.kind == "ALL":
+                    return ALL
+                if op.kind != "EMPTY":
+                    kids.append(op)
+            if not kids:
+                return EMPTY
+            if len(kids) == 1:
+                return kids[0]
+            return FilterOp("OR", kids)
+        if f.type == "NOT":
+            child = self._construct(f.children[0])
+            if child.kind == "ALL":
+                return EMPTY
+            if child.kind == "EMPTY":
+                return ALL
+            return FilterOp("NOT", [child])
+        return self._leaf(f.predicate)
+
+    def _leaf(self, p) -> FilterOp:
+        col = self.seg.column(p.column)
+        ev = get_predicate_evaluator(p, self.dictionary(p.column))
+        if ev.always_false:
+            return EMPTY
+        if ev.always_true:
+            return ALL
+        if col.is_sorted:
+            return FilterOp("SORTED", column=p.column, evaluator=ev, doc_ranges=self._sorted_ranges(col, ev))
+        if p.type != "RANGE" and col.inverted is not None:
+            return FilterOp("INV", column=p.column, evaluator=ev)
+        return FilterOp("SCAN", column=p.column, evaluator=ev)
+
+    @staticmethod
+    def _sorted_ranges(col, ev: DictPredicateEvaluator) -> List[Tuple[int, int]]:
+        pairs = np.frombuffer(col.sorted_index, dtype=">i4").reshape(-1, 2)
+        if ev.kind == "RANGE":
+            return [(int(pairs[ev.start, 0]), int(pairs[ev.end - 1, 1]))]
+        ids = sorted(ev.ids)  # matching (inclusive) or non-matching (exclusive) ids
+        ranges: List[Tuple[int, int]] = []
+        for i in ids:
+            s, e = int(pairs[i, 0]), int(pairs[i, 1])
+            if ranges and s == ranges[-1][1] + 1:
+                ranges[-1] = (ranges[-1][0], e)
+            else:
+                ranges.append((s, e))
+        return ranges  # exclusive predicates complement these in the kernel (negate)
+
+
+def emit_program(op: FilterOp, col_index: Dict[str, int], keep: list) -> List[FilterNode]:
+    """Prefix-order program of pgpu_filter_node; `keep` holds the ctypes arrays alive."""
+    out: List[FilterNode] = []
+
+    def ids_array(vals: Sequence[int]):
+        arr = (C.c_int32 * max(1, len(vals)))(*vals)
+        keep.append(arr)
+        return C.cast(arr, C.POINTER(C.c_int32)), len(vals)
+
+    def rec(o: FilterOp):
+        if o.kind in ("EMPTY", "ALL"):
+            out.append(FilterNode(op=_lib.PGPU_F_EMPTY if o.kind == "EMPTY" else _lib.PGPU_F_MATCH_ALL))
+        elif o.kind == "SCAN":
+            ev = o.evaluator
+            n = FilterNode(op=_lib.PGPU_F_SCAN, column=col_index[o.column], negate=1 if ev.is_exclusive else 0)
+            if ev.kind == "RANGE":
+                n.pred, n.lo, n.hi = _lib.PGPU_PRED_RANGE, ev.start, ev.end
+            else:
+                ids = sorted(ev.ids)
+                if ids and ids[-1] - ids[0] + 1 == len(ids):
+                    n.pred, n.lo, n.hi = _lib.PGPU_PRED_RANGE, ids[0], ids[-1] + 1
+                else:
+                    n.pred = _lib.PGPU_PRED_SET
+                    n.ids, n.num_ids = ids_array(ids)
+            out.append(n)
+        elif o.kind == "INV":
+            ev = o.evaluator
+            ids = ev.non_matching_dict_ids() if ev.is_exclusive else ev.matching_dict_ids()
+            n = FilterNode(op=_lib.PGPU_F_INVERTED, column=col_index[o.column], negate=1 if ev.is_exclusive else 0)
+            n.ids, n.num_ids = ids_array(ids)
+            out.append(n)
+        elif o.kind == "SORTED":
+            flat = [v for r in o.doc_ranges for v in r]
+            n = FilterNode(op=_lib.PGPU_F_SORTED, column=col_index[o.column],
+                           negate=1 if o.evaluator.is_exclusive and o.evaluator.kind == "SET" else 0)
+            n.ids, _ = ids_array(flat)
+            n.num_ids = len(o.doc_ranges)
+            out.append(n)
+        elif o.kind in ("AND", "OR"):
+            b, ce, e = ((_lib.PGPU_F_AND_BEGIN, _lib.PGPU_F_AND_CHILD_END, _lib.PGPU_F_AND_END) if o.kind == "AND"
+                        else (_lib.PGPU_F_OR_BEGIN, _lib.PGPU_F_OR_CHILD_END, _lib.PGPU_F_OR_END))
+            out.append(FilterNode(op=b))
+            for ch in o.children:
+                rec(ch)
+                out.append(FilterNode(op=ce))
+            out.append(FilterNode(op=e))
+        elif o.kind == "NOT":
+            out.append(FilterNode(op=_lib.PGPU_F_NOT))
+            rec(o.children[0])
+        else:
+            raise ValueError(o.kind)
+
+    rec(op)
+    return out
+
+
+# ---- results ---------------------------------------------------------------------------------------------------
+@dataclass
+class ExecutionStats:
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0   # GPU's own count of forward-index entries evaluated
+    num_entries_scanned_post_filter: int = 0
+    num_total_docs: int = 0
+    num_segments_processed: int = 0
+    kernel_ms: float = 0.0
+    sparse_sector_bytes: int = 0
+    dense_bytes: int = 0
+
+
+@dataclass
+class GroupTable:
+    """Compacted partial table: global keys + cells (section 0 = count, then one section per non-COUNT agg)."""
+
+    keys: np.ndarray          # int64 [n]
+    cells: np.ndarray         # int64 [n, nsec]
+    layout: TableLayout
+
+
+@dataclass
+class QueryResult:
+    query: QueryContext
+    aggregation_result: Optional[List] = None        # aggregation-only: final values in aggregation order
+    group_rows: Optional[List[tuple]] = None         # group-by: (group values..., final agg values...) all groups
+    rows: Optional[List[tuple]] = None               # SELECT-ordered rows after ORDER BY / LIMIT
+    stats: ExecutionStats = field(default_factory=ExecutionStats)
+    intermediate: Optional[dict] = None              # group values -> list of intermediate values
+
+
+def final_value(fn: str, cell_count: int, cell: Optional[int], op: int, vtype: int):
+    """AggregationFunction.extractFinalResult on a merged cell."""
+    if fn == "COUNT":
+        return int(cell_count)
+    if fn == "SUM":
+        return float(cell) if op == PGPU_RED_SUM_I64 else float(np.int64(cell).view(np.float64))
+    if fn in ("MIN", "MAX"):
+        if cell_count == 0:
+            return math.inf if fn == "MIN" else -math.inf
+        return _lib.decode_minmax_key(int(cell), vtype)
+    if fn == "AVG":
+        if cell_count == 0:
+            return -math.inf  # AvgAggregationFunction DEFAULT_FINAL_RESULT
+        s = float(cell) if op == PGPU_RED_SUM_I64 else float(np.int64(cell).view(np.float64))
+        return s / cell_count
+    raise ValueError(fn)
+
+
+def intermediate_value(fn: str, cell_count: int, cell, op: int, vtype: int):
+    if fn == "AVG":
+        s = float(cell) if op == PGPU_RED_SUM_I64 else float(np.int64(cell).view(np.float64))
+        return (s, int(cell_count))
+    return final_value(fn, cell_count, cell, op, vtype)
+
+
+def order_and_limit(query: QueryContext, rows: List[tuple]) -> List[tuple]:
+    """Broker-side ORDER BY / LIMIT over final rows (GroupByDataTableReducer, IndexedTable.finish)."""
+    names = list(query.group_by) + [a.result_name for a in query.aggregations]
+    if query.order_by:
+        for ob in reversed(query.order_by):
+            idx = names.index(ob.expression)
+            rows = sorted(rows, key=lambda r, i=idx: r[i], reverse=not ob.ascending)
+    return rows[: query.limit]
+
+
+def to_select_order(query: QueryContext, row: tuple) -> tuple:
+    names = list(query.group_by) + [a.result_name for a in query.aggregations]
+    out = []
+    for s in query.select:
+        key = s if isinstance(s, str) else s.result_name
+        out.append(row[names.index(key)])
+    return tuple(out)
+
+
+# ---- plan maker ------------------------------------------------------------------------------------------------
+class GpuPlanMaker:
+    """PlanMaker for the GPU path (core/plan/maker/PlanMaker.java:36-59): one launch per query per GPU."""
+
+    def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
+                 max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
+                 collect_stats: bool = False):
+        self.ctx = ctx
+        self.num_groups_limit = num_groups_limit
+        self.max_init_group_holder_capacity = max_init_group_holder_capacity
+        self.collect_stats = collect_stats
+        self._global_dicts: Dict[tuple, tuple] = {}
+
+    # -- global group dictionaries --
+    def global_dictionary(self, column: str, segments: Sequence[GpuSegment]):
+        """Global dictionary of a group column (sorted union of the segments' dictionaries unless a wider one was
+        installed by set_global_dictionary) and per-segment remap buffers (None = identity)."""
+        key = (column, tuple(id(s) for s in segments))
+        hit = self._global_dicts.get(key)
+        if hit is not None:
+            return hit
+        dicts = [s.dictionaries[column] for s in segments]
+        first = dicts[0]
+        if isinstance(first, list):
+            glob = sorted(set().union(*[set(d) for d in dicts]))
+        else:
+            glob = np.unique(np.concatenate(dicts)) if len(dicts) > 1 else np.asarray(first)
+        return self.set_global_dictionary(column, segments, glob)
+
+    def set_global_dictionary(self, column: str, segments: Sequence[GpuSegment], glob):
+        key = (column, tuple(id(s) for s in segments))
+        remaps = []
+        if isinstance(glob, list):
+            pos = {v: i for i, v in enumerate(glob)}
+        for s in segments:
+            d = s.dictionaries[column]
+            if len(d) == len(glob) and (list(d) == list(glob) if isinstance(d, list) else np.array_equal(d, glob)):
+                remaps.append(None)
+                continue
+            if isinstance(glob, list):
+                t = np.array([pos[v] for v in d], dtype=np.int32)
+            else:
+                t = np.searchsorted(glob, d).astype(np.int32)
+            remaps.append(self.ctx.remap((s.name, id(s), column, len(glob)), t))
+        hit = (glob, remaps)
+        self._global_dicts[key] = hit
+        return hit
+
+    def _check_group_limit(self, query: QueryContext, seg: GpuSegment) -> None:
+        prod = 1
+        for g in query.group_by:
+            prod *= seg.column(g).cardinality
+        if prod <= self.max_init_group_holder_capacity:
+            return  # ArrayBasedHolder: no limit
+        if prod <= self.num_groups_limit:
+            return  # map-based holder can never reach the limit
+        raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                   f"segment {seg.name}: group key space {prod} exceeds numGroupsLimit "
+                                   f"{self.num_groups_limit}; first-seen truncation is served by the CPU plan")
+
+    def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment]):
+        """Build the pgpu_query_desc (and the ctypes objects it points to)."""
+        keep: list = []
+        columns = query.columns
+        col_index = {c: i for i, c in enumerate(columns)}
+        plans = (SegmentPlan * len(segments))()
+        globals_ = [self.global_dictionary(g, segments) for g in query.group_by]
+        for si, seg in enumerate(segments):
+            if query.group_by:
+                self._check_group_limit(query, seg)
+            cmap = (C.c_int32 * max(1, len(columns)))(*[seg.slots[c] for c in columns])
+            keep.append(cmap)
+            op = SegmentFilterPlanner(seg).build(query.filter)
+            nodes = [] if op.kind == "ALL" else emit_program(op, col_index, keep)
+            arr = (FilterNode * max(1, len(nodes)))(*nodes)
+            keep.append(arr)
+            plans[si].segment = seg.handle
+            plans[si].column_map = cmap
+            plans[si].filter = arr
+            plans[si].num_filter_nodes = len(nodes)
+            if query.group_by:
+                rm = (C.c_void_p * len(query.group_by))(
+                    *[(g[1][si].handle if g[1][si] is not None else None) for g in globals_])
+                keep.append(rm)
+                plans[si].group_remap = rm
+        keep.append(plans)
+        aggs = (Agg * len(query.aggregations))(
+            *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
+        keep.append(aggs)
+        gcols = (C.c_int32 * max(1, len(query.group_by)))(*[col_index[g] for g in query.group_by])
+        gcards = (C.c_int32 * max(1, len(query.group_by)))(*[len(g[0]) for g in globals_])
+        keep += [gcols, gcards]
+        desc = QueryDesc(num_columns=len(columns), num_segments=len(segments), segments=plans,
+                         num_aggs=len(query.aggregations), num_group_columns=len(query.group_by), aggs=aggs,
+                         group_columns=gcols, group_cardinalities=gcards,
+                         flags=_lib.PGPU_Q_STATS if self.collect_stats else 0)
+        return desc, keep, globals_
+
+    def layout(self, desc: QueryDesc) -> TableLayout:
+        L = TableLayout()
+        _lib.check(self.ctx._lib.pgpu_table_layout_of(C.byref(desc), C.byref(L)))
+        return L
+
+    def execute_table(self, query: QueryContext, segments: Sequence[GpuSegment]):
+        """Run the query; return the compacted partial table + stats (single GPU)."""
+        desc, keep, globals_ = self.build_desc(query, segments)
+        L = self.layout(desc)
+        cap = int(min(L.num_keys, 1 << 26))
+        keys = np.empty(max(cap, 1), dtype=np.int64)
+        cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
+        n = C.c_uint64()
+        st = QueryStats()
+        _lib.check(self.ctx._lib.pgpu_query_execute(self.ctx.handle, C.byref(desc),
+                                                    keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                    cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
+                                                    C.byref(st)))
+        table = GroupTable(keys[: n.value].copy(), cells[: n.value].copy(), L)
+        return table, st, globals_
+
+    def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
+        table, st, globals_ = self.execute_table(query, segments)
+        stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
+                               num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
+                               num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
+                               num_total_docs=st.num_total_docs, num_segments_processed=len(segments),
+                               kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
+                               dense_bytes=st.dense_bytes)
+        return finish(query, table, [g[0] for g in globals_], stats)
+
+
+def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats: ExecutionStats) -> QueryResult:
+    """Decode a (merged) partial table into final results."""
+    L = table.layout
+    res = QueryResult(query=query, stats=stats)
+    aggs = query.aggregations
+
+    def values_of(row_cells):
+        cnt = int(row_cells[0])
+        fin, inter = [], []
+        for ai, a in enumerate(aggs):
+            sec = L.agg_section[ai]
+            cell = int(row_cells[sec]) if sec > 0 else None
+            op = L.section_op[sec]
+            vt = L.agg_value_type[ai]
+            fin.append(final_value(a.function, cnt, cell, op, vt))
+            inter.append(intermediate_value(a.function, cnt, cell, op, vt))
+        return fin, inter
+
+    if not query.group_by:
+        if len(table.keys):
+            row = table.cells[0]
+        else:
+            row = np.zeros(L.num_sections, dtype=np.int64)
+            for s in range(L.num_sections):
+                op = L.section_op[s]
+                row[s] = np.iinfo(np.int64).max if op == PGPU_RED_MIN_I64 else (
+                    np.iinfo(np.int64).min if op == PGPU_RED_MAX_I64 else 0)
+        fin, inter = values_of(row)
+        res.aggregation_result = fin
+        res.intermediate = {(): inter}
+        res.rows = [tuple(fin)]
+        return res
+    cards = [len(g) for g in global_dicts]
+    group_rows = []
+    inter_map = {}
+    for k, row in zip(table.keys.tolist(), table.cells):
+        vals = []
+        for g, card in zip(global_dicts, cards):
+            gid = k % card
+            k //= card
+            v = g[gid]
+            vals.append(v.item() if hasattr(v, "item") else v)
+        fin, inter = values_of(row)
+        group_rows.append(tuple(vals) + tuple(fin))
+        inter_map[tuple(vals)] = inter
+    res.group_rows = group_rows
+    res.intermediate = inter_map
+    res.rows = [to_select_order(query, r) for r in order_and_limit(query, group_rows)]
+    return res

@@ -1,0 +1,135 @@
+"""Dictionary-based predicate evaluation on the host (what the GPU receives are dict-id ranges and sets).
+
+Restates, for sorted immutable dictionaries:
+  * ``BaseImmutableDictionary.binarySearch`` / ``insertionIndexOf`` / ``indexOf``
+    (seglocal/segment/index/readers/BaseImmutableDictionary.java:125-270, IntDictionary.java:33-34, ...)
+  * ``EqualsPredicateEvaluatorFactory.DictionaryBasedEqPredicateEvaluator``        (:85-113)
+  * ``NotEqualsPredicateEvaluatorFactory.DictionaryBasedNeqPredicateEvaluator``    (:85-130)
+  * ``InPredicateEvaluatorFactory.DictionaryBasedInPredicateEvaluator``            (:142-182)
+  * ``NotInPredicateEvaluatorFactory.DictionaryBasedNotInPredicateEvaluator``      (:142-200)
+  * ``RangePredicateEvaluatorFactory.SortedDictionaryBasedRangePredicateEvaluator`` (:114-198)
+all under core/operator/filter/predicate/.  Literal parsing follows the stored type: integral literals for
+INT/LONG columns (a fractional literal is compared numerically, the NumericalFilterOptimizer outcome),
+doubles for FLOAT/DOUBLE, strings compared by code point for STRING.
+"""
+from __future__ import annotations
+
+import bisect
+from dataclasses import dataclass
+from fractions import Fraction
+from typing import List, Sequence, Union
+
+import numpy as np
+
+from ._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING
+from .query import UNBOUNDED, Predicate
+
+
+def _key(value: str, data_type: int):
+    if data_type == PGPU_STRING:
+        return value
+    if data_type in (PGPU_INT, PGPU_LONG):
+        f = Fraction(value)
+        return int(f) if f.denominator == 1 else f
+    if data_type == PGPU_FLOAT:
+        return float(np.float32(float(value)))
+    return float(value)
+
+
+class SortedDictionary:
+    """Sorted dictionary values with the reference's binary-search contract."""
+
+    def __init__(self, values: Union[np.ndarray, Sequence[str]], data_type: int):
+        self.data_type = data_type
+        if data_type == PGPU_STRING:
+            self.values: List = list(values)
+        elif data_type in (PGPU_INT, PGPU_LONG):
+            self.values = [int(v) for v in values]
+        else:
+            self.values = [float(v) for v in values]
+
+    def __len__(self) -> int:
+        return len(self.values)
+
+    def insertion_index_of(self, literal: str) -> int:
+        """>= 0: index of an exact match; < 0: -(insertion point + 1)."""
+        k = _key(literal, self.data_type)
+        i = bisect.bisect_left(self.values, k)
+        if i < len(self.values) and self.values[i] == k:
+            return i
+        return -(i + 1)
+
+    def index_of(self, literal: str) -> int:
+        i = self.insertion_index_of(literal)
+        return i if i >= 0 else -1
+
+
+@dataclass
+class DictPredicateEvaluator:
+    """Result of predicate evaluation against one segment's dictionary."""
+
+    predicate: Predicate
+    cardinality: int
+    kind: str                    # "RANGE" or "SET"
+    start: int = 0               # RANGE [start, end)
+    end: int = 0
+    ids: Sequence[int] = ()      # SET: matching ids (inclusive predicates) or non-matching ids (exclusive)
+    always_true: bool = False
+    always_false: bool = False
+
+    @property
+    def is_exclusive(self) -> bool:
+        return self.predicate.is_exclusive
+
+    def matching_dict_ids(self) -> List[int]:
+        if self.kind == "RANGE":
+            return list(range(self.start, self.end))
+        if not self.is_exclusive:
+            return sorted(self.ids)
+        bad = set(self.ids)
+        return [i for i in range(self.cardinality) if i not in bad]
+
+    def non_matching_dict_ids(self) -> List[int]:
+        if self.kind == "SET" and self.is_exclusive:
+            return sorted(self.ids)
+        good = set(self.matching_dict_ids())
+        return [i for i in range(self.cardinality) if i not in good]
+
+
+def get_predicate_evaluator(p: Predicate, dictionary: SortedDictionary) -> DictPredicateEvaluator:
+    """PredicateEvaluatorProvider.getPredicateEvaluator for dictionary-encoded columns
+    (core/operator/filter/predicate/PredicateEvaluatorProvider.java:38-89)."""
+    card = len(dictionary)
+    if p.type == "EQ":
+        i = dictionary.index_of(p.values[0])
+        if i < 0:
+            return DictPredicateEvaluator(p, card, "SET", ids=(), always_false=True)
+        return DictPredicateEvaluator(p, card, "SET", ids=(i,), always_true=card == 1)
+    if p.type == "NOT_EQ":
+        i = dictionary.index_of(p.values[0])
+        if i < 0:
+            return DictPredicateEvaluator(p, card, "SET", ids=(), always_true=True)
+        return DictPredicateEvaluator(p, card, "SET", ids=(i,), always_false=card == 1)
+    if p.type == "IN":
+        ids = sorted({i for i in (dictionary.index_of(v) for v in p.values) if i >= 0})
+        return DictPredicateEvaluator(p, card, "SET", ids=tuple(ids), always_false=len(ids) == 0,
+                                      always_true=len(ids) == card)
+    if p.type == "NOT_IN":
+        ids = sorted({i for i in (dictionary.index_of(v) for v in p.values) if i >= 0})
+        return DictPredicateEvaluator(p, card, "SET", ids=tuple(ids), always_true=len(ids) == 0,
+                                      always_false=len(ids) == card)
+    if p.type == "RANGE":
+        if p.lower == UNBOUNDED:
+            start = 0
+        else:
+            ins = dictionary.insertion_index_of(p.lower)
+            start = -(ins + 1) if ins < 0 else (ins if p.lower_inclusive else ins + 1)
+        if p.upper == UNBOUNDED:
+            end = card
+        else:
+            ins = dictionary.insertion_index_of(p.upper)
+            end = -(ins + 1) if ins < 0 else (ins + 1 if p.upper_inclusive else ins)
+        n = end - start
+        return DictPredicateEvaluator(p, card, "RANGE", start=start, end=end, always_false=n <= 0,
+                                      always_true=n == card)
+    raise ValueError(f"unsupported predicate type {p.type}")

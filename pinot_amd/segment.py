@@ -1,0 +1,221 @@
+"""Immutable segment model and HBM residency (the IndexingOverrides seam).
+
+``SegmentData`` holds, per column, exactly the bytes a Pinot server has in its ``PinotDataBuffer``s after
+``ImmutableSegmentLoader.load`` (seglocal/indexsegment/immutable/ImmutableSegmentLoader.java:153-214):
+
+* dictionary      ``<col>.dict``             sorted unique values, big-endian (BaseImmutableDictionary.java:40-322)
+* forward index   ``<col>.sv.unsorted.fwd``  fixed-bit, MSB-first (FixedBitSVForwardIndexReaderV2.java:62-96)
+* sorted index    ``<col>.sv.sorted.fwd``    (start, end) per dict id (SortedIndexReaderImpl.java:37-121)
+* inverted index  ``<col>.bitmap.inv``       offsets + Roaring bitmaps (BitmapInvertedIndexReader.java:45-61)
+
+(file names: segspi/V1Constants.java:25-105).  ``GpuSegment`` copies them to HBM once
+(``pgpu_segment_add_*``), the analogue of an ``IndexingOverride`` wrapping ``newForwardIndexReader`` /
+``newInvertedIndexReader`` / ``newSortedIndexReader`` (segspi/index/IndexingOverrides.java:82-92).  The host keeps
+the decoded dictionary values: predicates are evaluated against them on the host, as the reference's
+PredicateEvaluators do (core/operator/filter/predicate/PredicateEvaluatorProvider.java:38-89).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING
+
+TYPE_NAMES = {"INT": PGPU_INT, "LONG": PGPU_LONG, "FLOAT": PGPU_FLOAT, "DOUBLE": PGPU_DOUBLE, "STRING": PGPU_STRING}
+_BE_DTYPE = {PGPU_INT: ">i4", PGPU_LONG: ">i8", PGPU_FLOAT: ">f4", PGPU_DOUBLE: ">f8"}
+_NATIVE = {PGPU_INT: np.int32, PGPU_LONG: np.int64, PGPU_FLOAT: np.float32, PGPU_DOUBLE: np.float64}
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue (seglocal/io/util/PinotDataBitSet.java:59-71)."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
+
+
+@dataclass
+class ColumnIndexes:
+    """Per-column index buffers of one immutable segment (PhysicalColumnIndexContainer wiring)."""
+
+    name: str
+    data_type: int
+    cardinality: int
+    dictionary: Union[bytes, Sequence[str], None] = None  # BE bytes (numeric) or sorted strings
+    forward: Optional[bytes] = None          # fixed-bit forward index (unsorted columns)
+    sorted_index: Optional[bytes] = None     # sorted columns: also their forward index
+    inverted: Optional[bytes] = None
+    forward_device: Optional[int] = None     # device pointer alternative to `forward` (PGPU_MEM_DEVICE)
+    forward_device_bytes: int = 0
+
+    @property
+    def bits_per_value(self) -> int:
+        return num_bits_per_value(self.cardinality - 1)
+
+    @property
+    def is_sorted(self) -> bool:
+        return self.sorted_index is not None
+
+    def dictionary_values(self) -> Union[np.ndarray, List[str]]:
+        if self.data_type == PGPU_STRING:
+            return list(self.dictionary)
+        return np.frombuffer(self.dictionary, dtype=_BE_DTYPE[self.data_type]).astype(_NATIVE[self.data_type])
+
+
+@dataclass
+class SegmentData:
+    name: str
+    num_docs: int
+    columns: Dict[str, ColumnIndexes] = field(default_factory=dict)
+
+    def column(self, name: str) -> ColumnIndexes:
+        try:
+            return self.columns[name]
+        except KeyError:
+            raise KeyError(f"segment {self.name} has no column {name!r}") from None
+
+
+class GpuContext:
+    """One HIP device (one process per GPU); wraps pgpu_init / pgpu_shutdown."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        h = C.c_void_p()
+        _lib.check(self._lib.pgpu_init(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+        self._remap_cache: Dict[tuple, "DeviceBuffer"] = {}
+
+    def close(self) -> None:
+        if self.handle:
+            for b in self._remap_cache.values():
+                b.release()
+            self._remap_cache.clear()
+            self._lib.pgpu_shutdown(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def kernel_geometry(self):
+        g, t, b = C.c_int32(), C.c_int32(), C.c_int32()
+        _lib.check(self._lib.pgpu_kernel_geometry(self.handle, C.byref(g), C.byref(t), C.byref(b)))
+        return g.value, t.value, b.value
+
+    def remap(self, key: tuple, table: np.ndarray) -> "DeviceBuffer":
+        buf = self._remap_cache.get(key)
+        if buf is None:
+            buf = DeviceBuffer.upload_int32(self, table)
+            self._remap_cache[key] = buf
+        return buf
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: GpuContext, handle: C.c_void_p):
+        self.ctx = ctx
+        self.handle = handle
+
+    @staticmethod
+    def upload_int32(ctx: GpuContext, arr: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(arr, dtype=np.int32)
+        h = C.c_void_p()
+        _lib.check(ctx._lib.pgpu_remap_upload(ctx.handle, a.ctypes.data_as(C.POINTER(C.c_int32)), len(a),
+                                              C.byref(h)))
+        return DeviceBuffer(ctx, h)
+
+    def release(self) -> None:
+        if self.handle:
+            self.ctx._lib.pgpu_buffer_release(self.handle)
+            self.handle = None
+
+
+class GpuSegment:
+    """An immutable segment resident in HBM plus the host-side dictionaries used for predicate evaluation."""
+
+    def __init__(self, ctx: GpuContext, data: SegmentData, columns: Optional[Sequence[str]] = None,
+                 _incremental: bool = False):
+        self.ctx = ctx
+        self.data = data
+        self.name = data.name
+        self.num_docs = data.num_docs
+        names = list(columns) if columns is not None else list(data.columns)
+        self.slots: Dict[str, int] = {}
+        self.dictionaries: Dict[str, Union[np.ndarray, List[str]]] = {}
+        lib = ctx._lib
+        h = C.c_void_p()
+        _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, len(names), C.byref(h)))
+        self.handle = h
+        self._capacity = len(names)
+        if _incremental:
+            return
+        try:
+            for n in names:
+                self.add_column(data.column(n))
+            self.seal()
+        except Exception:
+            self.release()
+            raise
+
+    @classmethod
+    def begin(cls, ctx: GpuContext, name: str, num_docs: int, num_columns: int) -> "GpuSegment":
+        """Incremental upload: add_column() per column, then seal()."""
+        data = SegmentData(name, num_docs)
+        return cls(ctx, data, columns=[f"_{i}" for i in range(num_columns)], _incremental=True)
+
+    def add_column(self, col: ColumnIndexes) -> None:
+        if len(self.slots) >= self._capacity:
+            raise ValueError("segment column capacity exceeded")
+        slot = len(self.slots)
+        self._upload_column(slot, col)
+        self.slots[col.name] = slot
+        self.dictionaries[col.name] = col.dictionary_values()
+        self.data.columns[col.name] = col
+
+    def seal(self) -> None:
+        _lib.check(self.ctx._lib.pgpu_segment_seal(self.handle))
+
+    def _upload_column(self, slot: int, col: ColumnIndexes) -> None:
+        lib = self.ctx._lib
+        seg = self.handle
+        card = col.cardinality
+        if col.data_type == PGPU_STRING:
+            _lib.check(lib.pgpu_segment_add_dictionary(seg, slot, PGPU_STRING, None, 0, card))
+        else:
+            d = col.dictionary
+            _lib.check(lib.pgpu_segment_add_dictionary(seg, slot, col.data_type, d, len(d), card))
+        if col.sorted_index is not None:
+            s = col.sorted_index
+            _lib.check(lib.pgpu_segment_add_sorted_index(seg, slot, s, len(s), card))
+        elif col.forward_device is not None:
+            _lib.check(lib.pgpu_segment_add_forward_index(seg, slot, C.c_void_p(col.forward_device),
+                                                          col.forward_device_bytes, col.bits_per_value, card,
+                                                          _lib.PGPU_MEM_DEVICE))
+        elif col.forward is not None:
+            f = col.forward
+            _lib.check(lib.pgpu_segment_add_forward_index(seg, slot, f, len(f), col.bits_per_value, card,
+                                                          _lib.PGPU_MEM_HOST))
+        if col.inverted is not None:
+            inv = col.inverted
+            _lib.check(lib.pgpu_segment_add_inverted_index(seg, slot, inv, len(inv), card))
+
+    def column(self, name: str) -> ColumnIndexes:
+        return self.data.column(name)
+
+    def has_column(self, name: str) -> bool:
+        return name in self.slots
+
+    def device_bytes(self) -> int:
+        n = C.c_uint64()
+        _lib.check(self.ctx._lib.pgpu_segment_device_bytes(self.handle, C.byref(n)))
+        return n.value
+
+    def release(self) -> None:
+        if self.handle:
+            self.ctx._lib.pgpu_segment_release(self.handle)
+            self.handle = None

@@ -1,0 +1,193 @@
+"""Synthetic segment sets for the BASELINE workloads (bench.py and the GPU tests).
+
+Dictionary values are generated on the host (small); forward indexes are generated directly in HBM by
+libpinotgpu_synth.so and uploaded with ``pgpu_segment_add_forward_index(..., PGPU_MEM_DEVICE)``.  Every dict id is a
+counter-based hash of (seed, doc) that ``dict_ids_cpu`` restates in numpy, so any generated segment can be rebuilt
+bit-identically on the CPU (parity tests, CPU baseline).
+
+Workloads (one GPU's shard, weak scaling: rank r owns global segments r*S .. r*S+S-1):
+  adanalytics  config 5  daysSinceEpoch 10-bit, accountId 20-bit, clicks / impressions 16-bit metric dicts
+  range_in     config 2  r 16-bit, i 4-bit, m 16-bit metric
+  groupby1m    config 4  k 20-bit (1,048,576 keys), m 16-bit metric
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from ._lib import PGPU_INT, SYNTH_LIB_PATH
+from .segment import ColumnIndexes, GpuContext, GpuSegment, SegmentData, num_bits_per_value
+
+M64 = (1 << 64) - 1
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15))
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def dict_ids_cpu(seed: int, num_docs: int, card: int, doc0: int = 0, cdf: Optional[np.ndarray] = None) -> np.ndarray:
+    """numpy restatement of synth.hip's synth_id for docs [doc0, doc0 + num_docs)."""
+    with np.errstate(over="ignore"):
+        docs = np.arange(doc0, doc0 + num_docs, dtype=np.uint64)
+        u = (splitmix64_np(np.uint64(seed) ^ (docs * np.uint64(0xD1B54A32D192ED03))) >> np.uint64(32))
+    if cdf is None:
+        return ((u * np.uint64(card)) >> np.uint64(32)).astype(np.int32)
+    return np.searchsorted(cdf.astype(np.uint64), u, side="right").astype(np.int32)
+
+
+def column_seed(base: int, segment: int, column: str) -> int:
+    h = base
+    for ch in column.encode():
+        h = splitmix64((h * 131 + ch) & M64)
+    return splitmix64((h ^ (segment * 0x9E3779B97F4A7C15)) & M64)
+
+
+def zipf_cdf(card: int, s: float) -> np.ndarray:
+    """uint32 CDF table (scaled to 2^32) of a Zipf(s) distribution over ranks 0..card-1."""
+    w = 1.0 / np.power(np.arange(1, card + 1, dtype=np.float64), s)
+    c = np.cumsum(w)
+    c /= c[-1]
+    t = np.minimum(np.floor(c * 4294967296.0), 4294967295.0).astype(np.uint64)
+    t[-1] = 4294967295
+    return t.astype(np.uint32)
+
+
+# ---- dictionaries -------------------------------------------------------------------------------------------
+def sorted_distinct_in(card: int, limit: int, seed: int) -> np.ndarray:
+    """`card` sorted distinct INT values spread uniformly over [0, limit): stride buckets + hashed offset."""
+    step = limit // card
+    k = np.arange(card, dtype=np.uint64)
+    off = (splitmix64_np(np.uint64(seed) ^ k) % np.uint64(max(step, 1))).astype(np.int64)
+    return (np.arange(card, dtype=np.int64) * step + off).astype(np.int32)
+
+
+@dataclass
+class SynthColumn:
+    name: str
+    cardinality: int
+    values: Callable[[], np.ndarray]   # sorted INT dictionary
+    dist: str = "uniform"
+    zipf_s: float = 1.1
+
+
+@dataclass
+class Workload:
+    name: str
+    table: str
+    columns: List[SynthColumn]
+    sql: str
+    options: Dict
+    seed: int
+    description: str
+
+
+def _days():
+    return np.arange(17500, 17500 + 1024, dtype=np.int32)
+
+
+def _accounts():
+    k = np.arange(1 << 20, dtype=np.int64)
+    return (123456789 + (k - (1 << 19)) * 61).astype(np.int32)  # contains 123456789 at k = 2^19
+
+
+WORKLOADS: Dict[str, Workload] = {
+    "adanalytics": Workload(
+        "adanalytics", "adAnalytics",
+        [SynthColumn("daysSinceEpoch", 1024, _days),
+         SynthColumn("accountId", 1 << 20, _accounts),
+         SynthColumn("clicks", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 11)),
+         SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
+        "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
+        "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
+        "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
+        {}, 5, "config 5: AdAnalytics filtered GROUP BY SUM (README example query)"),
+    "range_in": Workload(
+        "range_in", "synth",
+        [SynthColumn("r", 1 << 16, lambda: (np.arange(1 << 16, dtype=np.int32) * 7 + 3)),
+         SynthColumn("i", 16, lambda: np.arange(16, dtype=np.int32) * 100),
+         SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 13))],
+        "SELECT COUNT(*), SUM(m) FROM synth WHERE r BETWEEN 114691 AND 344060 AND i IN (100, 500, 900)",
+        {}, 1, "config 2: COUNT(*)+SUM(metric) WHERE range AND IN"),
+    "groupby1m": Workload(
+        "groupby1m", "synth",
+        [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3),
+         SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
+        "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
+        {"num_groups_limit": 2_000_000}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT"),
+}
+
+
+class SynthLib:
+    def __init__(self, path: str = SYNTH_LIB_PATH):
+        if not os.path.exists(path):
+            raise ImportError(f"{path} is missing: run __graft_entry__.build()")
+        self.lib = C.CDLL(path)
+        self.lib.synth_fixed_bit.restype = C.c_int
+        self.lib.synth_fixed_bit.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_uint64, C.c_void_p,
+                                             C.c_void_p]
+
+
+def forward_index_bytes(num_docs: int, bits: int) -> int:
+    return (num_docs * bits + 7) // 8
+
+
+def build_segment_cpu(w: Workload, segment: int, num_docs: int, pack: Callable) -> SegmentData:
+    """Host-side twin of build_segment_gpu: `pack(ids, bits) -> bytes` is the caller's fixed-bit writer."""
+    seg = SegmentData(f"{w.name}_{segment}", num_docs)
+    for c in w.columns:
+        vals = c.values()
+        cdf = zipf_cdf(c.cardinality, c.zipf_s) if c.dist == "zipf" else None
+        ids = dict_ids_cpu(column_seed(w.seed, segment, c.name), num_docs, c.cardinality, cdf=cdf)
+        seg.columns[c.name] = ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=vals.astype(">i4").tobytes(),
+                                            forward=pack(ids, num_bits_per_value(c.cardinality - 1)))
+    return seg
+
+
+def build_segments_gpu(ctx: GpuContext, w: Workload, segment_ids: List[int], num_docs: int) -> List[GpuSegment]:
+    """Generate the forward indexes in HBM (torch scratch buffer) and upload them as PGPU_MEM_DEVICE sources."""
+    import torch
+
+    lib = SynthLib().lib
+    dev = torch.device("cuda", ctx.device)
+    cdfs = {}
+    dicts = {c.name: c.values().astype(">i4").tobytes() for c in w.columns}
+    max_bytes = max(forward_index_bytes(num_docs, num_bits_per_value(c.cardinality - 1)) for c in w.columns)
+    scratch = torch.empty(((max_bytes + 64) // 4) * 4, dtype=torch.uint8, device=dev)
+    out = []
+    for s in segment_ids:
+        gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns))
+        for c in w.columns:
+            bits = num_bits_per_value(c.cardinality - 1)
+            cdf_ptr = None
+            if c.dist == "zipf":
+                if c.name not in cdfs:
+                    cdfs[c.name] = torch.from_numpy(zipf_cdf(c.cardinality, c.zipf_s).view(np.int32)).to(dev)
+                cdf_ptr = cdfs[c.name].data_ptr()
+            rc = lib.synth_fixed_bit(scratch.data_ptr(), num_docs, bits, c.cardinality,
+                                     column_seed(w.seed, s, c.name), cdf_ptr,
+                                     torch.cuda.current_stream(dev).cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"synth_fixed_bit failed ({rc})")
+            torch.cuda.synchronize(dev)
+            gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],
+                                        forward_device=scratch.data_ptr(),
+                                        forward_device_bytes=forward_index_bytes(num_docs, bits)))
+            gs.data.columns[c.name].forward_device = None  # the scratch buffer is reused by the next column
+        gs.seal()
+        out.append(gs)
+    del scratch
+    return out

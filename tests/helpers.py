@@ -1,0 +1,75 @@
+"""Shared test fixtures: segments built by the oracle's writers from the committed golden data."""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import numpy as np
+
+from pinot_amd._lib import PGPU_INT, PGPU_STRING
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load_kat():
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        return json.load(f)
+
+
+def sv_columns():
+    d = np.load(os.path.join(GOLDEN, "test_data_sv.npz"))
+    out = {}
+    for c in d.files:
+        a = d[c]
+        out[c] = (PGPU_STRING, a.tolist()) if a.dtype.kind == "U" else (PGPU_INT, a)
+    return out
+
+
+def sv_segment():
+    """BaseSingleValueQueriesTest's segment: 30000 rows, 11 columns, no inverted index loaded."""
+    from oracle.segment_writer import build_segment
+    return build_segment("testTable_126164076_167572854", sv_columns())
+
+
+def fast_count_segment():
+    """FastFilteredCountTest.java:104-134: 1000 rows; class/sorted with inverted indexes, sorted column sorted."""
+    from oracle.segment_writer import build_segment
+    n = 1000
+    i = np.arange(n, dtype=np.int32)
+    cols = {"sorted": (PGPU_INT, i), "class": (PGPU_INT, i % 8), "intRangeCol": (PGPU_INT, n - i)}
+    return build_segment("testSegment", cols, inverted=["class", "sorted"])
+
+
+def baseball_segment():
+    """baseballStats QuickStart table: inverted index on playerID, teamID (offline table config)."""
+    from oracle.segment_writer import build_segment
+    d = np.load(os.path.join(GOLDEN, "baseball.npz"))
+    cols = {"playerID": (PGPU_STRING, d["playerID"].tolist()), "yearID": (PGPU_INT, d["yearID"]),
+            "teamID": (PGPU_STRING, d["teamID"].tolist()), "playerName": (PGPU_STRING, d["playerName"].tolist()),
+            "runs": (PGPU_INT, d["runs"])}
+    return build_segment("baseballStats_OFFLINE_0", cols, inverted=["playerID", "teamID"])
+
+
+def close(a, b, rel=1e-9):
+    if isinstance(a, (int, np.integer)) and isinstance(b, (int, np.integer)):
+        return int(a) == int(b)
+    a, b = float(a), float(b)
+    if math.isinf(a) or math.isinf(b):
+        return a == b
+    return a == b or abs(a - b) <= rel * max(abs(a), abs(b))
+
+
+def rows_close(r1, r2, rel=1e-9):
+    if len(r1) != len(r2):
+        return False
+    for x, y in zip(r1, r2):
+        if len(x) != len(y):
+            return False
+        for a, b in zip(x, y):
+            if isinstance(a, str) or isinstance(b, str):
+                if a != b:
+                    return False
+            elif not close(a, b, rel):
+                return False
+    return True

@@ -1,0 +1,261 @@
+"""GPU parity: the HIP path through the C ABI against the reference's KATs and the CPU oracle (MI355X only).
+
+Bar: counts, doc-id sets and integer sums bit-exact; double sums / averages within 1e-9 relative (north_star).
+numEntriesScannedInFilter is the GPU's own count of evaluated forward-index entries and is
+compared to the reference only where the two models coincide (a single scan leaf).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import engine
+from oracle.segment_writer import build_segment
+from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING, UnsupportedPlanError
+from pinot_amd.plan import GpuPlanMaker
+from pinot_amd.query import parse_sql
+from pinot_amd.segment import GpuSegment
+from tests.helpers import (baseball_segment, close, fast_count_segment, load_kat, rows_close, sv_segment)
+
+pytestmark = pytest.mark.gpu
+KAT = load_kat()
+
+
+@pytest.fixture(scope="module")
+def sv(gpu_ctx):
+    seg = sv_segment()
+    g = GpuSegment(gpu_ctx, seg)
+    yield seg, g
+    g.release()
+
+
+def _gpu(gpu_ctx, q, segs, **kw):
+    return GpuPlanMaker(gpu_ctx, **kw).execute(q, segs)
+
+
+def _assert_same(res, ref, rel=1e-9):
+    if res.aggregation_result is not None:
+        assert len(res.aggregation_result) == len(ref.aggregation_result)
+        for a, b in zip(res.aggregation_result, ref.aggregation_result):
+            assert close(a, b, rel), (res.aggregation_result, ref.aggregation_result)
+    else:
+        g = {r[: len(res.query.group_by)]: r for r in res.group_rows}
+        o = {r[: len(res.query.group_by)]: r for r in ref.group_rows}
+        assert set(g) == set(o)
+        for k in g:
+            assert rows_close([g[k]], [o[k]], rel), (k, g[k], o[k])
+    assert res.stats.num_docs_scanned == ref.num_docs_scanned
+    assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
+    assert res.stats.num_total_docs == ref.num_total_docs
+
+
+# ---- reference KATs ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", KAT["inner_segment"]["cases"], ids=lambda c: f"{c['group_by'].strip() or 'agg'}-{c['filter']}")
+def test_inner_segment_kat_gpu(gpu_ctx, sv, case):
+    seg, g = sv
+    sql = KAT["inner_segment"]["aggregation_query"] + (KAT["filter"] if case["filter"] else "") + case["group_by"]
+    q = parse_sql(sql)
+    if len(q.group_by) >= 5:
+        # LongMapBased / ArrayMapBased key spaces (> 2^31 raw keys) are served by the CPU plan in this build
+        with pytest.raises(UnsupportedPlanError):
+            _gpu(gpu_ctx, q, [g])
+        return
+    res = _gpu(gpu_ctx, q, [g])
+    st = res.stats
+    assert [st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs] == \
+        [case["stats"][0], case["stats"][2], case["stats"][3]]
+    v = res.intermediate[tuple(case["group"])] if case["group_by"] else res.intermediate[()]
+    got = [v[0], int(v[1]), int(v[2]), int(v[3]), int(v[4][0]), v[4][1]]
+    assert got == case["result"]
+
+
+@pytest.mark.parametrize("case", KAT["inter_segment"]["cases"], ids=lambda c: c["sql"][:60])
+def test_inter_segment_kat_gpu(gpu_ctx, sv, case):
+    seg, g = sv
+    q = parse_sql(case["sql"].replace("{FILTER}", KAT["filter"]))
+    res = _gpu(gpu_ctx, q, [g] * 4)
+    st = res.stats
+    assert [st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs] == \
+        [case["stats"][0], case["stats"][2], case["stats"][3]]
+    assert rows_close([list(x) for x in res.rows], case["rows"], rel=case.get("delta", 1e-12))
+
+
+@pytest.mark.parametrize("case", KAT["filter_operators"]["cases"], ids=lambda c: c["source"])
+def test_filter_operator_vectors_gpu(gpu_ctx, case):
+    """AND/OR/NOT over inverted-index (Roaring) leaves: the literal doc-id vectors of the reference's tests."""
+    from tests.test_oracle_kat import _filter_segment, expr_sql
+    seg = _filter_segment(case)
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        q = parse_sql(f"SELECT COUNT(*) FROM t WHERE {expr_sql(case['expr'])}")
+        res = _gpu(gpu_ctx, q, [g])
+        assert res.aggregation_result[0] == len(case["expected"])
+        # doc-id set: group by a per-doc unique column is not available; check via SUM of doc ids
+        docs = np.arange(case["num_docs"], dtype=np.int32)
+        seg2 = build_segment("ids", {**{k: (PGPU_INT, v) for k, v in _cols(seg).items()}, "docid": (PGPU_INT, docs)},
+                             inverted=[c for c in seg.columns])
+        g2 = GpuSegment(gpu_ctx, seg2)
+        q2 = parse_sql(f"SELECT docid, COUNT(*) FROM t WHERE {expr_sql(case['expr'])} GROUP BY docid LIMIT 1000")
+        res2 = _gpu(gpu_ctx, q2, [g2])
+        assert sorted(r[0] for r in res2.group_rows) == case["expected"]
+        g2.release()
+    finally:
+        g.release()
+
+
+def _cols(seg):
+    from oracle.engine import DecodedSegment
+    ds = DecodedSegment(seg)
+    return {c: ds.values(c).astype(np.int32) for c in seg.columns}
+
+
+@pytest.mark.parametrize("case", KAT["fast_filtered_count"]["cases"], ids=lambda c: c[0][34:])
+def test_fast_filtered_count_gpu(gpu_ctx, case):
+    seg = fast_count_segment()
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        res = _gpu(gpu_ctx, parse_sql(case[0]), [g])
+        assert res.aggregation_result[0] == case[1]
+    finally:
+        g.release()
+
+
+def test_baseball_quickstart_gpu(gpu_ctx):
+    """Config 1: baseballStats quickstart query, GPU vs oracle (STRING group key, inverted indexes present)."""
+    seg = baseball_segment()
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        q = parse_sql("SELECT playerName, SUM(runs) FROM baseballStats WHERE yearID > 2000 GROUP BY playerName "
+                      "ORDER BY SUM(runs) DESC LIMIT 10")
+        res = _gpu(gpu_ctx, q, [g])
+        ref = engine.execute(q, [seg])
+        _assert_same(res, ref)
+        assert [r[0] for r in res.rows] == [r[0] for r in ref.rows]
+    finally:
+        g.release()
+
+
+# ---- randomized parity against the oracle ------------------------------------------------------------------------
+def _random_segment(rng, n, name="rand", inverted=(), types=None):
+    cols = {}
+    cards = {"a": 3, "b": 16, "c": 1000, "d": 70_000, "e": 2, "m": 5000, "f": 300, "g": 40}
+    for c, card in cards.items():
+        base = rng.choice(np.arange(card * 3, dtype=np.int64), size=card, replace=False)
+        vals = base[rng.integers(0, card, n)]
+        dt = (types or {}).get(c, PGPU_INT)
+        if dt == PGPU_DOUBLE:
+            vals = vals.astype(np.float64) * 0.37 - 5.0
+        elif dt == PGPU_FLOAT:
+            vals = (vals.astype(np.float32) * np.float32(0.25)) - np.float32(3.0)
+        elif dt == PGPU_LONG:
+            vals = vals.astype(np.int64) * 1_000_003 - 7
+        else:
+            vals = vals.astype(np.int32)
+        cols[c] = (dt, vals)
+    return build_segment(name, cols, inverted=inverted)
+
+
+QUERIES = [
+    "SELECT COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE b IN (30, 3, 9) AND c > 1500",
+    "SELECT COUNT(*), SUM(m), MAX(f) FROM t WHERE d BETWEEN 30000 AND 150000",
+    "SELECT COUNT(*), SUM(f) FROM t WHERE NOT (a = 3 OR b NOT IN (0, 3, 6, 9, 12))",
+    "SELECT COUNT(*), MIN(m) FROM t WHERE (a <> 0 AND c < 900) OR (d >= 200000 AND e = 1) OR NOT g > 60",
+    "SELECT b, COUNT(*), SUM(m), AVG(f) FROM t WHERE c < 2000 GROUP BY b",
+    "SELECT a, b, SUM(m), MIN(m), MAX(m) FROM t WHERE d < 100000 GROUP BY a, b",
+    "SELECT c, SUM(m), COUNT(*) FROM t GROUP BY c ORDER BY SUM(m) DESC LIMIT 20",
+    "SELECT d, SUM(m), MAX(m) FROM t WHERE b = 12 GROUP BY d ORDER BY d LIMIT 50",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE d IN (3, 99999) AND a = 6",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE c = 123456789",
+    "SELECT f, g, COUNT(*), SUM(m) FROM t WHERE e = 0 AND (b > 20 OR a = 3) GROUP BY f, g",
+]
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_random_segments_vs_oracle(gpu_ctx, n, qi):
+    rng = np.random.default_rng(1000 + n)
+    segs = [_random_segment(rng, n, f"s{i}") for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(QUERIES[qi])
+        res = _gpu(gpu_ctx, q, gs)
+        ref = engine.execute(q, segs)
+        _assert_same(res, ref)
+    finally:
+        for g in gs:
+            g.release()
+
+
+@pytest.mark.parametrize("types", [{"m": PGPU_DOUBLE, "f": PGPU_FLOAT}, {"m": PGPU_LONG, "f": PGPU_DOUBLE}])
+@pytest.mark.parametrize("qi", [0, 1, 5, 6])
+def test_value_types_vs_oracle(gpu_ctx, types, qi):
+    rng = np.random.default_rng(77)
+    segs = [_random_segment(rng, 50_000, f"t{i}", types=types) for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(QUERIES[qi])
+        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
+
+
+@pytest.mark.parametrize("qi", [1, 3, 4, 9])
+def test_inverted_leaves_vs_oracle(gpu_ctx, qi):
+    """The same queries with inverted indexes loaded: EQ/IN/NOT IN/NEQ leaves become Roaring bitmap ORs."""
+    rng = np.random.default_rng(5)
+    segs = [_random_segment(rng, 150_001, f"i{i}", inverted=["a", "b", "d", "e", "g"]) for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(QUERIES[qi])
+        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
+
+
+def test_group_limit_unsupported(gpu_ctx):
+    rng = np.random.default_rng(9)
+    seg = _random_segment(rng, 10_000)
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        with pytest.raises(UnsupportedPlanError):
+            GpuPlanMaker(gpu_ctx, num_groups_limit=50_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=100_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
+        assert sum(r[1] for r in res.group_rows) == 10_000
+    finally:
+        g.release()
+
+
+def test_empty_segment(gpu_ctx):
+    seg = build_segment("empty", {"x": (PGPU_INT, np.array([5], np.int32))})
+    seg.num_docs = 0
+    seg.columns["x"].forward = b""
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        res = _gpu(gpu_ctx, parse_sql("SELECT COUNT(*), SUM(x), MIN(x), MAX(x), AVG(x) FROM t"), [g])
+        assert res.aggregation_result == [0, 0.0, math.inf, -math.inf, -math.inf]
+    finally:
+        g.release()
+
+
+# ---- synthetic generator parity ---------------------------------------------------------------------------------
+def test_synth_generator_matches_cpu(gpu_ctx):
+    import torch
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import SynthLib, dict_ids_cpu, zipf_cdf
+    lib = SynthLib().lib
+    for bits, card, n, dist in [(4, 16, 100_001, None), (10, 1024, 65_536, None), (16, 65536, 33_333, None),
+                                (20, 1 << 20, 8192 * 3 + 5, None), (20, 1 << 20, 50_000, "zipf")]:
+        seed = 12345 + bits
+        cdf = zipf_cdf(card, 1.1) if dist else None
+        out = torch.zeros((n * bits + 31) // 32 * 4 + 64, dtype=torch.uint8, device="cuda")
+        cdf_t = torch.from_numpy(cdf.view(np.int32)).cuda() if dist else None
+        rc = lib.synth_fixed_bit(out.data_ptr(), n, bits, card, seed, cdf_t.data_ptr() if dist else None,
+                                 torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().tobytes()[: (n * bits + 7) // 8]
+        exp = pack_fixed_bit(dict_ids_cpu(seed, n, card, cdf=cdf), bits)
+        assert got == exp, (bits, card, n, dist)
