@@ -61,12 +61,14 @@ def main():
     from pinot_amd.synth import WORKLOADS, build_segments_gpu
 
     w = WORKLOADS[args.workload]
+    log = (lambda *a: print(f"[bench rank {rank}]", *a, file=sys.stderr, flush=True))
     ctx = GpuContext(local)
     seg_ids = list(range(rank * args.segments, (rank + 1) * args.segments))
     t0 = time.time()
     segs = build_segments_gpu(ctx, w, seg_ids, args.docs)
     torch.cuda.synchronize()
     gen_s = time.time() - t0
+    log(f"generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
     opts = dict(w.options)
     q = parse_sql(w.sql)
     pm = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000))
@@ -85,6 +87,7 @@ def main():
     out_bytes = 8 * 1
     algo_bytes = st.dense_bytes + st.sparse_sector_bytes + 32 * st.num_docs_scanned * n_value_cols + out_bytes
 
+    log(f"stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, {st.kernel_ms:.3f} ms")
     for _ in range(args.warmup):
         ex.execute(q, segs)
     torch.cuda.synchronize()
@@ -113,6 +116,7 @@ def main():
     achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
 
     # small parity check of the same workload against the oracle (2 x 2^18-doc segments)
+    log(f"timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
     check = None
     if rank == 0 and not args.no_check:
         check = parity_check(ctx, w, q, opts)

@@ -108,10 +108,12 @@ class DistributedExecutor:
         if table is None:
             table = torch.empty(n, dtype=torch.int64, device=self.device)
             self._tables[n] = table
-        stream = torch.cuda.current_stream(self.device)
+        # libpinotgpu runs on its own HIP runtime and stream (torch may bundle another runtime): the table
+        # memory is shared through the process's GPU address space and ordered by explicit synchronisation.
+        torch.cuda.current_stream(self.device).synchronize()
         qh = C.c_void_p()
         lib = self.pm.ctx._lib
-        _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), C.c_void_p(stream.cuda_stream),
+        _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
                                          C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
         st = QueryStats()
         try:
@@ -125,6 +127,7 @@ class DistributedExecutor:
             import torch.distributed as dist
             dist.all_reduce(counts, group=self.group)
             docs_scanned, total_docs = (int(x) for x in counts.tolist())
+            torch.cuda.current_stream(self.device).synchronize()
         else:
             docs_scanned, total_docs = st.num_docs_scanned, st.num_total_docs
         if self.rank != 0:
@@ -134,7 +137,7 @@ class DistributedExecutor:
         cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
         ng = C.c_uint64()
         _lib.check(lib.pgpu_table_compact(self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()),
-                                          C.c_void_p(stream.cuda_stream), keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                          None, keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                           cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(ng)))
         gt = GroupTable(keys[: ng.value], cells[: ng.value], L)
         stats = ExecutionStats(num_docs_scanned=docs_scanned,

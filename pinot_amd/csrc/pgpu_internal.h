@@ -57,7 +57,8 @@ struct DevSeg {
   int32_t prog_len;
   int32_t col_begin;              // index of its first DevColumn (ncols per segment)
   int32_t remap_begin;            // index of its first remap pointer (ngcols per segment)
-  int32_t pad0, pad1;
+  int32_t pf_pc;                  // instruction whose column is register-prefetched one tile ahead (-1: none)
+  int32_t pad1;
 };
 
 // Filter instruction with statically resolved mask slots.

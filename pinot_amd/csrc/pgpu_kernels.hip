@@ -46,7 +46,6 @@ struct __attribute__((aligned(16))) Smem {
   int32_t goff[NG + 1];                  // exclusive prefix of per-group match counts
   int32_t slot_count[PGPU_MAX_SLOTS];    // popcount of each AND accumulator
   int32_t nvalid;
-  int32_t nmatch;
   uint32_t sectors[TILE / 256 * 32 / 32 + 16];  // touched 32-B sectors of a sparse read (stats mode)
   int64_t accw[NW][PGPU_MAX_AGGS];       // AGG mode: per-wave accumulators
   int64_t bstats[PGPU_NSTATS];
@@ -256,6 +255,35 @@ __device__ void or_bitmap(Smem& sm, const DevColumn& c, const TileCtx& t, uint32
   }
 }
 
+// Compact the docs of `mask` (tile-relative) into sm.list (ascending); zeroes mask slot `zero_slot` on the way
+// (>= 0).  Returns the count.  Contains two __syncthreads().
+__device__ __forceinline__ int compact_mask(Smem& sm, const uint64_t* mask, int zero_slot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 64) {
+    const int g = threadIdx.x;
+    const int c = __popcll(mask[g]);
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    sm.goff[g] = x - c;
+    if (g == 63) sm.goff[NG] = x;
+  }
+  __syncthreads();
+  for (int g = wave; g < NG; g += NW) {
+    const uint64_t m = mask[g];
+    if ((m >> lane) & 1ull) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      sm.list[sm.goff[g] + below] = (uint16_t)(g * 64 + lane);
+    }
+  }
+  if (zero_slot >= 0 && threadIdx.x < 64) sm.masks[zero_slot][threadIdx.x] = 0ull;
+  __syncthreads();
+  return sm.goff[NG];
+}
+
 // ---- filter program ------------------------------------------------------------------------------------------
 // Returns with the final match mask in sm.masks[0] (or sm.valid when the program is empty) -> *final_slot.
 __device__ int run_filter(Smem& sm, const DevParams& p, const TileCtx& t, const DevColumn* cols,
@@ -278,10 +306,13 @@ __device__ int run_filter(Smem& sm, const DevParams& p, const TileCtx& t, const 
         const uint64_t* care = care_mask(sm, in.care);
         const int ncare = care_count(sm, in.care);
         const uint32_t b = (uint32_t)c.bits;
-        const bool dense = c.kind == PGPU_COL_FIXED_BIT && ncare * 32 >= t.ndocs;
+        const bool prestaged = pc == s.pf_pc;
+        const bool dense = prestaged || (c.kind == PGPU_COL_FIXED_BIT && ncare * 32 >= t.ndocs);
         if (dense) {
-          stage_column(sm, c.fwd, t.tile_in_seg, b);
-          __syncthreads();
+          if (!prestaged) {
+            stage_column(sm, c.fwd, t.tile_in_seg, b);
+            __syncthreads();
+          }
           if (threadIdx.x == 0) {
             scanned += t.ndocs;
             dense_bytes += ((int64_t)t.ndocs * b + 7) / 8;
@@ -303,17 +334,15 @@ __device__ int run_filter(Smem& sm, const DevParams& p, const TileCtx& t, const 
             __syncthreads();
           }
           if (threadIdx.x == 0) scanned += ncare;
-          for (int g = wave; g < NG; g += NW) {
-            const uint64_t cm = care[g];
-            bool m = false;
-            if ((cm >> lane) & 1ull) {
-              const int j = g * 64 + lane;
-              uint32_t id = get_id(sm, c, t, j, false);
-              m = eval_pred(in, p.pool, id);
-              if (stats) mark_sectors(sm, j, b);
-            }
-            uint64_t bal = __ballot(m);
-            if (lane == 0) sm.masks[in.dst][g] = bal;
+          // Compact the care docs (fewer than ndocs/32 <= 128 here) into sm.list, then one thread per candidate
+          // fetches its two words: a single memory round trip for the whole tile, no per-group serialisation.
+          const int nc = compact_mask(sm, care, in.dst);
+          for (int k = threadIdx.x; k < nc; k += NT) {
+            const int j = sm.list[k];
+            const uint32_t id = get_id(sm, c, t, j, false);
+            if (eval_pred(in, p.pool, id))
+              atomicOr((unsigned long long*)&sm.masks[in.dst][j >> 6], 1ull << (j & 63));
+            if (stats) mark_sectors(sm, j, b);
           }
           if (stats) {
             __syncthreads();
@@ -394,6 +423,52 @@ __device__ int run_filter(Smem& sm, const DevParams& p, const TileCtx& t, const 
   return 0;
 }
 
+// ---- register prefetch of the driving scan column -------------------------------------------------------------
+// The first SCAN of a segment's program (under AND_BEGINs only) is evaluated densely on every tile; its bytes
+// for the NEXT tile are loaded into registers while the current tile runs, then written to LDS at the top of
+// the next iteration, so the workgroup's dominant stream is always in flight (T14-style issue-early/write-late).
+#define PF_REGS 4  // ceil(32 * 32 / NT) 16-B chunks per thread for b <= 32
+
+__device__ __forceinline__ int seg_of_tile(const DevParams& p, int tile) {
+  int lo = 0, hi = p.nseg - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (p.segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int prefetch_regs(const DevParams& p, int tile, u32x4 (&pf)[PF_REGS]) {
+  if (tile >= p.total_tiles) return 0;
+  const DevSeg& sg = p.segs[seg_of_tile(p, tile)];
+  if (sg.pf_pc < 0) return 0;
+  const DevInstr& in = p.instrs[sg.prog_begin + sg.pf_pc];
+  const DevColumn& c = p.cols[sg.col_begin + in.col];
+  const int b = c.bits;
+  const u32x4* src = (const u32x4*)(c.fwd + (size_t)(tile - sg.tile_begin) * (TILE / 32) * b);
+  const int n16 = (TILE / 128) * b;
+#pragma unroll
+  for (int k = 0; k < PF_REGS; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < n16) pf[k] = src[i];
+  }
+  return b;
+}
+
+__device__ __forceinline__ void write_prefetched(Smem& sm, const u32x4 (&pf)[PF_REGS], int b) {
+  const int n16 = (TILE / 128) * b;
+  u32x4* dst = (u32x4*)(sm.stage + 4);
+#pragma unroll
+  for (int k = 0; k < PF_REGS; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < n16) {
+      u32x4 v = pf[k];
+      v.x = bswap32(v.x); v.y = bswap32(v.y); v.z = bswap32(v.z); v.w = bswap32(v.w);
+      dst[i] = v;
+    }
+  }
+}
+
 // ---- the query kernel ----------------------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(NT) void query_kernel(DevParams p) {
@@ -414,17 +489,15 @@ __global__ __launch_bounds__(NT) void query_kernel(DevParams p) {
     }
   }
   int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;  // thread 0 owns these
+  u32x4 pf[PF_REGS];
+  int pf_bits = prefetch_regs(p, blockIdx.x, pf);
   __syncthreads();
 
   for (int tile = blockIdx.x; tile < p.total_tiles; tile += gridDim.x) {
-    // segment of this tile (uniform binary search over tile_begin)
-    int lo = 0, hi = p.nseg - 1;
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (p.segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
-    }
     TileCtx t;
-    t.seg = &p.segs[lo];
+    t.seg = &p.segs[seg_of_tile(p, tile)];
+    if (pf_bits) write_prefetched(sm, pf, pf_bits);   // this tile's driving column -> LDS
+    pf_bits = prefetch_regs(p, tile + gridDim.x, pf);  // next tile's bytes stay in flight during this tile
     t.tile_in_seg = tile - t.seg->tile_begin;
     t.doc0 = t.tile_in_seg * TILE;
     t.ndocs = min(TILE, t.seg->num_docs - t.doc0);
@@ -441,30 +514,8 @@ __global__ __launch_bounds__(NT) void query_kernel(DevParams p) {
     const int fslot = run_filter(sm, p, t, cols, scanned, sector_bytes, dense_bytes);
     const uint64_t* fmask = fslot < 0 ? sm.valid : sm.masks[0];
 
-    // compaction of matching docs -> sm.list
-    if (threadIdx.x < 64) {
-      const int g = threadIdx.x;
-      int c = __popcll(fmask[g] & sm.valid[g]);
-      // exclusive scan across the 64 lanes of wave 0
-      int x = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      sm.goff[g] = x - c;
-      if (g == 63) sm.nmatch = x;
-    }
-    __syncthreads();
-    for (int g = wave; g < NG; g += NW) {
-      const uint64_t m = fmask[g] & sm.valid[g];
-      if ((m >> lane) & 1ull) {
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        sm.list[sm.goff[g] + below] = (uint16_t)(g * 64 + lane);
-      }
-    }
-    __syncthreads();
-    const int nm = sm.nmatch;
+    // compaction of matching docs -> sm.list (final masks never exceed the valid docs)
+    const int nm = compact_mask(sm, fmask, -1);
     if (threadIdx.x == 0) matched += nm;
     if (nm == 0) continue;  // uniform
     const bool dense_post = nm * 32 >= t.ndocs;

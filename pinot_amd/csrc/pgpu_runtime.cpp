@@ -850,6 +850,14 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       if (rc) return rc;
     }
     ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
+    // driving scan: the first SCAN reached through AND_BEGINs only is dense on every tile -> prefetch it
+    ds.pf_pc = -1;
+    for (int i = 0; i < ds.prog_len; ++i) {
+      const DevInstr& in = pk.instrs[ds.prog_begin + i];
+      if (in.op == PGPU_I_AND_BEGIN) continue;
+      if (in.op == PGPU_I_SCAN && pk.cols[ds.col_begin + in.col].kind == PGPU_COL_FIXED_BIT) ds.pf_pc = i;
+      break;
+    }
     pk.segs.push_back(ds);
     tiles += (seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
   }

@@ -60,6 +60,22 @@ __global__ __launch_bounds__(256) void synth_fixed_bit_kernel(uint32_t* out, int
 
 }  // namespace
 
+// Scratch buffers come from this library's HIP runtime (the one libpinotgpu.so uses), never from another
+// runtime that may be loaded in the same process (e.g. a framework's bundled HIP).
+extern "C" void* synth_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+extern "C" int synth_free(void* p) { return hipFree(p) == hipSuccess ? 0 : -1; }
+extern "C" int synth_sync(void) { return hipDeviceSynchronize() == hipSuccess ? 0 : -1; }
+extern "C" int synth_copy_to_host(void* dst, const void* src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int synth_copy_from_host(void* dst, const void* src, uint64_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int synth_fixed_bit(void* dev_out, int64_t num_docs, int32_t bits, int32_t card, uint64_t seed,
                                const void* dev_cdf, void* stream) {
   if (!dev_out || num_docs < 0 || bits < 1 || bits > 32 || card < 1) return -1;

@@ -77,15 +77,9 @@ class SegmentFilterPlanner:
 
     def __init__(self, seg: GpuSegment):
         self.seg = seg
-        self._dicts: Dict[str, SortedDictionary] = {}
 
     def dictionary(self, column: str) -> SortedDictionary:
-        d = self._dicts.get(column)
-        if d is None:
-            col = self.seg.column(column)
-            d = SortedDictionary(self.seg.dictionaries[column], col.data_type)
-            self._dicts[column] = d
-        return d
+        return self.seg.sorted_dictionary(column)
 
     def build(self, f: Optional[FilterContext]) -> FilterOp:
         return ALL if f is None else self._construct(f)
@@ -135,14 +129,14 @@ class SegmentFilterPlanner:
         if ev.always_true:
             return ALL
         if col.is_sorted:
-            return FilterOp("SORTED", column=p.column, evaluator=ev, doc_ranges=self._sorted_ranges(col, ev))
+            return FilterOp("SORTED", column=p.column, evaluator=ev,
+                            doc_ranges=self._sorted_ranges(self.seg.sorted_pairs(p.column), ev))
         if p.type != "RANGE" and col.inverted is not None:
             return FilterOp("INV", column=p.column, evaluator=ev)
         return FilterOp("SCAN", column=p.column, evaluator=ev)
 
     @staticmethod
-    def _sorted_ranges(col, ev: DictPredicateEvaluator) -> List[Tuple[int, int]]:
-        pairs = np.frombuffer(col.sorted_index, dtype=">i4").reshape(-1, 2)
+    def _sorted_ranges(pairs: np.ndarray, ev: DictPredicateEvaluator) -> List[Tuple[int, int]]:
         if ev.kind == "RANGE":
             return [(int(pairs[ev.start, 0]), int(pairs[ev.end - 1, 1]))]
         ids = sorted(ev.ids)  # matching (inclusive) or non-matching (exclusive) ids

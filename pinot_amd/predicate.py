@@ -37,27 +37,35 @@ def _key(value: str, data_type: int):
 
 
 class SortedDictionary:
-    """Sorted dictionary values with the reference's binary-search contract."""
+    """Sorted dictionary values with the reference's binary-search contract (numpy searchsorted for numeric
+    dictionaries, bisect for strings)."""
 
     def __init__(self, values: Union[np.ndarray, Sequence[str]], data_type: int):
         self.data_type = data_type
         if data_type == PGPU_STRING:
-            self.values: List = list(values)
+            self.values = list(values)
         elif data_type in (PGPU_INT, PGPU_LONG):
-            self.values = [int(v) for v in values]
+            self.values = np.asarray(values, dtype=np.int64)
         else:
-            self.values = [float(v) for v in values]
+            self.values = np.asarray(values, dtype=np.float64)
+        self._n = len(self.values)
 
     def __len__(self) -> int:
-        return len(self.values)
+        return self._n
 
     def insertion_index_of(self, literal: str) -> int:
         """>= 0: index of an exact match; < 0: -(insertion point + 1)."""
         k = _key(literal, self.data_type)
-        i = bisect.bisect_left(self.values, k)
-        if i < len(self.values) and self.values[i] == k:
-            return i
-        return -(i + 1)
+        if self.data_type == PGPU_STRING:
+            i = bisect.bisect_left(self.values, k)
+            found = i < self._n and self.values[i] == k
+        elif isinstance(k, Fraction):  # fractional literal on an integer dictionary: never equal
+            i = int(np.searchsorted(self.values, float(k), side="left"))
+            found = False
+        else:
+            i = int(np.searchsorted(self.values, k, side="left"))
+            found = i < self._n and self.values[i] == k
+        return i if found else -(i + 1)
 
     def index_of(self, literal: str) -> int:
         i = self.insertion_index_of(literal)

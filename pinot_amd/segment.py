@@ -207,6 +207,24 @@ class GpuSegment:
     def column(self, name: str) -> ColumnIndexes:
         return self.data.column(name)
 
+    def sorted_dictionary(self, name: str):
+        """Host dictionary used by the predicate evaluators (built once per segment column)."""
+        cache = self.__dict__.setdefault("_sorted_dicts", {})
+        d = cache.get(name)
+        if d is None:
+            from .predicate import SortedDictionary
+            d = SortedDictionary(self.dictionaries[name], self.column(name).data_type)
+            cache[name] = d
+        return d
+
+    def sorted_pairs(self, name: str) -> np.ndarray:
+        cache = self.__dict__.setdefault("_sorted_pairs", {})
+        p = cache.get(name)
+        if p is None:
+            p = np.frombuffer(self.column(name).sorted_index, dtype=">i4").reshape(-1, 2).astype(np.int64)
+            cache[name] = p
+        return p
+
     def has_column(self, name: str) -> bool:
         return name in self.slots
 

@@ -139,6 +139,29 @@ class SynthLib:
         self.lib.synth_fixed_bit.restype = C.c_int
         self.lib.synth_fixed_bit.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_uint64, C.c_void_p,
                                              C.c_void_p]
+        self.lib.synth_alloc.restype = C.c_void_p
+        self.lib.synth_alloc.argtypes = [C.c_uint64]
+        self.lib.synth_free.argtypes = [C.c_void_p]
+        self.lib.synth_sync.restype = C.c_int
+        self.lib.synth_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        self.lib.synth_copy_to_host.restype = C.c_int
+
+    def alloc(self, nbytes: int) -> int:
+        p = self.lib.synth_alloc(nbytes)
+        if not p:
+            raise MemoryError(f"synth_alloc({nbytes}) failed")
+        return p
+
+    def generate(self, dev_out: int, num_docs: int, bits: int, card: int, seed: int, dev_cdf=None) -> None:
+        rc = self.lib.synth_fixed_bit(dev_out, num_docs, bits, card, seed, dev_cdf, None)
+        if rc != 0 or self.lib.synth_sync() != 0:
+            raise RuntimeError(f"synth_fixed_bit failed ({rc})")
+
+    def to_host(self, dev: int, nbytes: int) -> bytes:
+        buf = C.create_string_buffer(nbytes)
+        if self.lib.synth_copy_to_host(buf, dev, nbytes) != 0:
+            raise RuntimeError("synth_copy_to_host failed")
+        return buf.raw
 
 
 def forward_index_bytes(num_docs: int, bits: int) -> int:
@@ -158,36 +181,43 @@ def build_segment_cpu(w: Workload, segment: int, num_docs: int, pack: Callable) 
 
 
 def build_segments_gpu(ctx: GpuContext, w: Workload, segment_ids: List[int], num_docs: int) -> List[GpuSegment]:
-    """Generate the forward indexes in HBM (torch scratch buffer) and upload them as PGPU_MEM_DEVICE sources."""
-    import torch
-
-    lib = SynthLib().lib
-    dev = torch.device("cuda", ctx.device)
-    cdfs = {}
+    """Generate the forward indexes in HBM and upload them as PGPU_MEM_DEVICE sources (D2D copies inside the
+    same HIP runtime as libpinotgpu; no host round trip)."""
+    sl = SynthLib()
     dicts = {c.name: c.values().astype(">i4").tobytes() for c in w.columns}
     max_bytes = max(forward_index_bytes(num_docs, num_bits_per_value(c.cardinality - 1)) for c in w.columns)
-    scratch = torch.empty(((max_bytes + 64) // 4) * 4, dtype=torch.uint8, device=dev)
+    scratch = sl.alloc(((max_bytes + 64) // 4) * 4)
+    cdfs = {}
     out = []
-    for s in segment_ids:
-        gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns))
+    try:
         for c in w.columns:
-            bits = num_bits_per_value(c.cardinality - 1)
-            cdf_ptr = None
             if c.dist == "zipf":
-                if c.name not in cdfs:
-                    cdfs[c.name] = torch.from_numpy(zipf_cdf(c.cardinality, c.zipf_s).view(np.int32)).to(dev)
-                cdf_ptr = cdfs[c.name].data_ptr()
-            rc = lib.synth_fixed_bit(scratch.data_ptr(), num_docs, bits, c.cardinality,
-                                     column_seed(w.seed, s, c.name), cdf_ptr,
-                                     torch.cuda.current_stream(dev).cuda_stream)
-            if rc != 0:
-                raise RuntimeError(f"synth_fixed_bit failed ({rc})")
-            torch.cuda.synchronize(dev)
-            gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],
-                                        forward_device=scratch.data_ptr(),
-                                        forward_device_bytes=forward_index_bytes(num_docs, bits)))
-            gs.data.columns[c.name].forward_device = None  # the scratch buffer is reused by the next column
-        gs.seal()
-        out.append(gs)
-    del scratch
+                table = zipf_cdf(c.cardinality, c.zipf_s)
+                p = sl.alloc(table.nbytes)
+                _h2d(sl, p, table)
+                cdfs[c.name] = p
+        for s in segment_ids:
+            gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns))
+            for c in w.columns:
+                bits = num_bits_per_value(c.cardinality - 1)
+                sl.generate(scratch, num_docs, bits, c.cardinality, column_seed(w.seed, s, c.name), cdfs.get(c.name))
+                gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],
+                                            forward_device=scratch,
+                                            forward_device_bytes=forward_index_bytes(num_docs, bits)))
+                gs.data.columns[c.name].forward_device = None  # the scratch buffer is reused by the next column
+            gs.seal()
+            out.append(gs)
+    finally:
+        sl.lib.synth_free(scratch)
+        for p in cdfs.values():
+            sl.lib.synth_free(p)
     return out
+
+
+def _h2d(sl: SynthLib, dev: int, arr: np.ndarray) -> None:
+    lib = sl.lib
+    lib.synth_copy_from_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    lib.synth_copy_from_host.restype = C.c_int
+    a = np.ascontiguousarray(arr)
+    if lib.synth_copy_from_host(dev, a.ctypes.data, a.nbytes) != 0:
+        raise RuntimeError("synth_copy_from_host failed")

@@ -10,6 +10,14 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libpinotgpu.so")
+    # torch ships its own HIP runtime; when both are used in one process let torch initialise first
+    # (libpinotgpu.so never hands its pointers or streams to torch; see pinot_amd/combine.py).
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
 
 
 @pytest.fixture(scope="session")

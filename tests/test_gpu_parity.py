@@ -217,19 +217,19 @@ def test_inverted_leaves_vs_oracle(gpu_ctx, qi):
 
 def test_group_limit_unsupported(gpu_ctx):
     rng = np.random.default_rng(9)
-    seg = _random_segment(rng, 10_000)
+    seg = _random_segment(rng, 200_000)  # column d: ~66k distinct values present -> IntMap holder
     g = GpuSegment(gpu_ctx, seg)
     try:
         with pytest.raises(UnsupportedPlanError):
             GpuPlanMaker(gpu_ctx, num_groups_limit=50_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
         res = GpuPlanMaker(gpu_ctx, num_groups_limit=100_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
-        assert sum(r[1] for r in res.group_rows) == 10_000
+        assert sum(r[1] for r in res.group_rows) == 200_000
     finally:
         g.release()
 
 
 def test_empty_segment(gpu_ctx):
-    seg = build_segment("empty", {"x": (PGPU_INT, np.array([5], np.int32))})
+    seg = build_segment("empty", {"x": (PGPU_INT, np.array([5], np.int32))}, sorted_columns=[])
     seg.num_docs = 0
     seg.columns["x"].forward = b""
     g = GpuSegment(gpu_ctx, seg)
@@ -242,20 +242,45 @@ def test_empty_segment(gpu_ctx):
 
 # ---- synthetic generator parity ---------------------------------------------------------------------------------
 def test_synth_generator_matches_cpu(gpu_ctx):
-    import torch
+    """The HBM generator used by bench.py writes exactly the bytes the CPU restatement writes."""
     from oracle.segment_writer import pack_fixed_bit
-    from pinot_amd.synth import SynthLib, dict_ids_cpu, zipf_cdf
-    lib = SynthLib().lib
+    from pinot_amd.synth import SynthLib, _h2d, dict_ids_cpu, zipf_cdf
+    sl = SynthLib()
     for bits, card, n, dist in [(4, 16, 100_001, None), (10, 1024, 65_536, None), (16, 65536, 33_333, None),
-                                (20, 1 << 20, 8192 * 3 + 5, None), (20, 1 << 20, 50_000, "zipf")]:
+                                (20, 1 << 20, 8192 * 3 + 5, None), (20, 1 << 20, 50_000, "zipf"), (1, 2, 777, None),
+                                (32, 1 << 31, 9_999, None)]:
         seed = 12345 + bits
         cdf = zipf_cdf(card, 1.1) if dist else None
-        out = torch.zeros((n * bits + 31) // 32 * 4 + 64, dtype=torch.uint8, device="cuda")
-        cdf_t = torch.from_numpy(cdf.view(np.int32)).cuda() if dist else None
-        rc = lib.synth_fixed_bit(out.data_ptr(), n, bits, card, seed, cdf_t.data_ptr() if dist else None,
-                                 torch.cuda.current_stream().cuda_stream)
-        assert rc == 0
-        torch.cuda.synchronize()
-        got = out.cpu().numpy().tobytes()[: (n * bits + 7) // 8]
+        nbytes = (n * bits + 31) // 32 * 4 + 64
+        out = sl.alloc(nbytes)
+        cdf_p = None
+        try:
+            if dist:
+                cdf_p = sl.alloc(cdf.nbytes)
+                _h2d(sl, cdf_p, cdf)
+            sl.generate(out, n, bits, card, seed, cdf_p)
+            got = sl.to_host(out, (n * bits + 7) // 8)
+        finally:
+            sl.lib.synth_free(out)
+            if cdf_p:
+                sl.lib.synth_free(cdf_p)
         exp = pack_fixed_bit(dict_ids_cpu(seed, n, card, cdf=cdf), bits)
         assert got == exp, (bits, card, n, dist)
+
+
+def test_synth_segments_upload_d2d(gpu_ctx):
+    """GPU-generated segments (device-to-device upload) answer exactly like the same segments built on the host."""
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import WORKLOADS, build_segment_cpu, build_segments_gpu
+    for wn in ("range_in", "adanalytics", "groupby1m"):
+        w = WORKLOADS[wn]
+        n = 300_007
+        gsegs = build_segments_gpu(gpu_ctx, w, [3, 4], n)
+        hsegs = [build_segment_cpu(w, s, n, pack_fixed_bit) for s in (3, 4)]
+        q = parse_sql(w.sql)
+        opts = dict(num_groups_limit=w.options.get("num_groups_limit", 100_000))
+        res = GpuPlanMaker(gpu_ctx, **opts).execute(q, gsegs)
+        ref = engine.execute(q, hsegs, **opts)
+        _assert_same(res, ref)
+        for g in gsegs:
+            g.release()
