@@ -11,14 +11,15 @@
 #pragma once
 #include <stdint.h>
 
-#define PGPU_TILE 4096          // docs per workgroup tile (multiple of 128 => 16-B aligned tile byte offsets)
-#define PGPU_BLOCK 256          // threads per workgroup (4 waves of 64)
+#define PGPU_TILE 4096          // forward-index padding granularity in docs (whole tiles are always readable)
+#define PGPU_WAVE_TILE 2048     // docs per wave tile: lane l owns docs [32l, 32l+32); 256*b bytes, 16-B aligned
+#define PGPU_BLOCK 256          // threads per workgroup (4 independent waves of 64)
 #define PGPU_WAVES (PGPU_BLOCK / 64)
 #define PGPU_GROUPS (PGPU_TILE / 64)
-#define PGPU_MAX_SLOTS 8        // filter mask slots (nesting depth of AND/OR/NOT)
+#define PGPU_MAX_SLOTS 8        // per-lane mask words (7 filter slots + 1 scratch row)
 #define PGPU_MAX_AGGS 16
 #define PGPU_MAX_GCOLS 8
-#define PGPU_LDS_TABLE_BYTES (48 * 1024)
+#define PGPU_LDS_TABLE_BYTES (16 * 1024)
 
 // column kinds
 #define PGPU_COL_NONE 0
@@ -78,7 +79,7 @@ struct DevSeg {
 struct DevInstr {
   int32_t op;
   int32_t col;      // query column
-  int32_t pred;     // PGPU_PRED_RANGE / SET
+  int32_t pred;     // 0 RANGE, 1 SET (bitset in the pool), 2 LIST (<= 8 ids in the pool)
   int32_t negate;
   int32_t lo, hi;
   int32_t pool_off; // int32 pool offset (SET bitset, id list, doc ranges)
@@ -115,8 +116,8 @@ struct DevParams {
   const int32_t* pool;
   const int32_t* const* remaps;   // [nseg * ngcols], nullptr = identity
   int64_t* table;                 // [nsec][G]
-  int64_t* slab;                  // AGG mode: [grid][nsec]; all modes: stats [grid][PGPU_NSTATS] after it
-  int64_t* stats;                 // [grid][PGPU_NSTATS]
+  int64_t* slab;                  // AGG mode: [waves][nsec]
+  int64_t* stats;                 // [waves][PGPU_NSTATS]
   uint64_t G;
   int32_t nseg;
   int32_t total_tiles;
@@ -126,6 +127,8 @@ struct DevParams {
   int32_t nsec;
   int32_t mode;
   int32_t flags;
+  int32_t pf_words;               // words of the driving column per wave tile (64 * max bits), 0 = no prefetch
+  int32_t pad0;
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];

@@ -1,18 +1,21 @@
 // HIP kernels of the MI355X segment query path (gfx950 / CDNA4).
 //
-// One launch runs a whole query over every segment a GPU owns.  A persistent grid of workgroups strides over
-// (segment, 4096-doc tile) pairs; per tile a workgroup
-//   1. interprets the segment's filter program (K1: fixed-bit unpack fused with dict-id RANGE/SET predicates;
-//      K2: Roaring array/bitmap/run containers OR-ed into tile masks; sorted-index doc ranges; AND/OR/NOT on
-//      64-bit ballot masks in LDS),
-//   2. compacts the matching doc ids of the tile into an LDS list,
-//   3. computes group keys from the group-by columns' dict ids (remapped to global ids) and
-//   4. aggregates COUNT/SUM/MIN/MAX/AVG into per-thread registers (aggregation only), an LDS-privatised dense
-//      table (small key spaces) or the global dense table (large key spaces)  (K3).
-// Columns are read in one of two modes, chosen per tile from the density of the docs that still matter:
-//   dense : the tile's bytes of the forward index are streamed into LDS with 16-B coalesced loads and
-//           byte-swapped once; each lane then unpacks doc (64*g + lane) with one v_alignbit.
-//   sparse: only the docs of the care mask fetch their two words from HBM (sector-granular traffic).
+// One launch runs a whole query over every segment a GPU owns.  Work unit = a WAVE TILE of 2048 consecutive docs
+// of one segment; every wave of the persistent grid walks its own wave tiles independently (no workgroup barrier
+// in the main loop), and inside a wave tile LANE l OWNS DOCS [32l, 32l+32): the 32*b bits of a lane are exactly b
+// consecutive big-endian words of the FixedBitSVForwardIndexWriter stream, so a lane unpacks its 32 dict ids with
+// compile-time shifts (one template instantiation per bit width) and every filter mask is one 32-bit word per lane.
+//
+//   K1  fixed-bit unpack fused with dict-id RANGE / SET / LIST predicates:
+//         dense  — the lane's b words (the "driving" column of the filter is DMA'd into LDS one wave tile ahead
+//                  with global_load_lds; other columns are loaded straight to VGPRs),
+//         sparse — when the docs that still matter are < 1/32 of the tile, only those docs gather their two
+//                  words (32-B-sector-granular traffic).
+//   K2  Roaring array / bitmap / run containers (BitmapBasedFilterOperator), sorted-index doc ranges, and the
+//       AND / OR / NOT algebra on the per-lane mask words (short-circuit of AND when a wave tile empties).
+//   K3  COUNT / SUM / MIN / MAX / AVG: per-lane register accumulators + wave reduction (aggregation only), or
+//       group keys (mixed-radix global dict ids) with atomics into an LDS-privatised dense table (small key
+//       spaces) or the HBM dense table (large key spaces).
 //
 // Reference hot loops this replaces (file:line under pinot-core/... and pinot-segment-local/...):
 //   FixedBitIntReader.read32 / PinotDataBitSet.readInt           seglocal/io/util/PinotDataBitSet.java:78-165
@@ -29,58 +32,31 @@
 #include "../../include/pinot_gpu.h"
 #include "pgpu_internal.h"
 
-#define TILE PGPU_TILE
 #define NT PGPU_BLOCK
 #define NW PGPU_WAVES
-#define NG PGPU_GROUPS
+#define WT PGPU_WAVE_TILE  // 2048 docs per wave tile
+#define MAXS PGPU_MAX_SLOTS
 
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-struct __attribute__((aligned(16))) Smem {
-  uint32_t stage[TILE + 16];             // staged forward-index words of one column (byte-swapped), at +4
-  uint64_t masks[PGPU_MAX_SLOTS][NG];    // filter mask slots
-  uint64_t valid[NG];                    // docs < num_docs
-  uint16_t list[TILE];                   // compacted matching doc offsets
-  int32_t goff[NG + 1];                  // exclusive prefix of per-group match counts
-  int32_t slot_count[PGPU_MAX_SLOTS];    // popcount of each AND accumulator
-  int32_t nvalid;
-  uint32_t sectors[TILE / 256 * 32 / 32 + 16];  // touched 32-B sectors of a sparse read (stats mode)
-  int64_t accw[NW][PGPU_MAX_AGGS];       // AGG mode: per-wave accumulators
-  int64_t bstats[PGPU_NSTATS];
-};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// Loads through the global address space: segment pointers reach the kernel inside structs in HBM, so the
+// compiler only sees generic pointers and would emit flat_* (which also count against lgkmcnt and stall LDS).
+#define GAS __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T gld(const T* p, size_t i) { return ((const GAS T*)p)[i]; }
 __device__ __forceinline__ uint32_t lowmask(uint32_t b) { return 0xFFFFFFFFu >> (32u - b); }
+// Bit i of a lane mask word as v_bfe_u32 with inline operands (a `1u << i` test makes the compiler keep 32
+// materialised constants live in VGPRs across the unrolled doc loops).
+__device__ __forceinline__ uint32_t lane_bit(uint32_t m, int i) { return __builtin_amdgcn_ubfe(m, (uint32_t)i, 1u); }
 
-// Value whose last bit is stream bit e-1 (MSB-first), from byte-swapped words st[] (st[-1] readable).
-__device__ __forceinline__ uint32_t extract_lds(const uint32_t* st, uint32_t e, uint32_t b) {
-  uint32_t we = (e - 1u) >> 5;
-  uint32_t r = e - (we << 5);  // 1..32 bits of the value in word we
-  uint32_t lo = st[(int)we - 1];
-  uint32_t hi = st[we];
-  return __builtin_amdgcn_alignbit(lo, hi, 32u - r) & lowmask(b);
-}
-
-// Same from the raw big-endian words in HBM; e is the segment-level end bit.
-__device__ __forceinline__ uint32_t extract_global(const uint32_t* __restrict__ words, uint64_t e, uint32_t b) {
-  uint64_t we = (e - 1u) >> 5;
-  uint32_t r = (uint32_t)(e - (we << 5));
-  uint32_t hi = bswap32(words[we]);
-  uint32_t lo = we ? bswap32(words[we - 1]) : 0u;
-  return __builtin_amdgcn_alignbit(lo, hi, 32u - r) & lowmask(b);
-}
-
-// SortedIndexReaderImpl.getDictId: last dict id whose start <= doc (binary search over the start offsets).
-__device__ __forceinline__ uint32_t sorted_dict_id(const int32_t* __restrict__ pairs, int32_t card, int32_t doc) {
-  int32_t lo = 0, hi = card - 1;
-  while (lo <= hi) {
-    int32_t mid = (lo + hi) >> 1;
-    if (pairs[2 * mid] <= doc) lo = mid + 1; else hi = mid - 1;
-  }
-  return (uint32_t)hi;
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
@@ -103,535 +79,670 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
   return v;
 }
+// Wave-uniform total (readfirstlane: callers branch on it as a scalar).
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return __builtin_amdgcn_readfirstlane(v);
 }
 
 // Order-preserving int64 key of a dictionary value (MIN/MAX sections).
 __device__ __forceinline__ int64_t minmax_key(const void* dict, int32_t vtype, uint32_t id) {
   switch (vtype) {
-    case PGPU_INT: return (int64_t)((const int32_t*)dict)[id];
-    case PGPU_LONG: return ((const int64_t*)dict)[id];
+    case PGPU_INT: return (int64_t)gld((const int32_t*)dict, id);
+    case PGPU_LONG: return gld((const int64_t*)dict, id);
     case PGPU_FLOAT: {
-      double d = (double)((const float*)dict)[id];
-      int64_t b = __double_as_longlong(d);
+      int64_t b = __double_as_longlong((double)gld((const float*)dict, id));
       return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
     }
     default: {
-      int64_t b = __double_as_longlong(((const double*)dict)[id]);
+      int64_t b = __double_as_longlong(gld((const double*)dict, id));
       return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
     }
   }
 }
 __device__ __forceinline__ int64_t value_i64(const void* dict, int32_t vtype, uint32_t id) {
-  return vtype == PGPU_INT ? (int64_t)((const int32_t*)dict)[id] : ((const int64_t*)dict)[id];
+  return vtype == PGPU_INT ? (int64_t)gld((const int32_t*)dict, id) : gld((const int64_t*)dict, id);
 }
 __device__ __forceinline__ double value_f64(const void* dict, int32_t vtype, uint32_t id) {
-  return vtype == PGPU_FLOAT ? (double)((const float*)dict)[id] : ((const double*)dict)[id];
+  return vtype == PGPU_FLOAT ? (double)gld((const float*)dict, id) : gld((const double*)dict, id);
 }
-
 __device__ __forceinline__ int64_t sec_identity(int32_t op) {
   return op == PGPU_RED_MIN_I64 ? INT64_MAX : (op == PGPU_RED_MAX_I64 ? INT64_MIN : 0);
 }
 
-// ---- staging -------------------------------------------------------------------------------------------------
-// Copy the tile's ceil(TILE*b/128) 16-B chunks of the forward index into Smem.stage (+4 words), byte-swapped.
-__device__ __forceinline__ void stage_column(Smem& sm, const uint32_t* __restrict__ fwd, int32_t tile_in_seg,
-                                             uint32_t b) {
-  const u32x4* src = (const u32x4*)(fwd + (size_t)tile_in_seg * (TILE / 32) * b);
-  u32x4* dst = (u32x4*)(sm.stage + 4);
-  const int n16 = (TILE / 128) * b;
-  for (int i = threadIdx.x; i < n16; i += NT) {
-    u32x4 v = src[i];
-    v.x = bswap32(v.x); v.y = bswap32(v.y); v.z = bswap32(v.z); v.w = bswap32(v.w);
-    dst[i] = v;
-  }
-}
-
-struct TileCtx {
-  const DevSeg* seg;
-  int32_t tile_in_seg;
-  int32_t doc0;      // first doc of the tile (segment-local)
-  int32_t ndocs;     // docs of the tile inside the segment
+// ---- per-wave LDS carve ----------------------------------------------------------------------------------------
+// dynamic LDS of a workgroup: [NW][MAXS][64] slot words | [NW][pf_words] driving-column buffers |
+//                             [NW][MAX_AGGS] int64 accumulators | LDS group table [nsec][G] (mode LDS)
+struct Carve {
+  uint32_t* slots;   // this wave's [MAXS][64]
+  uint32_t* pf;      // this wave's driving-column buffer (pf_words)
+  int64_t* accw;     // this wave's [MAX_AGGS]
+  int64_t* ltab;     // workgroup table
+  bool* pf_have;     // a DMA into pf is in flight
+  int pf_words;
 };
 
-// Dict id of tile-relative doc j of column c, from the staged copy (dense) or HBM (sparse).
-__device__ __forceinline__ uint32_t get_id(const Smem& sm, const DevColumn& c, const TileCtx& t, int j,
-                                           bool staged) {
-  if (c.kind == PGPU_COL_SORTED) return sorted_dict_id(c.sorted, c.card, t.doc0 + j);
-  const uint32_t b = (uint32_t)c.bits;
-  if (staged) return extract_lds(sm.stage + 4, (uint32_t)(j + 1) * b, b);
-  return extract_global(c.fwd, (uint64_t)(t.doc0 + j + 1) * b, b);
+__device__ __forceinline__ uint32_t& slot(const Carve& cv, int s) { return cv.slots[s * 64 + (threadIdx.x & 63)]; }
+
+struct WTile {
+  const DevSeg* seg;
+  const DevColumn* cols;
+  int32_t tile_in_seg;
+  int32_t doc0;      // first doc of the wave tile (segment-local)
+  int32_t ndocs;     // docs of the wave tile inside the segment (1..2048)
+  uint32_t valid;    // this lane's valid-doc word
+  int32_t lane_doc0; // doc0 + 32 * lane
+};
+
+// ---- fixed-bit extraction (compile-time bit width) -------------------------------------------------------------
+// w[] = the lane's B words, byte-swapped (MSB-first bit order); value i occupies bits [i*B, (i+1)*B).
+template <int B>
+__device__ __forceinline__ uint32_t extract_c(const uint32_t (&w)[B], int i) {
+  const int o = i * B;
+  const int k = o >> 5, sh = o & 31;
+  if (sh + B <= 32) return (w[k] >> (32 - sh - B)) & lowmask(B);
+  return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64 - sh - B) & lowmask(B);
 }
 
-__device__ __forceinline__ bool eval_pred(const DevInstr& in, const int32_t* __restrict__ pool, uint32_t id) {
-  bool m;
-  if (in.pred == PGPU_PRED_RANGE) {
-    m = (id - (uint32_t)in.lo) < (uint32_t)(in.hi - in.lo);
+// This lane's index, opaque to loop-invariant code motion: the per-bit-width lane offsets (lane * B for 31
+// widths) would otherwise be hoisted out of the tile loop and pin ~30 VGPRs for the kernel's lifetime.
+__device__ __forceinline__ uint32_t opaque_lane() {
+  uint32_t l;
+  asm volatile("v_and_b32 %0, 63, %1" : "=v"(l) : "v"(threadIdx.x));
+  return l;
+}
+
+// The lane's B words of column `fwd` in wave tile `tile_in_seg`, straight from HBM (byte-swapped).
+template <int B>
+__device__ __forceinline__ void load_lane_words(const uint32_t* __restrict__ fwd, int tile_in_seg, uint32_t (&w)[B]) {
+  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
+  if constexpr (B % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < B; k += 4) {
+      const u32x4 v = *(const GAS u32x4*)(src + k);
+      w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+    }
+  } else if constexpr (B % 2 == 0) {
+#pragma unroll
+    for (int k = 0; k < B; k += 2) {
+      const u32x2 v = *(const GAS u32x2*)(src + k);
+      w[k] = v.x; w[k + 1] = v.y;
+    }
   } else {
-    m = (pool[in.pool_off + (id >> 5)] >> (id & 31)) & 1;
+#pragma unroll
+    for (int k = 0; k < B; ++k) w[k] = src[k];
   }
-  return m != (in.negate != 0);
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(w[k]);
 }
 
-// Block-wide popcount of mask slot `s` (wave 0 computes, result in sm.slot_count[s]); caller syncs.
-__device__ __forceinline__ void count_slot(Smem& sm, int s) {
-  if (threadIdx.x < 64) {
-    int c = __popcll(sm.masks[s][threadIdx.x]);
-    c = wave_sum_i32(c);
-    if (threadIdx.x == 0) sm.slot_count[s] = c;
+// The lane's B words from the LDS copy of the wave tile (linear stream order, raw big-endian).
+template <int B>
+__device__ __forceinline__ void lds_lane_words(const uint32_t* buf, uint32_t (&w)[B]) {
+  const uint32_t* src = buf + opaque_lane() * B;
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(src[k]);
+}
+
+// ---- fixed-bit decode: ONE inlined dispatch site per source keeps the 31 bit-width variants out of every consumer
+template <int B>
+__device__ __forceinline__ void unpack_b(const uint32_t (&w)[B], uint32_t (&ids)[32]) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) ids[i] = extract_c<B>(w, i);
+}
+template <int B>
+__device__ __forceinline__ void decode_hbm_b(const uint32_t* fwd, int tile_in_seg, uint32_t (&ids)[32]) {
+  uint32_t w[B];
+  load_lane_words<B>(fwd, tile_in_seg, w);
+  unpack_b<B>(w, ids);
+}
+template <int B>
+__device__ __forceinline__ void decode_lds_b(const uint32_t* buf, uint32_t (&ids)[32]) {
+  uint32_t w[B];
+  lds_lane_words<B>(buf, w);
+  unpack_b<B>(w, ids);
+}
+
+#define PGPU_DISPATCH_B(b, CALL)                                                                     \
+  switch (b) {                                                                                       \
+    case 1: CALL(1); break;   case 2: CALL(2); break;   case 3: CALL(3); break;   case 4: CALL(4); break;   \
+    case 5: CALL(5); break;   case 6: CALL(6); break;   case 7: CALL(7); break;   case 8: CALL(8); break;   \
+    case 9: CALL(9); break;   case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break; \
+    case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break; case 16: CALL(16); break; \
+    case 17: CALL(17); break; case 18: CALL(18); break; case 19: CALL(19); break; case 20: CALL(20); break; \
+    case 21: CALL(21); break; case 22: CALL(22); break; case 23: CALL(23); break; case 24: CALL(24); break; \
+    case 25: CALL(25); break; case 26: CALL(26); break; case 27: CALL(27); break; case 28: CALL(28); break; \
+    case 29: CALL(29); break; case 30: CALL(30); break; default: CALL(31); break;                   \
   }
+
+// The lane's 32 dict ids of column c in the wave tile, from HBM.
+__device__ __forceinline__ void decode_hbm(const DevColumn& c, int tile_in_seg, uint32_t (&ids)[32]) {
+#define DEC_CALL(B) decode_hbm_b<B>(c.fwd, tile_in_seg, ids)
+  PGPU_DISPATCH_B(c.bits, DEC_CALL)
+#undef DEC_CALL
+}
+// ... from the LDS copy of the wave tile (the prefetched driving column).
+__device__ __forceinline__ void decode_lds(int bits, const uint32_t* buf, uint32_t (&ids)[32]) {
+#define DEC_CALL(B) decode_lds_b<B>(buf, ids)
+  PGPU_DISPATCH_B(bits, DEC_CALL)
+#undef DEC_CALL
 }
 
-__device__ __forceinline__ const uint64_t* care_mask(const Smem& sm, int care) {
-  return care < 0 ? sm.valid : sm.masks[care];
-}
-__device__ __forceinline__ int care_count(const Smem& sm, int care) {
-  return care < 0 ? sm.nvalid : sm.slot_count[care];
+// ---- predicates -----------------------------------------------------------------------------------------------
+#define PRED_RANGE 0
+#define PRED_SET 1   // bitset over dict ids in the pool
+#define PRED_LIST 2  // up to 8 ids in the pool
+
+struct Pred {
+  int kind;
+  uint32_t lo, span;         // RANGE: (id - lo) < span
+  const uint32_t* bits;      // SET
+  uint32_t ids[8];           // LIST
+  bool negate;
+};
+
+__device__ __forceinline__ Pred make_pred(const DevInstr& in, const int32_t* pool) {
+  Pred p;
+  p.kind = in.pred;
+  p.negate = in.negate != 0;
+  p.lo = (uint32_t)in.lo;
+  p.span = (uint32_t)(in.hi - in.lo);
+  p.bits = (const uint32_t*)(pool + in.pool_off);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p.ids[k] = (p.kind == PRED_LIST && k < in.n) ? (uint32_t)pool[in.pool_off + k] : 0xFFFFFFFFu;
+  return p;
 }
 
-// Sector bookkeeping for a sparse read of doc j (stats mode): bytes [j*b/8, ((j+1)*b-1)/8] of the tile.
-__device__ __forceinline__ void mark_sectors(Smem& sm, int j, uint32_t b) {
-  uint32_t s0 = ((uint32_t)j * b) >> 8;             // 32-B sector = 256 bits
-  uint32_t s1 = ((uint32_t)(j + 1) * b - 1u) >> 8;
-  atomicOr(&sm.sectors[s0 >> 5], 1u << (s0 & 31));
-  if (s1 != s0) atomicOr(&sm.sectors[s1 >> 5], 1u << (s1 & 31));
+__device__ __forceinline__ bool eval_pred(const Pred& p, uint32_t id) {
+  bool m;
+  if (p.kind == PRED_RANGE) {
+    m = (id - p.lo) < p.span;
+  } else if (p.kind == PRED_LIST) {
+    m = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= id == p.ids[k];
+  } else {
+    m = (gld(p.bits, id >> 5) >> (id & 31)) & 1u;
+  }
+  return m != p.negate;
 }
 
-// OR the tile slice of one Roaring bitmap (dict id `id` of column c) into mask slot `dst` (LDS atomics).
-__device__ void or_bitmap(Smem& sm, const DevColumn& c, const TileCtx& t, uint32_t id, int dst) {
+// The lane's 32 predicate bits for its decoded ids.
+__device__ __forceinline__ uint32_t pred_ids(const uint32_t (&ids)[32], const Pred& p) {
+  // bits are shifted in from doc 31 down to doc 0 (v_lshl_or with inline operands)
+  uint32_t m = 0;
+  if (p.kind == PRED_RANGE) {
+#pragma unroll
+    for (int i = 31; i >= 0; --i) m = (m << 1) | (uint32_t)((ids[i] - p.lo) < p.span);
+  } else if (p.kind == PRED_LIST) {
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+      bool h = false;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h |= ids[i] == p.ids[k];
+      m = (m << 1) | (uint32_t)h;
+    }
+  } else {
+#pragma unroll
+    for (int i = 31; i >= 0; --i) m = (m << 1) | ((gld(p.bits, ids[i] >> 5) >> (ids[i] & 31)) & 1u);
+  }
+  return p.negate ? ~m : m;
+}
+
+// ---- sparse access --------------------------------------------------------------------------------------------
+// SortedIndexReaderImpl.getDictId: last dict id whose start <= doc.
+__device__ __forceinline__ uint32_t sorted_dict_id(const int32_t* __restrict__ pairs, int32_t card, int32_t doc) {
+  int32_t lo = 0, hi = card - 1;
+  while (lo <= hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (gld(pairs, 2 * (size_t)mid) <= doc) lo = mid + 1; else hi = mid - 1;
+  }
+  return (uint32_t)hi;
+}
+
+// Dict id of segment doc `d` gathered from HBM (two big-endian words around its bits).
+__device__ __forceinline__ uint32_t gather_id(const DevColumn& c, int32_t d) {
+  if (c.kind == PGPU_COL_SORTED) return sorted_dict_id(c.sorted, c.card, d);
+  const uint32_t b = (uint32_t)c.bits;
+  const uint64_t e = (uint64_t)(d + 1) * b;
+  const uint64_t we = (e - 1u) >> 5;
+  const uint32_t r = (uint32_t)(e - (we << 5));
+  const uint32_t hi = bswap32(gld(c.fwd, we));
+  const uint32_t lo = we ? bswap32(gld(c.fwd, we - 1)) : 0u;
+  return __builtin_amdgcn_alignbit(lo, hi, 32u - r) & lowmask(b);
+}
+
+__device__ __forceinline__ void mark_sectors(uint32_t* sect, uint32_t j, uint32_t b) {
+  const uint32_t s0 = (j * b) >> 8, s1 = ((j + 1) * b - 1) >> 8;  // 32-B sector = 256 bits
+  atomicOr(&sect[s0 >> 5], 1u << (s0 & 31));
+  if (s1 != s0) atomicOr(&sect[s1 >> 5], 1u << (s1 & 31));
+}
+
+// Sparse scan: predicate bits for the docs of `care` only, two candidates per round trip.
+__device__ __forceinline__ uint32_t scan_sparse(const DevColumn& c, const WTile& t, const Pred& p, uint32_t care,
+                                                uint32_t* sect) {
+  uint32_t m = 0, left = care;
+  const uint32_t jbase = (uint32_t)(t.lane_doc0 - t.doc0);
+  while (__ballot(left != 0)) {
+    const bool h0 = left != 0;
+    const int i0 = h0 ? __builtin_ctz(left) : 0;
+    left &= left - 1;
+    const bool h1 = left != 0;
+    const int i1 = h1 ? __builtin_ctz(left) : 0;
+    left &= left - 1;
+    uint32_t id0 = 0, id1 = 0;
+    if (h0) id0 = gather_id(c, t.lane_doc0 + i0);
+    if (h1) id1 = gather_id(c, t.lane_doc0 + i1);
+    if (h0 && eval_pred(p, id0)) m |= 1u << i0;
+    if (h1 && eval_pred(p, id1)) m |= 1u << i1;
+    if (sect) {
+      if (h0) mark_sectors(sect, jbase + i0, (uint32_t)c.bits);
+      if (h1) mark_sectors(sect, jbase + i1, (uint32_t)c.bits);
+    }
+  }
+  return m;
+}
+
+// ---- Roaring containers / sorted ranges ---------------------------------------------------------------------------
+// Bits of the wave tile covered by one Roaring bitmap (dict id `id`), for this lane's 32 docs.
+__device__ __noinline__ uint32_t bitmap_word(const DevColumn& c, const WTile& t, uint32_t id, uint32_t* lds_words) {
   const uint32_t key = (uint32_t)t.doc0 >> 16;
-  const uint32_t lo16 = (uint32_t)t.doc0 & 0xFFFFu;  // tile start within the 65536-doc chunk
+  const uint32_t lo16 = (uint32_t)t.doc0 & 0xFFFFu;  // multiple of 2048
+  const int lane = threadIdx.x & 63;
   int32_t a = (int32_t)c.inv_dir[id], z = (int32_t)c.inv_dir[id + 1] - 1;
   int32_t ci = -1;
-  while (a <= z) {  // containers are sorted by key
-    int32_t mid = (a + z) >> 1;
-    uint32_t k = c.inv_ct[mid].key;
+  while (a <= z) {
+    const int32_t mid = (a + z) >> 1;
+    const uint32_t k = c.inv_ct[mid].key;
     if (k == key) { ci = mid; break; }
     if (k < key) a = mid + 1; else z = mid - 1;
   }
-  if (ci < 0) return;
+  if (ci < 0) return 0u;
   const DevContainer ct = c.inv_ct[ci];
+  const uint32_t my0 = lo16 + 32u * lane;  // my first doc within the container
   if (ct.type == PGPU_CT_BITMAP) {
-    const uint64_t* w = (const uint64_t*)(c.inv_data + ct.offset) + (lo16 >> 6);
-    for (int g = threadIdx.x; g < NG; g += NT) {
-      uint64_t v = w[g];
-      if (v) atomicOr((unsigned long long*)&sm.masks[dst][g], (unsigned long long)v);
-    }
-  } else if (ct.type == PGPU_CT_ARRAY) {
-    const uint16_t* v = (const uint16_t*)(c.inv_data + ct.offset);
-    // first index with v >= lo16 and first with v >= lo16 + TILE
-    int32_t l = 0, h = (int32_t)ct.card;
-    while (l < h) { int32_t m = (l + h) >> 1; if (v[m] < lo16) l = m + 1; else h = m; }
-    int32_t first = l;
-    h = (int32_t)ct.card;
-    while (l < h) { int32_t m = (l + h) >> 1; if ((uint32_t)v[m] < lo16 + TILE) l = m + 1; else h = m; }
-    for (int32_t i = first + threadIdx.x; i < l; i += NT) {
-      uint32_t off = (uint32_t)v[i] - lo16;
-      atomicOr((unsigned long long*)&sm.masks[dst][off >> 6], 1ull << (off & 63));
-    }
-  } else {  // RUN: pairs (start, length-1)
+    return ((const uint32_t*)(c.inv_data + ct.offset))[my0 >> 5];
+  }
+  if (ct.type == PGPU_CT_RUN) {
     const uint16_t* r = (const uint16_t*)(c.inv_data + ct.offset);
     int32_t l = 0, h = (int32_t)ct.card;
-    // first run whose end >= lo16
-    while (l < h) {
-      int32_t m = (l + h) >> 1;
+    while (l < h) {  // first run whose end >= lo16
+      const int32_t m = (l + h) >> 1;
       if ((uint32_t)r[2 * m] + r[2 * m + 1] < lo16) l = m + 1; else h = m;
     }
-    for (int32_t i = l + threadIdx.x; i < (int32_t)ct.card; i += NT) {
-      uint32_t s = r[2 * i], e = s + r[2 * i + 1];  // inclusive
-      if (s >= lo16 + TILE) break;
-      uint32_t s2 = s < lo16 ? 0u : s - lo16;
-      uint32_t e2 = (e >= lo16 + TILE ? lo16 + TILE - 1 : e) - lo16;
-      for (uint32_t w = s2 >> 6; w <= (e2 >> 6); ++w) {
-        uint32_t bs = w == (s2 >> 6) ? (s2 & 63) : 0u;
-        uint32_t be = w == (e2 >> 6) ? (e2 & 63) : 63u;
-        uint64_t mk = (~0ull >> (63 - be)) & (~0ull << bs);
-        atomicOr((unsigned long long*)&sm.masks[dst][w], (unsigned long long)mk);
+    uint32_t w = 0;
+    for (int32_t i = l; i < (int32_t)ct.card; ++i) {  // uniform loop over the runs overlapping the tile
+      const uint32_t s = r[2 * i], e = s + r[2 * i + 1];
+      if (s >= lo16 + WT) break;
+      if (e >= my0 && s <= my0 + 31) {
+        const uint32_t bs = s > my0 ? s - my0 : 0u, be = e < my0 + 31 ? e - my0 : 31u;
+        w |= (0xFFFFFFFFu >> (31 - be)) & (0xFFFFFFFFu << bs);
       }
     }
+    return w;
   }
+  // ARRAY: values in [lo16, lo16 + WT) scattered to their owner lanes through LDS
+  const uint16_t* v = (const uint16_t*)(c.inv_data + ct.offset);
+  int32_t l = 0, h = (int32_t)ct.card;
+  while (l < h) { const int32_t m = (l + h) >> 1; if (v[m] < lo16) l = m + 1; else h = m; }
+  const int32_t first = l;
+  h = (int32_t)ct.card;
+  while (l < h) { const int32_t m = (l + h) >> 1; if ((uint32_t)v[m] < lo16 + WT) l = m + 1; else h = m; }
+  lds_words[lane] = 0u;
+  wave_sync();
+  for (int32_t i = first + lane; i < l; i += 64) {
+    const uint32_t off = (uint32_t)v[i] - lo16;
+    atomicOr(&lds_words[off >> 5], 1u << (off & 31));
+  }
+  wave_sync();
+  const uint32_t w = lds_words[lane];
+  wave_sync();
+  return w;
 }
 
-// Compact the docs of `mask` (tile-relative) into sm.list (ascending); zeroes mask slot `zero_slot` on the way
-// (>= 0).  Returns the count.  Contains two __syncthreads().
-__device__ __forceinline__ int compact_mask(Smem& sm, const uint64_t* mask, int zero_slot) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x < 64) {
-    const int g = threadIdx.x;
-    const int c = __popcll(mask[g]);
-    int x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    sm.goff[g] = x - c;
-    if (g == 63) sm.goff[NG] = x;
-  }
-  __syncthreads();
-  for (int g = wave; g < NG; g += NW) {
-    const uint64_t m = mask[g];
-    if ((m >> lane) & 1ull) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      sm.list[sm.goff[g] + below] = (uint16_t)(g * 64 + lane);
+__device__ __noinline__ uint32_t sorted_ranges_word(const int32_t* rg, int n, const WTile& t) {
+  const int32_t d0 = t.lane_doc0, d1 = d0 + 31;
+  const int32_t w0 = t.doc0, w1 = t.doc0 + WT - 1;
+  int32_t l = 0, h = n;
+  while (l < h) { const int32_t m = (l + h) >> 1; if (rg[2 * m + 1] < w0) l = m + 1; else h = m; }
+  uint32_t w = 0;
+  for (int32_t i = l; i < n; ++i) {  // uniform over the ranges overlapping the wave tile
+    const int32_t s = rg[2 * i], e = rg[2 * i + 1];
+    if (s > w1) break;
+    if (e >= d0 && s <= d1) {
+      const int32_t bs = s > d0 ? s - d0 : 0, be = e < d1 ? e - d0 : 31;
+      w |= (0xFFFFFFFFu >> (31 - be)) & (0xFFFFFFFFu << bs);
     }
   }
-  if (zero_slot >= 0 && threadIdx.x < 64) sm.masks[zero_slot][threadIdx.x] = 0ull;
-  __syncthreads();
-  return sm.goff[NG];
+  return w;
 }
 
-// ---- filter program ------------------------------------------------------------------------------------------
-// Returns with the final match mask in sm.masks[0] (or sm.valid when the program is empty) -> *final_slot.
-__device__ int run_filter(Smem& sm, const DevParams& p, const TileCtx& t, const DevColumn* cols,
-                          int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes) {
-  const DevSeg& s = *t.seg;
-  if (s.prog_len == 0) return -1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int pc = 0;
-  while (pc < s.prog_len) {
-    const DevInstr in = p.instrs[s.prog_begin + pc];
-    int next = pc + 1;
-    switch (in.op) {
-      case PGPU_I_ALL:
-      case PGPU_I_EMPTY:
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] = in.op == PGPU_I_ALL ? sm.valid[threadIdx.x] : 0ull;
-        __syncthreads();
-        break;
-      case PGPU_I_SCAN: {
-        const DevColumn& c = cols[in.col];
-        const uint64_t* care = care_mask(sm, in.care);
-        const int ncare = care_count(sm, in.care);
-        const uint32_t b = (uint32_t)c.bits;
-        const bool prestaged = pc == s.pf_pc;
-        const bool dense = prestaged || (c.kind == PGPU_COL_FIXED_BIT && ncare * 32 >= t.ndocs);
-        if (dense) {
-          if (!prestaged) {
-            stage_column(sm, c.fwd, t.tile_in_seg, b);
-            __syncthreads();
-          }
-          if (threadIdx.x == 0) {
-            scanned += t.ndocs;
-            dense_bytes += ((int64_t)t.ndocs * b + 7) / 8;
-          }
-          for (int g = wave; g < NG; g += NW) {
-            const int j = g * 64 + lane;
-            bool m = false;
-            if (j < t.ndocs) {
-              uint32_t id = extract_lds(sm.stage + 4, (uint32_t)(j + 1) * b, b);
-              m = eval_pred(in, p.pool, id);
-            }
-            uint64_t bal = __ballot(m);
-            if (lane == 0) sm.masks[in.dst][g] = bal;
-          }
-        } else {
-          const bool stats = (p.flags & PGPU_FLAG_STATS) && c.kind == PGPU_COL_FIXED_BIT;
-          if (stats) {
-            for (int i = threadIdx.x; i < (int)(sizeof(sm.sectors) / 4); i += NT) sm.sectors[i] = 0;
-            __syncthreads();
-          }
-          if (threadIdx.x == 0) scanned += ncare;
-          // Compact the care docs (fewer than ndocs/32 <= 128 here) into sm.list, then one thread per candidate
-          // fetches its two words: a single memory round trip for the whole tile, no per-group serialisation.
-          const int nc = compact_mask(sm, care, in.dst);
-          for (int k = threadIdx.x; k < nc; k += NT) {
-            const int j = sm.list[k];
-            const uint32_t id = get_id(sm, c, t, j, false);
-            if (eval_pred(in, p.pool, id))
-              atomicOr((unsigned long long*)&sm.masks[in.dst][j >> 6], 1ull << (j & 63));
-            if (stats) mark_sectors(sm, j, b);
-          }
-          if (stats) {
-            __syncthreads();
-            if (threadIdx.x < 64) {
-              int cnt = 0;
-              for (int i = threadIdx.x; i < (int)(sizeof(sm.sectors) / 4); i += 64) cnt += __popc(sm.sectors[i]);
-              cnt = wave_sum_i32(cnt);
-              if (threadIdx.x == 0) sector_bytes += 32ll * cnt;
-            }
-          }
-        }
-        __syncthreads();
-        break;
-      }
-      case PGPU_I_INV: {
-        const DevColumn& c = cols[in.col];
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] = 0ull;
-        __syncthreads();
-        for (int i = 0; i < in.n; ++i) or_bitmap(sm, c, t, (uint32_t)p.pool[in.pool_off + i], in.dst);
-        __syncthreads();
-        if (in.negate) {
-          if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] = ~sm.masks[in.dst][threadIdx.x] & sm.valid[threadIdx.x];
-          __syncthreads();
-        }
-        break;
-      }
-      case PGPU_I_SORTED: {
-        if (threadIdx.x < 64) {
-          const int g = threadIdx.x;
-          const int32_t d0 = t.doc0 + g * 64, d1 = d0 + 63;
-          const int32_t* rg = p.pool + in.pool_off;
-          // first range whose end >= d0
-          int32_t l = 0, h = in.n;
-          while (l < h) { int32_t m = (l + h) >> 1; if (rg[2 * m + 1] < d0) l = m + 1; else h = m; }
-          uint64_t mk = 0;
-          for (int32_t i = l; i < in.n; ++i) {
-            int32_t s0 = rg[2 * i], e0 = rg[2 * i + 1];
-            if (s0 > d1) break;
-            int32_t bs = s0 < d0 ? 0 : s0 - d0;
-            int32_t be = e0 > d1 ? 63 : e0 - d0;
-            mk |= (~0ull >> (63 - be)) & (~0ull << bs);
-          }
-          if (in.negate) mk = ~mk;
-          sm.masks[in.dst][g] = mk & sm.valid[g];
-        }
-        __syncthreads();
-        break;
-      }
-      case PGPU_I_AND_BEGIN:
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] = care_mask(sm, in.care)[threadIdx.x];
-        if (threadIdx.x == 0) sm.slot_count[in.dst] = care_count(sm, in.care);
-        __syncthreads();
-        break;
-      case PGPU_I_AND_CHILD:
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] &= sm.masks[in.src][threadIdx.x];
-        count_slot(sm, in.dst);
-        __syncthreads();
-        if (sm.slot_count[in.dst] == 0) next = in.jump;
-        break;
-      case PGPU_I_OR_BEGIN:
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] = 0ull;
-        __syncthreads();
-        break;
-      case PGPU_I_OR_CHILD:
-        if (threadIdx.x < 64) sm.masks[in.dst][threadIdx.x] |= sm.masks[in.src][threadIdx.x];
-        __syncthreads();
-        break;
-      case PGPU_I_NOT:
-        if (threadIdx.x < 64)
-          sm.masks[in.dst][threadIdx.x] = ~sm.masks[in.src][threadIdx.x] & care_mask(sm, in.care)[threadIdx.x];
-        __syncthreads();
-        break;
-      default:  // AND_END / OR_END: result already in dst
-        break;
-    }
-    pc = next;
-  }
-  return 0;
-}
-
-// ---- register prefetch of the driving scan column -------------------------------------------------------------
-// The first SCAN of a segment's program (under AND_BEGINs only) is evaluated densely on every tile; its bytes
-// for the NEXT tile are loaded into registers while the current tile runs, then written to LDS at the top of
-// the next iteration, so the workgroup's dominant stream is always in flight (T14-style issue-early/write-late).
-#define PF_REGS 4  // ceil(32 * 32 / NT) 16-B chunks per thread for b <= 32
-
+// ---- driving-column prefetch (LDS DMA one wave tile ahead) ---------------------------------------------------------
 __device__ __forceinline__ int seg_of_tile(const DevParams& p, int tile) {
   int lo = 0, hi = p.nseg - 1;
   while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
+    const int mid = (lo + hi + 1) >> 1;
     if (p.segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
   }
   return lo;
 }
 
-__device__ __forceinline__ int prefetch_regs(const DevParams& p, int tile, u32x4 (&pf)[PF_REGS]) {
-  if (tile >= p.total_tiles) return 0;
+// Issue global_load_lds (16 B per lane, 1 KiB per instruction) of the driving column of wave tile `tile` into
+// `buf`; returns false when that tile's segment has no driving column.  The caller has finished reading `buf`.
+__device__ __forceinline__ bool prefetch_tile(const DevParams& p, int tile, uint32_t* buf) {
+  if (tile >= p.total_tiles) return false;
   const DevSeg& sg = p.segs[seg_of_tile(p, tile)];
-  if (sg.pf_pc < 0) return 0;
+  if (sg.pf_pc < 0) return false;
   const DevInstr& in = p.instrs[sg.prog_begin + sg.pf_pc];
   const DevColumn& c = p.cols[sg.col_begin + in.col];
   const int b = c.bits;
-  const u32x4* src = (const u32x4*)(c.fwd + (size_t)(tile - sg.tile_begin) * (TILE / 32) * b);
-  const int n16 = (TILE / 128) * b;
-#pragma unroll
-  for (int k = 0; k < PF_REGS; ++k) {
-    const int i = threadIdx.x + k * NT;
-    if (i < n16) pf[k] = src[i];
-  }
-  return b;
-}
-
-__device__ __forceinline__ void write_prefetched(Smem& sm, const u32x4 (&pf)[PF_REGS], int b) {
-  const int n16 = (TILE / 128) * b;
-  u32x4* dst = (u32x4*)(sm.stage + 4);
-#pragma unroll
-  for (int k = 0; k < PF_REGS; ++k) {
-    const int i = threadIdx.x + k * NT;
-    if (i < n16) {
-      u32x4 v = pf[k];
-      v.x = bswap32(v.x); v.y = bswap32(v.y); v.z = bswap32(v.z); v.w = bswap32(v.w);
-      dst[i] = v;
+  const char* src = (const char*)(c.fwd + (size_t)(tile - sg.tile_begin) * 64 * b);
+  const int lane = threadIdx.x & 63;
+  const int chunks = (b + 3) >> 2;  // 1 KiB chunks of the 256*b-byte wave tile (last one may be partial)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of buf are complete (WAR)
+  for (int k = 0; k < chunks; ++k) {
+    const int byte = k * 1024 + lane * 16;
+    if (byte < 256 * b) {
+      __builtin_amdgcn_global_load_lds((const void*)(src + byte),
+                                       (__attribute__((address_space(3))) void*)(buf + k * 256), 16, 0, 0);
     }
   }
+  return true;
 }
 
-// ---- the query kernel ----------------------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(NT) void query_kernel(DevParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
-  __shared__ Smem sm;
-  uint32_t* keys = (uint32_t*)dyn_smem;                 // MODE != AGG: group key per compacted entry
-  int64_t* ltab = (int64_t*)(dyn_smem + TILE * 4);      // MODE == LDS: [nsec][G]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---- filter program ------------------------------------------------------------------------------------------------
+// Returns this lane's match word for the wave tile.  The driving column (instruction pf_pc) of this tile is in
+// cv.pf; once it is decoded the DMA of the next tile (`next_tile`) is issued into the same buffer (*pf_issued).
+__device__ __forceinline__ uint32_t run_filter(const DevParams& p, const Carve& cv, const WTile& t, int next_tile,
+                                               bool* pf_issued, uint32_t* scratch_words, int64_t& scanned,
+                                               int64_t& sector_bytes, int64_t& dense_bytes) {
+  const DevSeg& s = *t.seg;
+  if (s.prog_len == 0) return t.valid;
+  const bool stats = p.flags & PGPU_FLAG_STATS;
+  const int lane = threadIdx.x & 63;
+  int pc = 0;
+  while (pc < s.prog_len) {
+    const DevInstr in = p.instrs[s.prog_begin + pc];
+    int next = pc + 1;
+    const uint32_t care = in.care < 0 ? t.valid : slot(cv, in.care);
+    switch (in.op) {
+      case PGPU_I_ALL: slot(cv, in.dst) = t.valid; break;
+      case PGPU_I_EMPTY: slot(cv, in.dst) = 0u; break;
+      case PGPU_I_SCAN: {
+        const DevColumn& c = t.cols[in.col];
+        const Pred pr = make_pred(in, p.pool);
+        const bool prestaged = pc == s.pf_pc;
+        int ncare = 0;
+        if (!prestaged) ncare = wave_sum_i32(__popc(care));
+        const bool dense = prestaged || (c.kind == PGPU_COL_FIXED_BIT && ncare * 32 >= t.ndocs);
+        uint32_t m;
+        if (dense) {
+          uint32_t ids[32];
+          if (prestaged) {
+            decode_lds(c.bits, cv.pf, ids);
+            *pf_issued = true;
+            cv.pf_have[0] = prefetch_tile(p, next_tile, cv.pf);
+          } else {
+            decode_hbm(c, t.tile_in_seg, ids);
+          }
+          m = pred_ids(ids, pr) & t.valid;
+          if (lane == 0) {
+            scanned += t.ndocs;
+            dense_bytes += ((int64_t)t.ndocs * c.bits + 7) / 8;
+          }
+        } else {
+          uint32_t* sect = nullptr;
+          if (stats && c.kind == PGPU_COL_FIXED_BIT) {
+            sect = scratch_words;
+            scratch_words[lane] = 0u;  // 64 words = 2048 sectors >= 2048 docs * 31 bits / 256
+            wave_sync();
+          }
+          m = scan_sparse(c, t, pr, care, sect);
+          if (sect) {
+            wave_sync();
+            const int cnt = wave_sum_i32(__popc(scratch_words[lane]));
+            if (lane == 0) sector_bytes += 32ll * cnt;
+            wave_sync();
+          }
+          if (lane == 0) scanned += ncare;
+        }
+        slot(cv, in.dst) = m & care;
+        break;
+      }
+      case PGPU_I_INV: {
+        const DevColumn& c = t.cols[in.col];
+        uint32_t m = 0;
+        for (int i = 0; i < in.n; ++i) m |= bitmap_word(c, t, (uint32_t)p.pool[in.pool_off + i], scratch_words);
+        if (in.negate) m = ~m;
+        slot(cv, in.dst) = m & t.valid;
+        break;
+      }
+      case PGPU_I_SORTED: {
+        uint32_t m = sorted_ranges_word(p.pool + in.pool_off, in.n, t);
+        if (in.negate) m = ~m;
+        slot(cv, in.dst) = m & t.valid;
+        break;
+      }
+      case PGPU_I_AND_BEGIN: slot(cv, in.dst) = care; break;
+      case PGPU_I_AND_CHILD: {
+        const uint32_t a = slot(cv, in.dst) & slot(cv, in.src);
+        slot(cv, in.dst) = a;
+        if (!__ballot(a != 0u)) next = in.jump;
+        break;
+      }
+      case PGPU_I_OR_BEGIN: slot(cv, in.dst) = 0u; break;
+      case PGPU_I_OR_CHILD: slot(cv, in.dst) |= slot(cv, in.src); break;
+      case PGPU_I_NOT: slot(cv, in.dst) = ~slot(cv, in.src) & care; break;
+      default: break;  // AND_END / OR_END
+    }
+    pc = next;
+  }
+  return slot(cv, 0);
+}
 
+// ---- aggregation ---------------------------------------------------------------------------------------------------
+struct Acc {
+  int64_t i;
+  double d;
+};
+
+__device__ __forceinline__ void acc_add(Acc& a, const DevAgg& ag, const DevColumn& c, uint32_t id) {
+  if (ag.op == PGPU_RED_SUM_I64) a.i += value_i64(c.dict, ag.vtype, id);
+  else if (ag.op == PGPU_RED_SUM_F64) a.d += value_f64(c.dict, ag.vtype, id);
+  else {
+    const int64_t k = minmax_key(c.dict, ag.vtype, id);
+    a.i = ag.op == PGPU_RED_MIN_I64 ? (k < a.i ? k : a.i) : (k > a.i ? k : a.i);
+  }
+}
+
+// table update for one doc: `tab` = LDS or HBM dense table, section-major
+__device__ __forceinline__ void table_update(int64_t* tab, uint64_t G, const DevAgg& ag, const DevColumn& c,
+                                             uint32_t key, uint32_t id) {
+  int64_t* cell = tab + (size_t)ag.sec * G + key;
+  if (ag.op == PGPU_RED_SUM_I64) atomicAdd((unsigned long long*)cell, (unsigned long long)value_i64(c.dict, ag.vtype, id));
+  else if (ag.op == PGPU_RED_SUM_F64) atomicAdd((double*)cell, value_f64(c.dict, ag.vtype, id));
+  else if (ag.op == PGPU_RED_MIN_I64) atomicMin((long long*)cell, (long long)minmax_key(c.dict, ag.vtype, id));
+  else atomicMax((long long*)cell, (long long)minmax_key(c.dict, ag.vtype, id));
+}
+
+// ---- the query kernel ----------------------------------------------------------------------------------------------
+template <int MODE>
+// amdgpu_waves_per_eu(4): 128 VGPRs -> 4 waves per SIMD (16 per CU) to keep enough sparse gathers in flight
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void query_kernel(DevParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  // the wave index through readfirstlane: everything derived from it (tile, segment, program, columns, bit
+  // widths) is then provably wave-uniform and lives in SGPRs, and the bit-width switch is a scalar branch
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Carve cv;
+  {
+    unsigned char* base = dyn_smem;
+    cv.slots = (uint32_t*)base + wave * MAXS * 64;
+    base += NW * MAXS * 64 * 4;
+    cv.pf_words = p.pf_words;
+    cv.pf = (uint32_t*)base + wave * (size_t)p.pf_words;
+    base += NW * (size_t)p.pf_words * 4;
+    cv.accw = (int64_t*)base + wave * PGPU_MAX_AGGS;
+    base += NW * PGPU_MAX_AGGS * 8;
+    cv.ltab = (int64_t*)base;
+  }
+  uint32_t* scratch = cv.slots + (MAXS - 1) * 64;  // the last slot row doubles as per-wave LDS scratch
   if (MODE == PGPU_MODE_LDS) {
     const int n = p.nsec * (int)p.G;
-    for (int i = threadIdx.x; i < n; i += NT) ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+    for (int i = threadIdx.x; i < n; i += NT) cv.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
   }
-  if (MODE == PGPU_MODE_AGG) {
-    for (int i = threadIdx.x; i < NW * PGPU_MAX_AGGS; i += NT) {
-      int a = i % PGPU_MAX_AGGS;
-      sm.accw[i / PGPU_MAX_AGGS][a] = a < p.nagg ? sec_identity(p.aggs[a].op) : 0;
-    }
-  }
-  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;  // thread 0 owns these
-  u32x4 pf[PF_REGS];
-  int pf_bits = prefetch_regs(p, blockIdx.x, pf);
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.accw[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
   __syncthreads();
 
-  for (int tile = blockIdx.x; tile < p.total_tiles; tile += gridDim.x) {
-    TileCtx t;
-    t.seg = &p.segs[seg_of_tile(p, tile)];
-    if (pf_bits) write_prefetched(sm, pf, pf_bits);   // this tile's driving column -> LDS
-    pf_bits = prefetch_regs(p, tile + gridDim.x, pf);  // next tile's bytes stay in flight during this tile
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;  // lane 0 of each wave owns these
+  const int gw = blockIdx.x * NW + wave, nwaves = gridDim.x * NW;
+  bool have[1];
+  cv.pf_have = have;
+  have[0] = prefetch_tile(p, gw, cv.pf);
+  for (int tile = gw; tile < p.total_tiles; tile += nwaves) {
+    const int sidx = seg_of_tile(p, tile);
+    WTile t;
+    t.seg = &p.segs[sidx];
+    t.cols = p.cols + t.seg->col_begin;
     t.tile_in_seg = tile - t.seg->tile_begin;
-    t.doc0 = t.tile_in_seg * TILE;
-    t.ndocs = min(TILE, t.seg->num_docs - t.doc0);
-    const DevColumn* cols = p.cols + t.seg->col_begin;
-
-    if (threadIdx.x < 64) {
-      const int g = threadIdx.x;
-      const int rem = t.ndocs - g * 64;
-      sm.valid[g] = rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : (~0ull >> (64 - rem)));
+    t.doc0 = t.tile_in_seg * WT;
+    t.ndocs = min(WT, t.seg->num_docs - t.doc0);
+    t.lane_doc0 = t.doc0 + 32 * lane;
+    {
+      const int rem = t.ndocs - 32 * lane;
+      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
     }
-    if (threadIdx.x == 0) sm.nvalid = t.ndocs;
-    __syncthreads();
-
-    const int fslot = run_filter(sm, p, t, cols, scanned, sector_bytes, dense_bytes);
-    const uint64_t* fmask = fslot < 0 ? sm.valid : sm.masks[0];
-
-    // compaction of matching docs -> sm.list (final masks never exceed the valid docs)
-    const int nm = compact_mask(sm, fmask, -1);
-    if (threadIdx.x == 0) matched += nm;
+    // this tile's driving column has landed in cv.pf (issued one tile ago)
+    if (have[0]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    bool issued = false;
+    const uint32_t mm = run_filter(p, cv, t, tile + nwaves, &issued, scratch, scanned, sector_bytes, dense_bytes);
+    if (!issued) have[0] = prefetch_tile(p, tile + nwaves, cv.pf);
+    const int nm = wave_sum_i32(__popc(mm));
+    if (lane == 0) matched += nm;
     if (nm == 0) continue;  // uniform
     const bool dense_post = nm * 32 >= t.ndocs;
 
-    // group keys
-    if (MODE != PGPU_MODE_AGG) {
-      for (int gc = 0; gc < p.ngcols; ++gc) {
-        const DevColumn& c = cols[p.gcols[gc]];
-        const int32_t* remap = p.remaps[t.seg->remap_begin + gc];
-        const bool staged = dense_post && c.kind == PGPU_COL_FIXED_BIT;
-        if (staged) {
-          stage_column(sm, c.fwd, t.tile_in_seg, (uint32_t)c.bits);
-          __syncthreads();
-          if (threadIdx.x == 0) dense_bytes += ((int64_t)t.ndocs * c.bits + 7) / 8;
+    if (MODE == PGPU_MODE_AGG) {
+      for (int a = 0; a < p.nagg; ++a) {
+        const DevAgg ag = p.aggs[a];
+        if (ag.fn == PGPU_AGG_COUNT) continue;
+        const DevColumn& c = t.cols[ag.col];
+        Acc acc;
+        acc.i = sec_identity(ag.op);
+        acc.d = 0.0;
+        if (dense_post && c.kind == PGPU_COL_FIXED_BIT) {
+          uint32_t ids[32];
+          decode_hbm(c, t.tile_in_seg, ids);
+#pragma unroll
+          for (int i = 0; i < 32; ++i)
+            if (lane_bit(mm, i)) acc_add(acc, ag, c, ids[i]);
+        } else {
+          for (uint32_t left = mm; left; left &= left - 1)
+            acc_add(acc, ag, c, gather_id(c, t.lane_doc0 + __builtin_ctz(left)));
         }
-        const uint32_t stride = p.gstride[gc];
-        for (int k = threadIdx.x; k < nm; k += NT) {
-          uint32_t id = get_id(sm, c, t, sm.list[k], staged);
-          uint32_t gid = remap ? (uint32_t)remap[id] : id;
-          keys[k] = (gc == 0 ? 0u : keys[k]) + gid * stride;
+        if (ag.op == PGPU_RED_SUM_I64) acc.i = wave_sum_i64(acc.i);
+        else if (ag.op == PGPU_RED_SUM_F64) acc.d = wave_sum_f64(acc.d);
+        else if (ag.op == PGPU_RED_MIN_I64) acc.i = wave_min_i64(acc.i);
+        else acc.i = wave_max_i64(acc.i);
+        if (lane == 0) {
+          int64_t& cell = cv.accw[a];
+          if (ag.op == PGPU_RED_SUM_I64) cell += acc.i;
+          else if (ag.op == PGPU_RED_SUM_F64) cell = __double_as_longlong(__longlong_as_double(cell) + acc.d);
+          else if (ag.op == PGPU_RED_MIN_I64) cell = acc.i < cell ? acc.i : cell;
+          else cell = acc.i > cell ? acc.i : cell;
         }
-        __syncthreads();
       }
-      // COUNT section (section 0)
-      for (int k = threadIdx.x; k < nm; k += NT) {
-        const uint32_t key = keys[k];
-        if (MODE == PGPU_MODE_LDS) atomicAdd((unsigned long long*)&ltab[key], 1ull);
-        else atomicAdd((unsigned long long*)&p.table[key], 1ull);
-      }
-    }
-
-    // aggregations
-    int staged_col = -1;
-    for (int a = 0; a < p.nagg; ++a) {
-      const DevAgg ag = p.aggs[a];
-      if (ag.fn == PGPU_AGG_COUNT) continue;
-      const DevColumn& c = cols[ag.col];
-      const bool staged = dense_post && c.kind == PGPU_COL_FIXED_BIT;
-      if (staged && staged_col != ag.col) {
-        __syncthreads();
-        stage_column(sm, c.fwd, t.tile_in_seg, (uint32_t)c.bits);
-        __syncthreads();
-        staged_col = ag.col;
-        if (threadIdx.x == 0) dense_bytes += ((int64_t)t.ndocs * c.bits + 7) / 8;
-      }
-      if (MODE == PGPU_MODE_AGG) {
-        int64_t acc = sec_identity(ag.op);
-        double dacc = 0.0;
-        for (int k = threadIdx.x; k < nm; k += NT) {
-          uint32_t id = get_id(sm, c, t, sm.list[k], staged);
-          if (ag.op == PGPU_RED_SUM_I64) acc += value_i64(c.dict, ag.vtype, id);
-          else if (ag.op == PGPU_RED_SUM_F64) dacc += value_f64(c.dict, ag.vtype, id);
-          else {
-            int64_t kk = minmax_key(c.dict, ag.vtype, id);
-            acc = ag.op == PGPU_RED_MIN_I64 ? (kk < acc ? kk : acc) : (kk > acc ? kk : acc);
+    } else {
+      int64_t* tab = MODE == PGPU_MODE_LDS ? cv.ltab : p.table;
+      bool all_fixed = true;
+      for (int gc = 0; gc < p.ngcols; ++gc) all_fixed &= t.cols[p.gcols[gc]].kind == PGPU_COL_FIXED_BIT;
+      for (int a = 0; a < p.nagg; ++a)
+        if (p.aggs[a].fn != PGPU_AGG_COUNT) all_fixed &= t.cols[p.aggs[a].col].kind == PGPU_COL_FIXED_BIT;
+      if (dense_post && all_fixed) {
+        // one pass over [group columns..., aggregations...]: a single decode site for all of them
+        uint32_t key[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) key[i] = 0u;
+        const int nops = p.ngcols + (p.nagg > 0 ? p.nagg : 1);
+        for (int op = 0; op < nops; ++op) {
+          if (op == p.ngcols) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+              if (lane_bit(mm, i)) atomicAdd((unsigned long long*)&tab[key[i]], 1ull);
+          }
+          const bool is_key = op < p.ngcols;
+          DevAgg ag;
+          int col;
+          if (is_key) {
+            col = p.gcols[op];
+          } else {
+            if (op - p.ngcols >= p.nagg) break;
+            ag = p.aggs[op - p.ngcols];
+            if (ag.fn == PGPU_AGG_COUNT) continue;
+            col = ag.col;
+          }
+          const DevColumn& c = t.cols[col];
+          uint32_t ids[32];
+          decode_hbm(c, t.tile_in_seg, ids);
+          if (is_key) {
+            const int32_t* remap = p.remaps[t.seg->remap_begin + op];
+            const uint32_t stride = p.gstride[op];
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+              if (lane_bit(mm, i)) key[i] += (remap ? (uint32_t)gld(remap, ids[i]) : ids[i]) * stride;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+              if (lane_bit(mm, i)) table_update(tab, p.G, ag, c, key[i], ids[i]);
           }
         }
-        if (ag.op == PGPU_RED_SUM_I64) acc = wave_sum_i64(acc);
-        else if (ag.op == PGPU_RED_SUM_F64) dacc = wave_sum_f64(dacc);
-        else if (ag.op == PGPU_RED_MIN_I64) acc = wave_min_i64(acc);
-        else acc = wave_max_i64(acc);
-        if (lane == 0) {
-          int64_t& cell = sm.accw[wave][a];
-          if (ag.op == PGPU_RED_SUM_I64) cell += acc;
-          else if (ag.op == PGPU_RED_SUM_F64) cell = __double_as_longlong(__longlong_as_double(cell) + dacc);
-          else if (ag.op == PGPU_RED_MIN_I64) cell = acc < cell ? acc : cell;
-          else cell = acc > cell ? acc : cell;
-        }
       } else {
-        int64_t* secp = (MODE == PGPU_MODE_LDS ? ltab : p.table) + (size_t)ag.sec * p.G;
-        for (int k = threadIdx.x; k < nm; k += NT) {
-          uint32_t id = get_id(sm, c, t, sm.list[k], staged);
-          const uint32_t key = keys[k];
-          if (ag.op == PGPU_RED_SUM_I64)
-            atomicAdd((unsigned long long*)&secp[key], (unsigned long long)value_i64(c.dict, ag.vtype, id));
-          else if (ag.op == PGPU_RED_SUM_F64)
-            atomicAdd((double*)&secp[key], value_f64(c.dict, ag.vtype, id));
-          else if (ag.op == PGPU_RED_MIN_I64)
-            atomicMin((long long*)&secp[key], (long long)minmax_key(c.dict, ag.vtype, id));
-          else
-            atomicMax((long long*)&secp[key], (long long)minmax_key(c.dict, ag.vtype, id));
+        for (uint32_t left = mm; __ballot(left != 0); left &= left - 1) {
+          if (!left) continue;
+          const int32_t d = t.lane_doc0 + __builtin_ctz(left);
+          uint32_t key = 0;
+          for (int gc = 0; gc < p.ngcols; ++gc) {
+            const DevColumn& c = t.cols[p.gcols[gc]];
+            const int32_t* remap = p.remaps[t.seg->remap_begin + gc];
+            const uint32_t id = gather_id(c, d);
+            key += (remap ? (uint32_t)gld(remap, id) : id) * p.gstride[gc];
+          }
+          atomicAdd((unsigned long long*)&tab[key], 1ull);
+          for (int a = 0; a < p.nagg; ++a) {
+            const DevAgg ag = p.aggs[a];
+            if (ag.fn == PGPU_AGG_COUNT) continue;
+            const DevColumn& c = t.cols[ag.col];
+            table_update(tab, p.G, ag, c, key, gather_id(c, d));
+          }
         }
       }
     }
-    __syncthreads();
   }
+  if (have[0]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- block epilogue ----
-  __syncthreads();
+  // ---- epilogue ----
+  if (lane == 0) {
+    int64_t* st = p.stats + (size_t)(blockIdx.x * NW + wave) * PGPU_NSTATS;
+    st[PGPU_STAT_MATCHED] = matched;
+    st[PGPU_STAT_SCANNED] = scanned;
+    st[PGPU_STAT_SECTOR_BYTES] = sector_bytes;
+    st[PGPU_STAT_DENSE_BYTES] = dense_bytes;
+  }
   if (MODE == PGPU_MODE_AGG) {
-    // slab[block][sec]: section 0 = matched count
-    int64_t* slab = p.slab + (size_t)blockIdx.x * p.nsec;
-    if (threadIdx.x == 0) slab[0] = matched;
-    if (threadIdx.x < p.nagg) {
-      const int a = threadIdx.x;
-      const DevAgg ag = p.aggs[a];
-      if (ag.fn != PGPU_AGG_COUNT) {
-        int64_t v = sm.accw[0][a];
-        for (int w = 1; w < NW; ++w) {
-          const int64_t x = sm.accw[w][a];
-          if (ag.op == PGPU_RED_SUM_I64) v += x;
-          else if (ag.op == PGPU_RED_SUM_F64) v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x));
-          else if (ag.op == PGPU_RED_MIN_I64) v = x < v ? x : v;
-          else v = x > v ? x : v;
-        }
-        slab[ag.sec] = v;
-      }
-    }
+    // slab[wave][sec]: section 0 = matched count; reduced in wave order by finalize_kernel (deterministic)
+    int64_t* slab = p.slab + (size_t)(blockIdx.x * NW + wave) * p.nsec;
+    if (lane == 0) slab[0] = matched;
+    if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) slab[p.aggs[lane].sec] = cv.accw[lane];
   } else if (MODE == PGPU_MODE_LDS) {
+    __syncthreads();
     const int G = (int)p.G;
     for (int key = threadIdx.x; key < G; key += NT) {
-      const int64_t cnt = ltab[key];
+      const int64_t cnt = cv.ltab[key];
       if (cnt == 0) continue;
       atomicAdd((unsigned long long*)&p.table[key], (unsigned long long)cnt);
       for (int s = 1; s < p.nsec; ++s) {
-        const int64_t v = ltab[s * G + key];
+        const int64_t v = cv.ltab[s * G + key];
         int64_t* dst = &p.table[(size_t)s * p.G + key];
         switch (p.sec_op[s]) {
           case PGPU_RED_SUM_I64: atomicAdd((unsigned long long*)dst, (unsigned long long)v); break;
@@ -642,13 +753,6 @@ __global__ __launch_bounds__(NT) void query_kernel(DevParams p) {
       }
     }
   }
-  if (threadIdx.x == 0) {
-    int64_t* st = p.stats + (size_t)blockIdx.x * PGPU_NSTATS;
-    st[PGPU_STAT_MATCHED] = matched;
-    st[PGPU_STAT_SCANNED] = scanned;
-    st[PGPU_STAT_SECTOR_BYTES] = sector_bytes;
-    st[PGPU_STAT_DENSE_BYTES] = dense_bytes;
-  }
 }
 
 // Table init: count/sum sections 0, MIN +max, MAX -max.
@@ -658,29 +762,45 @@ __global__ void table_init_kernel(int64_t* table, uint64_t G, int32_t nsec, DevP
     table[i] = sec_identity(p.sec_op[i / G]);
 }
 
-// Reduce AGG-mode slabs (in block order: deterministic) into the G=1 table; reduce stats.
-__global__ void finalize_kernel(DevParams p, int32_t nblocks, int64_t* stats_out) {
-  const int s = threadIdx.x;
-  if (p.mode == PGPU_MODE_AGG && s < p.nsec) {
-    const int op = p.sec_op[s];
-    int64_t v = sec_identity(op);
-    for (int b = 0; b < nblocks; ++b) {
-      const int64_t x = p.slab[(size_t)b * p.nsec + s];
-      if (op == PGPU_RED_SUM_I64) v += x;
-      else if (op == PGPU_RED_SUM_F64) v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x));
-      else if (op == PGPU_RED_MIN_I64) v = x < v ? x : v;
-      else v = x > v ? x : v;
-    }
-    p.table[s] = v;
+// Reduce AGG-mode slabs into the G=1 table and the per-wave stats: block x reduces column x (a section, then the
+// PGPU_NSTATS stats) over all waves with a fixed-shape tree, so double sums are deterministic.
+__global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nslabs, int64_t* stats_out) {
+  __shared__ int64_t red[256];
+  const int col = blockIdx.x;
+  const bool is_stat = col >= p.nsec;
+  if (!is_stat && p.mode != PGPU_MODE_AGG) return;
+  const int op = is_stat ? PGPU_RED_SUM_I64 : p.sec_op[col];
+  const int64_t* src = is_stat ? p.stats + (col - p.nsec) : p.slab + col;
+  const int stride = is_stat ? PGPU_NSTATS : p.nsec;
+  int64_t v = sec_identity(op);
+  for (int b = threadIdx.x; b < nslabs; b += 256) {
+    const int64_t x = src[(size_t)b * stride];
+    if (op == PGPU_RED_SUM_I64) v += x;
+    else if (op == PGPU_RED_SUM_F64) v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x));
+    else if (op == PGPU_RED_MIN_I64) v = x < v ? x : v;
+    else v = x > v ? x : v;
   }
-  if (s < PGPU_NSTATS) {
-    int64_t v = 0;
-    for (int b = 0; b < nblocks; ++b) v += p.stats[(size_t)b * PGPU_NSTATS + s];
-    stats_out[s] = v;
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const int64_t x = red[threadIdx.x + o];
+      int64_t y = red[threadIdx.x];
+      if (op == PGPU_RED_SUM_I64) y += x;
+      else if (op == PGPU_RED_SUM_F64) y = __double_as_longlong(__longlong_as_double(y) + __longlong_as_double(x));
+      else if (op == PGPU_RED_MIN_I64) y = x < y ? x : y;
+      else y = x > y ? x : y;
+      red[threadIdx.x] = y;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (is_stat) stats_out[col - p.nsec] = red[0];
+    else p.table[col] = red[0];
   }
 }
 
-// ---- compaction of a dense table (keys with count > 0) ----------------------------------------------------
+// ---- compaction of a dense table (keys with count > 0) -------------------------------------------------------------
 #define CMP_BLOCK 256
 #define CMP_PER_BLOCK 4096
 
@@ -703,7 +823,6 @@ __global__ void compact_count_kernel(const int64_t* table, uint64_t G, int32_t* 
 }
 
 __global__ void compact_scan_kernel(int32_t* block_counts, int32_t nblocks, int64_t* total) {
-  // single thread: nblocks <= a few 10^4
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     int64_t run = 0;
     for (int b = 0; b < nblocks; ++b) {
@@ -747,8 +866,12 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 
 }  // namespace
 
-// ---- host-side launch helpers (called by pgpu_runtime.cpp) ----------------------------------------------------
-size_t pgpu_static_smem_bytes() { return sizeof(Smem); }
+// ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
+size_t pgpu_dyn_smem_bytes(int mode, int pf_words, uint64_t table_bytes) {
+  size_t n = (size_t)NW * MAXS * 64 * 4 + (size_t)NW * pf_words * 4 + (size_t)NW * PGPU_MAX_AGGS * 8;
+  if (mode == PGPU_MODE_LDS) n += table_bytes;
+  return n;
+}
 
 hipError_t pgpu_occupancy(int mode, size_t dyn_smem, int* blocks_per_cu) {
   switch (mode) {
@@ -785,8 +908,8 @@ hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipS
   return hipGetLastError();
 }
 
-hipError_t pgpu_launch_finalize(const DevParams& p, int nblocks, int64_t* stats_out, hipStream_t st) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, st, p, nblocks, stats_out);
+hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(p.nsec + PGPU_NSTATS), dim3(256), 0, st, p, nslabs, stats_out);
   return hipGetLastError();
 }
 

@@ -26,11 +26,11 @@
 #include "pgpu_internal.h"
 
 // kernels (pgpu_kernels.hip)
-size_t pgpu_static_smem_bytes();
+size_t pgpu_dyn_smem_bytes(int mode, int pf_words, uint64_t table_bytes);
 hipError_t pgpu_occupancy(int mode, size_t dyn_smem, int* blocks_per_cu);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
-hipError_t pgpu_launch_finalize(const DevParams& p, int nblocks, int64_t* stats_out, hipStream_t st);
+hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts, int64_t* total,
                                int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
 
@@ -591,7 +591,7 @@ int pgpu_kernel_geometry(pgpu_context* ctx, int32_t* out_grid, int32_t* out_tile
   if (out_grid) {
     int bpc = 0;
     HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(pgpu_occupancy(PGPU_MODE_AGG, 0, &bpc));
+    HIP_TRY(pgpu_occupancy(PGPU_MODE_AGG, pgpu_dyn_smem_bytes(PGPU_MODE_AGG, 64 * 16, 0), &bpc));
     *out_grid = std::max(1, bpc) * ctx->num_cus;
   }
   return PGPU_OK;
@@ -646,7 +646,8 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
   };
   for (int i = 0; i < sp.num_filter_nodes; ++i) {
     const pgpu_filter_node& nd = sp.filter[i];
-    if (cur >= PGPU_MAX_SLOTS) return fail(PGPU_E_UNSUPPORTED, "filter nesting deeper than %d", PGPU_MAX_SLOTS);
+    if (cur >= PGPU_MAX_SLOTS - 1)
+      return fail(PGPU_E_UNSUPPORTED, "filter nesting deeper than %d", PGPU_MAX_SLOTS - 1);
     DevInstr in{};
     in.col = nd.column;
     in.negate = nd.negate ? 1 : 0;
@@ -670,6 +671,15 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
           in.lo = std::max(0, nd.lo);
           in.hi = std::min(nd.hi, c->card);
           if (in.hi < in.lo) in.hi = in.lo;
+        } else if (nd.pred == PGPU_PRED_SET && nd.num_ids <= 8) {
+          in.pred = 2;  // LIST: compared in registers
+          in.pool_off = (int32_t)pk.pool.size();
+          in.n = nd.num_ids;
+          for (int k = 0; k < nd.num_ids; ++k) {
+            const int32_t id = nd.ids[k];
+            if (id < 0 || id >= c->card) return fail(PGPU_E_INVALID, "SET id %d out of range", id);
+            pk.pool.push_back(id);
+          }
         } else if (nd.pred == PGPU_PRED_SET) {
           in.pool_off = (int32_t)pk.pool.size();
           pk.pool.resize(pk.pool.size() + (c->card + 31) / 32 + 1, 0);
@@ -859,7 +869,9 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       break;
     }
     pk.segs.push_back(ds);
-    tiles += (seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
+    tiles += (seg->num_docs + PGPU_WAVE_TILE - 1) / PGPU_WAVE_TILE;
+    if (ds.pf_pc >= 0)
+      p.pf_words = std::max(p.pf_words, 64 * pk.cols[ds.col_begin + pk.instrs[ds.prog_begin + ds.pf_pc].col].bits);
   }
   p.nseg = q->num_segments;
   p.total_tiles = tiles;
@@ -889,21 +901,17 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   HIP_TRY(hipSetDevice(ctx->device));
 
   // mode and launch geometry
-  size_t dyn = 0;
-  if (q->num_group_columns == 0) {
-    p.mode = PGPU_MODE_AGG;
-  } else if (8ull * L.num_sections * L.num_keys + PGPU_TILE * 4 <= PGPU_LDS_TABLE_BYTES) {
-    p.mode = PGPU_MODE_LDS;
-    dyn = PGPU_TILE * 4 + 8ull * L.num_sections * L.num_keys;
-  } else {
-    p.mode = PGPU_MODE_GLOBAL;
-    dyn = PGPU_TILE * 4;
-  }
+  const uint64_t tbytes = 8ull * L.num_sections * L.num_keys;
+  if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
+  else if (tbytes <= PGPU_LDS_TABLE_BYTES) p.mode = PGPU_MODE_LDS;
+  else p.mode = PGPU_MODE_GLOBAL;
+  const size_t dyn = pgpu_dyn_smem_bytes(p.mode, p.pf_words, tbytes);
   int bpc = 0;
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (ctx->occ_cache[p.mode][0] == (int)dyn) bpc = ctx->occ_cache[p.mode][1];
   }
+  const int tiles_per_block = PGPU_WAVES;
   if (bpc <= 0) {
     HIP_TRY(pgpu_occupancy(p.mode, dyn, &bpc));
     if (bpc < 1) return fail(PGPU_E_HIP, "query kernel does not fit a CU (dyn LDS %zu)", dyn);
@@ -911,7 +919,8 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
     ctx->occ_cache[p.mode][0] = (int)dyn;
     ctx->occ_cache[p.mode][1] = bpc;
   }
-  const int grid = std::max(1, std::min(p.total_tiles, bpc * ctx->num_cus));
+  const int grid = std::max(1, std::min((p.total_tiles + tiles_per_block - 1) / tiles_per_block, bpc * ctx->num_cus));
+  const int nwaves = grid * PGPU_WAVES;
 
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
@@ -930,8 +939,8 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   const size_t total = align16(o_rem + pk.remaps.size() * sizeof(void*)) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total);
-  if (e == hipSuccess) e = ws->slab.ensure(8ull * grid * L.num_sections + 16);
-  if (e == hipSuccess) e = ws->stats.ensure(8ull * grid * PGPU_NSTATS + 16);
+  if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
+  if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
@@ -956,7 +965,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
   if (e == hipSuccess) e = pgpu_launch_query(p, grid, dyn, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
-  if (e == hipSuccess) e = pgpu_launch_finalize(p, grid, (int64_t*)ws->stats_out.p, st);
+  if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)ws->stats_out.p, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ws->h_stats.p, ws->stats_out.p, 8 * PGPU_NSTATS, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));

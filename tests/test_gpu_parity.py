@@ -248,7 +248,7 @@ def test_synth_generator_matches_cpu(gpu_ctx):
     sl = SynthLib()
     for bits, card, n, dist in [(4, 16, 100_001, None), (10, 1024, 65_536, None), (16, 65536, 33_333, None),
                                 (20, 1 << 20, 8192 * 3 + 5, None), (20, 1 << 20, 50_000, "zipf"), (1, 2, 777, None),
-                                (32, 1 << 31, 9_999, None)]:
+                                (31, (1 << 31) - 1, 9_999, None)]:
         seed = 12345 + bits
         cdf = zipf_cdf(card, 1.1) if dist else None
         nbytes = (n * bits + 31) // 32 * 4 + 64
