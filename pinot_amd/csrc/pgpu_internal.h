@@ -2,24 +2,49 @@
 //
 // HBM layout of one uploaded segment column (all copies made once at segment load):
 //   fwd       : the FixedBitSVForwardIndexWriter byte stream, unchanged (big-endian, MSB-first, b bits per doc),
-//               padded with zeros to a whole number of query tiles + 16 B so a tile is always a full 16-B-aligned
-//               read; words are byte-swapped inside the kernel (v_perm) while staging.
+//               padded with zeros to a whole number of PGPU_TILE docs + 16 B so every 2048-doc tile is a whole,
+//               16-B aligned run of 256*b bytes; words are byte-swapped in registers while decoding.
 //   sorted    : SortedIndexReaderImpl pairs converted to little-endian int32 (start, end) per dict id.
 //   dict      : dictionary values converted to little-endian native width (int32/int64/float/double).
 //   inverted  : the Roaring portable bytes of every bitmap, unchanged (little-endian), plus a container directory
 //               built on the host at upload: per dict id a [first, last) range of DevContainer records.
+//
+// Query kernel geometry (pgpu_kernels.hip): one 512-thread workgroup per CU.  Waves 0..1 are LOADERS: they stream
+// the "staged" forward-index columns of the workgroup's tiles into a ring of LDS slots with global_load_lds and
+// publish each slot behind a counted vmcnt.  Waves 2..7 are CONSUMERS: consumer c takes tiles c, c+6, ... of the
+// workgroup's contiguous tile range, decodes the staged columns out of LDS (lane l owns docs [32l, 32l+32) of the
+// 2048-doc tile), runs the dense filter program on 32-bit mask words, and either aggregates straight from the
+// decoded ids (dense aggregation) or queues candidate doc ids for batched per-doc gathers (residual filter +
+// sparse aggregation).  The loader's DMA queue never waits behind a consumer's gathers (separate waves, separate
+// vmcnt), which is what keeps enough bytes in flight per CU.
 #pragma once
 #include <stdint.h>
 
-#define PGPU_TILE 4096          // forward-index padding granularity in docs (whole tiles are always readable)
-#define PGPU_WAVE_TILE 2048     // docs per wave tile: lane l owns docs [32l, 32l+32); 256*b bytes, 16-B aligned
-#define PGPU_BLOCK 256          // threads per workgroup (4 independent waves of 64)
+#define PGPU_TILE 4096          // forward-index padding granularity in docs
+#define PGPU_WT 2048            // docs per tile: lane l owns docs [32l, 32l+32); 256*b bytes, 16-B aligned
+#define PGPU_WAVE_TILE PGPU_WT
+#define PGPU_BLOCK 512          // threads per workgroup: PGPU_NLOAD loader waves + consumer waves
 #define PGPU_WAVES (PGPU_BLOCK / 64)
-#define PGPU_GROUPS (PGPU_TILE / 64)
-#define PGPU_MAX_SLOTS 8        // per-lane mask words (7 filter slots + 1 scratch row)
+#define PGPU_NLOAD 2            // loader waves per workgroup (each keeps its own 63-instruction vmcnt budget)
+#define PGPU_NCONS (PGPU_WAVES - PGPU_NLOAD)
+#define PGPU_MAX_SLOTS 8        // per-consumer mask rows (filter slots + 1 scratch row)
 #define PGPU_MAX_AGGS 16
 #define PGPU_MAX_GCOLS 8
-#define PGPU_LDS_TABLE_BYTES (16 * 1024)
+#define PGPU_MAX_STAGE 6        // staged (LDS-streamed) columns per segment
+#define PGPU_RING_MAX 64        // ring slots (flag arrays are sized for this)
+#define PGPU_LIST 2304          // per-consumer list entries (int32): candidate queue / dense-agg key+value lists
+#define PGPU_CQ_FLUSH 256       // candidate-queue flush threshold (queue then still has room for a whole tile)
+#define PGPU_DOC_U 4            // candidate docs per lane per flush round
+#define PGPU_LDS_LIMIT 163840   // gfx950 LDS per CU
+#define PGPU_LDS_TABLE_BYTES (32 * 1024)
+#define PGPU_MAX_STAGE_INSTRS 31  // DMA instructions per tile (so two tiles always fit the 6-bit vmcnt)
+
+// per-consumer LDS area: mask rows | list | accumulators
+#define PGPU_CONS_MASK_BYTES (PGPU_MAX_SLOTS * 64 * 4)
+#define PGPU_CONS_LIST_BYTES (PGPU_LIST * 4)
+#define PGPU_CONS_ACC_BYTES (PGPU_MAX_AGGS * 8)
+#define PGPU_CONS_BYTES (PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES + PGPU_CONS_ACC_BYTES)
+#define PGPU_FLAG_BYTES (3 * PGPU_RING_MAX * 4)
 
 // column kinds
 #define PGPU_COL_NONE 0
@@ -51,15 +76,28 @@ struct DevColumn {
   int32_t dict_type;              // PGPU_INT .. PGPU_STRING
 };
 
+// Aggregation plan of a segment
+#define PGPU_AM_COUNT 0   // COUNT(*) only, no group-by: matched docs are only counted
+#define PGPU_AM_DENSE 1   // group / agg column ids decoded from the staged LDS slot
+#define PGPU_AM_SPARSE 2  // matched docs queued; ids gathered per doc
+
 struct DevSeg {
   int32_t num_docs;
   int32_t tile_begin;             // first global tile of this segment
-  int32_t prog_begin;             // first instruction
-  int32_t prog_len;
+  int32_t ntiles;
   int32_t col_begin;              // index of its first DevColumn (ncols per segment)
   int32_t remap_begin;            // index of its first remap pointer (ngcols per segment)
-  int32_t pf_pc;                  // instruction whose column is register-prefetched one tile ahead (-1: none)
-  int32_t pad1;
+  int32_t prog_begin, prog_len;   // dense program: mask words of 32 consecutive docs per lane
+  int32_t rprog_begin, rprog_len; // residual program: evaluated per queued candidate doc (0 = none)
+  int32_t nstage;                 // staged columns
+  int32_t stage_instrs;           // DMA instructions per tile for the staged columns
+  int32_t agg_mode;               // PGPU_AM_*
+  int32_t nreg;                   // AM_DENSE: columns decoded into registers before the slot is released
+                                  //           (-1: the slot is held for the whole tile)
+  int32_t reg_col[2];             // query columns of the register copies
+  int32_t pad0;
+  int32_t stage_col[PGPU_MAX_STAGE];   // query column of staged column j
+  int32_t stage_off[PGPU_MAX_STAGE];   // byte offset of its region in a ring slot
 };
 
 // Filter instruction with statically resolved mask slots.
@@ -79,16 +117,25 @@ struct DevSeg {
 struct DevInstr {
   int32_t op;
   int32_t col;      // query column
-  int32_t pred;     // 0 RANGE, 1 SET (bitset in the pool), 2 LIST (<= 8 ids in the pool)
+  int32_t pred;     // 0 RANGE, 1 SET (bitset in the pool), 2 LIST (<= 8 ids inline)
   int32_t negate;
   int32_t lo, hi;
-  int32_t pool_off; // int32 pool offset (SET bitset, id list, doc ranges)
+  int32_t pool_off; // int32 pool offset (SET bitset, bitmap ids, doc ranges)
   int32_t n;        // ids / ranges
   int32_t dst;      // written slot
   int32_t src;      // read slot (child / operand)
   int32_t care;     // care slot, -1 = valid docs
-  int32_t jump;     // AND short-circuit target (instruction index within the segment program)
+  int32_t jump;     // AND short-circuit target (instruction index within the program)
+  // SCAN leaves carry their column so one scalar load has everything the leaf needs
+  int32_t stage_off;  // byte offset of the staged region in a ring slot, -1 = read from HBM
+  int32_t bits;
+  int32_t kind;       // PGPU_COL_*
+  int32_t card;
+  const uint32_t* fwd;
+  const int32_t* sorted;
+  uint32_t ids[8];    // LIST ids
 };
+static_assert(sizeof(DevInstr) == 112, "DevInstr layout");
 
 struct DevAgg {
   int32_t fn;       // PGPU_AGG_*
@@ -118,6 +165,7 @@ struct DevParams {
   int64_t* table;                 // [nsec][G]
   int64_t* slab;                  // AGG mode: [waves][nsec]
   int64_t* stats;                 // [waves][PGPU_NSTATS]
+  int64_t* prof;                  // [waves][PGPU_NPROF] (PGPU_FLAG_PROFILE)
   uint64_t G;
   int32_t nseg;
   int32_t total_tiles;
@@ -127,8 +175,12 @@ struct DevParams {
   int32_t nsec;
   int32_t mode;
   int32_t flags;
-  int32_t pf_words;               // words of the driving column per wave tile (64 * max bits), 0 = no prefetch
-  int32_t pad0;
+  int32_t ring_slots;             // R
+  int32_t slot_bytes;             // S (multiple of 16)
+  int32_t inflight;               // loader's published-behind window (slots)
+  int32_t ltab_bytes;             // LDS group table bytes (MODE_LDS)
+  int32_t max_instrs;             // max DMA instructions of one tile (loader vmcnt budget)
+  int32_t pad1;
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];
@@ -136,3 +188,30 @@ struct DevParams {
 };
 
 #define PGPU_FLAG_STATS 1
+#define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)
+#define PGPU_NPROF 12
+// loader phases
+#define PGPU_P_L_TOTAL 0
+#define PGPU_P_L_FREE 1     // waiting for a free ring slot
+#define PGPU_P_L_PUB 2      // counted vmcnt waits before publishing
+#define PGPU_P_L_ISSUE 3    // DMA issue
+// consumer phases
+#define PGPU_P_C_TOTAL 4
+#define PGPU_P_C_FULL 5     // waiting for a published slot
+#define PGPU_P_C_FILTER 6   // dense filter program
+#define PGPU_P_C_AGG 7      // register copies, dense aggregation, queue pushes
+#define PGPU_P_C_FLUSH 8    // candidate-queue flushes
+#define PGPU_P_C_TILES 9    // tiles processed
+#define PGPU_P_C_FETCH 10   // filter: instruction fetch (scalar loads)
+#define PGPU_P_C_DECODE 11  // filter: SCAN leaf decode + predicate
+
+// LDS bytes of the query kernel for a given ring / table configuration.
+inline uint32_t pgpu_lds_bytes(int ring_slots, int slot_bytes, int ltab_bytes) {
+  return (uint32_t)(PGPU_FLAG_BYTES + PGPU_NCONS * PGPU_CONS_BYTES + ((ltab_bytes + 15) & ~15) +
+                    ring_slots * slot_bytes);
+}
+
+// Bytes of one staged column's region in a ring slot and its DMA instruction count.  Widths that are multiples of
+// 8 bits get 16 B of padding per lane record so the consumers' ds_read_b128 are bank-conflict free.
+inline int pgpu_stage_region_bytes(int bits) { return (bits % 8 == 0) ? 64 * (4 * bits + 16) : 256 * bits; }
+inline int pgpu_stage_instrs(int bits) { return (bits % 8 == 0) ? bits / 4 + 1 : (bits + 3) / 4; }

@@ -1,21 +1,26 @@
 // HIP kernels of the MI355X segment query path (gfx950 / CDNA4).
 //
-// One launch runs a whole query over every segment a GPU owns.  Work unit = a WAVE TILE of 2048 consecutive docs
-// of one segment; every wave of the persistent grid walks its own wave tiles independently (no workgroup barrier
-// in the main loop), and inside a wave tile LANE l OWNS DOCS [32l, 32l+32): the 32*b bits of a lane are exactly b
-// consecutive big-endian words of the FixedBitSVForwardIndexWriter stream, so a lane unpacks its 32 dict ids with
-// compile-time shifts (one template instantiation per bit width) and every filter mask is one 32-bit word per lane.
+// One launch runs a whole query over every segment a GPU owns.  Geometry (pgpu_internal.h): one 512-thread
+// workgroup per CU owns a contiguous range of 2048-doc tiles.
 //
-//   K1  fixed-bit unpack fused with dict-id RANGE / SET / LIST predicates:
-//         dense  — the lane's b words (the "driving" column of the filter is DMA'd into LDS one wave tile ahead
-//                  with global_load_lds; other columns are loaded straight to VGPRs),
-//         sparse — when the docs that still matter are < 1/32 of the tile, only those docs gather their two
-//                  words (32-B-sector-granular traffic).
-//   K2  Roaring array / bitmap / run containers (BitmapBasedFilterOperator), sorted-index doc ranges, and the
-//       AND / OR / NOT algebra on the per-lane mask words (short-circuit of AND when a wave tile empties).
-//   K3  COUNT / SUM / MIN / MAX / AVG: per-lane register accumulators + wave reduction (aggregation only), or
-//       group keys (mixed-radix global dict ids) with atomics into an LDS-privatised dense table (small key
-//       spaces) or the HBM dense table (large key spaces).
+//   LOADER (wave 0)      streams the tile's "staged" forward-index columns (the scan columns of the dense part of
+//                        the filter, plus the group / aggregation columns when most docs survive) into a ring of
+//                        LDS slots with global_load_lds (16 B per lane, 1 KiB per instruction), and publishes slot k
+//                        behind a counted `s_waitcnt vmcnt` once its bytes have landed.  It only ever waits for its
+//                        own DMAs, so tens of KiB stay in flight per CU regardless of what the consumers do.
+//   CONSUMERS (1..7)     consumer c takes tiles c, c+7, ...  Lane l owns docs [32l, 32l+32): its 32*b bits are b
+//                        consecutive big-endian words, read with the widest bank-conflict-free ds_read and unpacked
+//                        with compile-time shifts (one template instantiation per bit width) into 32 dict ids.
+//
+//   K1  fixed-bit unpack fused with dict-id RANGE / SET / LIST predicates -> one 32-bit match word per lane.
+//   K2  Roaring array / bitmap / run containers (BitmapBasedFilterOperator), sorted-index doc ranges, AND / OR / NOT
+//       on the match words (short-circuit of AND when a tile empties).
+//   K3  COUNT / SUM / MIN / MAX / AVG and dictionary-id GROUP BY: matched docs are compacted into an LDS list so
+//       every dictionary / remap gather and every table update runs with full lanes; per-lane partials + wave
+//       reductions (aggregation only), LDS-privatised dense tables (small key spaces) or HBM tables.
+//   Sparse work (a filter child too selective to stream, or aggregation columns under a selective filter) goes
+//   through a per-consumer candidate queue of doc ids, flushed in rounds of 64 lanes x U docs with every gather of
+//   a round issued before the first wait.
 //
 // Reference hot loops this replaces (file:line under pinot-core/... and pinot-segment-local/...):
 //   FixedBitIntReader.read32 / PinotDataBitSet.readInt           seglocal/io/util/PinotDataBitSet.java:78-165
@@ -33,61 +38,144 @@
 #include "pgpu_internal.h"
 
 #define NT PGPU_BLOCK
-#define NW PGPU_WAVES
-#define WT PGPU_WAVE_TILE  // 2048 docs per wave tile
+#define WT PGPU_WT
 #define MAXS PGPU_MAX_SLOTS
+#define U PGPU_DOC_U
+#define FI __device__ __forceinline__
 
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
 // Loads through the global address space: segment pointers reach the kernel inside structs in HBM, so the
 // compiler only sees generic pointers and would emit flat_* (which also count against lgkmcnt and stall LDS).
 #define GAS __attribute__((address_space(1)))
+#define LAS __attribute__((address_space(3)))
 template <class T>
-__device__ __forceinline__ T gld(const T* p, size_t i) { return ((const GAS T*)p)[i]; }
-__device__ __forceinline__ uint32_t lowmask(uint32_t b) { return 0xFFFFFFFFu >> (32u - b); }
-// Bit i of a lane mask word as v_bfe_u32 with inline operands (a `1u << i` test makes the compiler keep 32
-// materialised constants live in VGPRs across the unrolled doc loops).
-__device__ __forceinline__ uint32_t lane_bit(uint32_t m, int i) { return __builtin_amdgcn_ubfe(m, (uint32_t)i, 1u); }
+FI T gld(const T* p, size_t i) { return ((const GAS T*)p)[i]; }
+// Query metadata (segments, columns, instructions, pool) is read through the constant address space with
+// wave-uniform addresses so it becomes s_load (lgkmcnt) -- never a vector load that a vmcnt wait would order
+// behind the loader's DMAs -- and is never copied into a private array (dynamic indexing spills to scratch).
+#define CAS __attribute__((address_space(4)))
+template <class T>
+FI T cld(const T* p) {
+  if constexpr (sizeof(T) > 8) {  // structs: dword by dword (no copy constructor from an address-space lvalue)
+    static_assert(sizeof(T) % 4 == 0, "dword-sized metadata");
+    uint32_t w[sizeof(T) / 4];
+#pragma unroll
+    for (unsigned i = 0; i < sizeof(T) / 4; ++i) w[i] = ((const CAS uint32_t*)p)[i];
+    T v;
+    __builtin_memcpy(&v, w, sizeof(T));
+    return v;
+  } else {
+    return *(const CAS T*)p;
+  }
+}
+template <class T>
+FI T cld(const T* p, size_t i) { return ((const CAS T*)p)[i]; }
+FI int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// Phase timers (PGPU_FLAG_PROFILE): shader clock via s_memtime, accumulated per wave.
+struct Prof {
+  bool on;
+  int64_t t[PGPU_NPROF];
+};
+FI int64_t now(const Prof& pf) { return pf.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0; }
+#define PROF_ADD(pf, k, since) do { if ((pf).on) (pf).t[k] += (int64_t)__builtin_amdgcn_s_memtime() - (since); } while (0)
+FI uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+FI uint32_t lowmask(uint32_t b) { return 0xFFFFFFFFu >> (32u - b); }
+// Bit i of a mask word as v_bfe_u32 with inline operands.
+FI uint32_t lane_bit(uint32_t m, int i) { return __builtin_amdgcn_ubfe(m, (uint32_t)i, 1u); }
+FI int lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ void wave_sync() {
+FI void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+FI int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ double wave_sum_f64(double v) {
+FI double wave_sum_f64(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+FI int64_t wave_min_i64(int64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
   return v;
 }
-__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+FI int64_t wave_max_i64(int64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { int64_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
   return v;
 }
-// Wave-uniform total (readfirstlane: callers branch on it as a scalar).
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return __builtin_amdgcn_readfirstlane(v);
+// DPP lane moves (VALU, no LDS round trip).  Callers run with all 64 lanes active.
+#define DPP_QUAD_1032 0xB1
+#define DPP_QUAD_2301 0x4E
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_ROW_MIRROR 0x140
+#define DPP_ROW_HALF_MIRROR 0x141
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+template <int CTRL, int ROWS = 0xF>
+FI int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, true); }
+
+// Wave-uniform total (an SGPR value: callers branch on it as a scalar).
+FI int wave_sum_i32(int v) {
+  v += dpp<DPP_QUAD_1032>(v);
+  v += dpp<DPP_QUAD_2301>(v);
+  v += dpp<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp<DPP_ROW_MIRROR>(v);  // every lane of a 16-lane row holds the row total
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+// Exclusive prefix sum over the wave's lanes (row scans + row broadcasts).
+FI int wave_excl_scan(int v) {
+  int x = v;
+  x += dpp<DPP_ROW_SHR(1)>(x);
+  x += dpp<DPP_ROW_SHR(2)>(x);
+  x += dpp<DPP_ROW_SHR(4)>(x);
+  x += dpp<DPP_ROW_SHR(8)>(x);
+  x += __builtin_amdgcn_update_dpp(0, x, DPP_ROW_BCAST15, 0xA, 0xF, false);
+  x += __builtin_amdgcn_update_dpp(0, x, DPP_ROW_BCAST31, 0xC, 0xF, false);
+  return x - v;
+}
+
+// ---- LDS flags (ring hand-off between the loader and the consumers) ----------------------------------------------
+FI int flag_load(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+FI void flag_store(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// The loader's flag accesses as inline asm: the compiler would otherwise guard every LDS access of the loader
+// with `s_waitcnt vmcnt(0)` (it cannot prove the flags do not alias the in-flight LDS-DMA destinations).
+FI uint32_t lds_off(const void* p) { return (uint32_t)(size_t)(const LAS void*)p; }
+FI int loader_flag_load(const int* p) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off(p)) : "memory");
+  return sgpr(v);
+}
+FI void loader_flag_store(int* p, int v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the immediate must be a constant).
+FI void wait_vmcnt(int n) {
+#define VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+  switch (n) {
+    VMC(0) VMC(1) VMC(2) VMC(3) VMC(4) VMC(5) VMC(6) VMC(7) VMC(8) VMC(9) VMC(10) VMC(11) VMC(12) VMC(13) VMC(14)
+    VMC(15) VMC(16) VMC(17) VMC(18) VMC(19) VMC(20) VMC(21) VMC(22) VMC(23) VMC(24) VMC(25) VMC(26) VMC(27)
+    VMC(28) VMC(29) VMC(30) VMC(31) VMC(32) VMC(33) VMC(34) VMC(35) VMC(36) VMC(37) VMC(38) VMC(39) VMC(40)
+    VMC(41) VMC(42) VMC(43) VMC(44) VMC(45) VMC(46) VMC(47) VMC(48) VMC(49) VMC(50) VMC(51) VMC(52) VMC(53)
+    VMC(54) VMC(55) VMC(56) VMC(57) VMC(58) VMC(59) VMC(60) VMC(61) VMC(62)
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+#undef VMC
 }
 
 // Order-preserving int64 key of a dictionary value (MIN/MAX sections).
-__device__ __forceinline__ int64_t minmax_key(const void* dict, int32_t vtype, uint32_t id) {
+FI int64_t minmax_key(const void* dict, int32_t vtype, uint32_t id) {
   switch (vtype) {
     case PGPU_INT: return (int64_t)gld((const int32_t*)dict, id);
     case PGPU_LONG: return gld((const int64_t*)dict, id);
@@ -101,72 +189,106 @@ __device__ __forceinline__ int64_t minmax_key(const void* dict, int32_t vtype, u
     }
   }
 }
-__device__ __forceinline__ int64_t value_i64(const void* dict, int32_t vtype, uint32_t id) {
-  return vtype == PGPU_INT ? (int64_t)gld((const int32_t*)dict, id) : gld((const int64_t*)dict, id);
-}
-__device__ __forceinline__ double value_f64(const void* dict, int32_t vtype, uint32_t id) {
-  return vtype == PGPU_FLOAT ? (double)gld((const float*)dict, id) : gld((const double*)dict, id);
-}
-__device__ __forceinline__ int64_t sec_identity(int32_t op) {
+FI int64_t sec_identity(int32_t op) {
   return op == PGPU_RED_MIN_I64 ? INT64_MAX : (op == PGPU_RED_MAX_I64 ? INT64_MIN : 0);
 }
 
-// ---- per-wave LDS carve ----------------------------------------------------------------------------------------
-// dynamic LDS of a workgroup: [NW][MAXS][64] slot words | [NW][pf_words] driving-column buffers |
-//                             [NW][MAX_AGGS] int64 accumulators | LDS group table [nsec][G] (mode LDS)
-struct Carve {
-  uint32_t* slots;   // this wave's [MAXS][64]
-  uint32_t* pf;      // this wave's driving-column buffer (pf_words)
-  int64_t* accw;     // this wave's [MAX_AGGS]
-  int64_t* ltab;     // workgroup table
-  bool* pf_have;     // a DMA into pf is in flight
-  int pf_words;
-};
-
-__device__ __forceinline__ uint32_t& slot(const Carve& cv, int s) { return cv.slots[s * 64 + (threadIdx.x & 63)]; }
-
-struct WTile {
-  const DevSeg* seg;
-  const DevColumn* cols;
-  int32_t tile_in_seg;
-  int32_t doc0;      // first doc of the wave tile (segment-local)
-  int32_t ndocs;     // docs of the wave tile inside the segment (1..2048)
-  uint32_t valid;    // this lane's valid-doc word
-  int32_t lane_doc0; // doc0 + 32 * lane
-};
+// Dictionary values dict[idx[r]] as the 8-byte cells their section reduces: int64 for integer SUM, float64 bits
+// for floating SUM, order-preserving key for MIN/MAX.  The (uniform) type dispatch sits outside the unrolled
+// gathers so all N loads are in flight before the first use.
+FI int64_t key_of_double(double d) {
+  const int64_t b = __double_as_longlong(d);
+  return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
+}
+template <int N>
+FI void gather_cells(const void* dict, int32_t vtype, int32_t op, const uint32_t (&idx)[N], int64_t (&out)[N]) {
+  if (vtype == PGPU_INT || vtype == PGPU_FLOAT) {
+    uint32_t raw[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) raw[r] = gld((const uint32_t*)dict, idx[r]);
+    if (vtype == PGPU_INT) {
+#pragma unroll
+      for (int r = 0; r < N; ++r) out[r] = (int64_t)(int32_t)raw[r];  // SUM_I64 value == MIN/MAX key
+    } else {
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const double d = (double)__uint_as_float(raw[r]);
+        out[r] = op == PGPU_RED_SUM_F64 ? __double_as_longlong(d) : key_of_double(d);
+      }
+    }
+  } else {
+    int64_t raw[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) raw[r] = gld((const int64_t*)dict, idx[r]);
+    if (vtype == PGPU_LONG) {
+#pragma unroll
+      for (int r = 0; r < N; ++r) out[r] = raw[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < N; ++r) out[r] = op == PGPU_RED_SUM_F64 ? raw[r] : key_of_double(__longlong_as_double(raw[r]));
+    }
+  }
+}
+FI int64_t cell_combine(int32_t op, int64_t a, int64_t b) {
+  if (op == PGPU_RED_SUM_I64) return a + b;
+  if (op == PGPU_RED_SUM_F64) return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
+  if (op == PGPU_RED_MIN_I64) return b < a ? b : a;
+  return b > a ? b : a;
+}
+FI int64_t wave_combine(int32_t op, int64_t v) {
+  if (op == PGPU_RED_SUM_I64) return wave_sum_i64(v);
+  if (op == PGPU_RED_SUM_F64) return __double_as_longlong(wave_sum_f64(__longlong_as_double(v)));
+  if (op == PGPU_RED_MIN_I64) return wave_min_i64(v);
+  return wave_max_i64(v);
+}
+// Atomic table update (LDS or HBM cell).
+FI void cell_atomic(int64_t* cell, int32_t op, int64_t v) {
+  if (op == PGPU_RED_SUM_I64) atomicAdd((unsigned long long*)cell, (unsigned long long)v);
+  else if (op == PGPU_RED_SUM_F64) atomicAdd((double*)cell, __longlong_as_double(v));
+  else if (op == PGPU_RED_MIN_I64) atomicMin((long long*)cell, (long long)v);
+  else atomicMax((long long*)cell, (long long)v);
+}
 
 // ---- fixed-bit extraction (compile-time bit width) -------------------------------------------------------------
 // w[] = the lane's B words, byte-swapped (MSB-first bit order); value i occupies bits [i*B, (i+1)*B).
 template <int B>
-__device__ __forceinline__ uint32_t extract_c(const uint32_t (&w)[B], int i) {
+FI uint32_t extract_c(const uint32_t (&w)[B], int i) {
   const int o = i * B;
   const int k = o >> 5, sh = o & 31;
   if (sh + B <= 32) return (w[k] >> (32 - sh - B)) & lowmask(B);
   return __builtin_amdgcn_alignbit(w[k], w[k + 1], 64 - sh - B) & lowmask(B);
 }
+template <int B>
+FI void unpack_b(const uint32_t (&w)[B], uint32_t (&ids)[32]) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) ids[i] = extract_c<B>(w, i);
+}
 
-// This lane's index, opaque to loop-invariant code motion: the per-bit-width lane offsets (lane * B for 31
-// widths) would otherwise be hoisted out of the tile loop and pin ~30 VGPRs for the kernel's lifetime.
-__device__ __forceinline__ uint32_t opaque_lane() {
+// This lane's index, opaque to loop-invariant code motion (per-bit-width lane offsets would otherwise be hoisted
+// out of the tile loop and pin ~30 VGPRs for the kernel's lifetime).
+FI uint32_t opaque_lane() {
   uint32_t l;
   asm volatile("v_and_b32 %0, 63, %1" : "=v"(l) : "v"(threadIdx.x));
   return l;
 }
 
-// The lane's B words of column `fwd` in wave tile `tile_in_seg`, straight from HBM (byte-swapped).
+// The lane's B words of a staged column region in a ring slot.  Record stride: B dwords, +4 when B % 8 == 0
+// (pgpu_stage_region_bytes); read width: b128 when B % 4 == 0, b64 when B % 2 == 0, b32 otherwise -- every
+// combination is bank-conflict free for a wave's lane groups.
 template <int B>
-__device__ __forceinline__ void load_lane_words(const uint32_t* __restrict__ fwd, int tile_in_seg, uint32_t (&w)[B]) {
-  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
+FI void slot_lane_words(const uint32_t* region, uint32_t (&w)[B]) {
+  constexpr int stride = (B % 8 == 0) ? B + 4 : B;
+  const LAS uint32_t* src = (const LAS uint32_t*)region + opaque_lane() * stride;
   if constexpr (B % 4 == 0) {
 #pragma unroll
     for (int k = 0; k < B; k += 4) {
-      const u32x4 v = *(const GAS u32x4*)(src + k);
+      const u32x4 v = *(const LAS u32x4*)(src + k);
       w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
     }
   } else if constexpr (B % 2 == 0) {
 #pragma unroll
     for (int k = 0; k < B; k += 2) {
-      const u32x2 v = *(const GAS u32x2*)(src + k);
+      const u32x2 v = *(const LAS u32x2*)(src + k);
       w[k] = v.x; w[k + 1] = v.y;
     }
   } else {
@@ -176,31 +298,19 @@ __device__ __forceinline__ void load_lane_words(const uint32_t* __restrict__ fwd
 #pragma unroll
   for (int k = 0; k < B; ++k) w[k] = bswap32(w[k]);
 }
-
-// The lane's B words from the LDS copy of the wave tile (linear stream order, raw big-endian).
+// The lane's B words of tile `tile_in_seg` straight from HBM (fallback for a dense column that is not staged).
 template <int B>
-__device__ __forceinline__ void lds_lane_words(const uint32_t* buf, uint32_t (&w)[B]) {
-  const uint32_t* src = buf + opaque_lane() * B;
+FI void hbm_lane_words(const uint32_t* fwd, int tile_in_seg, uint32_t (&w)[B]) {
+  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
 #pragma unroll
   for (int k = 0; k < B; ++k) w[k] = bswap32(src[k]);
 }
 
-// ---- fixed-bit decode: ONE inlined dispatch site per source keeps the 31 bit-width variants out of every consumer
 template <int B>
-__device__ __forceinline__ void unpack_b(const uint32_t (&w)[B], uint32_t (&ids)[32]) {
-#pragma unroll
-  for (int i = 0; i < 32; ++i) ids[i] = extract_c<B>(w, i);
-}
-template <int B>
-__device__ __forceinline__ void decode_hbm_b(const uint32_t* fwd, int tile_in_seg, uint32_t (&ids)[32]) {
+FI void decode_b(const uint32_t* region, const uint32_t* fwd, int tile_in_seg, uint32_t (&ids)[32]) {
   uint32_t w[B];
-  load_lane_words<B>(fwd, tile_in_seg, w);
-  unpack_b<B>(w, ids);
-}
-template <int B>
-__device__ __forceinline__ void decode_lds_b(const uint32_t* buf, uint32_t (&ids)[32]) {
-  uint32_t w[B];
-  lds_lane_words<B>(buf, w);
+  if (region) slot_lane_words<B>(region, w);
+  else hbm_lane_words<B>(fwd, tile_in_seg, w);
   unpack_b<B>(w, ids);
 }
 
@@ -216,15 +326,10 @@ __device__ __forceinline__ void decode_lds_b(const uint32_t* buf, uint32_t (&ids
     case 29: CALL(29); break; case 30: CALL(30); break; default: CALL(31); break;                   \
   }
 
-// The lane's 32 dict ids of column c in the wave tile, from HBM.
-__device__ __forceinline__ void decode_hbm(const DevColumn& c, int tile_in_seg, uint32_t (&ids)[32]) {
-#define DEC_CALL(B) decode_hbm_b<B>(c.fwd, tile_in_seg, ids)
-  PGPU_DISPATCH_B(c.bits, DEC_CALL)
-#undef DEC_CALL
-}
-// ... from the LDS copy of the wave tile (the prefetched driving column).
-__device__ __forceinline__ void decode_lds(int bits, const uint32_t* buf, uint32_t (&ids)[32]) {
-#define DEC_CALL(B) decode_lds_b<B>(buf, ids)
+// The lane's 32 dict ids of a column: from its staged slot region (region != nullptr) or from HBM.  Callers keep
+// the number of call sites (each inlines all 31 widths) to three: filter scan, register copies, aggregation.
+FI void decode_ids(int bits, const uint32_t* region, const uint32_t* fwd, int tile_in_seg, uint32_t (&ids)[32]) {
+#define DEC_CALL(B) decode_b<B>(region, fwd, tile_in_seg, ids)
   PGPU_DISPATCH_B(bits, DEC_CALL)
 #undef DEC_CALL
 }
@@ -242,7 +347,7 @@ struct Pred {
   bool negate;
 };
 
-__device__ __forceinline__ Pred make_pred(const DevInstr& in, const int32_t* pool) {
+FI Pred make_pred(const DevInstr& in, const int32_t* pool) {
   Pred p;
   p.kind = in.pred;
   p.negate = in.negate != 0;
@@ -250,11 +355,11 @@ __device__ __forceinline__ Pred make_pred(const DevInstr& in, const int32_t* poo
   p.span = (uint32_t)(in.hi - in.lo);
   p.bits = (const uint32_t*)(pool + in.pool_off);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p.ids[k] = (p.kind == PRED_LIST && k < in.n) ? (uint32_t)pool[in.pool_off + k] : 0xFFFFFFFFu;
+  for (int k = 0; k < 8; ++k) p.ids[k] = in.ids[k];  // unused entries are 0xFFFFFFFF (host)
   return p;
 }
 
-__device__ __forceinline__ bool eval_pred(const Pred& p, uint32_t id) {
+FI bool eval_pred(const Pred& p, uint32_t id) {
   bool m;
   if (p.kind == PRED_RANGE) {
     m = (id - p.lo) < p.span;
@@ -269,8 +374,7 @@ __device__ __forceinline__ bool eval_pred(const Pred& p, uint32_t id) {
 }
 
 // The lane's 32 predicate bits for its decoded ids.
-__device__ __forceinline__ uint32_t pred_ids(const uint32_t (&ids)[32], const Pred& p) {
-  // bits are shifted in from doc 31 down to doc 0 (v_lshl_or with inline operands)
+FI uint32_t pred_ids(const uint32_t (&ids)[32], const Pred& p) {
   uint32_t m = 0;
   if (p.kind == PRED_RANGE) {
 #pragma unroll
@@ -290,9 +394,9 @@ __device__ __forceinline__ uint32_t pred_ids(const uint32_t (&ids)[32], const Pr
   return p.negate ? ~m : m;
 }
 
-// ---- sparse access --------------------------------------------------------------------------------------------
+// ---- per-doc access ---------------------------------------------------------------------------------------------
 // SortedIndexReaderImpl.getDictId: last dict id whose start <= doc.
-__device__ __forceinline__ uint32_t sorted_dict_id(const int32_t* __restrict__ pairs, int32_t card, int32_t doc) {
+FI uint32_t sorted_dict_id(const int32_t* __restrict__ pairs, int32_t card, int32_t doc) {
   int32_t lo = 0, hi = card - 1;
   while (lo <= hi) {
     const int32_t mid = (lo + hi) >> 1;
@@ -301,71 +405,101 @@ __device__ __forceinline__ uint32_t sorted_dict_id(const int32_t* __restrict__ p
   return (uint32_t)hi;
 }
 
-// Dict id of segment doc `d` gathered from HBM (two big-endian words around its bits).
-__device__ __forceinline__ uint32_t gather_id(const DevColumn& c, int32_t d) {
-  if (c.kind == PGPU_COL_SORTED) return sorted_dict_id(c.sorted, c.card, d);
-  const uint32_t b = (uint32_t)c.bits;
-  const uint64_t e = (uint64_t)(d + 1) * b;
-  const uint64_t we = (e - 1u) >> 5;
-  const uint32_t r = (uint32_t)(e - (we << 5));
-  const uint32_t hi = bswap32(gld(c.fwd, we));
-  const uint32_t lo = we ? bswap32(gld(c.fwd, we - 1)) : 0u;
-  return __builtin_amdgcn_alignbit(lo, hi, 32u - r) & lowmask(b);
-}
-
-__device__ __forceinline__ void mark_sectors(uint32_t* sect, uint32_t j, uint32_t b) {
-  const uint32_t s0 = (j * b) >> 8, s1 = ((j + 1) * b - 1) >> 8;  // 32-B sector = 256 bits
-  atomicOr(&sect[s0 >> 5], 1u << (s0 & 31));
-  if (s1 != s0) atomicOr(&sect[s1 >> 5], 1u << (s1 & 31));
-}
-
-// Sparse scan: predicate bits for the docs of `care` only, two candidates per round trip.
-__device__ __forceinline__ uint32_t scan_sparse(const DevColumn& c, const WTile& t, const Pred& p, uint32_t care,
-                                                uint32_t* sect) {
-  uint32_t m = 0, left = care;
-  const uint32_t jbase = (uint32_t)(t.lane_doc0 - t.doc0);
-  while (__ballot(left != 0)) {
-    const bool h0 = left != 0;
-    const int i0 = h0 ? __builtin_ctz(left) : 0;
-    left &= left - 1;
-    const bool h1 = left != 0;
-    const int i1 = h1 ? __builtin_ctz(left) : 0;
-    left &= left - 1;
-    uint32_t id0 = 0, id1 = 0;
-    if (h0) id0 = gather_id(c, t.lane_doc0 + i0);
-    if (h1) id1 = gather_id(c, t.lane_doc0 + i1);
-    if (h0 && eval_pred(p, id0)) m |= 1u << i0;
-    if (h1 && eval_pred(p, id1)) m |= 1u << i1;
-    if (sect) {
-      if (h0) mark_sectors(sect, jbase + i0, (uint32_t)c.bits);
-      if (h1) mark_sectors(sect, jbase + i1, (uint32_t)c.bits);
-    }
+// Dict ids of segment docs d[u] gathered from HBM: two big-endian words around each doc's bits, all 2N loads
+// (unconditional loads of valid addresses) issued before the first use.
+struct ColRef {
+  const uint32_t* fwd;
+  const int32_t* sorted;
+  int32_t kind, bits, card;
+};
+template <int N>
+FI void gather_ids(const ColRef& c, const int32_t (&d)[N], uint32_t (&id)[N]) {
+  if (c.kind == PGPU_COL_SORTED) {
+#pragma unroll
+    for (int u = 0; u < N; ++u) id[u] = sorted_dict_id(c.sorted, c.card, d[u]);
+    return;
   }
-  return m;
+  const uint32_t b = (uint32_t)c.bits;
+  uint32_t hi[N], lo[N], r[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const uint64_t e = (uint64_t)(d[u] + 1) * b;
+    const uint64_t we = (e - 1u) >> 5;
+    r[u] = (uint32_t)(e - (we << 5));
+    hi[u] = gld(c.fwd, we);
+    lo[u] = we ? gld(c.fwd, we - 1) : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) id[u] = __builtin_amdgcn_alignbit(bswap32(lo[u]), bswap32(hi[u]), 32u - r[u]) & lowmask(b);
+}
+FI ColRef colref(const DevColumn& c) { return ColRef{c.fwd, c.sorted, c.kind, c.bits, c.card}; }
+FI ColRef colref(const DevInstr& in) { return ColRef{in.fwd, in.sorted, in.kind, in.bits, in.card}; }
+template <int N>
+FI void remap_ids(const int32_t* remap, uint32_t (&id)[N]) {
+  if (!remap) return;
+#pragma unroll
+  for (int u = 0; u < N; ++u) id[u] = (uint32_t)gld(remap, id[u]);
 }
 
-// ---- Roaring containers / sorted ranges ---------------------------------------------------------------------------
-// Bits of the wave tile covered by one Roaring bitmap (dict id `id`), for this lane's 32 docs.
-__device__ __noinline__ uint32_t bitmap_word(const DevColumn& c, const WTile& t, uint32_t id, uint32_t* lds_words) {
-  const uint32_t key = (uint32_t)t.doc0 >> 16;
-  const uint32_t lo16 = (uint32_t)t.doc0 & 0xFFFFu;  // multiple of 2048
-  const int lane = threadIdx.x & 63;
-  int32_t a = (int32_t)c.inv_dir[id], z = (int32_t)c.inv_dir[id + 1] - 1;
+// Roaring probe for one doc (per-doc filter leaves): is `d` in the bitmap of dict id `id`?
+struct InvIndex {
+  const uint32_t* dir;
+  const DevContainer* ct;
+  const uint8_t* data;
+};
+__device__ __noinline__ bool bitmap_contains(InvIndex c, uint32_t id, uint32_t d) {
+  const uint32_t key = d >> 16, lo16 = d & 0xFFFFu;
+  int32_t a = (int32_t)gld(c.dir, id), z = (int32_t)gld(c.dir, id + 1) - 1;
+  while (a <= z) {
+    const int32_t mid = (a + z) >> 1;
+    const DevContainer ct = c.ct[mid];
+    if (ct.key == key) {
+      if (ct.type == PGPU_CT_BITMAP) return (gld((const uint32_t*)(c.data + ct.offset), lo16 >> 5) >> (lo16 & 31)) & 1u;
+      if (ct.type == PGPU_CT_RUN) {
+        const uint16_t* r = (const uint16_t*)(c.data + ct.offset);
+        int32_t l = 0, h = (int32_t)ct.card - 1;
+        while (l <= h) {  // last run whose start <= lo16
+          const int32_t m = (l + h) >> 1;
+          if (r[2 * m] <= lo16) l = m + 1; else h = m - 1;
+        }
+        return h >= 0 && lo16 <= (uint32_t)r[2 * h] + r[2 * h + 1];
+      }
+      const uint16_t* v = (const uint16_t*)(c.data + ct.offset);
+      int32_t l = 0, h = (int32_t)ct.card - 1;
+      while (l <= h) {
+        const int32_t m = (l + h) >> 1;
+        if (v[m] == lo16) return true;
+        if (v[m] < lo16) l = m + 1; else h = m - 1;
+      }
+      return false;
+    }
+    if (ct.key < key) a = mid + 1; else z = mid - 1;
+  }
+  return false;
+}
+
+// ---- Roaring containers / sorted ranges for a whole tile -------------------------------------------------------
+// Bits of the tile covered by one Roaring bitmap (dict id `id`), for this lane's 32 docs.
+__device__ __noinline__ uint32_t bitmap_word(InvIndex c, int32_t doc0, uint32_t id, uint32_t* lds_words) {
+  const uint32_t key = (uint32_t)doc0 >> 16;
+  const uint32_t lo16 = (uint32_t)doc0 & 0xFFFFu;  // multiple of 2048
+  const int lane = lane_id();
+  int32_t a = (int32_t)c.dir[id], z = (int32_t)c.dir[id + 1] - 1;
   int32_t ci = -1;
   while (a <= z) {
     const int32_t mid = (a + z) >> 1;
-    const uint32_t k = c.inv_ct[mid].key;
+    const uint32_t k = c.ct[mid].key;
     if (k == key) { ci = mid; break; }
     if (k < key) a = mid + 1; else z = mid - 1;
   }
   if (ci < 0) return 0u;
-  const DevContainer ct = c.inv_ct[ci];
+  const DevContainer ct = c.ct[ci];
   const uint32_t my0 = lo16 + 32u * lane;  // my first doc within the container
   if (ct.type == PGPU_CT_BITMAP) {
-    return ((const uint32_t*)(c.inv_data + ct.offset))[my0 >> 5];
+    return gld((const uint32_t*)(c.data + ct.offset), my0 >> 5);
   }
   if (ct.type == PGPU_CT_RUN) {
-    const uint16_t* r = (const uint16_t*)(c.inv_data + ct.offset);
+    const uint16_t* r = (const uint16_t*)(c.data + ct.offset);
     int32_t l = 0, h = (int32_t)ct.card;
     while (l < h) {  // first run whose end >= lo16
       const int32_t m = (l + h) >> 1;
@@ -383,7 +517,7 @@ __device__ __noinline__ uint32_t bitmap_word(const DevColumn& c, const WTile& t,
     return w;
   }
   // ARRAY: values in [lo16, lo16 + WT) scattered to their owner lanes through LDS
-  const uint16_t* v = (const uint16_t*)(c.inv_data + ct.offset);
+  const uint16_t* v = (const uint16_t*)(c.data + ct.offset);
   int32_t l = 0, h = (int32_t)ct.card;
   while (l < h) { const int32_t m = (l + h) >> 1; if (v[m] < lo16) l = m + 1; else h = m; }
   const int32_t first = l;
@@ -401,13 +535,13 @@ __device__ __noinline__ uint32_t bitmap_word(const DevColumn& c, const WTile& t,
   return w;
 }
 
-__device__ __noinline__ uint32_t sorted_ranges_word(const int32_t* rg, int n, const WTile& t) {
-  const int32_t d0 = t.lane_doc0, d1 = d0 + 31;
-  const int32_t w0 = t.doc0, w1 = t.doc0 + WT - 1;
+__device__ __noinline__ uint32_t sorted_ranges_word(const int32_t* rg, int n, int32_t doc0) {
+  const int32_t d0 = doc0 + 32 * lane_id(), d1 = d0 + 31;
+  const int32_t w0 = doc0, w1 = doc0 + WT - 1;
   int32_t l = 0, h = n;
   while (l < h) { const int32_t m = (l + h) >> 1; if (rg[2 * m + 1] < w0) l = m + 1; else h = m; }
   uint32_t w = 0;
-  for (int32_t i = l; i < n; ++i) {  // uniform over the ranges overlapping the wave tile
+  for (int32_t i = l; i < n; ++i) {  // uniform over the ranges overlapping the tile
     const int32_t s = rg[2 * i], e = rg[2 * i + 1];
     if (s > w1) break;
     if (e >= d0 && s <= d1) {
@@ -418,339 +552,791 @@ __device__ __noinline__ uint32_t sorted_ranges_word(const int32_t* rg, int n, co
   return w;
 }
 
-// ---- driving-column prefetch (LDS DMA one wave tile ahead) ---------------------------------------------------------
-__device__ __forceinline__ int seg_of_tile(const DevParams& p, int tile) {
+FI bool in_sorted_ranges(const int32_t* rg, int n, int32_t d) {
+  int32_t l = 0, h = n;
+  while (l < h) { const int32_t m = (l + h) >> 1; if (rg[2 * m + 1] < d) l = m + 1; else h = m; }
+  return l < n && rg[2 * l] <= d;
+}
+
+// ---- workgroup LDS carve ------------------------------------------------------------------------------------------
+// [full flags | free flags | loader instr counts] | 7 x consumer area | LDS group table | ring slots
+struct Lds {
+  int* full;
+  int* freef;
+  int* icnt;
+  unsigned char* cons;
+  int64_t* ltab;
+  unsigned char* ring;
+};
+
+FI Lds carve(unsigned char* base, const DevParams& p) {
+  Lds L;
+  L.full = (int*)base;
+  L.freef = L.full + PGPU_RING_MAX;
+  L.icnt = L.freef + PGPU_RING_MAX;
+  L.cons = base + PGPU_FLAG_BYTES;
+  L.ltab = (int64_t*)(L.cons + PGPU_NCONS * PGPU_CONS_BYTES);
+  L.ring = (unsigned char*)L.ltab + ((p.ltab_bytes + 15) & ~15);
+  return L;
+}
+
+// Segment / tile cursor over a contiguous global tile range (the segment's tile count is cached: advancing costs
+// a scalar load only when it crosses into the next segment).
+struct Cursor {
+  int seg;
+  int tile_in_seg;
+  int ntiles;
+};
+
+FI Cursor cursor_at(const DevParams& p, int tile) {
   int lo = 0, hi = p.nseg - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (p.segs[mid].tile_begin <= tile) lo = mid; else hi = mid - 1;
+    if (cld(&p.segs[mid].tile_begin) <= tile) lo = mid; else hi = mid - 1;
   }
-  return lo;
+  Cursor c;
+  c.seg = lo;
+  c.tile_in_seg = tile - cld(&p.segs[lo].tile_begin);
+  c.ntiles = cld(&p.segs[lo].ntiles);
+  return c;
+}
+// Returns true when the cursor moved into another segment.
+FI bool cursor_advance(const DevParams& p, Cursor& c, int k) {
+  c.tile_in_seg += k;
+  bool moved = false;
+  while (c.tile_in_seg >= c.ntiles && c.seg < p.nseg - 1) {
+    c.tile_in_seg -= c.ntiles;
+    ++c.seg;
+    c.ntiles = cld(&p.segs[c.seg].ntiles);
+    moved = true;
+  }
+  return moved;
 }
 
-// Issue global_load_lds (16 B per lane, 1 KiB per instruction) of the driving column of wave tile `tile` into
-// `buf`; returns false when that tile's segment has no driving column.  The caller has finished reading `buf`.
-__device__ __forceinline__ bool prefetch_tile(const DevParams& p, int tile, uint32_t* buf) {
-  if (tile >= p.total_tiles) return false;
-  const DevSeg& sg = p.segs[seg_of_tile(p, tile)];
-  if (sg.pf_pc < 0) return false;
-  const DevInstr& in = p.instrs[sg.prog_begin + sg.pf_pc];
-  const DevColumn& c = p.cols[sg.col_begin + in.col];
-  const int b = c.bits;
-  const char* src = (const char*)(c.fwd + (size_t)(tile - sg.tile_begin) * 64 * b);
-  const int lane = threadIdx.x & 63;
-  const int chunks = (b + 3) >> 2;  // 1 KiB chunks of the 256*b-byte wave tile (last one may be partial)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of buf are complete (WAR)
-  for (int k = 0; k < chunks; ++k) {
-    const int byte = k * 1024 + lane * 16;
-    if (byte < 256 * b) {
-      __builtin_amdgcn_global_load_lds((const void*)(src + byte),
-                                       (__attribute__((address_space(3))) void*)(buf + k * 256), 16, 0, 0);
+// ================================================================================================================
+// LOADER
+// ================================================================================================================
+// The loader's copy of its current segment's staging plan, in SGPRs (fixed-size, statically indexed).
+struct StageCache {
+  int nst;
+  int instrs;
+  const char* fwd[PGPU_MAX_STAGE];
+  int bits[PGPU_MAX_STAGE];
+  int off[PGPU_MAX_STAGE];
+};
+FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
+  const DevSeg* sg = p.segs + seg;
+  sc.nst = cld(&sg->nstage);
+  sc.instrs = cld(&sg->stage_instrs);
+  const DevColumn* cols = p.cols + cld(&sg->col_begin);
+#pragma unroll
+  for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
+    if (j < sc.nst) {
+      const int qc = cld(&sg->stage_col[j]);
+      sc.fwd[j] = (const char*)cld(&cols[qc].fwd);
+      sc.bits[j] = cld(&cols[qc].bits);
+      sc.off[j] = cld(&sg->stage_off[j]);
+    } else {
+      sc.fwd[j] = nullptr;
+      sc.bits[j] = 0;
+      sc.off[j] = 0;
     }
   }
-  return true;
 }
 
-// ---- filter program ------------------------------------------------------------------------------------------------
-// Returns this lane's match word for the wave tile.  The driving column (instruction pf_pc) of this tile is in
-// cv.pf; once it is decoded the DMA of the next tile (`next_tile`) is issued into the same buffer (*pf_issued).
-__device__ __forceinline__ uint32_t run_filter(const DevParams& p, const Carve& cv, const WTile& t, int next_tile,
-                                               bool* pf_issued, uint32_t* scratch_words, int64_t& scanned,
-                                               int64_t& sector_bytes, int64_t& dense_bytes) {
-  const DevSeg& s = *t.seg;
-  if (s.prog_len == 0) return t.valid;
-  const bool stats = p.flags & PGPU_FLAG_STATS;
-  const int lane = threadIdx.x & 63;
+// DMA the staged columns of one tile into `slot` (16 B per lane, 1 KiB per instruction; widths that are multiples
+// of 8 bits skip one 16-B pad chunk per lane record, pgpu_stage_region_bytes).
+FI void issue_tile(const StageCache& sc, int tile_in_seg, unsigned char* slot) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
+    if (j >= sc.nst) break;
+    const int b = sc.bits[j];
+    const char* src = sc.fwd[j] + (size_t)tile_in_seg * 256 * b;
+    unsigned char* dst = slot + sc.off[j];
+    if (b % 8 != 0) {
+      const int ninstr = (b + 3) >> 2;
+      const char* ls = src + 16 * lane;
+      for (int k = 0; k < ninstr; ++k) {
+        if (64 * k + lane < 16 * b)
+          __builtin_amdgcn_global_load_lds((const void*)(ls + 1024 * k), (LAS void*)(dst + 1024 * k), 16, 0, 0);
+      }
+    } else {
+      const int q = b >> 2, ninstr = q + 1;  // q chunks + 1 pad chunk per lane record
+      for (int k = 0; k < ninstr; ++k) {
+        const int pos = 64 * k + lane;
+        const int r = pos / (q + 1), s = pos - r * (q + 1);
+        if (s < q)
+          __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (r * q + s)), (LAS void*)(dst + 1024 * k), 16, 0,
+                                           0);
+      }
+    }
+  }
+}
+
+// Loader `li` streams tiles li, li + NLOAD, ... of the workgroup's range into ring slot (seq % R).  Slot k is
+// published (FULL = k+1) once its DMAs have landed, which the loader learns from a counted vmcnt: it keeps at most
+// `inflight` of its own unpublished tiles and 63 instructions queued.
+FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Prof& pf) {
+  if (li >= ntiles) return;
+  const int64_t t_start = now(pf);
+  const int R = p.ring_slots, S = p.slot_bytes, P = p.inflight, budget = 63 - p.max_instrs;
+  // issue cursor and its staging plan; publish cursor (instruction count of the oldest unpublished tile)
+  Cursor ci = cursor_at(p, t0 + li), cp = ci;
+  StageCache sc;
+  load_stage(p, ci.seg, sc);
+  int cp_instrs = sc.instrs;
+  int seq = li, pub = li, pend = 0, slot = li % R, pslot = slot, nunpub = 0;
+  auto publish_one = [&]() {
+    const int64_t t0w = now(pf);
+    wait_vmcnt(pend - cp_instrs);
+    PROF_ADD(pf, PGPU_P_L_PUB, t0w);
+    loader_flag_store(&L.full[pslot], pub + 1);
+    pend -= cp_instrs;
+    --nunpub;
+    pub += PGPU_NLOAD;
+    pslot += PGPU_NLOAD;
+    if (pslot >= R) pslot -= R;
+    if (pub < ntiles && cursor_advance(p, cp, PGPU_NLOAD)) cp_instrs = cld(&p.segs[cp.seg].stage_instrs);
+  };
+  for (;;) {
+    while (nunpub > 0 && (nunpub > P || pend > budget || seq >= ntiles)) publish_one();
+    if (seq >= ntiles) break;
+    if (seq >= R) {
+      // the slot's previous tile must have been consumed; publish what is in flight while waiting
+      const int64_t t0f = now(pf);
+      while (loader_flag_load(&L.freef[slot]) < seq - R + 1) {
+        if (nunpub > 0) publish_one();
+        else __builtin_amdgcn_s_sleep(1);
+      }
+      PROF_ADD(pf, PGPU_P_L_FREE, t0f);
+    }
+    const int64_t t0i = now(pf);
+    issue_tile(sc, ci.tile_in_seg, L.ring + (size_t)slot * S);
+    PROF_ADD(pf, PGPU_P_L_ISSUE, t0i);
+    pend += sc.instrs;
+    ++nunpub;
+    seq += PGPU_NLOAD;
+    slot += PGPU_NLOAD;
+    if (slot >= R) slot -= R;
+    if (seq < ntiles && cursor_advance(p, ci, PGPU_NLOAD)) load_stage(p, ci.seg, sc);
+  }
+  PROF_ADD(pf, PGPU_P_L_TOTAL, t_start);
+}
+
+// ================================================================================================================
+// CONSUMERS
+// ================================================================================================================
+struct Cons {
+  uint32_t* masks;  // [MAXS][64]
+  int32_t* list;    // [PGPU_LIST]
+  int64_t* acc;     // [MAX_AGGS]  aggregation-only partials of this wave
+};
+
+// Scalars of the consumer's current segment (SGPRs); arrays stay behind `sg` and are read with cld.
+struct SegState {
+  const DevSeg* sg;
+  const DevColumn* cols;
+  const int32_t* const* remaps;
+  int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
+};
+FI void load_seg(const DevParams& p, int seg, SegState& ss) {
+  const DevSeg* sg = p.segs + seg;
+  ss.sg = sg;
+  ss.cols = p.cols + cld(&sg->col_begin);
+  ss.remaps = p.remaps + cld(&sg->remap_begin);
+  ss.num_docs = cld(&sg->num_docs);
+  ss.nstage = cld(&sg->nstage);
+  ss.prog_begin = cld(&sg->prog_begin);
+  ss.prog_len = cld(&sg->prog_len);
+  ss.rprog_begin = cld(&sg->rprog_begin);
+  ss.rprog_len = cld(&sg->rprog_len);
+  ss.agg_mode = cld(&sg->agg_mode);
+  ss.nreg = cld(&sg->nreg);
+  ss.reg_col0 = cld(&sg->reg_col[0]);
+  ss.reg_col1 = cld(&sg->reg_col[1]);
+}
+FI DevColumn col_of(const SegState& ss, int col) { return cld(ss.cols + col); }
+
+FI uint32_t& mrow(const Cons& c, int s) { return c.masks[s * 64 + lane_id()]; }
+
+// Staged-region pointer of query column `col` in `slot` (nullptr: not staged / slot released).
+FI const uint32_t* staged_region(const SegState& ss, const unsigned char* slot, int col) {
+  if (!slot) return nullptr;
+  for (int j = 0; j < ss.nstage; ++j)
+    if (cld(&ss.sg->stage_col[j]) == col) return (const uint32_t*)(slot + cld(&ss.sg->stage_off[j]));
+  return nullptr;
+}
+
+// Filter program interpreter over mask words.  Leaf evaluation is delegated to a context:
+//   TileCtx - word = this lane's 32 consecutive docs of a tile (dense program)
+//   DocCtx  - word = this lane's U queued candidate docs (residual program)
+struct TileCtx {
+  const SegState* ss;
+  const unsigned char* slot;
+  int tile_in_seg;
+  int32_t doc0;
+  int32_t lane_doc0;
+  uint32_t valid;
+};
+struct DocCtx {
+  const SegState* ss;
+  int32_t doc[U];
+  uint32_t valid;
+};
+
+FI uint32_t leaf_scan(const DevParams& p, const TileCtx& t, const DevInstr& in, uint32_t care, int64_t& dense_bytes) {
+  const Pred pr = make_pred(in, p.pool);
+  if (in.kind == PGPU_COL_FIXED_BIT) {
+    const uint32_t* region = in.stage_off >= 0 && t.slot ? (const uint32_t*)(t.slot + in.stage_off) : nullptr;
+    if (!region && lane_id() == 0) dense_bytes += (int64_t)WT * in.bits / 8;
+    uint32_t ids[32];
+    decode_ids(in.bits, region, in.fwd, t.tile_in_seg, ids);
+    return pred_ids(ids, pr) & care;
+  }
+  // sorted column scanned: per-doc binary search for the care docs
+  uint32_t m = 0;
+  for (uint32_t left = care; left; left &= left - 1) {
+    const int i = __builtin_ctz(left);
+    if (eval_pred(pr, sorted_dict_id(in.sorted, in.card, t.lane_doc0 + i))) m |= 1u << i;
+  }
+  return m;
+}
+FI uint32_t leaf_scan(const DevParams& p, const DocCtx& t, const DevInstr& in, uint32_t care, int64_t&) {
+  const Pred pr = make_pred(in, p.pool);
+  uint32_t ids[U];
+  gather_ids(colref(in), t.doc, ids);
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) m |= (uint32_t)eval_pred(pr, ids[u]) << u;
+  return m & care;
+}
+FI uint32_t leaf_inv(const DevParams& p, const TileCtx& t, const DevInstr& in, uint32_t* scratch) {
+  const DevColumn c = col_of(*t.ss, in.col);
+  uint32_t m = 0;
+  const InvIndex ix{c.inv_dir, c.inv_ct, c.inv_data};
+  for (int i = 0; i < in.n; ++i) m |= bitmap_word(ix, t.doc0, (uint32_t)cld(p.pool, in.pool_off + i), scratch);
+  return in.negate ? ~m : m;
+}
+FI uint32_t leaf_inv(const DevParams& p, const DocCtx& t, const DevInstr& in, uint32_t*) {
+  const DevColumn c = col_of(*t.ss, in.col);
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    bool h = false;
+    if ((t.valid >> u) & 1u)
+      for (int i = 0; i < in.n && !h; ++i)
+        h = bitmap_contains(InvIndex{c.inv_dir, c.inv_ct, c.inv_data}, (uint32_t)cld(p.pool, in.pool_off + i), (uint32_t)t.doc[u]);
+    m |= (uint32_t)h << u;
+  }
+  return in.negate ? ~m : m;
+}
+FI uint32_t leaf_sorted(const DevParams& p, const TileCtx& t, const DevInstr& in) {
+  const uint32_t m = sorted_ranges_word(p.pool + in.pool_off, in.n, t.doc0);
+  return in.negate ? ~m : m;
+}
+FI uint32_t leaf_sorted(const DevParams& p, const DocCtx& t, const DevInstr& in) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) m |= (uint32_t)in_sorted_ranges(p.pool + in.pool_off, in.n, t.doc[u]) << u;
+  return in.negate ? ~m : m;
+}
+
+template <class Ctx>
+FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, const Ctx& t, int64_t& scanned,
+                        int64_t& dense_bytes, Prof& pf) {
+  uint32_t* scratch = cv.masks + (MAXS - 1) * 64;
   int pc = 0;
-  while (pc < s.prog_len) {
-    const DevInstr in = p.instrs[s.prog_begin + pc];
+  while (pc < len) {
+    const int64_t tfe = now(pf);
+    const DevInstr in = cld(p.instrs + begin + pc);
+    if (pf.on) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      PROF_ADD(pf, PGPU_P_C_FETCH, tfe);
+    }
     int next = pc + 1;
-    const uint32_t care = in.care < 0 ? t.valid : slot(cv, in.care);
+    const uint32_t care = in.care < 0 ? t.valid : mrow(cv, in.care);
     switch (in.op) {
-      case PGPU_I_ALL: slot(cv, in.dst) = t.valid; break;
-      case PGPU_I_EMPTY: slot(cv, in.dst) = 0u; break;
+      case PGPU_I_ALL: mrow(cv, in.dst) = t.valid; break;
+      case PGPU_I_EMPTY: mrow(cv, in.dst) = 0u; break;
       case PGPU_I_SCAN: {
-        const DevColumn& c = t.cols[in.col];
-        const Pred pr = make_pred(in, p.pool);
-        const bool prestaged = pc == s.pf_pc;
-        int ncare = 0;
-        if (!prestaged) ncare = wave_sum_i32(__popc(care));
-        const bool dense = prestaged || (c.kind == PGPU_COL_FIXED_BIT && ncare * 32 >= t.ndocs);
-        uint32_t m;
-        if (dense) {
-          uint32_t ids[32];
-          if (prestaged) {
-            decode_lds(c.bits, cv.pf, ids);
-            *pf_issued = true;
-            cv.pf_have[0] = prefetch_tile(p, next_tile, cv.pf);
-          } else {
-            decode_hbm(c, t.tile_in_seg, ids);
-          }
-          m = pred_ids(ids, pr) & t.valid;
-          if (lane == 0) {
-            scanned += t.ndocs;
-            dense_bytes += ((int64_t)t.ndocs * c.bits + 7) / 8;
-          }
-        } else {
-          uint32_t* sect = nullptr;
-          if (stats && c.kind == PGPU_COL_FIXED_BIT) {
-            sect = scratch_words;
-            scratch_words[lane] = 0u;  // 64 words = 2048 sectors >= 2048 docs * 31 bits / 256
-            wave_sync();
-          }
-          m = scan_sparse(c, t, pr, care, sect);
-          if (sect) {
-            wave_sync();
-            const int cnt = wave_sum_i32(__popc(scratch_words[lane]));
-            if (lane == 0) sector_bytes += 32ll * cnt;
-            wave_sync();
-          }
-          if (lane == 0) scanned += ncare;
-        }
-        slot(cv, in.dst) = m & care;
-        break;
-      }
-      case PGPU_I_INV: {
-        const DevColumn& c = t.cols[in.col];
+        const int n = wave_sum_i32(__popc(care));
         uint32_t m = 0;
-        for (int i = 0; i < in.n; ++i) m |= bitmap_word(c, t, (uint32_t)p.pool[in.pool_off + i], scratch_words);
-        if (in.negate) m = ~m;
-        slot(cv, in.dst) = m & t.valid;
+        const int64_t tde = now(pf);
+        if (n) m = leaf_scan(p, t, in, care, dense_bytes);
+        if (pf.on) {
+          m = sgpr(m) == 0xdeadbeefu ? m + 1 : m;  // force completion before the timestamp
+          PROF_ADD(pf, PGPU_P_C_DECODE, tde);
+        }
+        if (lane_id() == 0) scanned += n;
+        mrow(cv, in.dst) = m;
         break;
       }
-      case PGPU_I_SORTED: {
-        uint32_t m = sorted_ranges_word(p.pool + in.pool_off, in.n, t);
-        if (in.negate) m = ~m;
-        slot(cv, in.dst) = m & t.valid;
-        break;
-      }
-      case PGPU_I_AND_BEGIN: slot(cv, in.dst) = care; break;
+      case PGPU_I_INV: mrow(cv, in.dst) = leaf_inv(p, t, in, scratch) & t.valid; break;
+      case PGPU_I_SORTED: mrow(cv, in.dst) = leaf_sorted(p, t, in) & t.valid; break;
+      case PGPU_I_AND_BEGIN: mrow(cv, in.dst) = care; break;
       case PGPU_I_AND_CHILD: {
-        const uint32_t a = slot(cv, in.dst) & slot(cv, in.src);
-        slot(cv, in.dst) = a;
+        const uint32_t a = mrow(cv, in.dst) & mrow(cv, in.src);
+        mrow(cv, in.dst) = a;
         if (!__ballot(a != 0u)) next = in.jump;
         break;
       }
-      case PGPU_I_OR_BEGIN: slot(cv, in.dst) = 0u; break;
-      case PGPU_I_OR_CHILD: slot(cv, in.dst) |= slot(cv, in.src); break;
-      case PGPU_I_NOT: slot(cv, in.dst) = ~slot(cv, in.src) & care; break;
+      case PGPU_I_OR_BEGIN: mrow(cv, in.dst) = 0u; break;
+      case PGPU_I_OR_CHILD: mrow(cv, in.dst) |= mrow(cv, in.src); break;
+      case PGPU_I_NOT: mrow(cv, in.dst) = ~mrow(cv, in.src) & care; break;
       default: break;  // AND_END / OR_END
     }
     pc = next;
   }
-  return slot(cv, 0);
+  return mrow(cv, 0);
 }
 
-// ---- aggregation ---------------------------------------------------------------------------------------------------
-struct Acc {
-  int64_t i;
-  double d;
+// ---- aggregation helpers ------------------------------------------------------------------------------------------
+// Fold this lane's partial `v` of agg slot `a` into the wave's LDS accumulator (aggregation-only mode).
+FI void acc_commit(const Cons& cv, int a, int32_t op, int64_t v) {
+  const int64_t r = wave_combine(op, v);
+  if (lane_id() == 0) cv.acc[a] = cell_combine(op, cv.acc[a], r);
+}
+// Per-lane register partials of the first NREG_ACC aggregations (reduced across the wave once, at the end);
+// further aggregations fold into the LDS accumulator immediately.
+#define NREG_ACC 4
+struct LaneAcc {
+  int64_t v[NREG_ACC];
 };
-
-__device__ __forceinline__ void acc_add(Acc& a, const DevAgg& ag, const DevColumn& c, uint32_t id) {
-  if (ag.op == PGPU_RED_SUM_I64) a.i += value_i64(c.dict, ag.vtype, id);
-  else if (ag.op == PGPU_RED_SUM_F64) a.d += value_f64(c.dict, ag.vtype, id);
-  else {
-    const int64_t k = minmax_key(c.dict, ag.vtype, id);
-    a.i = ag.op == PGPU_RED_MIN_I64 ? (k < a.i ? k : a.i) : (k > a.i ? k : a.i);
+FI void lacc_add(LaneAcc& la, const Cons& cv, int a, int32_t op, int64_t part) {
+  if (a < NREG_ACC) {
+#pragma unroll
+    for (int k = 0; k < NREG_ACC; ++k)
+      if (k == a) la.v[k] = cell_combine(op, la.v[k], part);
+  } else {
+    acc_commit(cv, a, op, part);
   }
 }
 
-// table update for one doc: `tab` = LDS or HBM dense table, section-major
-__device__ __forceinline__ void table_update(int64_t* tab, uint64_t G, const DevAgg& ag, const DevColumn& c,
-                                             uint32_t key, uint32_t id) {
-  int64_t* cell = tab + (size_t)ag.sec * G + key;
-  if (ag.op == PGPU_RED_SUM_I64) atomicAdd((unsigned long long*)cell, (unsigned long long)value_i64(c.dict, ag.vtype, id));
-  else if (ag.op == PGPU_RED_SUM_F64) atomicAdd((double*)cell, value_f64(c.dict, ag.vtype, id));
-  else if (ag.op == PGPU_RED_MIN_I64) atomicMin((long long*)cell, (long long)minmax_key(c.dict, ag.vtype, id));
-  else atomicMax((long long*)cell, (long long)minmax_key(c.dict, ag.vtype, id));
+
+template <int MODE>
+FI int64_t* table_base(const DevParams& p, const Lds& L) {
+  return MODE == PGPU_MODE_LDS ? L.ltab : p.table;
+}
+
+// Sparse (per-doc) aggregation of the survivors `m` among this lane's U docs: group key = mixed radix of the
+// remapped group ids, COUNT into section 0, every other aggregation gathers its id and dictionary value.
+template <int MODE>
+FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
+                   const int32_t (&doc)[U], uint32_t m) {
+  uint32_t key[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) key[u] = 0;
+  if (MODE != PGPU_MODE_AGG) {
+    for (int g = 0; g < p.ngcols; ++g) {
+      const DevColumn c = col_of(ss, p.gcols[g]);
+      const int32_t* remap = cld(ss.remaps, g);
+      uint32_t id[U];
+      gather_ids(colref(c), doc, id);
+#pragma unroll
+      for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
+      remap_ids(remap, id);
+#pragma unroll
+      for (int u = 0; u < U; ++u) key[u] += id[u] * p.gstride[g];
+    }
+    int64_t* tab = table_base<MODE>(p, L);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if ((m >> u) & 1u) atomicAdd((unsigned long long*)&tab[key[u]], 1ull);
+  }
+  for (int a = 0; a < p.nagg; ++a) {
+    const DevAgg ag = p.aggs[a];
+    if (ag.fn == PGPU_AGG_COUNT) continue;
+    const DevColumn c = col_of(ss, ag.col);
+    uint32_t id[U];
+    gather_ids(colref(c), doc, id);
+#pragma unroll
+    for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
+    int64_t v[U];
+    gather_cells(c.dict, ag.vtype, ag.op, id, v);
+    if (MODE == PGPU_MODE_AGG) {
+      int64_t part = sec_identity(ag.op);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if ((m >> u) & 1u) part = cell_combine(ag.op, part, v[u]);
+      lacc_add(la, cv, a, ag.op, part);
+    } else {
+      int64_t* tab = table_base<MODE>(p, L) + (size_t)ag.sec * p.G;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if ((m >> u) & 1u) cell_atomic(&tab[key[u]], ag.op, v[u]);
+    }
+  }
+}
+
+// 32-B sectors of a b-bit column first touched by `doc` after `prev_doc` (ascending entries; stats pass only).
+FI int new_sectors(uint32_t b, int32_t doc, bool live, int32_t prev_doc, bool prev_live) {
+  if (!live) return 0;
+  const int64_t s0 = ((int64_t)doc * b) >> 8, s1 = ((int64_t)(doc + 1) * b - 1) >> 8;
+  int64_t from = s0;
+  if (prev_live) {
+    const int64_t pe = ((int64_t)(prev_doc + 1) * b - 1) >> 8;
+    if (pe + 1 > from) from = pe + 1;
+  }
+  return s1 >= from ? (int)(s1 - from + 1) : 0;
+}
+
+// Flush the candidate queue (doc ids of one segment, ascending): residual filter per doc, then sparse aggregation.
+template <int MODE>
+FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, int n,
+                    int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
+  const int lane = lane_id();
+  const bool stats = p.flags & PGPU_FLAG_STATS;
+  wave_sync();
+  for (int base = 0; base < n; base += 64 * U) {
+    DocCtx d;
+    d.ss = &ss;
+    d.valid = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * 64 + lane;
+      const bool ok = e < n;
+      d.doc[u] = ok ? cv.list[e] : 0;
+      d.valid |= (uint32_t)ok << u;
+    }
+    uint32_t m = d.valid;
+    if (ss.rprog_len > 0) m = run_program(p, cv, ss.rprog_begin, ss.rprog_len, d, scanned, dense_bytes, pf);
+    const int nm = wave_sum_i32(__popc(m));
+    if (lane == 0) matched += nm;
+    if (stats) {
+      // 32-B sectors of every gathered forward index: residual scan columns over the candidates,
+      // aggregation / group columns over the survivors
+      int sec = 0;
+      for (int pc = 0; pc < ss.rprog_len; ++pc) {
+        const DevInstr in = cld(p.instrs + ss.rprog_begin + pc);
+        if (in.op != PGPU_I_SCAN || in.kind != PGPU_COL_FIXED_BIT) continue;
+        const uint32_t b = (uint32_t)in.bits;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int32_t pd = __shfl_up(d.doc[u], 1, 64);
+          sec += new_sectors(b, d.doc[u], (d.valid >> u) & 1u, pd, lane > 0);
+        }
+      }
+      if (nm && ss.agg_mode == PGPU_AM_SPARSE) {
+        for (int k = 0; k < p.ncols; ++k) {
+          bool used = false;
+          for (int g = 0; g < p.ngcols; ++g) used |= p.gcols[g] == k;
+          for (int a = 0; a < p.nagg; ++a) used |= p.aggs[a].fn != PGPU_AGG_COUNT && p.aggs[a].col == k;
+          if (!used) continue;
+          const DevColumn c = col_of(ss, k);
+          if (c.kind != PGPU_COL_FIXED_BIT) continue;
+          const uint32_t b = (uint32_t)c.bits;
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const bool live = (m >> u) & 1u;
+            const int32_t pd = __shfl_up(d.doc[u], 1, 64);
+            const bool pl = lane > 0 && __shfl_up((int)live, 1, 64);
+            sec += new_sectors(b, d.doc[u], live, pd, pl);
+          }
+        }
+      }
+      const int tot = wave_sum_i32(sec);
+      if (lane == 0) sector_bytes += 32ll * tot;
+    }
+    if (nm && ss.agg_mode == PGPU_AM_SPARSE) sparse_agg<MODE>(p, L, cv, la, ss, d.doc, m);
+  }
+  wave_sync();
+}
+
+// Dense aggregation of this lane's matched docs `mm` of the tile from decoded ids (registers or the held slot).
+// Per half tile (16 docs per lane): compact keys and ids of the matched docs into the LDS lists, then gather
+// dictionary values with full lanes (4 rounds in flight) and fold them into partials / table cells.
+template <int MODE>
+FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, const TileCtx& t,
+                  uint32_t mm, const uint32_t (&ra)[32], const uint32_t (&rb)[32]) {
+  const int lane = lane_id();
+  int32_t* klist = cv.list;                 // keys   [1024]
+  int32_t* vlist = cv.list + 1024;          // values [1024]
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t hm = (mm >> (16 * h)) & 0xFFFFu;
+    const int cnt = __popc(hm);
+    const int nh = wave_sum_i32(cnt);
+    if (nh == 0) continue;
+    const int off = wave_excl_scan(cnt);
+    // operand list: group columns first (keys), then the non-COUNT aggregations
+    uint32_t key[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) key[i] = 0;
+    const int nops = (MODE != PGPU_MODE_AGG ? p.ngcols : 0) + p.nagg;
+    for (int op = 0; op < nops; ++op) {
+      const bool is_key = MODE != PGPU_MODE_AGG && op < p.ngcols;
+      const int ai = op - (MODE != PGPU_MODE_AGG ? p.ngcols : 0);
+      DevAgg ag;
+      int col;
+      if (is_key) {
+        col = p.gcols[op];
+      } else {
+        ag = p.aggs[ai];
+        if (ag.fn == PGPU_AGG_COUNT) continue;
+        col = ag.col;
+      }
+      uint32_t lo[16];
+      {
+        uint32_t ids[32];
+        if (ss.nreg > 0 && col == ss.reg_col0) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) ids[i] = ra[i];
+        } else if (ss.nreg > 1 && col == ss.reg_col1) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) ids[i] = rb[i];
+        } else {
+          const DevColumn c = col_of(ss, col);
+          decode_ids(c.bits, staged_region(ss, t.slot, col), c.fwd, t.tile_in_seg, ids);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lo[i] = h ? ids[16 + i] : ids[i];
+      }
+      if (is_key) {
+        const int32_t* remap = cld(ss.remaps, op);
+        if (remap) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) lo[i] = lane_bit(hm, i) ? lo[i] : 0u;
+          remap_ids(remap, lo);
+        }
+        const uint32_t st = p.gstride[op];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) key[i] += lo[i] * st;
+        if (op == p.ngcols - 1) {
+          int k = off;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (lane_bit(hm, i)) klist[k++] = (int32_t)key[i];
+          wave_sync();
+          int64_t* tab = table_base<MODE>(p, L);
+          for (int e = lane; e < nh; e += 64) atomicAdd((unsigned long long*)&tab[(uint32_t)klist[e]], 1ull);
+        }
+        continue;
+      }
+      const DevColumn c = col_of(ss, col);
+      {
+        int k = off;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (lane_bit(hm, i)) vlist[k++] = (int32_t)lo[i];
+      }
+      wave_sync();
+      int64_t part = sec_identity(ag.op);
+      int64_t* tab = table_base<MODE>(p, L) + (size_t)ag.sec * p.G;
+      for (int r0 = 0; r0 * 64 < nh; r0 += 8) {
+        uint32_t idx[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int e = lane + 64 * (r0 + r);
+          idx[r] = e < nh ? (uint32_t)vlist[e] : 0u;
+        }
+        int64_t v[8];
+        gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int e = lane + 64 * (r0 + r);
+          if (e < nh) {
+            if (MODE == PGPU_MODE_AGG) part = cell_combine(ag.op, part, v[r]);
+            else cell_atomic(&tab[(uint32_t)klist[e]], ag.op, v[r]);
+          }
+        }
+      }
+      if (MODE == PGPU_MODE_AGG) lacc_add(la, cv, ai, ag.op, part);
+      wave_sync();
+    }
+    wave_sync();
+  }
+}
+
+struct Stats {
+  int64_t matched, scanned, sector_bytes, dense_bytes;
+};
+
+template <int MODE>
+FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  const int R = p.ring_slots, S = p.slot_bytes;
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * PGPU_CONS_BYTES;
+    cv.masks = (uint32_t*)base;
+    cv.list = (int32_t*)(base + PGPU_CONS_MASK_BYTES);
+    cv.acc = (int64_t*)(base + PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES);
+  }
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int qn = 0;  // candidate-queue entries (all of segment `ss`)
+  SegState ss;
+  int cseg = -1;
+  Cursor cur;
+  cur.seg = 0;
+  cur.tile_in_seg = 0;
+  cur.ntiles = 0;
+  if (cidx < ntiles) cur = cursor_at(p, t0 + cidx);
+  for (int seq = cidx;; seq += PGPU_NCONS) {
+    const bool end = seq >= ntiles;
+    if (!end && seq != cidx) cursor_advance(p, cur, PGPU_NCONS);
+    const int slot_i = seq % R;
+    const bool segchg = !end && cur.seg != cseg;
+    // single flush site: end of range, segment change, or threshold (the queue then still has room for a tile)
+    if (qn && (end || segchg || qn >= PGPU_CQ_FLUSH)) {
+      const int64_t tq = now(pf);
+      flush_queue<MODE>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+      PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+      qn = 0;
+    }
+    if (end) break;
+    if (segchg) {
+      cseg = cur.seg;
+      load_seg(p, cseg, ss);
+    }
+    unsigned char* slot = L.ring + (size_t)slot_i * S;
+    const int64_t tw = now(pf);
+    while (flag_load(&L.full[slot_i]) != seq + 1) __builtin_amdgcn_s_sleep(1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    PROF_ADD(pf, PGPU_P_C_FULL, tw);
+    const int64_t tf = now(pf);
+    if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+
+    TileCtx t;
+    t.ss = &ss;
+    t.slot = slot;
+    t.tile_in_seg = cur.tile_in_seg;
+    t.doc0 = cur.tile_in_seg * WT;
+    t.lane_doc0 = t.doc0 + 32 * lane;
+    {
+      const int ndocs = min(WT, ss.num_docs - t.doc0);
+      const int rem = ndocs - 32 * lane;
+      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+      if (p.flags & PGPU_FLAG_STATS)
+        for (int j = 0; j < ss.nstage; ++j) {
+          const int b = col_of(ss, cld(&ss.sg->stage_col[j])).bits;
+          if (lane == 0) dense_bytes += ((int64_t)ndocs * b + 7) / 8;
+        }
+    }
+    uint32_t mm = t.valid;
+    if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
+    const int nm = wave_sum_i32(__popc(mm));
+    PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+    const int64_t ta = now(pf);
+    const bool dense = ss.agg_mode == PGPU_AM_DENSE && nm;
+    uint32_t ra[32], rb[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) ra[i] = rb[i] = 0;
+    if (dense) {
+      // copy up to two aggregation / group columns to registers, then hand the slot back to the loader
+      for (int j = 0; j < ss.nreg; ++j) {
+        const int col = j == 0 ? ss.reg_col0 : ss.reg_col1;
+        const DevColumn c = col_of(ss, col);
+        uint32_t ids[32];
+        decode_ids(c.bits, staged_region(ss, slot, col), c.fwd, t.tile_in_seg, ids);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          if (j == 0) ra[i] = ids[i];
+          else rb[i] = ids[i];
+        }
+      }
+    }
+    const bool hold = dense && ss.nreg < 0;
+    if (!hold) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) flag_store(&L.freef[slot_i], seq + 1);
+      t.slot = nullptr;
+    }
+    if (nm) {
+      if (dense) {
+        if (lane == 0) matched += nm;
+        dense_agg<MODE>(p, L, cv, la, ss, t, mm, ra, rb);
+      } else if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
+        if (lane == 0) matched += nm;
+      } else {
+        // queue the candidates (doc ids ascending: lane order, then bit order)
+        int k = qn + wave_excl_scan(__popc(mm));
+        for (uint32_t left = mm; left; left &= left - 1) cv.list[k++] = t.lane_doc0 + __builtin_ctz(left);
+        qn += nm;
+      }
+    }
+    if (hold) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) flag_store(&L.freef[slot_i], seq + 1);
+    }
+    PROF_ADD(pf, PGPU_P_C_AGG, ta);
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  if (MODE == PGPU_MODE_AGG) {
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  }
+  Stats s;
+  s.matched = matched;
+  s.scanned = scanned;
+  s.sector_bytes = sector_bytes;
+  s.dense_bytes = dense_bytes;
+  return s;
 }
 
 // ---- the query kernel ----------------------------------------------------------------------------------------------
 template <int MODE>
-// amdgpu_waves_per_eu(4): 128 VGPRs -> 4 waves per SIMD (16 per CU) to keep enough sparse gathers in flight
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void query_kernel(DevParams p) {
+__global__ __launch_bounds__(NT, 1) void query_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
-  // the wave index through readfirstlane: everything derived from it (tile, segment, program, columns, bit
-  // widths) is then provably wave-uniform and lives in SGPRs, and the bit-width switch is a scalar branch
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  Carve cv;
-  {
-    unsigned char* base = dyn_smem;
-    cv.slots = (uint32_t*)base + wave * MAXS * 64;
-    base += NW * MAXS * 64 * 4;
-    cv.pf_words = p.pf_words;
-    cv.pf = (uint32_t*)base + wave * (size_t)p.pf_words;
-    base += NW * (size_t)p.pf_words * 4;
-    cv.accw = (int64_t*)base + wave * PGPU_MAX_AGGS;
-    base += NW * PGPU_MAX_AGGS * 8;
-    cv.ltab = (int64_t*)base;
-  }
-  uint32_t* scratch = cv.slots + (MAXS - 1) * 64;  // the last slot row doubles as per-wave LDS scratch
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve(dyn_smem, p);
+  for (int i = threadIdx.x; i < 3 * PGPU_RING_MAX; i += NT) L.full[i] = 0;
   if (MODE == PGPU_MODE_LDS) {
     const int n = p.nsec * (int)p.G;
-    for (int i = threadIdx.x; i < n; i += NT) cv.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+    for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
   }
-  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.accw[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
   __syncthreads();
-
-  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;  // lane 0 of each wave owns these
-  const int gw = blockIdx.x * NW + wave, nwaves = gridDim.x * NW;
-  bool have[1];
-  cv.pf_have = have;
-  have[0] = prefetch_tile(p, gw, cv.pf);
-  for (int tile = gw; tile < p.total_tiles; tile += nwaves) {
-    const int sidx = seg_of_tile(p, tile);
-    WTile t;
-    t.seg = &p.segs[sidx];
-    t.cols = p.cols + t.seg->col_begin;
-    t.tile_in_seg = tile - t.seg->tile_begin;
-    t.doc0 = t.tile_in_seg * WT;
-    t.ndocs = min(WT, t.seg->num_docs - t.doc0);
-    t.lane_doc0 = t.doc0 + 32 * lane;
-    {
-      const int rem = t.ndocs - 32 * lane;
-      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
-    }
-    // this tile's driving column has landed in cv.pf (issued one tile ago)
-    if (have[0]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    wave_sync();
-    bool issued = false;
-    const uint32_t mm = run_filter(p, cv, t, tile + nwaves, &issued, scratch, scanned, sector_bytes, dense_bytes);
-    if (!issued) have[0] = prefetch_tile(p, tile + nwaves, cv.pf);
-    const int nm = wave_sum_i32(__popc(mm));
-    if (lane == 0) matched += nm;
-    if (nm == 0) continue;  // uniform
-    const bool dense_post = nm * 32 >= t.ndocs;
-
-    if (MODE == PGPU_MODE_AGG) {
-      for (int a = 0; a < p.nagg; ++a) {
-        const DevAgg ag = p.aggs[a];
-        if (ag.fn == PGPU_AGG_COUNT) continue;
-        const DevColumn& c = t.cols[ag.col];
-        Acc acc;
-        acc.i = sec_identity(ag.op);
-        acc.d = 0.0;
-        if (dense_post && c.kind == PGPU_COL_FIXED_BIT) {
-          uint32_t ids[32];
-          decode_hbm(c, t.tile_in_seg, ids);
+  // this workgroup's contiguous tile range
+  const int t0 = (int)(((int64_t)p.total_tiles * blockIdx.x) / gridDim.x);
+  const int t1 = (int)(((int64_t)p.total_tiles * (blockIdx.x + 1)) / gridDim.x);
+  Stats st;
+  st.matched = st.scanned = st.sector_bytes = st.dense_bytes = 0;
+  Prof pf;
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
 #pragma unroll
-          for (int i = 0; i < 32; ++i)
-            if (lane_bit(mm, i)) acc_add(acc, ag, c, ids[i]);
-        } else {
-          for (uint32_t left = mm; left; left &= left - 1)
-            acc_add(acc, ag, c, gather_id(c, t.lane_doc0 + __builtin_ctz(left)));
-        }
-        if (ag.op == PGPU_RED_SUM_I64) acc.i = wave_sum_i64(acc.i);
-        else if (ag.op == PGPU_RED_SUM_F64) acc.d = wave_sum_f64(acc.d);
-        else if (ag.op == PGPU_RED_MIN_I64) acc.i = wave_min_i64(acc.i);
-        else acc.i = wave_max_i64(acc.i);
-        if (lane == 0) {
-          int64_t& cell = cv.accw[a];
-          if (ag.op == PGPU_RED_SUM_I64) cell += acc.i;
-          else if (ag.op == PGPU_RED_SUM_F64) cell = __double_as_longlong(__longlong_as_double(cell) + acc.d);
-          else if (ag.op == PGPU_RED_MIN_I64) cell = acc.i < cell ? acc.i : cell;
-          else cell = acc.i > cell ? acc.i : cell;
-        }
-      }
-    } else {
-      int64_t* tab = MODE == PGPU_MODE_LDS ? cv.ltab : p.table;
-      bool all_fixed = true;
-      for (int gc = 0; gc < p.ngcols; ++gc) all_fixed &= t.cols[p.gcols[gc]].kind == PGPU_COL_FIXED_BIT;
-      for (int a = 0; a < p.nagg; ++a)
-        if (p.aggs[a].fn != PGPU_AGG_COUNT) all_fixed &= t.cols[p.aggs[a].col].kind == PGPU_COL_FIXED_BIT;
-      if (dense_post && all_fixed) {
-        // one pass over [group columns..., aggregations...]: a single decode site for all of them
-        uint32_t key[32];
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+  if (wave < PGPU_NLOAD) loader(p, L, wave, t0, t1 - t0, pf);
+  else st = consumer<MODE>(p, L, wave - PGPU_NLOAD, t0, t1 - t0, pf);
+  if (pf.on && lane == 0) {
+    int64_t* o = p.prof + ((size_t)blockIdx.x * PGPU_WAVES + wave) * PGPU_NPROF;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) key[i] = 0u;
-        const int nops = p.ngcols + (p.nagg > 0 ? p.nagg : 1);
-        for (int op = 0; op < nops; ++op) {
-          if (op == p.ngcols) {
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-              if (lane_bit(mm, i)) atomicAdd((unsigned long long*)&tab[key[i]], 1ull);
-          }
-          const bool is_key = op < p.ngcols;
-          DevAgg ag;
-          int col;
-          if (is_key) {
-            col = p.gcols[op];
-          } else {
-            if (op - p.ngcols >= p.nagg) break;
-            ag = p.aggs[op - p.ngcols];
-            if (ag.fn == PGPU_AGG_COUNT) continue;
-            col = ag.col;
-          }
-          const DevColumn& c = t.cols[col];
-          uint32_t ids[32];
-          decode_hbm(c, t.tile_in_seg, ids);
-          if (is_key) {
-            const int32_t* remap = p.remaps[t.seg->remap_begin + op];
-            const uint32_t stride = p.gstride[op];
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-              if (lane_bit(mm, i)) key[i] += (remap ? (uint32_t)gld(remap, ids[i]) : ids[i]) * stride;
-          } else {
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-              if (lane_bit(mm, i)) table_update(tab, p.G, ag, c, key[i], ids[i]);
-          }
-        }
-      } else {
-        for (uint32_t left = mm; __ballot(left != 0); left &= left - 1) {
-          if (!left) continue;
-          const int32_t d = t.lane_doc0 + __builtin_ctz(left);
-          uint32_t key = 0;
-          for (int gc = 0; gc < p.ngcols; ++gc) {
-            const DevColumn& c = t.cols[p.gcols[gc]];
-            const int32_t* remap = p.remaps[t.seg->remap_begin + gc];
-            const uint32_t id = gather_id(c, d);
-            key += (remap ? (uint32_t)gld(remap, id) : id) * p.gstride[gc];
-          }
-          atomicAdd((unsigned long long*)&tab[key], 1ull);
-          for (int a = 0; a < p.nagg; ++a) {
-            const DevAgg ag = p.aggs[a];
-            if (ag.fn == PGPU_AGG_COUNT) continue;
-            const DevColumn& c = t.cols[ag.col];
-            table_update(tab, p.G, ag, c, key, gather_id(c, d));
-          }
-        }
-      }
-    }
+    for (int k = 0; k < PGPU_NPROF; ++k) o[k] = pf.t[k];
   }
-  if (have[0]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- epilogue ----
+  const size_t w = (size_t)blockIdx.x * PGPU_WAVES + wave;
   if (lane == 0) {
-    int64_t* st = p.stats + (size_t)(blockIdx.x * NW + wave) * PGPU_NSTATS;
-    st[PGPU_STAT_MATCHED] = matched;
-    st[PGPU_STAT_SCANNED] = scanned;
-    st[PGPU_STAT_SECTOR_BYTES] = sector_bytes;
-    st[PGPU_STAT_DENSE_BYTES] = dense_bytes;
+    int64_t* o = p.stats + w * PGPU_NSTATS;
+    o[PGPU_STAT_MATCHED] = st.matched;
+    o[PGPU_STAT_SCANNED] = st.scanned;
+    o[PGPU_STAT_SECTOR_BYTES] = st.sector_bytes;
+    o[PGPU_STAT_DENSE_BYTES] = st.dense_bytes;
   }
   if (MODE == PGPU_MODE_AGG) {
     // slab[wave][sec]: section 0 = matched count; reduced in wave order by finalize_kernel (deterministic)
-    int64_t* slab = p.slab + (size_t)(blockIdx.x * NW + wave) * p.nsec;
-    if (lane == 0) slab[0] = matched;
-    if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) slab[p.aggs[lane].sec] = cv.accw[lane];
+    int64_t* slab = p.slab + w * p.nsec;
+    if (lane == 0) slab[0] = st.matched;
+    if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) {
+      const int64_t* acc =
+          (const int64_t*)(L.cons + (size_t)(wave >= PGPU_NLOAD ? wave - PGPU_NLOAD : 0) * PGPU_CONS_BYTES +
+                           PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES);
+      slab[p.aggs[lane].sec] = wave < PGPU_NLOAD ? sec_identity(p.aggs[lane].op) : acc[lane];
+    }
   } else if (MODE == PGPU_MODE_LDS) {
     __syncthreads();
     const int G = (int)p.G;
     for (int key = threadIdx.x; key < G; key += NT) {
-      const int64_t cnt = cv.ltab[key];
+      const int64_t cnt = L.ltab[key];
       if (cnt == 0) continue;
       atomicAdd((unsigned long long*)&p.table[key], (unsigned long long)cnt);
-      for (int s = 1; s < p.nsec; ++s) {
-        const int64_t v = cv.ltab[s * G + key];
-        int64_t* dst = &p.table[(size_t)s * p.G + key];
-        switch (p.sec_op[s]) {
-          case PGPU_RED_SUM_I64: atomicAdd((unsigned long long*)dst, (unsigned long long)v); break;
-          case PGPU_RED_SUM_F64: atomicAdd((double*)dst, __longlong_as_double(v)); break;
-          case PGPU_RED_MIN_I64: atomicMin((long long*)dst, (long long)v); break;
-          default: atomicMax((long long*)dst, (long long)v); break;
-        }
-      }
+      for (int s = 1; s < p.nsec; ++s) cell_atomic(&p.table[(size_t)s * p.G + key], p.sec_op[s], L.ltab[s * G + key]);
     }
   }
 }
@@ -773,25 +1359,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nsla
   const int64_t* src = is_stat ? p.stats + (col - p.nsec) : p.slab + col;
   const int stride = is_stat ? PGPU_NSTATS : p.nsec;
   int64_t v = sec_identity(op);
-  for (int b = threadIdx.x; b < nslabs; b += 256) {
-    const int64_t x = src[(size_t)b * stride];
-    if (op == PGPU_RED_SUM_I64) v += x;
-    else if (op == PGPU_RED_SUM_F64) v = __double_as_longlong(__longlong_as_double(v) + __longlong_as_double(x));
-    else if (op == PGPU_RED_MIN_I64) v = x < v ? x : v;
-    else v = x > v ? x : v;
-  }
+  for (int b = threadIdx.x; b < nslabs; b += 256) v = cell_combine(op, v, src[(size_t)b * stride]);
   red[threadIdx.x] = v;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      const int64_t x = red[threadIdx.x + o];
-      int64_t y = red[threadIdx.x];
-      if (op == PGPU_RED_SUM_I64) y += x;
-      else if (op == PGPU_RED_SUM_F64) y = __double_as_longlong(__longlong_as_double(y) + __longlong_as_double(x));
-      else if (op == PGPU_RED_MIN_I64) y = x < y ? x : y;
-      else y = x > y ? x : y;
-      red[threadIdx.x] = y;
-    }
+    if (threadIdx.x < o) red[threadIdx.x] = cell_combine(op, red[threadIdx.x], red[threadIdx.x + o]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
@@ -867,21 +1439,16 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 }  // namespace
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
-size_t pgpu_dyn_smem_bytes(int mode, int pf_words, uint64_t table_bytes) {
-  size_t n = (size_t)NW * MAXS * 64 * 4 + (size_t)NW * pf_words * 4 + (size_t)NW * PGPU_MAX_AGGS * 8;
-  if (mode == PGPU_MODE_LDS) n += table_bytes;
-  return n;
-}
-
-hipError_t pgpu_occupancy(int mode, size_t dyn_smem, int* blocks_per_cu) {
-  switch (mode) {
-    case PGPU_MODE_AGG:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, query_kernel<PGPU_MODE_AGG>, NT, dyn_smem);
-    case PGPU_MODE_LDS:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, query_kernel<PGPU_MODE_LDS>, NT, dyn_smem);
-    default:
-      return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, query_kernel<PGPU_MODE_GLOBAL>, NT, dyn_smem);
-  }
+hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
+  hipError_t e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_AGG>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_LDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_GLOBAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_bytes);
+  return e;
 }
 
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {

@@ -14,8 +14,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -26,8 +28,7 @@
 #include "pgpu_internal.h"
 
 // kernels (pgpu_kernels.hip)
-size_t pgpu_dyn_smem_bytes(int mode, int pf_words, uint64_t table_bytes);
-hipError_t pgpu_occupancy(int mode, size_t dyn_smem, int* blocks_per_cu);
+hipError_t pgpu_prepare_query_kernels(size_t lds_bytes);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
@@ -64,6 +65,15 @@ inline uint32_t le32(const uint8_t* p) {
 }
 
 int type_width(int32_t t) { return (t == PGPU_INT || t == PGPU_FLOAT) ? 4 : 8; }
+
+// PGPU_PROFILE=1: the query kernel records per-wave phase cycles; pgpu_query_wait prints their averages.
+bool profile_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PGPU_PROFILE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 // Device buffer that frees itself.
 struct DevMem {
@@ -116,7 +126,7 @@ struct PinnedMem {
 struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells;
+  DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof;
   PinnedMem h_arena, h_stats, h_total;
   bool busy = false;
   ~Workspace() {
@@ -133,7 +143,7 @@ struct pgpu_context {
   int num_cus = 256;
   std::mutex mu;
   std::vector<std::unique_ptr<Workspace>> pool;
-  int occ_cache[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};  // mode -> (dyn smem, blocks/CU)
+  bool lds_ready = false;  // query kernels allowed the full 160 KiB of dynamic LDS
 };
 
 struct pgpu_buffer {
@@ -154,6 +164,8 @@ struct HostColumn {
   int32_t inv_card = 0;
   DevMem fwd, sorted, dict, inv_dir, inv_ct, inv_data;
   uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
+  std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
+  std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
 };
 
 }  // namespace
@@ -345,7 +357,7 @@ int pgpu_segment_add_forward_index(pgpu_segment* seg, int32_t column, const void
                                    int32_t bits_per_value, int32_t cardinality, int32_t mem_kind) {
   int rc = check_column(seg, column);
   if (rc) return rc;
-  if (bits_per_value < 1 || bits_per_value > 32) return fail(PGPU_E_INVALID, "bits_per_value %d", bits_per_value);
+  if (bits_per_value < 1 || bits_per_value > 31) return fail(PGPU_E_INVALID, "bits_per_value %d", bits_per_value);
   const uint64_t need = ((uint64_t)seg->num_docs * bits_per_value + 7) / 8;
   if (num_bytes < need || (!bytes && need))
     return fail(PGPU_E_INVALID, "forward index of column %d: %llu bytes < %llu needed", column,
@@ -386,6 +398,7 @@ int pgpu_segment_add_sorted_index(pgpu_segment* seg, int32_t column, const void*
     return fail(PGPU_E_INVALID, "sorted index of column %d ends at %d, numDocs %d", column, prev_end, seg->num_docs);
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.sorted, pairs.data(), pairs.size() * 4, pairs.size() * 4, PGPU_MEM_HOST));
+  c.sorted_pairs.swap(pairs);
   c.kind = PGPU_COL_SORTED;
   c.fwd_card = cardinality;
   c.fwd_bytes = num_bytes;
@@ -436,6 +449,7 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
   // BitmapInvertedIndexReader: offsets may be absolute (writer) or bitmap-relative; subtract the first one.
   const uint32_t first = be32(b);
   std::vector<uint32_t> dir(cardinality + 1);
+  std::vector<uint32_t> cards(cardinality, 0);
   std::vector<DevContainer> cts;
   std::vector<uint8_t> data;
   std::vector<ParsedContainer> parsed;
@@ -454,6 +468,11 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
       data.resize(off + pc.payload_bytes);
       memcpy(&data[off], pc.payload, pc.payload_bytes);
       cts.push_back(DevContainer{pc.key, pc.type, pc.card, (uint32_t)off});
+      if (pc.type == PGPU_CT_RUN) {
+        for (uint32_t r = 0; r < pc.card; ++r) cards[i] += (uint32_t)le16(pc.payload + 4 * r + 2) + 1;
+      } else {
+        cards[i] += pc.card;
+      }
       if (data.size() > 0xFFFFFFF0ull) return fail(PGPU_E_INVALID, "inverted index too large");
     }
   }
@@ -466,6 +485,7 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
   HIP_TRY(upload(c.inv_data, data.data(), data.size(), data.size() + 16, PGPU_MEM_HOST));
   c.inv_card = cardinality;
   c.inv_bytes = num_bytes;
+  c.inv_cards.swap(cards);
   return PGPU_OK;
 }
 
@@ -586,14 +606,9 @@ double pgpu_decode_minmax_key(int64_t key, int32_t value_type) {
 
 int pgpu_kernel_geometry(pgpu_context* ctx, int32_t* out_grid, int32_t* out_tile_docs, int32_t* out_block) {
   if (!ctx) return fail(PGPU_E_INVALID, "null ctx");
-  if (out_tile_docs) *out_tile_docs = PGPU_TILE;
+  if (out_tile_docs) *out_tile_docs = PGPU_WT;
   if (out_block) *out_block = PGPU_BLOCK;
-  if (out_grid) {
-    int bpc = 0;
-    HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(pgpu_occupancy(PGPU_MODE_AGG, pgpu_dyn_smem_bytes(PGPU_MODE_AGG, 64 * 16, 0), &bpc));
-    *out_grid = std::max(1, bpc) * ctx->num_cus;
-  }
+  if (out_grid) *out_grid = ctx->num_cus;  // one 512-thread workgroup per CU
   return PGPU_OK;
 }
 
@@ -608,11 +623,15 @@ struct Packer {
   std::vector<DevColumn> cols;
   std::vector<int32_t> pool;
   std::vector<const int32_t*> remaps;
+  int32_t slot_bytes = 0;   // largest staged region set of any segment
+  int32_t max_instrs = 0;   // most DMA instructions of one tile
+  int64_t tile_bytes = 0;   // largest staged bytes of one tile
+  double est_matched = 0;   // estimated matched docs (LDS-table decision)
 };
 
-// Convert one segment's prefix-order filter program into slot-resolved device instructions.
-int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_segment* seg,
-                   Packer& pk) {
+// Convert one prefix-order filter program into slot-resolved device instructions appended to pk.instrs.
+int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_filter_node* nodes, int count,
+                   const pgpu_segment* seg, Packer& pk) {
   struct Frame {
     int kind;  // 0 AND, 1 OR, 2 NOT
     int slot;
@@ -624,7 +643,13 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
   const int base = (int)pk.instrs.size();
   int cur = 0;     // slot the next node writes
   int care = -1;   // care slot of the next node
-  auto emit = [&](DevInstr in) { pk.instrs.push_back(in); return (int)pk.instrs.size() - 1 - base; };
+  auto emit = [&](DevInstr in) {
+    in.stage_off = -1;
+    if (in.pred != 2)
+      for (int k = 0; k < 8; ++k) in.ids[k] = 0xFFFFFFFFu;
+    pk.instrs.push_back(in);
+    return (int)pk.instrs.size() - 1 - base;
+  };
   auto close_nots = [&]() {
     while (!st.empty() && st.back().kind == 2) {
       DevInstr in{};
@@ -644,8 +669,8 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
     *out = &seg->dev[slot];
     return PGPU_OK;
   };
-  for (int i = 0; i < sp.num_filter_nodes; ++i) {
-    const pgpu_filter_node& nd = sp.filter[i];
+  for (int i = 0; i < count; ++i) {
+    const pgpu_filter_node& nd = nodes[i];
     if (cur >= PGPU_MAX_SLOTS - 1)
       return fail(PGPU_E_UNSUPPORTED, "filter nesting deeper than %d", PGPU_MAX_SLOTS - 1);
     DevInstr in{};
@@ -667,18 +692,23 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
         if (c->kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "SCAN on column %d without forward index", nd.column);
         in.op = PGPU_I_SCAN;
         in.pred = nd.pred;
+        in.bits = c->bits;
+        in.kind = c->kind;
+        in.card = c->card;
+        in.fwd = c->fwd;
+        in.sorted = c->sorted;
         if (nd.pred == PGPU_PRED_RANGE) {
           in.lo = std::max(0, nd.lo);
           in.hi = std::min(nd.hi, c->card);
           if (in.hi < in.lo) in.hi = in.lo;
         } else if (nd.pred == PGPU_PRED_SET && nd.num_ids <= 8) {
-          in.pred = 2;  // LIST: compared in registers
-          in.pool_off = (int32_t)pk.pool.size();
+          in.pred = 2;  // LIST: compared in registers, ids inline
           in.n = nd.num_ids;
+          for (int k = 0; k < 8; ++k) in.ids[k] = 0xFFFFFFFFu;
           for (int k = 0; k < nd.num_ids; ++k) {
             const int32_t id = nd.ids[k];
             if (id < 0 || id >= c->card) return fail(PGPU_E_INVALID, "SET id %d out of range", id);
-            pk.pool.push_back(id);
+            in.ids[k] = (uint32_t)id;
           }
         } else if (nd.pred == PGPU_PRED_SET) {
           in.pool_off = (int32_t)pk.pool.size();
@@ -792,7 +822,249 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
     }
   }
   if (!st.empty()) return fail(PGPU_E_INVALID, "unterminated filter program");
-  if (sp.num_filter_nodes > 0 && cur != 0) return fail(PGPU_E_INVALID, "filter program leaves slot %d", cur);
+  if (count > 0 && cur != 0) return fail(PGPU_E_INVALID, "filter program leaves slot %d", cur);
+  return PGPU_OK;
+}
+
+// ---- per-segment execution plan: which filter children stream through LDS, which run per candidate doc --------
+struct SegView {
+  const pgpu_query_desc* q;
+  const pgpu_segment_plan* sp;
+  const pgpu_segment* seg;
+  const pgpu_filter_node* nd;
+  int n;
+  const HostColumn* host(int qc) const { return &seg->cols[sp->column_map[qc]]; }
+  const DevColumn* dev(int qc) const { return &seg->dev[sp->column_map[qc]]; }
+};
+
+// Walk the subtree at node i: estimated fraction of docs it keeps (uniform-id model for scans; exact bitmap and
+// sorted-range cardinalities), plus the query columns of its SCAN leaves.  Returns the index past the subtree or
+// -1 on malformed input.  Estimates only steer the staging decision; results never depend on them.
+int analyze(const SegView& v, int i, double* sel, std::vector<int>* scans) {
+  if (i < 0 || i >= v.n) return -1;
+  const pgpu_filter_node& x = v.nd[i];
+  const double nd = std::max(1, v.seg->num_docs);
+  auto valid_col = [&](int qc) {
+    return qc >= 0 && qc < v.q->num_columns && v.sp->column_map[qc] >= 0 &&
+           v.sp->column_map[qc] < (int32_t)v.seg->dev.size();
+  };
+  switch (x.op) {
+    case PGPU_F_MATCH_ALL: *sel = 1.0; return i + 1;
+    case PGPU_F_EMPTY: *sel = 0.0; return i + 1;
+    case PGPU_F_SCAN: {
+      if (!valid_col(x.column)) return -1;
+      const double card = std::max(1, v.dev(x.column)->card);
+      double s = x.pred == PGPU_PRED_RANGE ? std::max(0, x.hi - x.lo) / card : std::max(0, x.num_ids) / card;
+      s = std::min(1.0, s);
+      *sel = x.negate ? 1.0 - s : s;
+      scans->push_back(x.column);
+      return i + 1;
+    }
+    case PGPU_F_INVERTED: {
+      if (!valid_col(x.column)) return -1;
+      const HostColumn* h = v.host(x.column);
+      double docs = 0;
+      for (int k = 0; k < x.num_ids; ++k)
+        if (x.ids[k] >= 0 && x.ids[k] < (int32_t)h->inv_cards.size()) docs += h->inv_cards[x.ids[k]];
+      const double s = std::min(1.0, docs / nd);
+      *sel = x.negate ? 1.0 - s : s;
+      return i + 1;
+    }
+    case PGPU_F_SORTED: {
+      double docs = 0;
+      for (int k = 0; k < x.num_ids; ++k) docs += std::max(0, x.ids[2 * k + 1] - x.ids[2 * k] + 1);
+      const double s = std::min(1.0, docs / nd);
+      *sel = x.negate ? 1.0 - s : s;
+      return i + 1;
+    }
+    case PGPU_F_AND_BEGIN:
+    case PGPU_F_OR_BEGIN: {
+      const bool is_and = x.op == PGPU_F_AND_BEGIN;
+      double acc = 1.0;  // AND: product of selectivities; OR: product of (1 - s)
+      int j = i + 1;
+      while (j < v.n && v.nd[j].op != (is_and ? PGPU_F_AND_END : PGPU_F_OR_END)) {
+        double cs;
+        j = analyze(v, j, &cs, scans);
+        if (j < 0 || j >= v.n || v.nd[j].op != (is_and ? PGPU_F_AND_CHILD_END : PGPU_F_OR_CHILD_END)) return -1;
+        acc *= is_and ? cs : 1.0 - cs;
+        ++j;
+      }
+      if (j >= v.n) return -1;
+      *sel = is_and ? acc : 1.0 - acc;
+      return j + 1;
+    }
+    case PGPU_F_NOT: {
+      double cs;
+      const int j = analyze(v, i + 1, &cs, scans);
+      *sel = 1.0 - cs;
+      return j;
+    }
+    default:
+      return -1;
+  }
+}
+
+// Fraction of a b-bit column's 32-B sectors that hold at least one doc when docs survive with density rho.
+double sector_touch(double rho, int bits) {
+  if (rho >= 1.0) return 1.0;
+  if (rho <= 0.0) return 0.0;
+  return 1.0 - std::pow(1.0 - rho, 256.0 / bits);
+}
+
+// A column is streamed (dense) when at least half of its sectors would be read anyway.
+constexpr double kDenseTouch = 0.5;
+constexpr int kMaxSlotBytes = 27 * 1024;  // keeps >= 3 ring slots next to the consumer areas
+
+int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_segment* seg,
+                 const DevParams& p, Packer& pk, DevSeg& ds) {
+  SegView v{q, &sp, seg, sp.filter, sp.num_filter_nodes};
+  // top-level AND children (node ranges [begin, end))
+  std::vector<std::pair<int, int>> kids;
+  if (v.n > 0) {
+    double s;
+    std::vector<int> scans;
+    const int e = analyze(v, 0, &s, &scans);
+    if (e != v.n) return fail(PGPU_E_INVALID, "malformed filter program");
+    if (v.nd[0].op == PGPU_F_AND_BEGIN) {
+      int j = 1;
+      while (v.nd[j].op != PGPU_F_AND_END) {
+        const int ce = analyze(v, j, &s, &scans);
+        kids.emplace_back(j, ce);
+        j = ce + 1;
+      }
+    } else {
+      kids.emplace_back(0, v.n);
+    }
+  }
+  // dense prefix of the children: every scan column of a dense child is read with >= kDenseTouch sector density
+  double rho = 1.0;
+  bool residual = false;
+  std::vector<int> dense_kids, resid_kids, staged;
+  auto add_stage = [&](int qc) {
+    if (std::find(staged.begin(), staged.end(), qc) == staged.end()) staged.push_back(qc);
+  };
+  for (size_t k = 0; k < kids.size(); ++k) {
+    double s;
+    std::vector<int> scans;
+    analyze(v, kids[k].first, &s, &scans);
+    bool dense = !residual;
+    for (int qc : scans)
+      if (dense && v.dev(qc)->kind == PGPU_COL_FIXED_BIT && sector_touch(rho, v.dev(qc)->bits) < kDenseTouch)
+        dense = false;
+    if (dense) {
+      dense_kids.push_back((int)k);
+      for (int qc : scans)
+        if (v.dev(qc)->kind == PGPU_COL_FIXED_BIT) add_stage(qc);
+    } else {
+      residual = true;
+      resid_kids.push_back((int)k);
+    }
+    rho *= s;
+  }
+  const size_t nfilter_stage = staged.size();
+  // aggregation plan
+  std::vector<int> aggcols;
+  auto add_agg = [&](int qc) {
+    if (std::find(aggcols.begin(), aggcols.end(), qc) == aggcols.end()) aggcols.push_back(qc);
+  };
+  for (int g = 0; g < q->num_group_columns; ++g) add_agg(q->group_columns[g]);
+  for (int a = 0; a < q->num_aggs; ++a)
+    if (q->aggs[a].fn != PGPU_AGG_COUNT) add_agg(q->aggs[a].column);
+  int agg_mode;
+  if (aggcols.empty()) {
+    agg_mode = PGPU_AM_COUNT;
+  } else if (residual) {
+    agg_mode = PGPU_AM_SPARSE;
+  } else {
+    bool dense = true;
+    for (int qc : aggcols)
+      dense &= v.dev(qc)->kind == PGPU_COL_FIXED_BIT && sector_touch(rho, v.dev(qc)->bits) >= kDenseTouch;
+    agg_mode = dense ? PGPU_AM_DENSE : PGPU_AM_SPARSE;
+    if (dense)
+      for (int qc : aggcols) add_stage(qc);
+  }
+  auto fits = [&]() {
+    int instrs = 0, bytes = 0;
+    for (int qc : staged) {
+      instrs += pgpu_stage_instrs(v.dev(qc)->bits);
+      bytes += pgpu_stage_region_bytes(v.dev(qc)->bits);
+    }
+    return staged.size() <= PGPU_MAX_STAGE && instrs <= PGPU_MAX_STAGE_INSTRS && bytes <= kMaxSlotBytes;
+  };
+  if (!fits() && agg_mode == PGPU_AM_DENSE) {
+    staged.resize(nfilter_stage);
+    agg_mode = PGPU_AM_SPARSE;
+  }
+  while (!fits()) staged.pop_back();  // remaining scans read their tiles straight from HBM
+  // programs
+  auto build = [&](const std::vector<int>& idx, std::vector<pgpu_filter_node>& out) {
+    pgpu_filter_node mark{};
+    if (idx.size() > 1) {
+      mark.op = PGPU_F_AND_BEGIN;
+      out.push_back(mark);
+    }
+    for (int k : idx) {
+      for (int i = kids[k].first; i < kids[k].second; ++i) out.push_back(v.nd[i]);
+      if (idx.size() > 1) {
+        mark.op = PGPU_F_AND_CHILD_END;
+        out.push_back(mark);
+      }
+    }
+    if (idx.size() > 1) {
+      mark.op = PGPU_F_AND_END;
+      out.push_back(mark);
+    }
+  };
+  std::vector<pgpu_filter_node> dn, rn;
+  build(dense_kids, dn);
+  build(resid_kids, rn);
+  ds.prog_begin = (int32_t)pk.instrs.size();
+  int rc = convert_filter(q, sp, dn.data(), (int)dn.size(), seg, pk);
+  if (rc) return rc;
+  ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
+  std::vector<int> stage_offs;
+  {
+    int o = 0;
+    for (int qc : staged) {
+      stage_offs.push_back(o);
+      o += pgpu_stage_region_bytes(v.dev(qc)->bits);
+    }
+  }
+  for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+    DevInstr& in = pk.instrs[i];
+    if (in.op != PGPU_I_SCAN) continue;
+    for (size_t j = 0; j < staged.size(); ++j)
+      if (staged[j] == in.col) in.stage_off = stage_offs[j];
+  }
+  ds.rprog_begin = (int32_t)pk.instrs.size();
+  rc = convert_filter(q, sp, rn.data(), (int)rn.size(), seg, pk);
+  if (rc) return rc;
+  ds.rprog_len = (int32_t)pk.instrs.size() - ds.rprog_begin;
+  // staging layout
+  ds.nstage = (int32_t)staged.size();
+  ds.stage_instrs = 0;
+  int off = 0;
+  for (size_t j = 0; j < staged.size(); ++j) {
+    const int b = v.dev(staged[j])->bits;
+    ds.stage_col[j] = staged[j];
+    ds.stage_off[j] = off;
+    off += pgpu_stage_region_bytes(b);
+    ds.stage_instrs += pgpu_stage_instrs(b);
+  }
+  pk.slot_bytes = std::max(pk.slot_bytes, off);
+  pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
+  int64_t tb = 0;
+  for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
+  pk.tile_bytes = std::max(pk.tile_bytes, tb);
+  pk.est_matched += rho * seg->num_docs;
+  ds.agg_mode = agg_mode;
+  ds.nreg = -1;
+  ds.reg_col[0] = ds.reg_col[1] = -1;
+  if (agg_mode == PGPU_AM_DENSE && aggcols.size() <= 2) {
+    ds.nreg = (int32_t)aggcols.size();
+    for (size_t j = 0; j < aggcols.size(); ++j) ds.reg_col[j] = aggcols[j];
+  }
+  (void)p;
   return PGPU_OK;
 }
 
@@ -804,6 +1076,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   p.nsec = L.num_sections;
   p.G = L.num_keys;
   p.flags = (q->flags & PGPU_Q_STATS) ? PGPU_FLAG_STATS : 0;
+  if (profile_enabled()) p.flags |= PGPU_FLAG_PROFILE;
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
   for (int g = 0; g < q->num_group_columns; ++g) {
@@ -820,7 +1093,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     p.aggs[a].op = L.section_op[L.agg_section[a]];
     p.aggs[a].vtype = L.agg_value_type[a];
   }
-  int tiles = 0;
+  int64_t tiles = 0;
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
     const pgpu_segment* seg = sp.segment;
@@ -829,8 +1102,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     if (!sp.column_map && q->num_columns) return fail(PGPU_E_INVALID, "segment %d: no column map", s);
     DevSeg ds{};
     ds.num_docs = seg->num_docs;
-    ds.tile_begin = tiles;
-    ds.prog_begin = (int32_t)pk.instrs.size();
+    ds.tile_begin = (int32_t)tiles;
+    ds.ntiles = (seg->num_docs + PGPU_WT - 1) / PGPU_WT;
     ds.col_begin = (int32_t)pk.cols.size();
     ds.remap_begin = (int32_t)pk.remaps.size();
     for (int c = 0; c < q->num_columns; ++c) {
@@ -855,26 +1128,15 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       if (c.kind == PGPU_COL_NONE || !c.dict) return fail(PGPU_E_INVALID, "segment %d: agg column not readable", s);
       if (c.dict_type != L.agg_value_type[a]) return fail(PGPU_E_INVALID, "segment %d: agg column type differs", s);
     }
-    if (sp.num_filter_nodes > 0) {
-      int rc = convert_filter(q, sp, seg, pk);
-      if (rc) return rc;
-    }
-    ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
-    // driving scan: the first SCAN reached through AND_BEGINs only is dense on every tile -> prefetch it
-    ds.pf_pc = -1;
-    for (int i = 0; i < ds.prog_len; ++i) {
-      const DevInstr& in = pk.instrs[ds.prog_begin + i];
-      if (in.op == PGPU_I_AND_BEGIN) continue;
-      if (in.op == PGPU_I_SCAN && pk.cols[ds.col_begin + in.col].kind == PGPU_COL_FIXED_BIT) ds.pf_pc = i;
-      break;
-    }
+    int rc = plan_segment(q, sp, seg, p, pk, ds);
+    if (rc) return rc;
     pk.segs.push_back(ds);
-    tiles += (seg->num_docs + PGPU_WAVE_TILE - 1) / PGPU_WAVE_TILE;
-    if (ds.pf_pc >= 0)
-      p.pf_words = std::max(p.pf_words, 64 * pk.cols[ds.col_begin + pk.instrs[ds.prog_begin + ds.pf_pc].col].bits);
+    tiles += ds.ntiles;
+    if (tiles > INT32_MAX / 2) return fail(PGPU_E_UNSUPPORTED, "too many docs in one launch");
   }
   p.nseg = q->num_segments;
-  p.total_tiles = tiles;
+  p.total_tiles = (int32_t)tiles;
+  p.max_instrs = pk.max_instrs;
   return PGPU_OK;
 }
 
@@ -900,26 +1162,35 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
 
-  // mode and launch geometry
+  // mode and LDS geometry: consumer areas, optional LDS group table, then as many ring slots as fit
   const uint64_t tbytes = 8ull * L.num_sections * L.num_keys;
+  const int S = (int)align16(std::max(16, pk.slot_bytes));
+  const size_t fixed = PGPU_FLAG_BYTES + (size_t)PGPU_NCONS * PGPU_CONS_BYTES;
+  // LDS-privatised table only when it fits next to >= 4 ring slots and enough docs are expected to match to pay
+  // for initialising and flushing one table copy per workgroup
+  const int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
+  const bool many = pk.est_matched > 4.0 * (double)L.num_keys * grid;
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
-  else if (tbytes <= PGPU_LDS_TABLE_BYTES) p.mode = PGPU_MODE_LDS;
+  else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && (PGPU_LDS_LIMIT - fixed - align16(tbytes)) / S >= 4)
+    p.mode = PGPU_MODE_LDS;
   else p.mode = PGPU_MODE_GLOBAL;
-  const size_t dyn = pgpu_dyn_smem_bytes(p.mode, p.pf_words, tbytes);
-  int bpc = 0;
+  p.ltab_bytes = p.mode == PGPU_MODE_LDS ? (int32_t)tbytes : 0;
+  const size_t avail = PGPU_LDS_LIMIT - fixed - align16(p.ltab_bytes);
+  p.slot_bytes = S;
+  p.ring_slots = (int32_t)std::min<size_t>(PGPU_RING_MAX, avail / S);
+  if (p.ring_slots < 2) return fail(PGPU_E_UNSUPPORTED, "staged tile of %d bytes leaves < 2 LDS ring slots", S);
+  // loader window: publish a slot once ~60 KiB of younger DMAs are queued behind it (enough bytes in flight per CU
+  // to cover HBM latency), never holding back more than the ring minus two slots
+  if (pk.tile_bytes == 0) p.inflight = 0;
+  else p.inflight = (int32_t)std::max<int64_t>(1, std::min<int64_t>(p.ring_slots - 2, (60 * 1024 + pk.tile_bytes - 1) / pk.tile_bytes));
+  const size_t dyn = pgpu_lds_bytes(p.ring_slots, S, p.ltab_bytes);
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (ctx->occ_cache[p.mode][0] == (int)dyn) bpc = ctx->occ_cache[p.mode][1];
+    if (!ctx->lds_ready) {
+      HIP_TRY(pgpu_prepare_query_kernels(PGPU_LDS_LIMIT));
+      ctx->lds_ready = true;
+    }
   }
-  const int tiles_per_block = PGPU_WAVES;
-  if (bpc <= 0) {
-    HIP_TRY(pgpu_occupancy(p.mode, dyn, &bpc));
-    if (bpc < 1) return fail(PGPU_E_HIP, "query kernel does not fit a CU (dyn LDS %zu)", dyn);
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->occ_cache[p.mode][0] = (int)dyn;
-    ctx->occ_cache[p.mode][1] = bpc;
-  }
-  const int grid = std::max(1, std::min((p.total_tiles + tiles_per_block - 1) / tiles_per_block, bpc * ctx->num_cus));
   const int nwaves = grid * PGPU_WAVES;
 
   Workspace* ws = acquire_ws(ctx, &rc);
@@ -943,6 +1214,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS);
+  if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   char* h = (char*)ws->h_arena.p;
   memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
@@ -959,6 +1231,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   p.table = (int64_t*)dev_table;
   p.slab = (int64_t*)ws->slab.p;
   p.stats = (int64_t*)ws->stats.p;
+  p.prof = (int64_t*)ws->prof.p;
 
   e = hipMemcpyAsync(ws->arena.p, ws->h_arena.p, total, hipMemcpyHostToDevice, st);
   if (e == hipSuccess && p.mode != PGPU_MODE_AGG) e = pgpu_launch_table_init(p, st);
@@ -984,6 +1257,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   return PGPU_OK;
 }
 
+
 int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
   HIP_TRY(hipSetDevice(qq->ctx->device));
@@ -996,6 +1270,24 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
+  if (qq->params.flags & PGPU_FLAG_PROFILE) {
+    const int nw = qq->grid * PGPU_WAVES;
+    std::vector<int64_t> pr((size_t)nw * PGPU_NPROF);
+    HIP_TRY(hipMemcpy(pr.data(), qq->params.prof, pr.size() * 8, hipMemcpyDeviceToHost));
+    double sum[PGPU_NPROF] = {0};
+    int nl = 0, nc = 0;
+    for (int w = 0; w < nw; ++w) {
+      const bool ld = (w % PGPU_WAVES) < PGPU_NLOAD;
+      ld ? ++nl : ++nc;
+      for (int k = 0; k < PGPU_NPROF; ++k) sum[k] += (double)pr[(size_t)w * PGPU_NPROF + k];
+    }
+    // raw s_memtime ticks per wave (shader clock)
+    fprintf(stderr,
+            "[pgpu profile] kernel %.3f ms | loader/wave: total %.0f free %.0f pub %.0f issue %.0f | consumer/wave: "
+            "total %.0f full %.0f filter %.0f (fetch %.0f decode %.0f) agg %.0f flush %.0f tiles %.1f\n",
+            ms, sum[0] / nl, sum[1] / nl, sum[2] / nl, sum[3] / nl, sum[4] / nc, sum[5] / nc, sum[6] / nc,
+            sum[10] / nc, sum[11] / nc, sum[7] / nc, sum[8] / nc, sum[9] / nc);
+  }
   if (out_stats) *out_stats = qq->stats;
   return PGPU_OK;
 }
