@@ -12,6 +12,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpinotgpu.so")
+PROF_LIB_PATH = os.path.join(_HERE, "libpinotgpu_prof.so")  # in-kernel phase counters (PGPU_PROFILE=1)
 SYNTH_LIB_PATH = os.path.join(_HERE, "libpinotgpu_synth.so")
 
 # ---- constants (mirror include/pinot_gpu.h) ------------------------------------------------------------------
@@ -109,11 +110,13 @@ SIGNATURES = [
 _lib = None
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load libpinotgpu.so (fails loudly when it was not built)."""
+def load(path: str = None) -> C.CDLL:
+    """Load libpinotgpu.so (fails loudly when it was not built); PGPU_PROFILE=1 selects the profiling build."""
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:
+        path = PROF_LIB_PATH if os.environ.get("PGPU_PROFILE") == "1" else LIB_PATH
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(path)

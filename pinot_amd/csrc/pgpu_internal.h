@@ -9,9 +9,9 @@
 //   inverted  : the Roaring portable bytes of every bitmap, unchanged (little-endian), plus a container directory
 //               built on the host at upload: per dict id a [first, last) range of DevContainer records.
 //
-// Query kernel geometry (pgpu_kernels.hip): one 512-thread workgroup per CU.  Waves 0..1 are LOADERS: they stream
+// Query kernel geometry (pgpu_kernels.hip): one workgroup per CU.  The first waves are LOADERS: they stream
 // the "staged" forward-index columns of the workgroup's tiles into a ring of LDS slots with global_load_lds and
-// publish each slot behind a counted vmcnt.  Waves 2..7 are CONSUMERS: consumer c takes tiles c, c+6, ... of the
+// publish each slot behind a counted vmcnt.  The other waves are CONSUMERS: consumer c takes tiles c, c+NCONS, ... of the
 // workgroup's contiguous tile range, decodes the staged columns out of LDS (lane l owns docs [32l, 32l+32) of the
 // 2048-doc tile), runs the dense filter program on 32-bit mask words, and either aggregates straight from the
 // decoded ids (dense aggregation) or queues candidate doc ids for batched per-doc gathers (residual filter +
@@ -23,27 +23,32 @@
 #define PGPU_TILE 4096          // forward-index padding granularity in docs
 #define PGPU_WT 2048            // docs per tile: lane l owns docs [32l, 32l+32); 256*b bytes, 16-B aligned
 #define PGPU_WAVE_TILE PGPU_WT
-#define PGPU_BLOCK 512          // threads per workgroup: PGPU_NLOAD loader waves + consumer waves
-#define PGPU_WAVES (PGPU_BLOCK / 64)
-#define PGPU_NLOAD 2            // loader waves per workgroup (each keeps its own 63-instruction vmcnt budget)
-#define PGPU_NCONS (PGPU_WAVES - PGPU_NLOAD)
+// Two kernel variants.  DENSE (some segment aggregates straight from staged tiles; register-heavy): 512 threads =
+// 2 loader + 6 consumer waves.  SPARSE (filter + candidate queue only): 1024 threads = 4 loader + 12 consumer
+// waves -- small-bit tiles need more loader issue slots and more consumer waves to hide per-tile latency.
+#define PGPU_THREADS(dense) ((dense) ? 512 : 1024)
+#define PGPU_WAVES_OF(dense) (PGPU_THREADS(dense) / 64)
+#define PGPU_NLOAD_OF(dense) ((dense) ? 2 : 4)   // loader waves (each keeps its own 63-instruction vmcnt budget)
+#define PGPU_NCONS_OF(dense) (PGPU_WAVES_OF(dense) - PGPU_NLOAD_OF(dense))
 #define PGPU_MAX_SLOTS 8        // per-consumer mask rows (filter slots + 1 scratch row)
 #define PGPU_MAX_AGGS 16
 #define PGPU_MAX_GCOLS 8
 #define PGPU_MAX_STAGE 6        // staged (LDS-streamed) columns per segment
 #define PGPU_RING_MAX 64        // ring slots (flag arrays are sized for this)
-#define PGPU_LIST 2304          // per-consumer list entries (int32): candidate queue / dense-agg key+value lists
+#define PGPU_CQ_CAP 2304        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile)
 #define PGPU_CQ_FLUSH 256       // candidate-queue flush threshold (queue then still has room for a whole tile)
+#define PGPU_CQ_TILES 32        // a queue spans at most 32 of the consumer's tiles (5-bit tile index)
+#define PGPU_AGG_LIST 1024      // dense-agg key / value list entries (int32 each, DENSE variant)
 #define PGPU_DOC_U 4            // candidate docs per lane per flush round
 #define PGPU_LDS_LIMIT 163840   // gfx950 LDS per CU
 #define PGPU_LDS_TABLE_BYTES (32 * 1024)
 #define PGPU_MAX_STAGE_INSTRS 31  // DMA instructions per tile (so two tiles always fit the 6-bit vmcnt)
 
-// per-consumer LDS area: mask rows | list | accumulators
+// per-consumer LDS area: mask rows | list (candidate queue; DENSE: also the key / value lists) | accumulators
 #define PGPU_CONS_MASK_BYTES (PGPU_MAX_SLOTS * 64 * 4)
-#define PGPU_CONS_LIST_BYTES (PGPU_LIST * 4)
+#define PGPU_CONS_LIST_BYTES_OF(dense) ((dense) ? 2 * PGPU_AGG_LIST * 4 + 1024 : PGPU_CQ_CAP * 2)
 #define PGPU_CONS_ACC_BYTES (PGPU_MAX_AGGS * 8)
-#define PGPU_CONS_BYTES (PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES + PGPU_CONS_ACC_BYTES)
+#define PGPU_CONS_BYTES_OF(dense) (PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(dense) + PGPU_CONS_ACC_BYTES)
 #define PGPU_FLAG_BYTES (3 * PGPU_RING_MAX * 4)
 
 // column kinds
@@ -180,7 +185,7 @@ struct DevParams {
   int32_t inflight;               // loader's published-behind window (slots)
   int32_t ltab_bytes;             // LDS group table bytes (MODE_LDS)
   int32_t max_instrs;             // max DMA instructions of one tile (loader vmcnt budget)
-  int32_t pad1;
+  int32_t dense;                  // kernel variant (PGPU_THREADS)
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];
@@ -206,9 +211,11 @@ struct DevParams {
 #define PGPU_P_C_DECODE 11  // filter: SCAN leaf decode + predicate
 
 // LDS bytes of the query kernel for a given ring / table configuration.
-inline uint32_t pgpu_lds_bytes(int ring_slots, int slot_bytes, int ltab_bytes) {
-  return (uint32_t)(PGPU_FLAG_BYTES + PGPU_NCONS * PGPU_CONS_BYTES + ((ltab_bytes + 15) & ~15) +
-                    ring_slots * slot_bytes);
+inline uint32_t pgpu_lds_fixed_bytes(int dense, int ltab_bytes) {
+  return (uint32_t)(PGPU_FLAG_BYTES + PGPU_NCONS_OF(dense) * PGPU_CONS_BYTES_OF(dense) + ((ltab_bytes + 15) & ~15));
+}
+inline uint32_t pgpu_lds_bytes(int dense, int ring_slots, int slot_bytes, int ltab_bytes) {
+  return pgpu_lds_fixed_bytes(dense, ltab_bytes) + (uint32_t)(ring_slots * slot_bytes);
 }
 
 // Bytes of one staged column's region in a ring slot and its DMA instruction count.  Widths that are multiples of

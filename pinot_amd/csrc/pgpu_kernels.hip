@@ -37,7 +37,6 @@
 #include "../../include/pinot_gpu.h"
 #include "pgpu_internal.h"
 
-#define NT PGPU_BLOCK
 #define WT PGPU_WT
 #define MAXS PGPU_MAX_SLOTS
 #define U PGPU_DOC_U
@@ -75,13 +74,26 @@ FI T cld(const T* p) {
 template <class T>
 FI T cld(const T* p, size_t i) { return ((const CAS T*)p)[i]; }
 FI int sgpr(int v) { return __builtin_amdgcn_readfirstlane(v); }
-// Phase timers (PGPU_FLAG_PROFILE): shader clock via s_memtime, accumulated per wave.
+// Phase timers: shader clock via s_memtime, accumulated per wave.  Compiled in only for the profiling build
+// (libpinotgpu_prof.so, -DPGPU_PROFILE_BUILD, loaded when PGPU_PROFILE=1): the counters cost SGPRs the product
+// build needs for the consumer's state.
+#ifdef PGPU_PROFILE_BUILD
 struct Prof {
   bool on;
   int64_t t[PGPU_NPROF];
 };
 FI int64_t now(const Prof& pf) { return pf.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0; }
 #define PROF_ADD(pf, k, since) do { if ((pf).on) (pf).t[k] += (int64_t)__builtin_amdgcn_s_memtime() - (since); } while (0)
+#define PROF_ON(pf) ((pf).on)
+#else
+struct Prof {
+  static constexpr bool on = false;
+  int64_t t[1];
+};
+FI int64_t now(const Prof&) { return 0; }
+#define PROF_ADD(pf, k, since) do { (void)(since); } while (0)
+#define PROF_ON(pf) false
+#endif
 FI uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 FI uint32_t lowmask(uint32_t b) { return 0xFFFFFFFFu >> (32u - b); }
 // Bit i of a mask word as v_bfe_u32 with inline operands.
@@ -569,13 +581,14 @@ struct Lds {
   unsigned char* ring;
 };
 
+template <int DENSE>
 FI Lds carve(unsigned char* base, const DevParams& p) {
   Lds L;
   L.full = (int*)base;
   L.freef = L.full + PGPU_RING_MAX;
   L.icnt = L.freef + PGPU_RING_MAX;
   L.cons = base + PGPU_FLAG_BYTES;
-  L.ltab = (int64_t*)(L.cons + PGPU_NCONS * PGPU_CONS_BYTES);
+  L.ltab = (int64_t*)(L.cons + PGPU_NCONS_OF(DENSE) * PGPU_CONS_BYTES_OF(DENSE));
   L.ring = (unsigned char*)L.ltab + ((p.ltab_bytes + 15) & ~15);
   return L;
 }
@@ -677,6 +690,7 @@ FI void issue_tile(const StageCache& sc, int tile_in_seg, unsigned char* slot) {
 // Loader `li` streams tiles li, li + NLOAD, ... of the workgroup's range into ring slot (seq % R).  Slot k is
 // published (FULL = k+1) once its DMAs have landed, which the loader learns from a counted vmcnt: it keeps at most
 // `inflight` of its own unpublished tiles and 63 instructions queued.
+template <int NLOAD>
 FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Prof& pf) {
   if (li >= ntiles) return;
   const int64_t t_start = now(pf);
@@ -694,10 +708,10 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
     loader_flag_store(&L.full[pslot], pub + 1);
     pend -= cp_instrs;
     --nunpub;
-    pub += PGPU_NLOAD;
-    pslot += PGPU_NLOAD;
-    if (pslot >= R) pslot -= R;
-    if (pub < ntiles && cursor_advance(p, cp, PGPU_NLOAD)) cp_instrs = cld(&p.segs[cp.seg].stage_instrs);
+    pub += NLOAD;
+    pslot += NLOAD;
+    while (pslot >= R) pslot -= R;
+    if (pub < ntiles && cursor_advance(p, cp, NLOAD)) cp_instrs = cld(&p.segs[cp.seg].stage_instrs);
   };
   for (;;) {
     while (nunpub > 0 && (nunpub > P || pend > budget || seq >= ntiles)) publish_one();
@@ -705,9 +719,14 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
     if (seq >= R) {
       // the slot's previous tile must have been consumed; publish what is in flight while waiting
       const int64_t t0f = now(pf);
-      while (loader_flag_load(&L.freef[slot]) < seq - R + 1) {
-        if (nunpub > 0) publish_one();
-        else __builtin_amdgcn_s_sleep(1);
+      for (int nap = 0; loader_flag_load(&L.freef[slot]) < seq - R + 1;) {
+        if (nunpub > 0) {
+          publish_one();
+        } else {
+          if (nap == 0) __builtin_amdgcn_s_sleep(2);
+          else __builtin_amdgcn_s_sleep(6);
+          nap = 1;
+        }
       }
       PROF_ADD(pf, PGPU_P_L_FREE, t0f);
     }
@@ -716,10 +735,10 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
     PROF_ADD(pf, PGPU_P_L_ISSUE, t0i);
     pend += sc.instrs;
     ++nunpub;
-    seq += PGPU_NLOAD;
-    slot += PGPU_NLOAD;
-    if (slot >= R) slot -= R;
-    if (seq < ntiles && cursor_advance(p, ci, PGPU_NLOAD)) load_stage(p, ci.seg, sc);
+    seq += NLOAD;
+    slot += NLOAD;
+    while (slot >= R) slot -= R;
+    if (seq < ntiles && cursor_advance(p, ci, NLOAD)) load_stage(p, ci.seg, sc);
   }
   PROF_ADD(pf, PGPU_P_L_TOTAL, t_start);
 }
@@ -729,7 +748,9 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
 // ================================================================================================================
 struct Cons {
   uint32_t* masks;  // [MAXS][64]
-  int32_t* list;    // [PGPU_LIST]
+  uint16_t* queue;  // candidate queue [PGPU_CQ_CAP]
+  int32_t* klist;   // DENSE: dense-agg keys [PGPU_AGG_LIST] (aliases the queue)
+  int32_t* vlist;   // DENSE: dense-agg values [PGPU_AGG_LIST]
   int64_t* acc;     // [MAX_AGGS]  aggregation-only partials of this wave
 };
 
@@ -850,7 +871,7 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
   while (pc < len) {
     const int64_t tfe = now(pf);
     const DevInstr in = cld(p.instrs + begin + pc);
-    if (pf.on) {
+    if (PROF_ON(pf)) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       PROF_ADD(pf, PGPU_P_C_FETCH, tfe);
     }
@@ -864,7 +885,7 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
         uint32_t m = 0;
         const int64_t tde = now(pf);
         if (n) m = leaf_scan(p, t, in, care, dense_bytes);
-        if (pf.on) {
+        if (PROF_ON(pf)) {
           m = sgpr(m) == 0xdeadbeefu ? m + 1 : m;  // force completion before the timestamp
           PROF_ADD(pf, PGPU_P_C_DECODE, tde);
         }
@@ -982,9 +1003,10 @@ FI int new_sectors(uint32_t b, int32_t doc, bool live, int32_t prev_doc, bool pr
 }
 
 // Flush the candidate queue (doc ids of one segment, ascending): residual filter per doc, then sparse aggregation.
-template <int MODE>
+template <int MODE, int NCONS>
 FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, int n,
-                    int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
+                    int q_tile0, int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes,
+                    Prof& pf) {
   const int lane = lane_id();
   const bool stats = p.flags & PGPU_FLAG_STATS;
   wave_sync();
@@ -996,7 +1018,8 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
     for (int u = 0; u < U; ++u) {
       const int e = base + u * 64 + lane;
       const bool ok = e < n;
-      d.doc[u] = ok ? cv.list[e] : 0;
+      const uint32_t q = ok ? (uint32_t)cv.queue[e] : 0u;
+      d.doc[u] = ok ? (q_tile0 + (int)(q >> 11) * NCONS) * WT + (int)(q & (WT - 1)) : 0;
       d.valid |= (uint32_t)ok << u;
     }
     uint32_t m = d.valid;
@@ -1050,8 +1073,8 @@ template <int MODE>
 FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, const TileCtx& t,
                   uint32_t mm, const uint32_t (&ra)[32], const uint32_t (&rb)[32]) {
   const int lane = lane_id();
-  int32_t* klist = cv.list;                 // keys   [1024]
-  int32_t* vlist = cv.list + 1024;          // values [1024]
+  int32_t* klist = cv.klist;  // keys   [PGPU_AGG_LIST]
+  int32_t* vlist = cv.vlist;  // values [PGPU_AGG_LIST]
 #pragma unroll 1
   for (int h = 0; h < 2; ++h) {
     const uint32_t hm = (mm >> (16 * h)) & 0xFFFFu;
@@ -1152,17 +1175,20 @@ struct Stats {
   int64_t matched, scanned, sector_bytes, dense_bytes;
 };
 
-template <int MODE>
+template <int MODE, int DENSE>
 FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NCONS = PGPU_NCONS_OF(DENSE);
   const int64_t t_start = now(pf);
   const int lane = lane_id();
   const int R = p.ring_slots, S = p.slot_bytes;
   Cons cv;
   {
-    unsigned char* base = L.cons + (size_t)cidx * PGPU_CONS_BYTES;
+    unsigned char* base = L.cons + (size_t)cidx * PGPU_CONS_BYTES_OF(DENSE);
     cv.masks = (uint32_t*)base;
-    cv.list = (int32_t*)(base + PGPU_CONS_MASK_BYTES);
-    cv.acc = (int64_t*)(base + PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES);
+    cv.queue = (uint16_t*)(base + PGPU_CONS_MASK_BYTES);
+    cv.klist = (int32_t*)(base + PGPU_CONS_MASK_BYTES);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(DENSE));
   }
   if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
   wave_sync();
@@ -1170,7 +1196,8 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   LaneAcc la;
 #pragma unroll
   for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
-  int qn = 0;  // candidate-queue entries (all of segment `ss`)
+  int qn = 0;       // candidate-queue entries (all of segment `ss`)
+  int q_tile0 = 0;  // tile (in segment) of the queue's first consumer tile
   SegState ss;
   int cseg = -1;
   Cursor cur;
@@ -1178,15 +1205,17 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   cur.tile_in_seg = 0;
   cur.ntiles = 0;
   if (cidx < ntiles) cur = cursor_at(p, t0 + cidx);
-  for (int seq = cidx;; seq += PGPU_NCONS) {
+  int slot_i = cidx % R - NCONS;
+  for (int seq = cidx;; seq += NCONS) {
     const bool end = seq >= ntiles;
-    if (!end && seq != cidx) cursor_advance(p, cur, PGPU_NCONS);
-    const int slot_i = seq % R;
+    if (!end && seq != cidx) cursor_advance(p, cur, NCONS);
+    slot_i += NCONS;
+    while (slot_i >= R) slot_i -= R;
     const bool segchg = !end && cur.seg != cseg;
     // single flush site: end of range, segment change, or threshold (the queue then still has room for a tile)
-    if (qn && (end || segchg || qn >= PGPU_CQ_FLUSH)) {
+    if (qn && (end || segchg || qn >= PGPU_CQ_FLUSH || cur.tile_in_seg - q_tile0 >= PGPU_CQ_TILES * NCONS)) {
       const int64_t tq = now(pf);
-      flush_queue<MODE>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, q_tile0, matched, scanned, sector_bytes, dense_bytes, pf);
       PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
       qn = 0;
     }
@@ -1197,11 +1226,19 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     }
     unsigned char* slot = L.ring + (size_t)slot_i * S;
     const int64_t tw = now(pf);
-    while (flag_load(&L.full[slot_i]) != seq + 1) __builtin_amdgcn_s_sleep(1);
+    // poll with back-off: the scalar ALU is shared by every wave of the CU
+    for (int nap = 0; flag_load(&L.full[slot_i]) != seq + 1; nap = nap < 3 ? nap + 1 : 3) {
+      if (nap == 0) __builtin_amdgcn_s_sleep(1);
+      else if (nap == 1) __builtin_amdgcn_s_sleep(2);
+      else if (nap == 2) __builtin_amdgcn_s_sleep(4);
+      else __builtin_amdgcn_s_sleep(8);
+    }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     PROF_ADD(pf, PGPU_P_C_FULL, tw);
     const int64_t tf = now(pf);
+#ifdef PGPU_PROFILE_BUILD
     if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+#endif
 
     TileCtx t;
     t.ss = &ss;
@@ -1224,11 +1261,11 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     const int nm = wave_sum_i32(__popc(mm));
     PROF_ADD(pf, PGPU_P_C_FILTER, tf);
     const int64_t ta = now(pf);
-    const bool dense = ss.agg_mode == PGPU_AM_DENSE && nm;
+    const bool dense = DENSE && ss.agg_mode == PGPU_AM_DENSE && nm;
     uint32_t ra[32], rb[32];
 #pragma unroll
     for (int i = 0; i < 32; ++i) ra[i] = rb[i] = 0;
-    if (dense) {
+    if (DENSE && dense) {
       // copy up to two aggregation / group columns to registers, then hand the slot back to the loader
       for (int j = 0; j < ss.nreg; ++j) {
         const int col = j == 0 ? ss.reg_col0 : ss.reg_col1;
@@ -1249,15 +1286,18 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
       t.slot = nullptr;
     }
     if (nm) {
-      if (dense) {
+      if (DENSE && dense) {
         if (lane == 0) matched += nm;
         dense_agg<MODE>(p, L, cv, la, ss, t, mm, ra, rb);
       } else if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
         if (lane == 0) matched += nm;
       } else {
-        // queue the candidates (doc ids ascending: lane order, then bit order)
+        // queue the candidates (ascending: lane order, then bit order) as consumer-tile index << 11 | doc in tile
+        if (qn == 0) q_tile0 = cur.tile_in_seg;
+        const uint32_t tag = (uint32_t)((cur.tile_in_seg - q_tile0) / NCONS) << 11;
         int k = qn + wave_excl_scan(__popc(mm));
-        for (uint32_t left = mm; left; left &= left - 1) cv.list[k++] = t.lane_doc0 + __builtin_ctz(left);
+        for (uint32_t left = mm; left; left &= left - 1)
+          cv.queue[k++] = (uint16_t)(tag | (uint32_t)(32 * lane + __builtin_ctz(left)));
         qn += nm;
       }
     }
@@ -1282,11 +1322,12 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
 }
 
 // ---- the query kernel ----------------------------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(NT, 1) void query_kernel(DevParams p) {
+template <int MODE, int DENSE>
+__global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams p) {
+  constexpr int NT = PGPU_THREADS(DENSE), NWAVES = PGPU_WAVES_OF(DENSE), NLOAD = PGPU_NLOAD_OF(DENSE);
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const Lds L = carve(dyn_smem, p);
+  const Lds L = carve<DENSE>(dyn_smem, p);
   for (int i = threadIdx.x; i < 3 * PGPU_RING_MAX; i += NT) L.full[i] = 0;
   if (MODE == PGPU_MODE_LDS) {
     const int n = p.nsec * (int)p.G;
@@ -1299,19 +1340,23 @@ __global__ __launch_bounds__(NT, 1) void query_kernel(DevParams p) {
   Stats st;
   st.matched = st.scanned = st.sector_bytes = st.dense_bytes = 0;
   Prof pf;
+#ifdef PGPU_PROFILE_BUILD
   pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
 #pragma unroll
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
-  if (wave < PGPU_NLOAD) loader(p, L, wave, t0, t1 - t0, pf);
-  else st = consumer<MODE>(p, L, wave - PGPU_NLOAD, t0, t1 - t0, pf);
+#endif
+  if (wave < NLOAD) loader<NLOAD>(p, L, wave, t0, t1 - t0, pf);
+  else st = consumer<MODE, DENSE>(p, L, wave - NLOAD, t0, t1 - t0, pf);
+  const size_t w = (size_t)blockIdx.x * NWAVES + wave;
+#ifdef PGPU_PROFILE_BUILD
   if (pf.on && lane == 0) {
-    int64_t* o = p.prof + ((size_t)blockIdx.x * PGPU_WAVES + wave) * PGPU_NPROF;
+    int64_t* o = p.prof + w * PGPU_NPROF;
 #pragma unroll
     for (int k = 0; k < PGPU_NPROF; ++k) o[k] = pf.t[k];
   }
+#endif
 
   // ---- epilogue ----
-  const size_t w = (size_t)blockIdx.x * PGPU_WAVES + wave;
   if (lane == 0) {
     int64_t* o = p.stats + w * PGPU_NSTATS;
     o[PGPU_STAT_MATCHED] = st.matched;
@@ -1325,9 +1370,9 @@ __global__ __launch_bounds__(NT, 1) void query_kernel(DevParams p) {
     if (lane == 0) slab[0] = st.matched;
     if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) {
       const int64_t* acc =
-          (const int64_t*)(L.cons + (size_t)(wave >= PGPU_NLOAD ? wave - PGPU_NLOAD : 0) * PGPU_CONS_BYTES +
-                           PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES);
-      slab[p.aggs[lane].sec] = wave < PGPU_NLOAD ? sec_identity(p.aggs[lane].op) : acc[lane];
+          (const int64_t*)(L.cons + (size_t)(wave >= NLOAD ? wave - NLOAD : 0) * PGPU_CONS_BYTES_OF(DENSE) +
+                           PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(DENSE));
+      slab[p.aggs[lane].sec] = wave < NLOAD ? sec_identity(p.aggs[lane].op) : acc[lane];
     }
   } else if (MODE == PGPU_MODE_LDS) {
     __syncthreads();
@@ -1439,15 +1484,18 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 }  // namespace
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
+#define PGPU_ALL_QUERY_KERNELS(X)                                                                          \
+  X(PGPU_MODE_AGG, 0) X(PGPU_MODE_LDS, 0) X(PGPU_MODE_GLOBAL, 0) X(PGPU_MODE_AGG, 1) X(PGPU_MODE_LDS, 1) \
+  X(PGPU_MODE_GLOBAL, 1)
+
 hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_AGG>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_LDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipError_t e = hipSuccess;
+#define SET_ATTR(M, D)                                                                                        \
+  if (e == hipSuccess)                                                                                        \
+    e = hipFuncSetAttribute((const void*)query_kernel<M, D>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                             (int)lds_bytes);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)query_kernel<PGPU_MODE_GLOBAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds_bytes);
+  PGPU_ALL_QUERY_KERNELS(SET_ATTR)
+#undef SET_ATTR
   return e;
 }
 
@@ -1461,18 +1509,14 @@ hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {
 }
 
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
-  switch (p.mode) {
-    case PGPU_MODE_AGG:
-      hipLaunchKernelGGL(query_kernel<PGPU_MODE_AGG>, dim3(grid), dim3(NT), dyn_smem, st, p);
-      break;
-    case PGPU_MODE_LDS:
-      hipLaunchKernelGGL(query_kernel<PGPU_MODE_LDS>, dim3(grid), dim3(NT), dyn_smem, st, p);
-      break;
-    default:
-      hipLaunchKernelGGL(query_kernel<PGPU_MODE_GLOBAL>, dim3(grid), dim3(NT), dyn_smem, st, p);
-      break;
+#define LAUNCH(M, D)                                                                                \
+  if (p.mode == M && p.dense == D) {                                                                \
+    hipLaunchKernelGGL((query_kernel<M, D>), dim3(grid), dim3(PGPU_THREADS(D)), dyn_smem, st, p); \
+    return hipGetLastError();                                                                       \
   }
-  return hipGetLastError();
+  PGPU_ALL_QUERY_KERNELS(LAUNCH)
+#undef LAUNCH
+  return hipErrorInvalidValue;
 }
 
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st) {

@@ -68,11 +68,15 @@ int type_width(int32_t t) { return (t == PGPU_INT || t == PGPU_FLOAT) ? 4 : 8; }
 
 // PGPU_PROFILE=1: the query kernel records per-wave phase cycles; pgpu_query_wait prints their averages.
 bool profile_enabled() {
+#ifdef PGPU_PROFILE_BUILD
   static const bool on = [] {
     const char* e = getenv("PGPU_PROFILE");
     return e && e[0] == '1';
   }();
   return on;
+#else
+  return false;  // phase counters exist only in libpinotgpu_prof.so
+#endif
 }
 
 // Device buffer that frees itself.
@@ -607,7 +611,7 @@ double pgpu_decode_minmax_key(int64_t key, int32_t value_type) {
 int pgpu_kernel_geometry(pgpu_context* ctx, int32_t* out_grid, int32_t* out_tile_docs, int32_t* out_block) {
   if (!ctx) return fail(PGPU_E_INVALID, "null ctx");
   if (out_tile_docs) *out_tile_docs = PGPU_WT;
-  if (out_block) *out_block = PGPU_BLOCK;
+  if (out_block) *out_block = PGPU_THREADS(0);
   if (out_grid) *out_grid = ctx->num_cus;  // one 512-thread workgroup per CU
   return PGPU_OK;
 }
@@ -1165,7 +1169,10 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   // mode and LDS geometry: consumer areas, optional LDS group table, then as many ring slots as fit
   const uint64_t tbytes = 8ull * L.num_sections * L.num_keys;
   const int S = (int)align16(std::max(16, pk.slot_bytes));
-  const size_t fixed = PGPU_FLAG_BYTES + (size_t)PGPU_NCONS * PGPU_CONS_BYTES;
+  bool any_dense = false;
+  for (const DevSeg& ds : pk.segs) any_dense |= ds.agg_mode == PGPU_AM_DENSE;
+  p.dense = any_dense ? 1 : 0;
+  const size_t fixed = pgpu_lds_fixed_bytes(p.dense, 0);
   // LDS-privatised table only when it fits next to >= 4 ring slots and enough docs are expected to match to pay
   // for initialising and flushing one table copy per workgroup
   const int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
@@ -1179,11 +1186,19 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   p.slot_bytes = S;
   p.ring_slots = (int32_t)std::min<size_t>(PGPU_RING_MAX, avail / S);
   if (p.ring_slots < 2) return fail(PGPU_E_UNSUPPORTED, "staged tile of %d bytes leaves < 2 LDS ring slots", S);
-  // loader window: publish a slot once ~60 KiB of younger DMAs are queued behind it (enough bytes in flight per CU
-  // to cover HBM latency), never holding back more than the ring minus two slots
-  if (pk.tile_bytes == 0) p.inflight = 0;
-  else p.inflight = (int32_t)std::max<int64_t>(1, std::min<int64_t>(p.ring_slots - 2, (60 * 1024 + pk.tile_bytes - 1) / pk.tile_bytes));
-  const size_t dyn = pgpu_lds_bytes(p.ring_slots, S, p.ltab_bytes);
+  // loader window (per loader wave): each loader publishes its oldest slot once `inflight` younger ones are
+  // queued behind it.  The NLOAD windows plus one published slot per consumer (and two spare) must fit the ring,
+  // otherwise consumers starve on slots that have landed but are not yet published; within that, aim for ~64 KiB
+  // of DMAs in flight per CU (HBM latency x per-CU bandwidth).
+  const int nload = PGPU_NLOAD_OF(p.dense), ncons = PGPU_NCONS_OF(p.dense);
+  if (pk.tile_bytes == 0) {
+    p.inflight = 0;
+  } else {
+    const int64_t by_ring = (p.ring_slots - ncons - 2) / nload;
+    const int64_t by_bytes = (64 * 1024 + nload * pk.tile_bytes - 1) / (nload * pk.tile_bytes);
+    p.inflight = (int32_t)std::max<int64_t>(1, std::min(by_ring, by_bytes));
+  }
+  const size_t dyn = pgpu_lds_bytes(p.dense, p.ring_slots, S, p.ltab_bytes);
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->lds_ready) {
@@ -1191,7 +1206,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
       ctx->lds_ready = true;
     }
   }
-  const int nwaves = grid * PGPU_WAVES;
+  const int nwaves = grid * PGPU_WAVES_OF(p.dense);
 
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
@@ -1271,13 +1286,13 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
   if (qq->params.flags & PGPU_FLAG_PROFILE) {
-    const int nw = qq->grid * PGPU_WAVES;
+    const int nw = qq->grid * PGPU_WAVES_OF(qq->params.dense);
     std::vector<int64_t> pr((size_t)nw * PGPU_NPROF);
     HIP_TRY(hipMemcpy(pr.data(), qq->params.prof, pr.size() * 8, hipMemcpyDeviceToHost));
     double sum[PGPU_NPROF] = {0};
     int nl = 0, nc = 0;
     for (int w = 0; w < nw; ++w) {
-      const bool ld = (w % PGPU_WAVES) < PGPU_NLOAD;
+      const bool ld = (w % PGPU_WAVES_OF(qq->params.dense)) < PGPU_NLOAD_OF(qq->params.dense);
       ld ? ++nl : ++nc;
       for (int k = 0; k < PGPU_NPROF; ++k) sum[k] += (double)pr[(size_t)w * PGPU_NPROF + k];
     }
