@@ -34,7 +34,10 @@ def parse_args():
     ap.add_argument("--workload", default="adanalytics")
     ap.add_argument("--segments", type=int, default=30, help="segments per GPU")
     ap.add_argument("--docs", type=int, default=1 << 25, help="docs per segment")
-    ap.add_argument("--cpu-sample-segments", type=int, default=4)
+    ap.add_argument("--cpu-sample-segments", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much time")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="queries in flight at N=1 (the host plans query i+1 while the GPU runs query i)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = Pinot default min(#seg, min(10, nproc/2))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the small GPU-vs-oracle check of this workload")
@@ -96,9 +99,20 @@ def main():
     kernel_ms = []
     t_start = time.perf_counter()
     result = None
-    for _ in range(args.steps):
-        result = ex.execute(q, segs)
-        kernel_ms.append(ex.last_stats.kernel_ms)
+    if world == 1 and args.inflight > 1:
+        # every step plans, launches and finishes one whole query; up to `inflight` are queued at once
+        pending = []
+        submitted = 0
+        for _ in range(args.steps):
+            while submitted < args.steps and len(pending) < args.inflight:
+                pending.append(pm.submit(q, segs))
+                submitted += 1
+            result = pm.collect(pending.pop(0))
+            kernel_ms.append(result.stats.kernel_ms)
+    else:
+        for _ in range(args.steps):
+            result = ex.execute(q, segs)
+            kernel_ms.append(ex.last_stats.kernel_ms)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -143,6 +157,7 @@ def main():
             "config": {"workload": args.workload, "description": w.description, "query": w.sql,
                        "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
                        "rows_per_gpu": rows_per_gpu, "total_rows": total_rows,
+                       "queries_in_flight": args.inflight if world == 1 else 1,
                        "parallelism": f"segments sharded over {world} GPU(s); partial tables all-reduced over RCCL"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -176,30 +191,47 @@ def _pmc_traffic(workload):
     return None
 
 
+# Looser variants of the bench queries (same plan shapes) so the parity sample matches rows, not only zero.
+PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789")}
+
+
 def parity_check(ctx, w, q, opts):
+    """GPU vs oracle on 2 small segments of the workload: the bench query and a looser variant of it."""
     from oracle import engine
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.query import parse_sql
     from pinot_amd.segment import GpuSegment
     from pinot_amd.synth import build_segment_cpu
 
-    segs = [build_segment_cpu(w, s, 1 << 18, pack_fixed_bit) for s in range(2)]
+    n = 1 << 19
+    segs = [build_segment_cpu(w, s, n, pack_fixed_bit) for s in range(2)]
     gs = [GpuSegment(ctx, s) for s in segs]
+    queries = [q]
+    if w.name in PARITY_VARIANTS:
+        a, b = PARITY_VARIANTS[w.name]
+        queries.append(parse_sql(w.sql.replace(a, b)))
+    out = {"docs": 2 * n, "matched": [], "ok": True}
     try:
-        res = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000)).execute(q, gs)
-        ref = engine.execute(q, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
-        if q.group_by:
-            ok = sorted(res.group_rows) == sorted(ref.group_rows)
-        else:
-            ok = list(res.aggregation_result) == list(ref.aggregation_result)
-        ok = ok and res.stats.num_docs_scanned == ref.num_docs_scanned
-        return {"docs": 2 * (1 << 18), "matched": ref.num_docs_scanned, "ok": bool(ok)}
+        for qq in queries:
+            res = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000)).execute(qq, gs)
+            ref = engine.execute(qq, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
+            if qq.group_by:
+                ok = sorted(res.group_rows) == sorted(ref.group_rows)
+            else:
+                ok = list(res.aggregation_result) == list(ref.aggregation_result)
+            ok = ok and res.stats.num_docs_scanned == ref.num_docs_scanned
+            out["matched"].append(ref.num_docs_scanned)
+            out["ok"] = bool(out["ok"] and ok)
+        return out
     finally:
         for g in gs:
             g.release()
 
 
 def cpu_baseline(w, q, args):
+    """Pinot's per-segment operators restated in C (oracle/pinot_cpu.c), timed on this host: the sample's
+    segments are queried repeatedly until ~args.cpu_seconds of wall time, with Pinot's default task count."""
     from oracle.cpu import CpuBaseline, synth_segment
 
     nseg = args.cpu_sample_segments
@@ -207,12 +239,16 @@ def cpu_baseline(w, q, args):
     nproc = os.cpu_count() or 1
     threads = args.cpu_threads or max(1, min(nseg, min(10, nproc // 2)))
     cb = CpuBaseline(q, segs)
-    dt, matched, _, _, _ = cb.run(threads)
-    return {"value": nseg * args.docs / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{nseg} segment(s) x {args.docs} docs of the same workload, oracle/pinot_cpu.c "
-                      f"(AndDocIdIterator over SVScanDocIdIterators, 10k-doc blocks, double SUM), "
+    total, runs = 0.0, 0
+    while runs == 0 or total < args.cpu_seconds:
+        dt, matched, _, _, _ = cb.run(threads)
+        total += dt
+        runs += 1
+    return {"value": runs * nseg * args.docs / total, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload, "
+                      f"oracle/pinot_cpu.c (AndDocIdIterator over SVScanDocIdIterators, 10k-doc blocks, double SUM), "
                       f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
-            "seconds": dt}
+            "seconds": total}
 
 
 if __name__ == "__main__":

@@ -80,7 +80,7 @@ int pgpu_last_error(char* buf, size_t len);
  *                    seglocal/segment/index/readers/BitmapInvertedIndexReader.java:45-61)
  */
 int pgpu_segment_create(pgpu_context* ctx, int32_t num_docs, int32_t num_columns, pgpu_segment** out_seg);
-/* bits_per_value = PinotDataBitSet.getNumBitsPerValue(cardinality - 1) (PinotDataBitSet.java:59-71), 1..32 */
+/* bits_per_value = PinotDataBitSet.getNumBitsPerValue(cardinality - 1) (PinotDataBitSet.java:59-71), 1..31 */
 int pgpu_segment_add_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
                                    int32_t bits_per_value, int32_t cardinality, int32_t mem_kind);
 int pgpu_segment_add_sorted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
@@ -236,7 +236,19 @@ int pgpu_query_release(pgpu_query* query);
 int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
                        int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups);
 
-/* Convenience: launch + wait + compact, table kept in a context-owned workspace. */
+/* Single-GPU asynchronous form (the combine operator of one server: BaseCombineOperator.getNextBlock submits the
+ * segments' work and blocks in mergeResults, core/operator/combine/BaseCombineOperator.java:79-146):
+ *   pgpu_query_submit  packs the plan, enqueues the query on a context-owned stream with its own partial table
+ *                      (and, for tables <= 8 MiB, the copy of the whole table to pinned host memory) and returns
+ *                      without synchronising; the caller's descriptor memory may be freed on return.
+ *   pgpu_query_collect waits, compacts the non-empty keys into out_keys / out_cells (as pgpu_table_compact) and
+ *                      releases the query (also on error).
+ * Several queries may be in flight on one context; each owns its workspace. */
+int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** out_query);
+int pgpu_query_collect(pgpu_query* query, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
+                       uint64_t* out_num_groups, pgpu_query_stats* out_stats);
+
+/* Convenience: submit + collect. */
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
                        uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);
 

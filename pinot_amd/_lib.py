@@ -101,6 +101,9 @@ SIGNATURES = [
     ("pgpu_query_release", C.c_int, [_P]),
     ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pgpu_query_submit", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(_P)]),
+    ("pgpu_query_collect", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
+                                     C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_decode_minmax_key", C.c_double, [C.c_int64, C.c_int32]),

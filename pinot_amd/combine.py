@@ -98,6 +98,11 @@ class DistributedExecutor:
         return hit
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
+        if self.world == 1:
+            # single GPU: no exchange step; launch, wait and compaction inside libpinotgpu (one synchronisation)
+            res = self.pm.execute(query, segments)
+            self.last_stats = res.stats
+            return res
         import torch
         if query.group_by:
             self._global_dicts(query, segments)

@@ -131,7 +131,7 @@ struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof;
-  PinnedMem h_arena, h_stats, h_total;
+  PinnedMem h_arena, h_stats, h_total, h_table;
   bool busy = false;
   ~Workspace() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -189,6 +189,10 @@ struct pgpu_query {
   DevParams params;
   int grid;
   pgpu_query_stats stats;
+  // pgpu_query_submit: the workspace owning the partial table, its layout, and whether it was copied back whole
+  Workspace* tws = nullptr;
+  pgpu_table_layout layout{};
+  bool small = false;
 };
 
 namespace {
@@ -1309,6 +1313,10 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
 
 int pgpu_query_release(pgpu_query* qq) {
   if (!qq) return PGPU_OK;
+  if (qq->tws) {
+    (void)hipStreamSynchronize(qq->stream);  // the table workspace may still be in use by the queued copy
+    release_ws(qq->ctx, qq->tws);
+  }
   release_ws(qq->ctx, qq->ws);
   delete qq;
   return PGPU_OK;
@@ -1365,15 +1373,14 @@ int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const
   return rc;
 }
 
-int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
-                       uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
-  if (!ctx || !q || !out_num_groups) return fail(PGPU_E_INVALID, "null argument");
+int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** out_query) {
+  if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   int err = 0;
-  Workspace* tws = acquire_ws(ctx, &err);  // owns the table buffer for this call
+  Workspace* tws = acquire_ws(ctx, &err);  // owns the partial table until pgpu_query_collect
   if (!tws) return err;
   const uint64_t bytes = 8ull * L.num_sections * L.num_keys;
   hipError_t e = tws->table.ensure(bytes);
@@ -1383,12 +1390,64 @@ int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out
   }
   pgpu_query* qq = nullptr;
   rc = pgpu_query_launch(ctx, q, tws->stream, tws->table.p, tws->table.n, &qq);
-  if (rc == PGPU_OK) rc = pgpu_query_wait(qq, out_stats);
-  if (rc == PGPU_OK)
-    rc = compact_into(ctx, qq->ws, &L, tws->table.p, tws->stream, out_keys, out_cells, capacity, out_num_groups);
-  if (qq) pgpu_query_release(qq);
-  release_ws(ctx, tws);
+  if (rc) {
+    release_ws(ctx, tws);
+    return rc;
+  }
+  qq->tws = tws;
+  qq->layout = L;
+  // small tables (aggregation only, or up to a few hundred thousand keys) come back whole, queued right behind
+  // the kernel, and are compacted on the host: pgpu_query_collect then synchronises once
+  qq->small = bytes <= (8u << 20);
+  if (qq->small) {
+    e = tws->h_table.ensure(bytes);
+    if (e == hipSuccess) e = hipMemcpyAsync(tws->h_table.p, tws->table.p, bytes, hipMemcpyDeviceToHost, tws->stream);
+    if (e != hipSuccess) {
+      pgpu_query_release(qq);
+      return fail(PGPU_E_HIP, "table copy: %s", hipGetErrorString(e));
+    }
+  }
+  *out_query = qq;
+  return PGPU_OK;
+}
+
+int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
+                       uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
+  if (!qq || !qq->tws || !out_num_groups) return fail(PGPU_E_INVALID, "query was not submitted");
+  int rc = pgpu_query_wait(qq, out_stats);
+  const pgpu_table_layout& L = qq->layout;
+  if (rc == PGPU_OK && qq->small) {
+    const int64_t* t = (const int64_t*)qq->tws->h_table.p;
+    const uint64_t G = L.num_keys;
+    const int nsec = L.num_sections;
+    uint64_t n = 0;
+    for (uint64_t k = 0; k < G; ++k) {
+      if (t[k] <= 0) continue;
+      if (n < capacity) {
+        out_keys[n] = (int64_t)k;
+        for (int sc = 0; sc < nsec; ++sc) out_cells[n * nsec + sc] = t[(size_t)sc * G + k];
+      }
+      ++n;
+    }
+    *out_num_groups = n;
+    if (n > capacity)
+      rc = fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
+                (unsigned long long)capacity);
+  } else if (rc == PGPU_OK) {
+    rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->stream, out_keys, out_cells, capacity,
+                      out_num_groups);
+  }
+  pgpu_query_release(qq);
   return rc;
+}
+
+int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
+                       uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
+  if (!ctx || !q || !out_num_groups) return fail(PGPU_E_INVALID, "null argument");
+  pgpu_query* qq = nullptr;
+  int rc = pgpu_query_submit(ctx, q, &qq);
+  if (rc) return rc;
+  return pgpu_query_collect(qq, out_keys, out_cells, capacity, out_num_groups, out_stats);
 }
 
 }  // extern "C"

@@ -385,31 +385,55 @@ class GpuPlanMaker:
         _lib.check(self.ctx._lib.pgpu_table_layout_of(C.byref(desc), C.byref(L)))
         return L
 
-    def execute_table(self, query: QueryContext, segments: Sequence[GpuSegment]):
-        """Run the query; return the compacted partial table + stats (single GPU)."""
+    def submit(self, query: QueryContext, segments: Sequence[GpuSegment]) -> "PendingQuery":
+        """Plan the query and enqueue it on the GPU without waiting (pgpu_query_submit).  Several queries may be
+        in flight: the host plans the next one while the GPU runs this one."""
         desc, keep, globals_ = self.build_desc(query, segments)
         L = self.layout(desc)
+        h = C.c_void_p()
+        _lib.check(self.ctx._lib.pgpu_query_submit(self.ctx.handle, C.byref(desc), C.byref(h)))
+        return PendingQuery(self, query, len(segments), h, L, globals_)
+
+    def collect(self, pending: "PendingQuery") -> QueryResult:
+        """Wait for a submitted query and finish it (pgpu_query_collect + ORDER BY / LIMIT on the host)."""
+        L = pending.layout
         cap = int(min(L.num_keys, 1 << 26))
         keys = np.empty(max(cap, 1), dtype=np.int64)
         cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
         n = C.c_uint64()
         st = QueryStats()
-        _lib.check(self.ctx._lib.pgpu_query_execute(self.ctx.handle, C.byref(desc),
-                                                    keys.ctypes.data_as(C.POINTER(C.c_int64)),
+        h, pending.handle = pending.handle, None
+        _lib.check(self.ctx._lib.pgpu_query_collect(h, keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                                     cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
                                                     C.byref(st)))
-        table = GroupTable(keys[: n.value].copy(), cells[: n.value].copy(), L)
-        return table, st, globals_
-
-    def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
-        table, st, globals_ = self.execute_table(query, segments)
+        table = GroupTable(keys[: n.value], cells[: n.value], L)
+        query = pending.query
         stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
                                num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
-                               num_total_docs=st.num_total_docs, num_segments_processed=len(segments),
+                               num_total_docs=st.num_total_docs, num_segments_processed=pending.num_segments,
                                kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
                                dense_bytes=st.dense_bytes)
-        return finish(query, table, [g[0] for g in globals_], stats)
+        return finish(query, table, [g[0] for g in pending.globals_], stats)
+
+    def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
+        return self.collect(self.submit(query, segments))
+
+
+@dataclass
+class PendingQuery:
+    """A submitted, not yet collected query (owns the libpinotgpu query handle)."""
+    maker: "GpuPlanMaker"
+    query: QueryContext
+    num_segments: int
+    handle: C.c_void_p
+    layout: TableLayout
+    globals_: list
+
+    def __del__(self):
+        if self.handle is not None and self.handle.value:
+            self.maker.ctx._lib.pgpu_query_release(self.handle)
+            self.handle = None
 
 
 def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats: ExecutionStats) -> QueryResult:

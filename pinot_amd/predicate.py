@@ -29,8 +29,11 @@ def _key(value: str, data_type: int):
     if data_type == PGPU_STRING:
         return value
     if data_type in (PGPU_INT, PGPU_LONG):
-        f = Fraction(value)
-        return int(f) if f.denominator == 1 else f
+        try:
+            return int(value)  # plain integral literal
+        except ValueError:
+            f = Fraction(value)
+            return int(f) if f.denominator == 1 else f
     if data_type == PGPU_FLOAT:
         return float(np.float32(float(value)))
     return float(value)
