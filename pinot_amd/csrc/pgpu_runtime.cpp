@@ -129,13 +129,14 @@ struct PinnedMem {
 
 struct Workspace {
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof;
   PinnedMem h_arena, h_stats, h_total, h_table;
   bool busy = false;
   ~Workspace() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -148,6 +149,13 @@ struct pgpu_context {
   std::mutex mu;
   std::vector<std::unique_ptr<Workspace>> pool;
   bool lds_ready = false;  // query kernels allowed the full 160 KiB of dynamic LDS
+  // pgpu_query_submit: all submitted queries run back to back on one stream (each kernel fills the GPU, so
+  // nothing is lost by serialising them, and their HIP events then time each kernel alone)
+  hipStream_t qstream = nullptr;
+  ~pgpu_context() {
+    pool.clear();
+    if (qstream) (void)hipStreamDestroy(qstream);
+  }
 };
 
 struct pgpu_buffer {
@@ -193,6 +201,7 @@ struct pgpu_query {
   Workspace* tws = nullptr;
   pgpu_table_layout layout{};
   bool small = false;
+  hipEvent_t done = nullptr;  // submitted queries: recorded after the last copy of this query
 };
 
 namespace {
@@ -209,6 +218,7 @@ Workspace* acquire_ws(pgpu_context* ctx, int* err) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&w->ev0);
   if (e == hipSuccess) e = hipEventCreate(&w->ev1);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     *err = fail(PGPU_E_HIP, "workspace creation failed: %s", hipGetErrorString(e));
     return nullptr;
@@ -1280,7 +1290,8 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
 int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
   HIP_TRY(hipSetDevice(qq->ctx->device));
-  HIP_TRY(hipStreamSynchronize(qq->stream));
+  if (qq->done) HIP_TRY(hipEventSynchronize(qq->done));
+  else HIP_TRY(hipStreamSynchronize(qq->stream));
   const int64_t* s = (const int64_t*)qq->ws->h_stats.p;
   qq->stats.num_docs_scanned = s[PGPU_STAT_MATCHED];
   qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED];
@@ -1313,10 +1324,10 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
 
 int pgpu_query_release(pgpu_query* qq) {
   if (!qq) return PGPU_OK;
-  if (qq->tws) {
-    (void)hipStreamSynchronize(qq->stream);  // the table workspace may still be in use by the queued copy
-    release_ws(qq->ctx, qq->tws);
-  }
+  // the workspaces may still be in use by queued work of this query
+  if (qq->done) (void)hipEventSynchronize(qq->done);
+  else (void)hipStreamSynchronize(qq->stream);
+  if (qq->tws) release_ws(qq->ctx, qq->tws);
   release_ws(qq->ctx, qq->ws);
   delete qq;
   return PGPU_OK;
@@ -1379,6 +1390,10 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   int rc = pgpu_table_layout_of(q, &L);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->qstream) HIP_TRY(hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking));
+  }
   int err = 0;
   Workspace* tws = acquire_ws(ctx, &err);  // owns the partial table until pgpu_query_collect
   if (!tws) return err;
@@ -1389,7 +1404,7 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
     return fail(PGPU_E_HIP, "table allocation: %s", hipGetErrorString(e));
   }
   pgpu_query* qq = nullptr;
-  rc = pgpu_query_launch(ctx, q, tws->stream, tws->table.p, tws->table.n, &qq);
+  rc = pgpu_query_launch(ctx, q, ctx->qstream, tws->table.p, tws->table.n, &qq);
   if (rc) {
     release_ws(ctx, tws);
     return rc;
@@ -1401,12 +1416,18 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   qq->small = bytes <= (8u << 20);
   if (qq->small) {
     e = tws->h_table.ensure(bytes);
-    if (e == hipSuccess) e = hipMemcpyAsync(tws->h_table.p, tws->table.p, bytes, hipMemcpyDeviceToHost, tws->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(tws->h_table.p, tws->table.p, bytes, hipMemcpyDeviceToHost, qq->stream);
     if (e != hipSuccess) {
       pgpu_query_release(qq);
       return fail(PGPU_E_HIP, "table copy: %s", hipGetErrorString(e));
     }
   }
+  e = hipEventRecord(tws->done, qq->stream);
+  if (e != hipSuccess) {
+    pgpu_query_release(qq);
+    return fail(PGPU_E_HIP, "event record: %s", hipGetErrorString(e));
+  }
+  qq->done = tws->done;
   *out_query = qq;
   return PGPU_OK;
 }
@@ -1434,7 +1455,8 @@ int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, ui
       rc = fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
                 (unsigned long long)capacity);
   } else if (rc == PGPU_OK) {
-    rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->stream, out_keys, out_cells, capacity,
+    // the table is complete (waited above): compact it on the query's own workspace stream
+    rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->ws->stream, out_keys, out_cells, capacity,
                       out_num_groups);
   }
   pgpu_query_release(qq);
