@@ -15,7 +15,8 @@
  *     calling thread is available through pgpu_last_error (thread-local), mirroring the processing-exception
  *     path of BaseCombineOperator.onException (core/operator/combine/BaseCombineOperator.java:177-179);
  *   - segment handles are immutable after pgpu_segment_seal and may be shared by concurrent queries;
- *   - pgpu_query_execute is re-entrant: each call takes its own workspace and HIP stream.
+ *   - queries are re-entrant: each takes its own workspace; submitted queries run in submission order on the
+ *     context's query stream (each kernel fills the GPU, so serialising them loses nothing).
  *
  * Dictionary ids are segment-local, exactly as in the reference: the host evaluates predicates against each
  * segment's dictionary (core/operator/filter/predicate/<X>PredicateEvaluatorFactory.java) and passes dict-id ranges /

@@ -1,14 +1,16 @@
 // HIP kernels of the MI355X segment query path (gfx950 / CDNA4).
 //
-// One launch runs a whole query over every segment a GPU owns.  Geometry (pgpu_internal.h): one 512-thread
-// workgroup per CU owns a contiguous range of 2048-doc tiles.
+// One launch runs a whole query over every segment a GPU owns.  Geometry (pgpu_internal.h): one workgroup per CU
+// (grid = min(#CUs, #tiles)) owns a contiguous range of 2048-doc tiles; two variants, chosen on the host:
+//   SPARSE  1024 threads = 4 loader + 12 consumer waves (~90 VGPRs) -- selective filters, candidate queues
+//   DENSE    512 threads = 2 loader +  6 consumer waves (~190 VGPRs) -- most docs survive, wide aggregation
 //
-//   LOADER (wave 0)      streams the tile's "staged" forward-index columns (the scan columns of the dense part of
+//   LOADERS              stream each tile's "staged" forward-index columns (the scan columns of the dense part of
 //                        the filter, plus the group / aggregation columns when most docs survive) into a ring of
-//                        LDS slots with global_load_lds (16 B per lane, 1 KiB per instruction), and publishes slot k
-//                        behind a counted `s_waitcnt vmcnt` once its bytes have landed.  It only ever waits for its
-//                        own DMAs, so tens of KiB stay in flight per CU regardless of what the consumers do.
-//   CONSUMERS (1..7)     consumer c takes tiles c, c+7, ...  Lane l owns docs [32l, 32l+32): its 32*b bits are b
+//                        LDS slots with global_load_lds (16 B per lane, 1 KiB per instruction), and publish slot k
+//                        behind a counted `s_waitcnt vmcnt` once its bytes have landed.  A loader only ever waits
+//                        for its own DMAs, so ~64 KiB stay in flight per CU regardless of what the consumers do.
+//   CONSUMERS            consumer c takes tiles c, c+NCONS, ...  Lane l owns docs [32l, 32l+32): its 32*b bits are b
 //                        consecutive big-endian words, read with the widest bank-conflict-free ds_read and unpacked
 //                        with compile-time shifts (one template instantiation per bit width) into 32 dict ids.
 //
