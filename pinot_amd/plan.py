@@ -228,14 +228,32 @@ class GroupTable:
     layout: TableLayout
 
 
-@dataclass
 class QueryResult:
-    query: QueryContext
-    aggregation_result: Optional[List] = None        # aggregation-only: final values in aggregation order
-    group_rows: Optional[List[tuple]] = None         # group-by: (group values..., final agg values...) all groups
-    rows: Optional[List[tuple]] = None               # SELECT-ordered rows after ORDER BY / LIMIT
-    stats: ExecutionStats = field(default_factory=ExecutionStats)
-    intermediate: Optional[dict] = None              # group values -> list of intermediate values
+    """Final result of one query.  For group-by, ``group_rows`` (every group) and ``intermediate`` are
+    materialised from the vectorised columns on first access; ``rows`` (after ORDER BY / LIMIT) always is."""
+
+    def __init__(self, query: QueryContext, stats: Optional[ExecutionStats] = None):
+        self.query = query
+        self.stats = stats if stats is not None else ExecutionStats()
+        self.aggregation_result: Optional[List] = None   # aggregation-only: final values in aggregation order
+        self.rows: Optional[List[tuple]] = None           # SELECT-ordered rows after ORDER BY / LIMIT
+        self._columns: Optional["GroupColumns"] = None
+        self._group_rows: Optional[List[tuple]] = None
+        self._intermediate: Optional[dict] = None
+
+    @property
+    def group_rows(self) -> Optional[List[tuple]]:
+        """group-by: (group values..., final agg values...) for every group, ascending by global key."""
+        if self._group_rows is None and self._columns is not None:
+            self._group_rows = self._columns.rows()
+        return self._group_rows
+
+    @property
+    def intermediate(self) -> Optional[dict]:
+        """group values -> intermediate values (AVG as (sum, count))."""
+        if self._intermediate is None and self._columns is not None:
+            self._intermediate = self._columns.intermediate()
+        return self._intermediate
 
 
 def final_value(fn: str, cell_count: int, cell: Optional[int], op: int, vtype: int):
@@ -465,23 +483,99 @@ def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats
                     np.iinfo(np.int64).min if op == PGPU_RED_MAX_I64 else 0)
         fin, inter = values_of(row)
         res.aggregation_result = fin
-        res.intermediate = {(): inter}
+        res._intermediate = {(): inter}
         res.rows = [tuple(fin)]
         return res
-    cards = [len(g) for g in global_dicts]
-    group_rows = []
-    inter_map = {}
-    for k, row in zip(table.keys.tolist(), table.cells):
-        vals = []
-        for g, card in zip(global_dicts, cards):
+    cols = GroupColumns(query, table, global_dicts)
+    res._columns = cols
+    res.rows = [to_select_order(query, r) for r in cols.rows(cols.order_and_limit())]
+    return res
+
+
+class GroupColumns:
+    """A compacted group table decoded column-wise (numpy): group values per group column and final values per
+    aggregation, so that ORDER BY / LIMIT over a million groups costs a sort, not a Python loop per group."""
+
+    def __init__(self, query: QueryContext, table: GroupTable, global_dicts: Sequence):
+        self.query = query
+        L = table.layout
+        k = table.keys.astype(np.int64, copy=True)
+        self.values = []
+        for g in global_dicts:
+            card = len(g)
             gid = k % card
             k //= card
-            v = g[gid]
-            vals.append(v.item() if hasattr(v, "item") else v)
-        fin, inter = values_of(row)
-        group_rows.append(tuple(vals) + tuple(fin))
-        inter_map[tuple(vals)] = inter
-    res.group_rows = group_rows
-    res.intermediate = inter_map
-    res.rows = [to_select_order(query, r) for r in order_and_limit(query, group_rows)]
-    return res
+            arr = np.asarray(g, dtype=object) if isinstance(g, list) else np.asarray(g)
+            self.values.append(arr[gid])
+        cnt = table.cells[:, 0] if len(table.keys) else np.zeros(0, dtype=np.int64)
+        self.count = cnt
+        self.finals, self.sums = [], []
+        for ai, a in enumerate(query.aggregations):
+            sec = L.agg_section[ai]
+            op = L.section_op[sec]
+            vt = L.agg_value_type[ai]
+            cell = table.cells[:, sec] if sec > 0 else None
+            fn = a.function
+            s = None
+            if fn == "COUNT":
+                f = cnt.astype(np.int64)
+            elif fn in ("SUM", "AVG"):
+                s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)
+                f = s if fn == "SUM" else s / cnt  # compacted groups have count > 0
+            else:  # MIN / MAX: order-preserving keys (pgpu_decode_minmax_key)
+                if vt in (PGPU_INT, PGPU_LONG):
+                    f = cell.astype(np.float64)
+                else:
+                    f = np.where(cell >= 0, cell, cell ^ np.int64(0x7FFFFFFFFFFFFFFF)).view(np.float64)
+            self.finals.append(f)
+            self.sums.append(s)
+
+    def __len__(self):
+        return len(self.count)
+
+    def order_and_limit(self) -> np.ndarray:
+        """Row indexes after ORDER BY / LIMIT: stable sort by each ORDER BY expression (GroupByDataTableReducer,
+        IndexedTable.finish), ties kept in ascending global-key order like ``order_and_limit``."""
+        q = self.query
+        n = len(self)
+        if not q.order_by:
+            return np.arange(min(n, q.limit))
+        names = list(q.group_by) + [a.result_name for a in q.aggregations]
+        columns = self.values + self.finals
+        keys = []
+        for ob in q.order_by:
+            c = columns[names.index(ob.expression)]
+            if c.dtype.kind in "iuf":
+                kk = c.astype(np.float64) if c.dtype.kind == "f" else c.astype(np.int64)
+            else:
+                kk = np.unique(c, return_inverse=True)[1].astype(np.int64)
+            keys.append(kk if ob.ascending else -kk)
+        if n > 4 * q.limit > 0:
+            # only rows whose primary key is at least as good as the limit-th one can be in the result
+            kth = np.partition(keys[0], q.limit - 1)[q.limit - 1]
+            cand = np.flatnonzero(keys[0] <= kth)
+            return cand[np.lexsort([k[cand] for k in keys[::-1]])][: q.limit]
+        return np.lexsort(keys[::-1])[: q.limit]
+
+    def rows(self, idx: Optional[np.ndarray] = None) -> List[tuple]:
+        sel = (lambda a: a) if idx is None else (lambda a: a[idx])
+        parts = [sel(v).tolist() for v in self.values]
+        for a, f in zip(self.query.aggregations, self.finals):
+            parts.append([int(x) for x in sel(f).tolist()] if a.function == "COUNT" else sel(f).tolist())
+        return [tuple(r) for r in zip(*parts)] if parts else []
+
+    def intermediate(self) -> dict:
+        out = {}
+        gv = [v.tolist() for v in self.values]
+        cnt = self.count.tolist()
+        cols = []
+        for a, f, s in zip(self.query.aggregations, self.finals, self.sums):
+            if a.function == "AVG":
+                cols.append([(x, c) for x, c in zip(s.tolist(), cnt)])
+            elif a.function == "COUNT":
+                cols.append([int(x) for x in f.tolist()])
+            else:
+                cols.append(f.tolist())
+        for i in range(len(cnt)):
+            out[tuple(g[i] for g in gv)] = [c[i] for c in cols]
+        return out
