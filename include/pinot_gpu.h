@@ -180,6 +180,12 @@ typedef struct {
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
+/* Group-by strategy for large key spaces: from 65,536 keys up, matched docs are written as records into
+ * per-(key partition, workgroup) regions and each partition is then aggregated in an LDS table (one aggregated
+ * column of a 4-byte type at most; otherwise HBM atomics).  These flags force it for any group-by shape the
+ * partitioned path supports, and shrink its regions so that the spill path runs (tests and tuning). */
+#define PGPU_Q_PARTITION 2ull
+#define PGPU_Q_PART_SPILL 4ull
 
 /* ---- partial-result table ----------------------------------------------------------------------------------
  * A query produces a dense table over G = prod(group_cardinalities) keys (G = 1 for aggregation only), laid out

@@ -29,7 +29,7 @@ PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
 PGPU_PRED_RANGE, PGPU_PRED_SET = 0, 1
 PGPU_AGG_COUNT, PGPU_AGG_SUM, PGPU_AGG_MIN, PGPU_AGG_MAX, PGPU_AGG_AVG = range(5)
 PGPU_RED_SUM_I64, PGPU_RED_SUM_F64, PGPU_RED_MIN_I64, PGPU_RED_MAX_I64 = range(4)
-PGPU_Q_STATS = 1
+PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL = 1, 2, 4
 
 
 class PinotGpuError(RuntimeError):

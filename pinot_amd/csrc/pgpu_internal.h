@@ -148,12 +148,19 @@ struct DevAgg {
   int32_t sec;      // table section (0 for COUNT)
   int32_t op;       // PGPU_RED_* of the section
   int32_t vtype;    // dictionary type
-  int32_t pad;
+  int32_t emit;     // PART mode: this aggregation's column is the one carried in the records (first such agg)
 };
 
 #define PGPU_MODE_AGG 0
 #define PGPU_MODE_LDS 1
 #define PGPU_MODE_GLOBAL 2
+// Large key spaces (G >= PGPU_PART_MIN_KEYS): the query kernel appends (key[, raw value]) records to per
+// (key partition, workgroup) regions in HBM, then part_reduce_kernel aggregates each partition in an LDS table.
+// Replaces one HBM atomic per (doc, section) with plain record stores + LDS atomics.
+#define PGPU_MODE_PART 3
+#define PGPU_PART_MIN_KEYS 65536
+#define PGPU_PART_LDS_BYTES (128 * 1024)   // phase-2 LDS table per partition (keys x sections x 8 B)
+#define PGPU_PART_MAX_PARTS 8192           // phase-1 LDS cursors (4 B each) must fit PGPU_LDS_TABLE_BYTES
 
 #define PGPU_STAT_MATCHED 0
 #define PGPU_STAT_SCANNED 1
@@ -186,6 +193,16 @@ struct DevParams {
   int32_t ltab_bytes;             // LDS group table bytes (MODE_LDS)
   int32_t max_instrs;             // max DMA instructions of one tile (loader vmcnt budget)
   int32_t dense;                  // kernel variant (PGPU_THREADS)
+  // PART mode: records of rw uint32 words {global key[, raw 4-byte dictionary value of column pcol]}; region of
+  // (partition q, workgroup w) = records [(q * grid + w) * rcap, +rcap); rcount[q * grid + w] = records written
+  uint32_t* recs;
+  uint32_t* rcount;
+  int32_t pshift;                 // keys per partition = 1 << pshift
+  int32_t nparts;
+  int32_t rcap;
+  int32_t rw;
+  int32_t pcol;                   // query column carried in the records (-1: COUNT only)
+  int32_t pad1;
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];

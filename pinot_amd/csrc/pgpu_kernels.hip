@@ -262,6 +262,17 @@ FI void cell_atomic(int64_t* cell, int32_t op, int64_t v) {
   else if (op == PGPU_RED_MIN_I64) atomicMin((long long*)cell, (long long)v);
   else atomicMax((long long*)cell, (long long)v);
 }
+// PART mode: a record carries the raw 4-byte dictionary value; each aggregation derives its cell from it.
+FI int64_t raw_to_cell(uint32_t raw, int32_t vtype, int32_t op) {
+  if (vtype == PGPU_INT) return (int64_t)(int32_t)raw;
+  const double d = (double)__uint_as_float(raw);
+  return op == PGPU_RED_SUM_F64 ? __double_as_longlong(d) : key_of_double(d);
+}
+template <int N>
+FI void gather_raw(const void* dict, const uint32_t (&idx)[N], uint32_t (&out)[N]) {
+#pragma unroll
+  for (int r = 0; r < N; ++r) out[r] = gld((const uint32_t*)dict, idx[r]);
+}
 
 // ---- fixed-bit extraction (compile-time bit width) -------------------------------------------------------------
 // w[] = the lane's B words, byte-swapped (MSB-first bit order); value i occupies bits [i*B, (i+1)*B).
@@ -942,6 +953,42 @@ FI int64_t* table_base(const DevParams& p, const Lds& L) {
   return MODE == PGPU_MODE_LDS ? L.ltab : p.table;
 }
 
+// PART mode: append the records {key[, raw]} of the live entries to this workgroup's region of each key's
+// partition.  All N slot reservations (LDS cursor atomics) are issued before the first store.  A full region
+// spills the doc straight into the HBM table with atomics: correct, only slower.
+FI void part_spill(const DevParams& p, uint32_t key, uint32_t raw) {
+  atomicAdd((unsigned long long*)&p.table[key], 1ull);
+  for (int a = 0; a < p.nagg; ++a) {
+    const DevAgg ag = p.aggs[a];
+    if (ag.fn == PGPU_AGG_COUNT) continue;
+    cell_atomic(&p.table[(size_t)ag.sec * p.G + key], ag.op, raw_to_cell(raw, ag.vtype, ag.op));
+  }
+}
+template <int N>
+FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], const uint32_t (&raw)[N], uint32_t live) {
+  uint32_t* cur = (uint32_t*)L.ltab;
+  uint32_t slot[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) slot[r] = ((live >> r) & 1u) ? atomicAdd(cur + (key[r] >> p.pshift), 1u) : 0u;
+  const uint32_t cap = (uint32_t)p.rcap;
+  uint32_t spill = 0;
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    if (!((live >> r) & 1u)) continue;
+    if (slot[r] < cap) {
+      const size_t rec = ((size_t)(key[r] >> p.pshift) * gridDim.x + blockIdx.x) * (size_t)cap + slot[r];
+      if (p.rw == 1) p.recs[rec] = key[r];
+      else *(u32x2*)(p.recs + 2 * rec) = u32x2{key[r], raw[r]};
+    } else {
+      spill |= 1u << r;
+    }
+  }
+  if (spill)
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      if ((spill >> r) & 1u) part_spill(p, key[r], raw[r]);
+}
+
 // Sparse (per-doc) aggregation of the survivors `m` among this lane's U docs: group key = mixed radix of the
 // remapped group ids, COUNT into section 0, every other aggregation gathers its id and dictionary value.
 template <int MODE>
@@ -961,6 +1008,21 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
       remap_ids(remap, id);
 #pragma unroll
       for (int u = 0; u < U; ++u) key[u] += id[u] * p.gstride[g];
+    }
+    if (MODE == PGPU_MODE_PART) {
+      uint32_t raw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) raw[u] = 0;
+      if (p.pcol >= 0) {
+        const DevColumn c = col_of(ss, p.pcol);
+        uint32_t id[U];
+        gather_ids(colref(c), doc, id);
+#pragma unroll
+        for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
+        gather_raw(c.dict, id, raw);
+      }
+      part_emit(p, L, key, raw, m);
+      return;
     }
     int64_t* tab = table_base<MODE>(p, L);
 #pragma unroll
@@ -1099,6 +1161,7 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
       } else {
         ag = p.aggs[ai];
         if (ag.fn == PGPU_AGG_COUNT) continue;
+        if (MODE == PGPU_MODE_PART && !ag.emit) continue;  // derived in phase 2 from the emitted column
         col = ag.col;
       }
       uint32_t lo[16];
@@ -1133,8 +1196,23 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
           for (int i = 0; i < 16; ++i)
             if (lane_bit(hm, i)) klist[k++] = (int32_t)key[i];
           wave_sync();
-          int64_t* tab = table_base<MODE>(p, L);
-          for (int e = lane; e < nh; e += 64) atomicAdd((unsigned long long*)&tab[(uint32_t)klist[e]], 1ull);
+          if (MODE == PGPU_MODE_PART) {
+            if (p.pcol < 0)
+              for (int r0 = 0; r0 * 64 < nh; r0 += 8) {
+                uint32_t kk[8], raw[8], live = 0;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                  const int e = lane + 64 * (r0 + r);
+                  kk[r] = e < nh ? (uint32_t)klist[e] : 0u;
+                  raw[r] = 0u;
+                  live |= (uint32_t)(e < nh) << r;
+                }
+                part_emit(p, L, kk, raw, live);
+              }
+          } else {
+            int64_t* tab = table_base<MODE>(p, L);
+            for (int e = lane; e < nh; e += 64) atomicAdd((unsigned long long*)&tab[(uint32_t)klist[e]], 1ull);
+          }
         }
         continue;
       }
@@ -1146,6 +1224,27 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
           if (lane_bit(hm, i)) vlist[k++] = (int32_t)lo[i];
       }
       wave_sync();
+      if (MODE == PGPU_MODE_PART) {
+        for (int r0 = 0; r0 * 64 < nh; r0 += 8) {
+          uint32_t idx[8], raw[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int e = lane + 64 * (r0 + r);
+            idx[r] = e < nh ? (uint32_t)vlist[e] : 0u;
+          }
+          gather_raw(c.dict, idx, raw);
+          uint32_t kk[8], live = 0;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int e = lane + 64 * (r0 + r);
+            kk[r] = e < nh ? (uint32_t)klist[e] : 0u;
+            live |= (uint32_t)(e < nh) << r;
+          }
+          part_emit(p, L, kk, raw, live);
+        }
+        wave_sync();
+        continue;
+      }
       int64_t part = sec_identity(ag.op);
       int64_t* tab = table_base<MODE>(p, L) + (size_t)ag.sec * p.G;
       for (int r0 = 0; r0 * 64 < nh; r0 += 8) {
@@ -1335,6 +1434,8 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
     const int n = p.nsec * (int)p.G;
     for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
   }
+  if (MODE == PGPU_MODE_PART)
+    for (int i = threadIdx.x; i < p.nparts; i += NT) ((uint32_t*)L.ltab)[i] = 0u;
   __syncthreads();
   // this workgroup's contiguous tile range
   const int t0 = (int)(((int64_t)p.total_tiles * blockIdx.x) / gridDim.x);
@@ -1384,6 +1485,67 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
       if (cnt == 0) continue;
       atomicAdd((unsigned long long*)&p.table[key], (unsigned long long)cnt);
       for (int s = 1; s < p.nsec; ++s) cell_atomic(&p.table[(size_t)s * p.G + key], p.sec_op[s], L.ltab[s * G + key]);
+    }
+  } else if (MODE == PGPU_MODE_PART) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < p.nparts; q += NT) {
+      const uint32_t n = ((const uint32_t*)L.ltab)[q];
+      p.rcount[(size_t)q * gridDim.x + blockIdx.x] = n < (uint32_t)p.rcap ? n : (uint32_t)p.rcap;
+    }
+  }
+}
+
+// PART mode, phase 2: workgroup q aggregates the records of key partition q (from every query workgroup's
+// region) into an LDS table [nsec][K], then folds it into the HBM table, which holds the identities plus the
+// phase-1 spills.  Records are read 4 per thread per round, all loads before the first LDS atomic.
+__global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
+  extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
+  const uint32_t K = 1u << p.pshift;
+  const uint32_t q = blockIdx.x;
+  const uint64_t key0 = (uint64_t)q * K;
+  const uint32_t nk = (uint32_t)min((uint64_t)K, p.G - key0);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)p.nsec * K; i += blockDim.x) ptab[i] = sec_identity(p.sec_op[i / K]);
+  __syncthreads();
+  constexpr int R = 4;
+  for (int w = 0; w < nwg; ++w) {
+    const uint32_t n = p.rcount[(size_t)q * nwg + w];
+    const size_t base = ((size_t)q * nwg + w) * (size_t)p.rcap;
+    for (uint32_t i0 = 0; i0 < n; i0 += R * blockDim.x) {
+      uint32_t key[R], raw[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t i = i0 + r * blockDim.x + threadIdx.x;
+        key[r] = 0xFFFFFFFFu;
+        raw[r] = 0;
+        if (i < n) {
+          if (p.rw == 1) {
+            key[r] = gld(p.recs, base + i);
+          } else {
+            const u32x2 v = gld((const u32x2*)p.recs, base + i);
+            key[r] = v.x;
+            raw[r] = v.y;
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (key[r] == 0xFFFFFFFFu) continue;
+        const uint32_t k = key[r] - (uint32_t)key0;
+        atomicAdd((unsigned long long*)&ptab[k], 1ull);
+        for (int a = 0; a < p.nagg; ++a) {
+          const DevAgg ag = p.aggs[a];
+          if (ag.fn == PGPU_AGG_COUNT) continue;
+          cell_atomic(&ptab[(size_t)ag.sec * K + k], ag.op, raw_to_cell(raw[r], ag.vtype, ag.op));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) {
+    if (ptab[k] == 0) continue;
+    for (int s = 0; s < p.nsec; ++s) {
+      int64_t* cell = &p.table[(size_t)s * p.G + key0 + k];
+      *cell = cell_combine(p.sec_op[s], *cell, ptab[(size_t)s * K + k]);
     }
   }
 }
@@ -1487,8 +1649,8 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
 #define PGPU_ALL_QUERY_KERNELS(X)                                                                          \
-  X(PGPU_MODE_AGG, 0) X(PGPU_MODE_LDS, 0) X(PGPU_MODE_GLOBAL, 0) X(PGPU_MODE_AGG, 1) X(PGPU_MODE_LDS, 1) \
-  X(PGPU_MODE_GLOBAL, 1)
+  X(PGPU_MODE_AGG, 0) X(PGPU_MODE_LDS, 0) X(PGPU_MODE_GLOBAL, 0) X(PGPU_MODE_PART, 0) X(PGPU_MODE_AGG, 1) \
+  X(PGPU_MODE_LDS, 1) X(PGPU_MODE_GLOBAL, 1) X(PGPU_MODE_PART, 1)
 
 hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
   hipError_t e = hipSuccess;
@@ -1498,7 +1660,16 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
                             (int)lds_bytes);
   PGPU_ALL_QUERY_KERNELS(SET_ATTR)
 #undef SET_ATTR
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PGPU_PART_LDS_BYTES);
   return e;
+}
+
+hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
+  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(p.nparts), dim3(1024), lds, st, p, nwg);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {

@@ -32,6 +32,7 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
+hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts, int64_t* total,
                                int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
 
@@ -130,7 +131,7 @@ struct PinnedMem {
 struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
-  DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof;
+  DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof, recs, rcount;
   PinnedMem h_arena, h_stats, h_total, h_table;
   bool busy = false;
   ~Workspace() {
@@ -1110,6 +1111,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     p.aggs[a].sec = L.agg_section[a];
     p.aggs[a].op = L.section_op[L.agg_section[a]];
     p.aggs[a].vtype = L.agg_value_type[a];
+    p.aggs[a].emit = 0;
   }
   int64_t tiles = 0;
   for (int s = 0; s < q->num_segments; ++s) {
@@ -1191,11 +1193,32 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   // for initialising and flushing one table copy per workgroup
   const int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
   const bool many = pk.est_matched > 4.0 * (double)L.num_keys * grid;
+  // partitioned group-by (PGPU_MODE_PART): large key spaces, at most one aggregated column of a 4-byte type
+  bool part_ok = q->num_group_columns > 0 &&
+                 (L.num_keys >= PGPU_PART_MIN_KEYS || (q->flags & PGPU_Q_PARTITION) != 0);
+  int pcol = -1;
+  for (int a = 0; a < q->num_aggs && part_ok; ++a) {
+    if (q->aggs[a].fn == PGPU_AGG_COUNT) continue;
+    if (pcol >= 0 && q->aggs[a].column != pcol) part_ok = false;
+    if (L.agg_value_type[a] != PGPU_INT && L.agg_value_type[a] != PGPU_FLOAT) part_ok = false;
+    if (pcol < 0) {
+      pcol = q->aggs[a].column;
+      p.aggs[a].emit = 1;
+    }
+  }
+  int pshift = 0;
+  while ((8ull * L.num_sections << (pshift + 1)) <= PGPU_PART_LDS_BYTES) ++pshift;
+  const uint64_t nparts = (L.num_keys + (1ull << pshift) - 1) >> pshift;
+  part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31);
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
-  else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && (PGPU_LDS_LIMIT - fixed - align16(tbytes)) / S >= 4)
+  else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && !(q->flags & PGPU_Q_PARTITION) &&
+           (PGPU_LDS_LIMIT - fixed - align16(tbytes)) / S >= 4)
     p.mode = PGPU_MODE_LDS;
+  else if (part_ok) p.mode = PGPU_MODE_PART;
   else p.mode = PGPU_MODE_GLOBAL;
-  p.ltab_bytes = p.mode == PGPU_MODE_LDS ? (int32_t)tbytes : 0;
+  if (p.mode != PGPU_MODE_PART)
+    for (int a = 0; a < q->num_aggs; ++a) p.aggs[a].emit = 0;
+  p.ltab_bytes = p.mode == PGPU_MODE_LDS ? (int32_t)tbytes : (p.mode == PGPU_MODE_PART ? (int32_t)(4 * nparts) : 0);
   const size_t avail = PGPU_LDS_LIMIT - fixed - align16(p.ltab_bytes);
   p.slot_bytes = S;
   p.ring_slots = (int32_t)std::min<size_t>(PGPU_RING_MAX, avail / S);
@@ -1245,6 +1268,32 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
+  if (p.mode == PGPU_MODE_PART) {
+    // region capacity: 1.25x the expected records per (partition, workgroup) + slack; full regions spill to
+    // HBM atomics, so an underestimate costs time, never correctness.  Bounded by half the free HBM.
+    p.pshift = pshift;
+    p.nparts = (int32_t)nparts;
+    p.pcol = pcol;
+    p.rw = pcol >= 0 ? 2 : 1;
+    const double per = pk.est_matched / ((double)grid * (double)nparts);
+    uint64_t cap = (uint64_t)(1.25 * per) + 32;
+    if (q->flags & PGPU_Q_PART_SPILL) cap = 16;
+    cap = (cap + 15) & ~15ull;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    const uint64_t regions = nparts * (uint64_t)grid;
+    const uint64_t have = ws->recs.n;
+    const uint64_t budget = std::max<uint64_t>(have, (uint64_t)free_b / 2);
+    const uint64_t max_cap = budget / (regions * 4ull * p.rw);
+    if (cap > max_cap) cap = max_cap & ~15ull;
+    if (cap > (uint64_t)INT32_MAX) cap = (uint64_t)INT32_MAX & ~15ull;
+    p.rcap = (int32_t)std::max<uint64_t>(cap, 16);
+    e = ws->recs.ensure(regions * (uint64_t)p.rcap * 4ull * p.rw);
+    if (e == hipSuccess) e = ws->rcount.ensure(4ull * regions);
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "group-by record buffers: %s", hipGetErrorString(e)));
+    p.recs = (uint32_t*)ws->recs.p;
+    p.rcount = (uint32_t*)ws->rcount.p;
+  }
   char* h = (char*)ws->h_arena.p;
   memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
   memcpy(h + o_ins, pk.instrs.data(), pk.instrs.size() * sizeof(DevInstr));
@@ -1266,6 +1315,7 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   if (e == hipSuccess && p.mode != PGPU_MODE_AGG) e = pgpu_launch_table_init(p, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
   if (e == hipSuccess) e = pgpu_launch_query(p, grid, dyn, st);
+  if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)ws->stats_out.p, st);
   if (e == hipSuccess)

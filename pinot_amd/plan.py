@@ -306,8 +306,9 @@ class GpuPlanMaker:
 
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
-                 collect_stats: bool = False):
+                 collect_stats: bool = False, query_flags: int = 0):
         self.ctx = ctx
+        self.query_flags = query_flags   # extra PGPU_Q_* flags (strategy overrides for tests / tuning)
         self.num_groups_limit = num_groups_limit
         self.max_init_group_holder_capacity = max_init_group_holder_capacity
         self.collect_stats = collect_stats
@@ -395,7 +396,7 @@ class GpuPlanMaker:
         desc = QueryDesc(num_columns=len(columns), num_segments=len(segments), segments=plans,
                          num_aggs=len(query.aggregations), num_group_columns=len(query.group_by), aggs=aggs,
                          group_columns=gcols, group_cardinalities=gcards,
-                         flags=_lib.PGPU_Q_STATS if self.collect_stats else 0)
+                         flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags)
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:

@@ -215,6 +215,56 @@ def test_inverted_leaves_vs_oracle(gpu_ctx, qi):
             g.release()
 
 
+PART_QUERIES = [
+    "SELECT d, SUM(m), MIN(m), MAX(m), AVG(m), COUNT(*) FROM t WHERE b < 12 GROUP BY d",
+    "SELECT c, COUNT(*) FROM t GROUP BY c ORDER BY COUNT(*) DESC LIMIT 30",
+    "SELECT a, b, c, SUM(f), MAX(f) FROM t WHERE NOT (e = 1 AND g > 10) GROUP BY a, b, c",
+    "SELECT f, g, COUNT(*), SUM(m), MIN(m) FROM t WHERE e = 0 AND (b > 20 OR a = 3) GROUP BY f, g",
+    "SELECT b, COUNT(*), SUM(m), AVG(f) FROM t WHERE c < 2000 GROUP BY b",   # two value columns: HBM atomics
+]
+
+
+@pytest.mark.parametrize("spill", [False, True], ids=["regions", "spill"])
+@pytest.mark.parametrize("qi", range(len(PART_QUERIES)))
+def test_partitioned_groupby_vs_oracle(gpu_ctx, qi, spill):
+    """PGPU_MODE_PART (records into per-partition regions + LDS reduce), forced for small key spaces too; with
+    PART_SPILL the regions hold 16 records so most docs take the HBM-atomic spill path."""
+    from pinot_amd._lib import PGPU_Q_PART_SPILL, PGPU_Q_PARTITION
+    rng = np.random.default_rng(31 + qi)
+    types = {"f": PGPU_FLOAT} if qi == 2 else None
+    segs = [_random_segment(rng, 60_001, f"p{i}", types=types) for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(PART_QUERIES[qi])
+        flags = PGPU_Q_PARTITION | (PGPU_Q_PART_SPILL if spill else 0)
+        res = _gpu(gpu_ctx, q, gs, num_groups_limit=1_000_000, query_flags=flags)
+        _assert_same(res, engine.execute(q, segs, num_groups_limit=1_000_000))
+    finally:
+        for g in gs:
+            g.release()
+
+
+def test_partitioned_groupby_large_key_space(gpu_ctx):
+    """G >= 65,536 selects the partitioned path by default (here ~600k global keys over 2 segments)."""
+    rng = np.random.default_rng(404)
+    segs = []
+    for i in range(2):
+        n = 300_000
+        k = rng.integers(0, 400_000, n).astype(np.int32) * 2 + i
+        m = rng.integers(-50_000, 50_000, n).astype(np.int32)
+        segs.append(build_segment(f"big{i}", {"k": (PGPU_INT, k), "m": (PGPU_INT, m)}))
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql("SELECT k, SUM(m), MAX(m), COUNT(*) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 100")
+        res = _gpu(gpu_ctx, q, gs, num_groups_limit=2_000_000)
+        ref = engine.execute(q, segs, num_groups_limit=2_000_000)
+        _assert_same(res, ref)
+        assert res.rows == ref.rows
+    finally:
+        for g in gs:
+            g.release()
+
+
 def test_group_limit_unsupported(gpu_ctx):
     rng = np.random.default_rng(9)
     seg = _random_segment(rng, 200_000)  # column d: ~66k distinct values present -> IntMap holder
