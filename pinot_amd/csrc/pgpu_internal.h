@@ -161,6 +161,7 @@ struct DevAgg {
 #define PGPU_PART_MIN_KEYS 65536
 #define PGPU_PART_LDS_BYTES (128 * 1024)   // phase-2 LDS table per partition (keys x sections x 8 B)
 #define PGPU_PART_MAX_PARTS 8192           // phase-1 LDS cursors (4 B each) must fit PGPU_LDS_TABLE_BYTES
+#define PGPU_PART_MAX_SECTIONS 5           // count + up to 4 value sections (part_reduce_kernel<NS>)
 
 #define PGPU_STAT_MATCHED 0
 #define PGPU_STAT_SCANNED 1

@@ -1438,8 +1438,13 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
     for (int i = threadIdx.x; i < p.nparts; i += NT) ((uint32_t*)L.ltab)[i] = 0u;
   __syncthreads();
   // this workgroup's contiguous tile range
-  const int t0 = (int)(((int64_t)p.total_tiles * blockIdx.x) / gridDim.x);
-  const int t1 = (int)(((int64_t)p.total_tiles * (blockIdx.x + 1)) / gridDim.x);
+  // XCD-aware placement: workgroups are dealt round-robin to the 8 XCDs, so logical rank (b % 8) * (grid / 8) +
+  // b / 8 gives each XCD one contiguous run of tiles -- a few segments, whose dictionaries then stay in that
+  // XCD's L2 instead of every XCD cycling through all of them
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
   Stats st;
   st.matched = st.scanned = st.sector_bytes = st.dense_bytes = 0;
   Prof pf;
@@ -1497,45 +1502,72 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
 
 // PART mode, phase 2: workgroup q aggregates the records of key partition q (from every query workgroup's
 // region) into an LDS table [nsec][K], then folds it into the HBM table, which holds the identities plus the
-// phase-1 spills.  Records are read 4 per thread per round, all loads before the first LDS atomic.
+// phase-1 spills.  NS = value sections (all reduce the records' one value column); R records per thread per
+// round, all loads issued before the first LDS atomic; section ops are uniform, so each round runs one
+// branch-free atomic loop per section.
+template <int NS>
 __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
   const uint32_t K = 1u << p.pshift;
   const uint32_t q = blockIdx.x;
   const uint64_t key0 = (uint64_t)q * K;
   const uint32_t nk = (uint32_t)min((uint64_t)K, p.G - key0);
-  for (uint32_t i = threadIdx.x; i < (uint32_t)p.nsec * K; i += blockDim.x) ptab[i] = sec_identity(p.sec_op[i / K]);
+  int32_t op[NS > 0 ? NS : 1];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) op[s] = p.sec_op[1 + s];
+  int32_t vt = PGPU_INT;
+  for (int a = 0; a < p.nagg; ++a)
+    if (p.aggs[a].fn != PGPU_AGG_COUNT) vt = p.aggs[a].vtype;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NS + 1) * K; i += blockDim.x)
+    ptab[i] = sec_identity(p.sec_op[i >> p.pshift]);
   __syncthreads();
-  constexpr int R = 4;
+  constexpr int R = 8;
   for (int w = 0; w < nwg; ++w) {
     const uint32_t n = p.rcount[(size_t)q * nwg + w];
     const size_t base = ((size_t)q * nwg + w) * (size_t)p.rcap;
     for (uint32_t i0 = 0; i0 < n; i0 += R * blockDim.x) {
-      uint32_t key[R], raw[R];
+      uint32_t k[R], raw[R];
+      bool ok[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint32_t i = i0 + r * blockDim.x + threadIdx.x;
-        key[r] = 0xFFFFFFFFu;
+        ok[r] = i < n;
+        k[r] = (uint32_t)key0;
         raw[r] = 0;
-        if (i < n) {
-          if (p.rw == 1) {
-            key[r] = gld(p.recs, base + i);
+        if (ok[r]) {
+          if (NS == 0) {
+            k[r] = gld(p.recs, base + i);
           } else {
             const u32x2 v = gld((const u32x2*)p.recs, base + i);
-            key[r] = v.x;
+            k[r] = v.x;
             raw[r] = v.y;
           }
         }
       }
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (key[r] == 0xFFFFFFFFu) continue;
-        const uint32_t k = key[r] - (uint32_t)key0;
-        atomicAdd((unsigned long long*)&ptab[k], 1ull);
-        for (int a = 0; a < p.nagg; ++a) {
-          const DevAgg ag = p.aggs[a];
-          if (ag.fn == PGPU_AGG_COUNT) continue;
-          cell_atomic(&ptab[(size_t)ag.sec * K + k], ag.op, raw_to_cell(raw[r], ag.vtype, ag.op));
+      for (int r = 0; r < R; ++r) k[r] -= (uint32_t)key0;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (ok[r]) atomicAdd((unsigned long long*)&ptab[k[r]], 1ull);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        int64_t* sec = ptab + (size_t)(1 + s) * K;
+        if (op[s] == PGPU_RED_SUM_I64) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (ok[r]) atomicAdd((unsigned long long*)&sec[k[r]], (unsigned long long)(int64_t)(int32_t)raw[r]);
+        } else if (op[s] == PGPU_RED_SUM_F64) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (ok[r]) atomicAdd((double*)&sec[k[r]], (double)__uint_as_float(raw[r]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            if (!ok[r]) continue;
+            const int64_t c = raw_to_cell(raw[r], vt, op[s]);
+            if (op[s] == PGPU_RED_MIN_I64) atomicMin((long long*)&sec[k[r]], (long long)c);
+            else atomicMax((long long*)&sec[k[r]], (long long)c);
+          }
         }
       }
     }
@@ -1543,7 +1575,8 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) {
     if (ptab[k] == 0) continue;
-    for (int s = 0; s < p.nsec; ++s) {
+#pragma unroll
+    for (int s = 0; s <= NS; ++s) {
       int64_t* cell = &p.table[(size_t)s * p.G + key0 + k];
       *cell = cell_combine(p.sec_op[s], *cell, ptab[(size_t)s * K + k]);
     }
@@ -1660,16 +1693,27 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
                             (int)lds_bytes);
   PGPU_ALL_QUERY_KERNELS(SET_ATTR)
 #undef SET_ATTR
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)part_reduce_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+#define PART_ATTR(NS)                                                                                       \
+  if (e == hipSuccess)                                                                                      \
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                             PGPU_PART_LDS_BYTES);
+  PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
+#undef PART_ATTR
   return e;
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
   const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
-  hipLaunchKernelGGL(part_reduce_kernel, dim3(p.nparts), dim3(1024), lds, st, p, nwg);
-  return hipGetLastError();
+  switch (p.nsec - 1) {
+#define PART_LAUNCH(NS)                                                                        \
+  case NS:                                                                                     \
+    hipLaunchKernelGGL(part_reduce_kernel<NS>, dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
+    return hipGetLastError();
+    PART_LAUNCH(0) PART_LAUNCH(1) PART_LAUNCH(2) PART_LAUNCH(3) PART_LAUNCH(4)
+#undef PART_LAUNCH
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {

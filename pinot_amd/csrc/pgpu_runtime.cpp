@@ -1209,7 +1209,8 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   int pshift = 0;
   while ((8ull * L.num_sections << (pshift + 1)) <= PGPU_PART_LDS_BYTES) ++pshift;
   const uint64_t nparts = (L.num_keys + (1ull << pshift) - 1) >> pshift;
-  part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31);
+  part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31) &&
+            L.num_sections <= PGPU_PART_MAX_SECTIONS;
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
   else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && !(q->flags & PGPU_Q_PARTITION) &&
            (PGPU_LDS_LIMIT - fixed - align16(tbytes)) / S >= 4)
