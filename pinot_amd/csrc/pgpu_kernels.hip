@@ -363,6 +363,7 @@ FI void decode_ids(int bits, const uint32_t* region, const uint32_t* fwd, int ti
 #define PRED_RANGE 0
 #define PRED_SET 1   // bitset over dict ids in the pool
 #define PRED_LIST 2  // up to 8 ids in the pool
+#define PRED_MASK 3  // columns of <= 64 ids: bit id of the 64-bit mask (lo | span << 32)
 
 struct Pred {
   int kind;
@@ -377,7 +378,7 @@ FI Pred make_pred(const DevInstr& in, const int32_t* pool) {
   p.kind = in.pred;
   p.negate = in.negate != 0;
   p.lo = (uint32_t)in.lo;
-  p.span = (uint32_t)(in.hi - in.lo);
+  p.span = in.pred == PRED_MASK ? (uint32_t)in.hi : (uint32_t)(in.hi - in.lo);
   p.bits = (const uint32_t*)(pool + in.pool_off);
 #pragma unroll
   for (int k = 0; k < 8; ++k) p.ids[k] = in.ids[k];  // unused entries are 0xFFFFFFFF (host)
@@ -388,6 +389,8 @@ FI bool eval_pred(const Pred& p, uint32_t id) {
   bool m;
   if (p.kind == PRED_RANGE) {
     m = (id - p.lo) < p.span;
+  } else if (p.kind == PRED_MASK) {
+    m = (uint32_t)((((uint64_t)p.span << 32) | p.lo) >> (id & 63)) & 1u;
   } else if (p.kind == PRED_LIST) {
     m = false;
 #pragma unroll
@@ -404,6 +407,10 @@ FI uint32_t pred_ids(const uint32_t (&ids)[32], const Pred& p) {
   if (p.kind == PRED_RANGE) {
 #pragma unroll
     for (int i = 31; i >= 0; --i) m = (m << 1) | (uint32_t)((ids[i] - p.lo) < p.span);
+  } else if (p.kind == PRED_MASK) {
+    const uint64_t mask = ((uint64_t)p.span << 32) | p.lo;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) m = (m << 1) | ((uint32_t)(mask >> (ids[i] & 63)) & 1u);
   } else if (p.kind == PRED_LIST) {
 #pragma unroll
     for (int i = 31; i >= 0; --i) {
@@ -1133,9 +1140,63 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
 // Dense aggregation of this lane's matched docs `mm` of the tile from decoded ids (registers or the held slot).
 // Per half tile (16 docs per lane): compact keys and ids of the matched docs into the LDS lists, then gather
 // dictionary values with full lanes (4 rounds in flight) and fold them into partials / table cells.
+// Aggregation-only, every aggregated column already in registers: the whole tile's matched ids are compacted into
+// the consumer's 2048-entry list (klist + vlist are contiguous), so all of the tile's dictionary gathers are in
+// flight together -- one gather latency per tile instead of one per half.
+FI bool agg_cols_in_regs(const DevParams& p, const SegState& ss) {
+  if (ss.nreg <= 0) return false;
+  for (int a = 0; a < p.nagg; ++a) {
+    const DevAgg ag = p.aggs[a];
+    if (ag.fn == PGPU_AGG_COUNT) continue;
+    if (ag.col != ss.reg_col0 && !(ss.nreg > 1 && ag.col == ss.reg_col1)) return false;
+  }
+  return true;
+}
+FI void dense_agg_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, uint32_t mm,
+                       const uint32_t (&ra)[32], const uint32_t (&rb)[32]) {
+  const int lane = lane_id();
+  const int cnt = __popc(mm);
+  const int nt = wave_sum_i32(cnt);
+  const int off = wave_excl_scan(cnt);
+  int32_t* list = cv.klist;  // [2 * PGPU_AGG_LIST] >= PGPU_WT
+  for (int a = 0; a < p.nagg; ++a) {
+    const DevAgg ag = p.aggs[a];
+    if (ag.fn == PGPU_AGG_COUNT) continue;
+    const bool r0 = ag.col == ss.reg_col0;
+    const DevColumn c = col_of(ss, ag.col);
+    {
+      int k = off;
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        if (lane_bit(mm, i)) list[k++] = (int32_t)(r0 ? ra[i] : rb[i]);
+    }
+    wave_sync();
+    int64_t part = sec_identity(ag.op);
+    for (int b0 = 0; b0 < nt; b0 += 64 * 8) {
+      uint32_t idx[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = b0 + lane + 64 * r;
+        idx[r] = e < nt ? (uint32_t)list[e] : 0u;
+      }
+      int64_t v[8];
+      gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (b0 + lane + 64 * r < nt) part = cell_combine(ag.op, part, v[r]);
+    }
+    lacc_add(la, cv, a, ag.op, part);
+    wave_sync();
+  }
+}
+
 template <int MODE>
 FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, const TileCtx& t,
                   uint32_t mm, const uint32_t (&ra)[32], const uint32_t (&rb)[32]) {
+  if (MODE == PGPU_MODE_AGG && agg_cols_in_regs(p, ss)) {
+    dense_agg_tile(p, cv, la, ss, mm, ra, rb);
+    return;
+  }
   const int lane = lane_id();
   int32_t* klist = cv.klist;  // keys   [PGPU_AGG_LIST]
   int32_t* vlist = cv.vlist;  // values [PGPU_AGG_LIST]

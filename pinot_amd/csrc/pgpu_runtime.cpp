@@ -720,6 +720,16 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
           in.lo = std::max(0, nd.lo);
           in.hi = std::min(nd.hi, c->card);
           if (in.hi < in.lo) in.hi = in.lo;
+        } else if (nd.pred == PGPU_PRED_SET && c->card <= 64) {
+          in.pred = 3;  // MASK: membership bit of a 64-bit id mask held in two SGPRs (lo, hi)
+          uint64_t mask = 0;
+          for (int k = 0; k < nd.num_ids; ++k) {
+            const int32_t id = nd.ids[k];
+            if (id < 0 || id >= c->card) return fail(PGPU_E_INVALID, "SET id %d out of range", id);
+            mask |= 1ull << id;
+          }
+          in.lo = (int32_t)(uint32_t)mask;
+          in.hi = (int32_t)(uint32_t)(mask >> 32);
         } else if (nd.pred == PGPU_PRED_SET && nd.num_ids <= 8) {
           in.pred = 2;  // LIST: compared in registers, ids inline
           in.n = nd.num_ids;
