@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/pinot_gpu.h"
 #include "pgpu_internal.h"
 
@@ -1675,6 +1677,28 @@ __global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nsla
   }
 }
 
+// ---- host <-> device transfers as kernels ---------------------------------------------------------------------------
+// Per-query metadata and results move through pinned host memory read / written by kernels (zero-copy), not
+// through DMA-engine copies: a DMA copy queued between two query kernels was measured to hold the next kernel
+// back by ~0.13 ms.
+// Prologue: blocks [0, ncopy) copy the packed metadata arena from pinned host memory into HBM, the remaining
+// blocks initialise the table (count / sum sections 0, MIN +max, MAX -max).
+__global__ __launch_bounds__(256) void prologue_kernel(const u32x4* __restrict__ src, u32x4* dst, uint32_t n16,
+                                                        int32_t ncopy, DevParams p) {
+  if ((int)blockIdx.x < ncopy) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += ncopy * 256) dst[i] = src[i];
+    return;
+  }
+  const uint64_t n = p.G * (uint64_t)p.nsec;
+  const uint64_t nb = gridDim.x - ncopy;
+  for (uint64_t i = (blockIdx.x - ncopy) * 256ull + threadIdx.x; i < n; i += nb * 256)
+    p.table[i] = sec_identity(p.sec_op[i / p.G]);
+}
+// Copy `words` int64 of a finished table into pinned host memory.
+__global__ __launch_bounds__(256) void export_kernel(const int64_t* __restrict__ src, int64_t* dst, uint64_t words) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) dst[i] = src[i];
+}
+
 // ---- compaction of a dense table (keys with count > 0) -------------------------------------------------------------
 #define CMP_BLOCK 256
 #define CMP_PER_BLOCK 4096
@@ -1795,6 +1819,27 @@ hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipS
   PGPU_ALL_QUERY_KERNELS(LAUNCH)
 #undef LAUNCH
   return hipErrorInvalidValue;
+}
+
+hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
+                                bool init_table, hipStream_t st) {
+  const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+  const int ncopy = std::max(1, std::min(16, (int)((n16 + 255) / 256)));
+  int ninit = 0;
+  if (init_table) {
+    const uint64_t n = p.G * (uint64_t)p.nsec;
+    ninit = (int)std::min<uint64_t>(4096, (n + 255) / 256);
+    if (ninit < 1) ninit = 1;
+  }
+  hipLaunchKernelGGL(prologue_kernel, dim3(ncopy + ninit), dim3(256), 0, st, (const u32x4*)host_arena,
+                     (u32x4*)dev_arena, n16, ncopy, p);
+  return hipGetLastError();
+}
+
+hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st) {
+  const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(64, (words + 255) / 256));
+  hipLaunchKernelGGL(export_kernel, dim3(blocks), dim3(256), 0, st, src, host_dst, words);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st) {

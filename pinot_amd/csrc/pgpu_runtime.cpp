@@ -33,6 +33,9 @@ hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
+hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
+                                bool init_table, hipStream_t st);
+hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts, int64_t* total,
                                int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
 
@@ -1176,8 +1179,9 @@ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 extern "C" {
 
-int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
-                      uint64_t table_bytes, pgpu_query** out_query) {
+// host_table (device-visible pointer into pinned host memory, or null): the finished table is also exported there
+static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
+                       uint64_t table_bytes, int64_t* host_table, pgpu_query** out_query) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
@@ -1322,15 +1326,19 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   p.stats = (int64_t*)ws->stats.p;
   p.prof = (int64_t*)ws->prof.p;
 
-  e = hipMemcpyAsync(ws->arena.p, ws->h_arena.p, total, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && p.mode != PGPU_MODE_AGG) e = pgpu_launch_table_init(p, st);
+  // metadata in and stats (and small tables) out through pinned host memory touched by kernels: no DMA-engine
+  // copy sits between two queries' kernels
+  void* h_arena_dev = nullptr;
+  void* h_stats_dev = nullptr;
+  e = hipHostGetDevicePointer(&h_arena_dev, ws->h_arena.p, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
+  if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
   if (e == hipSuccess) e = pgpu_launch_query(p, grid, dyn, st);
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
-  if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)ws->stats_out.p, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(ws->h_stats.p, ws->stats_out.p, 8 * PGPU_NSTATS, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
+  if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, L.num_keys * L.num_sections, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
 
   auto* qq = new pgpu_query();
@@ -1347,6 +1355,11 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   return PGPU_OK;
 }
 
+
+int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
+                      uint64_t table_bytes, pgpu_query** out_query) {
+  return launch_impl(ctx, q, stream, dev_table, table_bytes, nullptr, out_query);
+}
 
 int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
@@ -1464,25 +1477,27 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
     release_ws(ctx, tws);
     return fail(PGPU_E_HIP, "table allocation: %s", hipGetErrorString(e));
   }
+  // small tables (aggregation only, or up to a few hundred thousand keys) are exported whole into pinned host
+  // memory right behind the kernel and compacted on the host: pgpu_query_collect then synchronises once
+  const bool small = bytes <= (8u << 20);
+  void* h_table_dev = nullptr;
+  if (small) {
+    e = tws->h_table.ensure(bytes);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&h_table_dev, tws->h_table.p, 0);
+    if (e != hipSuccess) {
+      release_ws(ctx, tws);
+      return fail(PGPU_E_HIP, "host table buffer: %s", hipGetErrorString(e));
+    }
+  }
   pgpu_query* qq = nullptr;
-  rc = pgpu_query_launch(ctx, q, ctx->qstream, tws->table.p, tws->table.n, &qq);
+  rc = launch_impl(ctx, q, ctx->qstream, tws->table.p, tws->table.n, (int64_t*)h_table_dev, &qq);
   if (rc) {
     release_ws(ctx, tws);
     return rc;
   }
   qq->tws = tws;
   qq->layout = L;
-  // small tables (aggregation only, or up to a few hundred thousand keys) come back whole, queued right behind
-  // the kernel, and are compacted on the host: pgpu_query_collect then synchronises once
-  qq->small = bytes <= (8u << 20);
-  if (qq->small) {
-    e = tws->h_table.ensure(bytes);
-    if (e == hipSuccess) e = hipMemcpyAsync(tws->h_table.p, tws->table.p, bytes, hipMemcpyDeviceToHost, qq->stream);
-    if (e != hipSuccess) {
-      pgpu_query_release(qq);
-      return fail(PGPU_E_HIP, "table copy: %s", hipGetErrorString(e));
-    }
-  }
+  qq->small = small;
   e = hipEventRecord(tws->done, qq->stream);
   if (e != hipSuccess) {
     pgpu_query_release(qq);

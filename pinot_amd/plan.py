@@ -150,60 +150,68 @@ class SegmentFilterPlanner:
         return ranges  # exclusive predicates complement these in the kernel (negate)
 
 
-def emit_program(op: FilterOp, col_index: Dict[str, int], keep: list) -> List[FilterNode]:
-    """Prefix-order program of pgpu_filter_node; `keep` holds the ctypes arrays alive."""
-    out: List[FilterNode] = []
+# numpy images of the C structs (include/pinot_gpu.h; sizes checked against ctypes below), so a whole query's
+# per-segment programs are packed into a few buffers instead of thousands of ctypes objects
+NODE_DTYPE = np.dtype({"names": ["op", "column", "pred", "negate", "lo", "hi", "ids", "num_ids", "reserved"],
+                       "formats": ["<i4"] * 6 + ["<u8", "<i4", "<i4"],
+                       "offsets": [0, 4, 8, 12, 16, 20, 24, 32, 36], "itemsize": 40})
+PLAN_DTYPE = np.dtype({"names": ["segment", "column_map", "filter", "num_filter_nodes", "reserved", "group_remap"],
+                       "formats": ["<u8", "<u8", "<u8", "<i4", "<i4", "<u8"],
+                       "offsets": [0, 8, 16, 24, 28, 32], "itemsize": 40})
+assert NODE_DTYPE.itemsize == C.sizeof(FilterNode) and PLAN_DTYPE.itemsize == C.sizeof(SegmentPlan)
 
-    def ids_array(vals: Sequence[int]):
-        arr = (C.c_int32 * max(1, len(vals)))(*vals)
-        keep.append(arr)
-        return C.cast(arr, C.POINTER(C.c_int32)), len(vals)
+
+def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list) -> None:
+    """Append the prefix-order program of pgpu_filter_node as tuples (op, column, pred, negate, lo, hi, ids
+    offset, num_ids) to `nodes`; id lists go to the shared pool `ids` (offsets in int32 units)."""
+    F = _lib
+
+    def pool(vals: Sequence[int]) -> int:
+        off = len(ids)
+        ids.extend(vals)
+        return off
 
     def rec(o: FilterOp):
-        if o.kind in ("EMPTY", "ALL"):
-            out.append(FilterNode(op=_lib.PGPU_F_EMPTY if o.kind == "EMPTY" else _lib.PGPU_F_MATCH_ALL))
-        elif o.kind == "SCAN":
+        k = o.kind
+        if k == "EMPTY" or k == "ALL":
+            nodes.append((F.PGPU_F_EMPTY if k == "EMPTY" else F.PGPU_F_MATCH_ALL, 0, 0, 0, 0, 0, 0, 0))
+        elif k == "SCAN":
             ev = o.evaluator
-            n = FilterNode(op=_lib.PGPU_F_SCAN, column=col_index[o.column], negate=1 if ev.is_exclusive else 0)
+            neg = 1 if ev.is_exclusive else 0
             if ev.kind == "RANGE":
-                n.pred, n.lo, n.hi = _lib.PGPU_PRED_RANGE, ev.start, ev.end
+                nodes.append((F.PGPU_F_SCAN, col_index[o.column], F.PGPU_PRED_RANGE, neg, ev.start, ev.end, 0, 0))
             else:
-                ids = sorted(ev.ids)
-                if ids and ids[-1] - ids[0] + 1 == len(ids):
-                    n.pred, n.lo, n.hi = _lib.PGPU_PRED_RANGE, ids[0], ids[-1] + 1
+                sid = sorted(ev.ids)
+                if sid and sid[-1] - sid[0] + 1 == len(sid):
+                    nodes.append((F.PGPU_F_SCAN, col_index[o.column], F.PGPU_PRED_RANGE, neg, sid[0], sid[-1] + 1,
+                                  0, 0))
                 else:
-                    n.pred = _lib.PGPU_PRED_SET
-                    n.ids, n.num_ids = ids_array(ids)
-            out.append(n)
-        elif o.kind == "INV":
+                    nodes.append((F.PGPU_F_SCAN, col_index[o.column], F.PGPU_PRED_SET, neg, 0, 0, pool(sid),
+                                  len(sid)))
+        elif k == "INV":
             ev = o.evaluator
-            ids = ev.non_matching_dict_ids() if ev.is_exclusive else ev.matching_dict_ids()
-            n = FilterNode(op=_lib.PGPU_F_INVERTED, column=col_index[o.column], negate=1 if ev.is_exclusive else 0)
-            n.ids, n.num_ids = ids_array(ids)
-            out.append(n)
-        elif o.kind == "SORTED":
+            sid = ev.non_matching_dict_ids() if ev.is_exclusive else ev.matching_dict_ids()
+            nodes.append((F.PGPU_F_INVERTED, col_index[o.column], 0, 1 if ev.is_exclusive else 0, 0, 0,
+                          pool(sid), len(sid)))
+        elif k == "SORTED":
             flat = [v for r in o.doc_ranges for v in r]
-            n = FilterNode(op=_lib.PGPU_F_SORTED, column=col_index[o.column],
-                           negate=1 if o.evaluator.is_exclusive and o.evaluator.kind == "SET" else 0)
-            n.ids, _ = ids_array(flat)
-            n.num_ids = len(o.doc_ranges)
-            out.append(n)
-        elif o.kind in ("AND", "OR"):
-            b, ce, e = ((_lib.PGPU_F_AND_BEGIN, _lib.PGPU_F_AND_CHILD_END, _lib.PGPU_F_AND_END) if o.kind == "AND"
-                        else (_lib.PGPU_F_OR_BEGIN, _lib.PGPU_F_OR_CHILD_END, _lib.PGPU_F_OR_END))
-            out.append(FilterNode(op=b))
+            neg = 1 if o.evaluator.is_exclusive and o.evaluator.kind == "SET" else 0
+            nodes.append((F.PGPU_F_SORTED, col_index[o.column], 0, neg, 0, 0, pool(flat), len(o.doc_ranges)))
+        elif k == "AND" or k == "OR":
+            b, ce, e = ((F.PGPU_F_AND_BEGIN, F.PGPU_F_AND_CHILD_END, F.PGPU_F_AND_END) if k == "AND"
+                        else (F.PGPU_F_OR_BEGIN, F.PGPU_F_OR_CHILD_END, F.PGPU_F_OR_END))
+            nodes.append((b, 0, 0, 0, 0, 0, 0, 0))
             for ch in o.children:
                 rec(ch)
-                out.append(FilterNode(op=ce))
-            out.append(FilterNode(op=e))
-        elif o.kind == "NOT":
-            out.append(FilterNode(op=_lib.PGPU_F_NOT))
+                nodes.append((ce, 0, 0, 0, 0, 0, 0, 0))
+            nodes.append((e, 0, 0, 0, 0, 0, 0, 0))
+        elif k == "NOT":
+            nodes.append((F.PGPU_F_NOT, 0, 0, 0, 0, 0, 0, 0))
             rec(o.children[0])
         else:
-            raise ValueError(o.kind)
+            raise ValueError(k)
 
     rec(op)
-    return out
 
 
 # ---- results ---------------------------------------------------------------------------------------------------
@@ -362,39 +370,57 @@ class GpuPlanMaker:
                                    f"{self.num_groups_limit}; first-seen truncation is served by the CPU plan")
 
     def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment]):
-        """Build the pgpu_query_desc (and the ctypes objects it points to)."""
-        keep: list = []
+        """Build the pgpu_query_desc.  Returns (desc, keep, globals_): `keep` owns every buffer the descriptor
+        points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array)."""
         columns = query.columns
         col_index = {c: i for i, c in enumerate(columns)}
-        plans = (SegmentPlan * len(segments))()
+        nseg = len(segments)
         globals_ = [self.global_dictionary(g, segments) for g in query.group_by]
-        for si, seg in enumerate(segments):
+        nodes: list = []
+        ids: list = []
+        starts = []
+        cmaps = []
+        flt = query.filter
+        for seg in segments:
             if query.group_by:
                 self._check_group_limit(query, seg)
-            cmap = (C.c_int32 * max(1, len(columns)))(*[seg.slots[c] for c in columns])
-            keep.append(cmap)
-            op = SegmentFilterPlanner(seg).build(query.filter)
-            nodes = [] if op.kind == "ALL" else emit_program(op, col_index, keep)
-            arr = (FilterNode * max(1, len(nodes)))(*nodes)
-            keep.append(arr)
-            plans[si].segment = seg.handle
-            plans[si].column_map = cmap
-            plans[si].filter = arr
-            plans[si].num_filter_nodes = len(nodes)
-            if query.group_by:
-                rm = (C.c_void_p * len(query.group_by))(
-                    *[(g[1][si].handle if g[1][si] is not None else None) for g in globals_])
-                keep.append(rm)
-                plans[si].group_remap = rm
-        keep.append(plans)
+            slots = seg.slots
+            cmaps.append([slots[c] for c in columns] if columns else [0])
+            starts.append(len(nodes))
+            if flt is not None:
+                op = SegmentFilterPlanner(seg).build(flt)
+                if op.kind != "ALL":
+                    emit_program(op, col_index, nodes, ids)
+        starts.append(len(nodes))
+        cmap = np.array(cmaps, dtype=np.int32).reshape(nseg, max(1, len(columns)))
+        pool = np.array(ids if ids else [0], dtype=np.int32)
+        narr = np.zeros(max(1, len(nodes)), dtype=NODE_DTYPE)
+        if nodes:
+            t = np.array(nodes, dtype=np.int64)
+            for j, name in enumerate(("op", "column", "pred", "negate", "lo", "hi")):
+                narr[name] = t[:, j]
+            narr["ids"] = pool.ctypes.data + 4 * t[:, 6]
+            narr["num_ids"] = t[:, 7]
+        ng = len(query.group_by)
+        remap = np.zeros((nseg, max(1, ng)), dtype=np.uint64)
+        for g, (_, rms) in enumerate(globals_):
+            remap[:, g] = [(rm.handle.value or 0) if rm is not None else 0 for rm in rms]
+        plans = np.zeros(nseg, dtype=PLAN_DTYPE)
+        plans["segment"] = [seg.handle.value for seg in segments]
+        plans["column_map"] = cmap.ctypes.data + cmap.strides[0] * np.arange(nseg, dtype=np.uint64)
+        st = np.array(starts, dtype=np.int64)
+        plans["filter"] = narr.ctypes.data + NODE_DTYPE.itemsize * st[:-1].astype(np.uint64)
+        plans["num_filter_nodes"] = st[1:] - st[:-1]
+        if ng:
+            plans["group_remap"] = remap.ctypes.data + remap.strides[0] * np.arange(nseg, dtype=np.uint64)
         aggs = (Agg * len(query.aggregations))(
             *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
-        keep.append(aggs)
-        gcols = (C.c_int32 * max(1, len(query.group_by)))(*[col_index[g] for g in query.group_by])
-        gcards = (C.c_int32 * max(1, len(query.group_by)))(*[len(g[0]) for g in globals_])
-        keep += [gcols, gcards]
-        desc = QueryDesc(num_columns=len(columns), num_segments=len(segments), segments=plans,
-                         num_aggs=len(query.aggregations), num_group_columns=len(query.group_by), aggs=aggs,
+        gcols = (C.c_int32 * max(1, ng))(*[col_index[g] for g in query.group_by])
+        gcards = (C.c_int32 * max(1, ng))(*[len(g[0]) for g in globals_])
+        keep = [cmap, pool, narr, remap, plans, aggs, gcols, gcards]
+        desc = QueryDesc(num_columns=len(columns), num_segments=nseg,
+                         segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
+                         num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
                          group_columns=gcols, group_cardinalities=gcards,
                          flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags)
         return desc, keep, globals_

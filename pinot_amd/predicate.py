@@ -15,6 +15,7 @@ doubles for FLOAT/DOUBLE, strings compared by code point for STRING.
 from __future__ import annotations
 
 import bisect
+import functools
 from dataclasses import dataclass
 from fractions import Fraction
 from typing import List, Sequence, Union
@@ -25,7 +26,9 @@ from ._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING
 from .query import UNBOUNDED, Predicate
 
 
+@functools.lru_cache(maxsize=65536)
 def _key(value: str, data_type: int):
+    """Literal parsed as the column's stored type (memoised: the same literal is looked up in every segment)."""
     if data_type == PGPU_STRING:
         return value
     if data_type in (PGPU_INT, PGPU_LONG):
@@ -63,10 +66,10 @@ class SortedDictionary:
             i = bisect.bisect_left(self.values, k)
             found = i < self._n and self.values[i] == k
         elif isinstance(k, Fraction):  # fractional literal on an integer dictionary: never equal
-            i = int(np.searchsorted(self.values, float(k), side="left"))
+            i = int(self.values.searchsorted(float(k), side="left"))
             found = False
         else:
-            i = int(np.searchsorted(self.values, k, side="left"))
+            i = int(self.values.searchsorted(k, side="left"))
             found = i < self._n and self.values[i] == k
         return i if found else -(i + 1)
 
