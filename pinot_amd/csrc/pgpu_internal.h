@@ -35,8 +35,9 @@
 #define PGPU_MAX_GCOLS 8
 #define PGPU_MAX_STAGE 6        // staged (LDS-streamed) columns per segment
 #define PGPU_RING_MAX 64        // ring slots (flag arrays are sized for this)
-#define PGPU_CQ_CAP 2304        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile)
-#define PGPU_CQ_FLUSH 256       // candidate-queue flush threshold (queue then still has room for a whole tile)
+#define PGPU_CQ_CAP 1280        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile):
+                                // flush threshold + half a tile (a denser tile is queued in two halves)
+#define PGPU_CQ_FLUSH 256       // candidate-queue flush threshold
 #define PGPU_CQ_TILES 32        // a queue spans at most 32 of the consumer's tiles (5-bit tile index)
 #define PGPU_AGG_LIST 1024      // dense-agg key / value list entries (int32 each, DENSE variant)
 #define PGPU_DOC_U 4            // candidate docs per lane per flush round
@@ -45,10 +46,11 @@
 #define PGPU_MAX_STAGE_INSTRS 31  // DMA instructions per tile (so two tiles always fit the 6-bit vmcnt)
 
 // per-consumer LDS area: mask rows | list (candidate queue; DENSE: also the key / value lists) | accumulators
-#define PGPU_CONS_MASK_BYTES (PGPU_MAX_SLOTS * 64 * 4)
 #define PGPU_CONS_LIST_BYTES_OF(dense) ((dense) ? 2 * PGPU_AGG_LIST * 4 + 1024 : PGPU_CQ_CAP * 2)
 #define PGPU_CONS_ACC_BYTES (PGPU_MAX_AGGS * 8)
-#define PGPU_CONS_BYTES_OF(dense) (PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(dense) + PGPU_CONS_ACC_BYTES)
+// consumer LDS area: mask rows (only as many as the query's programs use, + 1 scratch row), list, partials
+#define PGPU_CONS_BYTES(dense, mask_rows) \
+  ((mask_rows) * 256 + PGPU_CONS_LIST_BYTES_OF(dense) + PGPU_CONS_ACC_BYTES + PGPU_CQ_TILES * 4)
 #define PGPU_FLAG_BYTES (3 * PGPU_RING_MAX * 4)
 
 // column kinds
@@ -203,6 +205,8 @@ struct DevParams {
   int32_t rcap;
   int32_t rw;
   int32_t pcol;                   // query column carried in the records (-1: COUNT only)
+  int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
+  int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
   int32_t pad1;
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
@@ -229,11 +233,12 @@ struct DevParams {
 #define PGPU_P_C_DECODE 11  // filter: SCAN leaf decode + predicate
 
 // LDS bytes of the query kernel for a given ring / table configuration.
-inline uint32_t pgpu_lds_fixed_bytes(int dense, int ltab_bytes) {
-  return (uint32_t)(PGPU_FLAG_BYTES + PGPU_NCONS_OF(dense) * PGPU_CONS_BYTES_OF(dense) + ((ltab_bytes + 15) & ~15));
+inline uint32_t pgpu_lds_fixed_bytes(int dense, int ltab_bytes, int mask_rows) {
+  return (uint32_t)(PGPU_FLAG_BYTES + PGPU_NCONS_OF(dense) * PGPU_CONS_BYTES(dense, mask_rows) +
+                    ((ltab_bytes + 15) & ~15));
 }
-inline uint32_t pgpu_lds_bytes(int dense, int ring_slots, int slot_bytes, int ltab_bytes) {
-  return pgpu_lds_fixed_bytes(dense, ltab_bytes) + (uint32_t)(ring_slots * slot_bytes);
+inline uint32_t pgpu_lds_bytes(int dense, int ring_slots, int slot_bytes, int ltab_bytes, int mask_rows) {
+  return pgpu_lds_fixed_bytes(dense, ltab_bytes, mask_rows) + (uint32_t)(ring_slots * slot_bytes);
 }
 
 // Bytes of one staged column's region in a ring slot and its DMA instruction count.  Widths that are multiples of

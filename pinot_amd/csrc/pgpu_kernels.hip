@@ -610,7 +610,7 @@ FI Lds carve(unsigned char* base, const DevParams& p) {
   L.freef = L.full + PGPU_RING_MAX;
   L.icnt = L.freef + PGPU_RING_MAX;
   L.cons = base + PGPU_FLAG_BYTES;
-  L.ltab = (int64_t*)(L.cons + PGPU_NCONS_OF(DENSE) * PGPU_CONS_BYTES_OF(DENSE));
+  L.ltab = (int64_t*)(L.cons + PGPU_NCONS_OF(DENSE) * p.cons_bytes);
   L.ring = (unsigned char*)L.ltab + ((p.ltab_bytes + 15) & ~15);
   return L;
 }
@@ -769,11 +769,12 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
 // CONSUMERS
 // ================================================================================================================
 struct Cons {
-  uint32_t* masks;  // [MAXS][64]
+  uint32_t* masks;  // [mask_rows][64]
   uint16_t* queue;  // candidate queue [PGPU_CQ_CAP]
   int32_t* klist;   // DENSE: dense-agg keys [PGPU_AGG_LIST] (aliases the queue)
   int32_t* vlist;   // DENSE: dense-agg values [PGPU_AGG_LIST]
   int64_t* acc;     // [MAX_AGGS]  aggregation-only partials of this wave
+  int32_t* qtiles;  // [PGPU_CQ_TILES] tile (in segment) of each queue tile index
 };
 
 // Scalars of the consumer's current segment (SGPRs); arrays stay behind `sg` and are read with cld.
@@ -888,7 +889,7 @@ FI uint32_t leaf_sorted(const DevParams& p, const DocCtx& t, const DevInstr& in)
 template <class Ctx>
 FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, const Ctx& t, int64_t& scanned,
                         int64_t& dense_bytes, Prof& pf) {
-  uint32_t* scratch = cv.masks + (MAXS - 1) * 64;
+  uint32_t* scratch = cv.masks + (p.mask_rows - 1) * 64;
   int pc = 0;
   while (pc < len) {
     const int64_t tfe = now(pf);
@@ -1078,8 +1079,7 @@ FI int new_sectors(uint32_t b, int32_t doc, bool live, int32_t prev_doc, bool pr
 // Flush the candidate queue (doc ids of one segment, ascending): residual filter per doc, then sparse aggregation.
 template <int MODE, int NCONS>
 FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, int n,
-                    int q_tile0, int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes,
-                    Prof& pf) {
+                    int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
   const int lane = lane_id();
   const bool stats = p.flags & PGPU_FLAG_STATS;
   wave_sync();
@@ -1092,7 +1092,7 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
       const int e = base + u * 64 + lane;
       const bool ok = e < n;
       const uint32_t q = ok ? (uint32_t)cv.queue[e] : 0u;
-      d.doc[u] = ok ? (q_tile0 + (int)(q >> 11) * NCONS) * WT + (int)(q & (WT - 1)) : 0;
+      d.doc[u] = ok ? cv.qtiles[q >> 11] * WT + (int)(q & (WT - 1)) : 0;
       d.valid |= (uint32_t)ok << u;
     }
     uint32_t m = d.valid;
@@ -1347,12 +1347,13 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   const int R = p.ring_slots, S = p.slot_bytes;
   Cons cv;
   {
-    unsigned char* base = L.cons + (size_t)cidx * PGPU_CONS_BYTES_OF(DENSE);
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
     cv.masks = (uint32_t*)base;
-    cv.queue = (uint16_t*)(base + PGPU_CONS_MASK_BYTES);
-    cv.klist = (int32_t*)(base + PGPU_CONS_MASK_BYTES);
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
     cv.vlist = cv.klist + PGPU_AGG_LIST;
-    cv.acc = (int64_t*)(base + PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(DENSE));
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(DENSE));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(DENSE) + PGPU_CONS_ACC_BYTES);
   }
   if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
   wave_sync();
@@ -1360,28 +1361,45 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   LaneAcc la;
 #pragma unroll
   for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
-  int qn = 0;       // candidate-queue entries (all of segment `ss`)
-  int q_tile0 = 0;  // tile (in segment) of the queue's first consumer tile
+  int qn = 0;  // candidate-queue entries (all of segment `ss`)
+  int qt = 0;  // tiles in the queue's tile table (cv.qtiles)
   SegState ss;
   int cseg = -1;
   Cursor cur;
   cur.seg = 0;
   cur.tile_in_seg = 0;
   cur.ntiles = 0;
-  if (cidx < ntiles) cur = cursor_at(p, t0 + cidx);
-  int slot_i = cidx % R - NCONS;
-  for (int seq = cidx;; seq += NCONS) {
-    const bool end = seq >= ntiles;
-    if (!end && seq != cidx) cursor_advance(p, cur, NCONS);
-    slot_i += NCONS;
-    while (slot_i >= R) slot_i -= R;
-    const bool segchg = !end && cur.seg != cseg;
-    // single flush site: end of range, segment change, or threshold (the queue then still has room for a tile)
-    if (qn && (end || segchg || qn >= PGPU_CQ_FLUSH || cur.tile_in_seg - q_tile0 >= PGPU_CQ_TILES * NCONS)) {
+  int prev = -1, slot_i = 0;
+  // Tiles are claimed dynamically, in order, from the workgroup's LDS counter: a consumer busy with a queue
+  // flush holds no claimed tile, so it never blocks the ring slot the loaders need next.
+  for (;;) {
+    if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES)) {
       const int64_t tq = now(pf);
-      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, q_tile0, matched, scanned, sector_bytes, dense_bytes, pf);
+      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
       PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
-      qn = 0;
+      qn = qt = 0;
+    }
+    int claim = 0;
+    if (lane == 0) claim = __hip_atomic_fetch_add(L.icnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int seq = __builtin_amdgcn_readlane(claim, 0);
+    const bool end = seq >= ntiles;
+    if (!end) {
+      if (prev < 0) {
+        cur = cursor_at(p, t0 + seq);
+        slot_i = seq % R;
+      } else {
+        cursor_advance(p, cur, seq - prev);
+        slot_i += seq - prev;
+        while (slot_i >= R) slot_i -= R;
+      }
+      prev = seq;
+    }
+    const bool segchg = !end && cur.seg != cseg;
+    if (qn && (end || segchg)) {
+      const int64_t tq = now(pf);
+      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+      PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+      qn = qt = 0;
     }
     if (end) break;
     if (segchg) {
@@ -1455,14 +1473,32 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
         dense_agg<MODE>(p, L, cv, la, ss, t, mm, ra, rb);
       } else if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
         if (lane == 0) matched += nm;
-      } else {
-        // queue the candidates (ascending: lane order, then bit order) as consumer-tile index << 11 | doc in tile
-        if (qn == 0) q_tile0 = cur.tile_in_seg;
-        const uint32_t tag = (uint32_t)((cur.tile_in_seg - q_tile0) / NCONS) << 11;
+      } else if (qn + nm <= PGPU_CQ_CAP) {
+        // queue the candidates (ascending: lane order, then bit order) as queue-tile index << 11 | doc in tile
+        if (lane == 0) cv.qtiles[qt] = cur.tile_in_seg;
+        const uint32_t tag = (uint32_t)qt << 11;
+        ++qt;
         int k = qn + wave_excl_scan(__popc(mm));
         for (uint32_t left = mm; left; left &= left - 1)
           cv.queue[k++] = (uint16_t)(tag | (uint32_t)(32 * lane + __builtin_ctz(left)));
         qn += nm;
+      } else {
+        // a dense tile does not fit behind the queued entries: flush them, then queue and flush the tile in two
+        // halves (lanes 0-31, 32-63: <= 1024 entries each)
+        if (qn) {
+          flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+          qn = qt = 0;
+        }
+        if (lane == 0) cv.qtiles[0] = cur.tile_in_seg;
+        for (int half = 0; half < 2; ++half) {
+          const uint32_t mh = (lane >> 5) == half ? mm : 0u;
+          const int nh = wave_sum_i32(__popc(mh));
+          if (nh == 0) continue;
+          int k = wave_excl_scan(__popc(mh));
+          for (uint32_t left = mh; left; left &= left - 1)
+            cv.queue[k++] = (uint16_t)(32 * lane + __builtin_ctz(left));
+          flush_queue<MODE, NCONS>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
+        }
       }
     }
     if (hold) {
@@ -1541,8 +1577,8 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
     if (lane == 0) slab[0] = st.matched;
     if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) {
       const int64_t* acc =
-          (const int64_t*)(L.cons + (size_t)(wave >= NLOAD ? wave - NLOAD : 0) * PGPU_CONS_BYTES_OF(DENSE) +
-                           PGPU_CONS_MASK_BYTES + PGPU_CONS_LIST_BYTES_OF(DENSE));
+          (const int64_t*)(L.cons + (size_t)(wave >= NLOAD ? wave - NLOAD : 0) * p.cons_bytes +
+                           p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(DENSE));
       slab[p.aggs[lane].sec] = wave < NLOAD ? sec_identity(p.aggs[lane].op) : acc[lane];
     }
   } else if (MODE == PGPU_MODE_LDS) {

@@ -1202,7 +1202,12 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   bool any_dense = false;
   for (const DevSeg& ds : pk.segs) any_dense |= ds.agg_mode == PGPU_AM_DENSE;
   p.dense = any_dense ? 1 : 0;
-  const size_t fixed = pgpu_lds_fixed_bytes(p.dense, 0);
+  // mask rows per consumer: the highest filter slot any program uses, + 1 scratch row (bitmap containers)
+  int max_slot = 0;
+  for (const DevInstr& in : pk.instrs) max_slot = std::max({max_slot, in.dst, in.src, in.care});
+  p.mask_rows = std::min(PGPU_MAX_SLOTS, max_slot + 2);
+  p.cons_bytes = PGPU_CONS_BYTES(p.dense, p.mask_rows);
+  const size_t fixed = pgpu_lds_fixed_bytes(p.dense, 0, p.mask_rows);
   // LDS-privatised table only when it fits next to >= 4 ring slots and enough docs are expected to match to pay
   // for initialising and flushing one table copy per workgroup
   const int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
@@ -1250,7 +1255,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     const int64_t by_bytes = (64 * 1024 + nload * pk.tile_bytes - 1) / (nload * pk.tile_bytes);
     p.inflight = (int32_t)std::max<int64_t>(1, std::min(by_ring, by_bytes));
   }
-  const size_t dyn = pgpu_lds_bytes(p.dense, p.ring_slots, S, p.ltab_bytes);
+  const size_t dyn = pgpu_lds_bytes(p.dense, p.ring_slots, S, p.ltab_bytes, p.mask_rows);
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->lds_ready) {

@@ -244,6 +244,24 @@ def test_partitioned_groupby_vs_oracle(gpu_ctx, qi, spill):
             g.release()
 
 
+@pytest.mark.parametrize("sql", [
+    "SELECT COUNT(*), SUM(a), SUM(b), SUM(c), SUM(d), SUM(e), SUM(f), SUM(g), SUM(m) FROM t WHERE e = 0",
+    "SELECT g, COUNT(*), SUM(a), SUM(b), SUM(c), MAX(d), MIN(f), SUM(m) FROM t WHERE b <> 3 GROUP BY g",
+])
+def test_wide_sparse_aggregation_dense_tiles(gpu_ctx, sql):
+    """More aggregated columns than can be staged: aggregation goes through the candidate queue although about
+    half (or most) of every tile matches, so whole tiles overflow the queue and are queued in two halves."""
+    rng = np.random.default_rng(808)
+    segs = [_random_segment(rng, 150_001, f"w{i}") for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(sql)
+        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
+
+
 def test_partitioned_groupby_large_key_space(gpu_ctx):
     """G >= 65,536 selects the partitioned path by default (here ~600k global keys over 2 segments)."""
     rng = np.random.default_rng(404)
