@@ -102,9 +102,11 @@ struct DevSeg {
   int32_t nreg;                   // AM_DENSE: columns decoded into registers before the slot is released
                                   //           (-1: the slot is held for the whole tile)
   int32_t reg_col[2];             // query columns of the register copies
-  int32_t pad0;
+  int32_t fast;                   // dense program is 1 staged SCAN leaf or an AND of 2 (RANGE / MASK predicates):
+                                  // evaluated in registers, without the interpreter (0 = interpret)
   int32_t stage_col[PGPU_MAX_STAGE];   // query column of staged column j
   int32_t stage_off[PGPU_MAX_STAGE];   // byte offset of its region in a ring slot
+  int32_t fast_ins[2];            // the fast leaves: instruction index within the dense program
 };
 
 // Filter instruction with statically resolved mask slots.

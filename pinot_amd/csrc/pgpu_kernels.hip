@@ -783,6 +783,10 @@ struct SegState {
   const DevColumn* cols;
   const int32_t* const* remaps;
   int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
+  // fast dense program (DevSeg::fast): per leaf bit width, staged offset, predicate kind / lo / span, negate
+  int32_t fast;
+  int32_t f_bits[2], f_off[2], f_kind[2], f_neg[2];
+  uint32_t f_lo[2], f_span[2];
 };
 FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   const DevSeg* sg = p.segs + seg;
@@ -799,6 +803,22 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   ss.nreg = cld(&sg->nreg);
   ss.reg_col0 = cld(&sg->reg_col[0]);
   ss.reg_col1 = cld(&sg->reg_col[1]);
+  ss.fast = cld(&sg->fast);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
+    ss.f_lo[j] = ss.f_span[j] = 0;
+    if (j < ss.fast) {
+      const DevInstr* in = p.instrs + ss.prog_begin + cld(&sg->fast_ins[j]);
+      ss.f_bits[j] = cld(&in->bits);
+      ss.f_off[j] = cld(&in->stage_off);
+      ss.f_kind[j] = cld(&in->pred);
+      ss.f_neg[j] = cld(&in->negate);
+      const int32_t lo = cld(&in->lo), hi = cld(&in->hi);
+      ss.f_lo[j] = (uint32_t)lo;
+      ss.f_span[j] = ss.f_kind[j] == PRED_MASK ? (uint32_t)hi : (uint32_t)(hi - lo);
+    }
+  }
 }
 FI DevColumn col_of(const SegState& ss, int col) { return cld(ss.cols + col); }
 
@@ -933,6 +953,38 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
     pc = next;
   }
   return mrow(cv, 0);
+}
+
+// Fast dense program (SegState::fast leaves ANDed, RANGE / MASK predicates on staged columns): evaluated in
+// registers -- no instruction fetch, no mask-row LDS round trips.  Same result and scan accounting as
+// run_program on the equivalent AND program (a leaf is evaluated only while some doc of the wave survives).
+FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) {
+  uint32_t m = t.valid;
+#pragma unroll 1
+  for (int j = 0; j < ss.fast; ++j) {
+    const int n = wave_sum_i32(__popc(m));
+    if (n == 0) return 0u;
+    if (lane_id() == 0) scanned += n;
+    const int bits = j ? ss.f_bits[1] : ss.f_bits[0];
+    const int off = j ? ss.f_off[1] : ss.f_off[0];
+    const int kind = j ? ss.f_kind[1] : ss.f_kind[0];
+    const uint32_t lo = j ? ss.f_lo[1] : ss.f_lo[0];
+    const uint32_t span = j ? ss.f_span[1] : ss.f_span[0];
+    const bool neg = (j ? ss.f_neg[1] : ss.f_neg[0]) != 0;
+    uint32_t ids[32];
+    decode_ids(bits, (const uint32_t*)(t.slot + off), nullptr, t.tile_in_seg, ids);
+    uint32_t r = 0;
+    if (kind == PRED_MASK) {
+      const uint64_t mask = ((uint64_t)span << 32) | lo;
+#pragma unroll
+      for (int i = 31; i >= 0; --i) r = (r << 1) | ((uint32_t)(mask >> (ids[i] & 63)) & 1u);
+    } else {
+#pragma unroll
+      for (int i = 31; i >= 0; --i) r = (r << 1) | (uint32_t)((ids[i] - lo) < span);
+    }
+    m &= neg ? ~r : r;
+  }
+  return m;
 }
 
 // ---- aggregation helpers ------------------------------------------------------------------------------------------
@@ -1439,7 +1491,8 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
         }
     }
     uint32_t mm = t.valid;
-    if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
+    if (ss.fast) mm = fast_filter(ss, t, scanned);
+    else if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
     const int nm = wave_sum_i32(__popc(mm));
     PROF_ADD(pf, PGPU_P_C_FILTER, tf);
     const int64_t ta = now(pf);

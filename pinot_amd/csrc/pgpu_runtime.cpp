@@ -1089,6 +1089,25 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
   pk.tile_bytes = std::max(pk.tile_bytes, tb);
   pk.est_matched += rho * seg->num_docs;
+  // fast dense program: one staged SCAN leaf, or AND_BEGIN (SCAN AND_CHILD){2} AND_END, RANGE / MASK predicates
+  ds.fast = 0;
+  ds.fast_ins[0] = ds.fast_ins[1] = -1;
+  {
+    int nscan = 0, nand = 0;
+    bool ok = ds.prog_len > 0;
+    for (int i = 0; i < ds.prog_len && ok; ++i) {
+      const DevInstr& in = pk.instrs[ds.prog_begin + i];
+      if (in.op == PGPU_I_SCAN) {
+        ok = nscan < 2 && in.kind == PGPU_COL_FIXED_BIT && in.stage_off >= 0 && (in.pred == 0 || in.pred == 3);
+        if (ok) ds.fast_ins[nscan++] = i;
+      } else if (in.op == PGPU_I_AND_BEGIN) {
+        ok = ++nand == 1 && i == 0;
+      } else {
+        ok = in.op == PGPU_I_AND_CHILD || in.op == PGPU_I_AND_END;
+      }
+    }
+    if (ok && nscan >= 1 && (nand == 0 ? ds.prog_len == 1 : ds.prog_len == 2 * nscan + 2)) ds.fast = nscan;
+  }
   ds.agg_mode = agg_mode;
   ds.nreg = -1;
   ds.reg_col[0] = ds.reg_col[1] = -1;
