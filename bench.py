@@ -95,7 +95,8 @@ def main():
         full = sum(s.column(c).cardinality * width for s in segs)
         dict_bytes += min(full, 32 * st.num_docs_scanned)
     out_bytes = 8 * max(1, len(r_stats.group_rows or [])) * (1 + len(q.aggregations))
-    algo_bytes = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + out_bytes
+    bitmap_bytes = inverted_bytes_read(q, segs)
+    algo_bytes = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
 
     log(f"stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, {st.kernel_ms:.3f} ms")
     for _ in range(args.warmup):
@@ -138,13 +139,11 @@ def main():
 
     # small parity check of the same workload against the oracle (2 x 2^18-doc segments)
     log(f"timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
-    check = None
-    if rank == 0 and not args.no_check:
-        check = parity_check(ctx, w, q, opts)
-
-    cpu = None
+    # the CPU leg (the only one that touches oracle/): Pinot's operators restated on the CPU, timed on this host,
+    # and a GPU-vs-CPU check of the same workload on small segments
+    check = cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(w, q, args)
+        cpu, check = cpu_baseline(ctx, w, q, opts, args)
 
     if rank == 0:
         traffic = _pmc_traffic(args.workload)
@@ -171,7 +170,8 @@ def main():
                          "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
                          "kernel_ms_avg": avg_kernel_ms,
                          "bytes_breakdown": {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
-                                             "dictionaries": dict_bytes, "output": out_bytes}},
+                                             "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes,
+                                             "output": out_bytes}},
             "cpu_baseline": cpu,
             "result": {"matched_docs_per_gpu": st.num_docs_scanned, "groups": (len(result.group_rows)
                        if result and result.group_rows is not None else None),
@@ -198,12 +198,35 @@ def _pmc_traffic(workload):
     return None
 
 
+def inverted_bytes_read(q, segs):
+    """Serialized bytes of every inverted-index bitmap the planned INV leaves read: per
+    segment, the bitmaps of the matching (or, for exclusive predicates, non-matching) dict ids."""
+    import numpy as np
+    from pinot_amd.plan import SegmentFilterPlanner
+
+    total = 0
+    for s in segs:
+        stack = [SegmentFilterPlanner(s).build(q.filter)] if q.filter is not None else []
+        while stack:
+            op = stack.pop()
+            stack.extend(op.children)
+            if op.kind != "INV":
+                continue
+            ev = op.evaluator
+            ids = ev.non_matching_dict_ids() if ev.is_exclusive else ev.matching_dict_ids()
+            inv = s.column(op.column).inverted
+            offs = np.frombuffer(inv, dtype=">i4", count=s.column(op.column).cardinality + 1).astype(np.int64)
+            total += int(sum(offs[i + 1] - offs[i] for i in ids))
+    return total
+
+
 # Looser variants of the bench queries (same plan shapes) so the parity sample matches rows, not only zero.
 PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789")}
 
 
 def parity_check(ctx, w, q, opts):
-    """GPU vs oracle on 2 small segments of the workload: the bench query and a looser variant of it."""
+    """GPU vs oracle on 2 small segments of the workload: the bench query and a looser variant of it
+    (called from the CPU leg only)."""
     from oracle import engine
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.plan import GpuPlanMaker
@@ -236,9 +259,42 @@ def parity_check(ctx, w, q, opts):
             g.release()
 
 
-def cpu_baseline(w, q, args):
-    """Pinot's per-segment operators restated in C (oracle/pinot_cpu.c), timed on this host: the sample's
-    segments are queried repeatedly until ~args.cpu_seconds of wall time, with Pinot's default task count."""
+def cpu_baseline(ctx, w, q, opts, args):
+    """The CPU leg: (1) Pinot's per-segment operators restated in C (oracle/pinot_cpu.c) timed on this host,
+    the sample's segments queried repeatedly until ~args.cpu_seconds of wall time with Pinot's default task
+    count; filters the C port does not cover (OR / NOT / index leaves) time the numpy restatement
+    (oracle/engine.py) instead; (2) the GPU-vs-oracle parity check (parity_check)."""
+    check = None if args.no_check else parity_check(ctx, w, q, opts)
+    from oracle import cpu as ocpu
+
+    try:
+        ocpu._leaves(q.filter)
+    except ValueError:
+        return engine_baseline(w, q, opts, args), check
+    return c_baseline(w, q, args), check
+
+
+def engine_baseline(w, q, opts, args):
+    from oracle import engine
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import build_segment_cpu
+
+    nseg, n = 2, 1 << 21
+    segs = [build_segment_cpu(w, s, n, pack_fixed_bit) for s in range(nseg)]
+    total, runs = 0.0, 0
+    while runs == 0 or total < args.cpu_seconds:
+        t = time.perf_counter()
+        engine.execute(q, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
+        total += time.perf_counter() - t
+        runs += 1
+    return {"value": runs * nseg * n / total, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} run(s) over {nseg} segment(s) x {n} docs of the same workload, oracle/engine.py "
+                      f"(numpy restatement of the filter operator tree incl. bitmap / sorted-index leaves; the C "
+                      f"port covers AND-of-scan filters only), 1 thread",
+            "seconds": total}
+
+
+def c_baseline(w, q, args):
     from oracle.cpu import CpuBaseline, synth_segment
 
     nseg = args.cpu_sample_segments

@@ -9,6 +9,8 @@ Workloads (one GPU's shard, weak scaling: rank r owns global se
   adanalytics  config 5  daysSinceEpoch 10-bit, accountId 20-bit, clicks / impressions 16-bit metric dicts
   range_in     config 2  r 16-bit, i 4-bit, m 16-bit metric
   groupby1m    config 4  k 20-bit (1,048,576 keys), m 16-bit metric
+  bitmap5      config 3  a/b/c/d inverted-indexed (card 4 / 16 / 64 / 256: bitmap, borderline, array, array
+                         containers), e sorted (card 256: doc ranges), m1 / m2 16-bit metrics
 """
 from __future__ import annotations
 
@@ -82,6 +84,7 @@ class SynthColumn:
     values: Callable[[], np.ndarray]   # sorted INT dictionary
     dist: str = "uniform"
     zipf_s: float = 1.1
+    index: str = "fwd"      # "fwd" forward index only, "inv" + bitmap inverted index, "sorted" sorted column
 
 
 @dataclass
@@ -128,7 +131,28 @@ WORKLOADS: Dict[str, Workload] = {
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
         {"num_groups_limit": 2_000_000}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT"),
+    "bitmap5": Workload(
+        "bitmap5", "bitmap5",
+        [SynthColumn("a", 4, lambda: np.arange(4, dtype=np.int32) * 10, index="inv"),
+         SynthColumn("b", 16, lambda: np.arange(16, dtype=np.int32) * 10, index="inv"),
+         SynthColumn("c", 64, lambda: np.arange(64, dtype=np.int32) * 10, index="inv"),
+         SynthColumn("d", 256, lambda: np.arange(256, dtype=np.int32) * 10, index="inv"),
+         SynthColumn("e", 256, lambda: np.arange(256, dtype=np.int32) * 10, index="sorted"),
+         SynthColumn("m1", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 15)),
+         SynthColumn("m2", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 16))],
+        "SELECT SUM(m1), SUM(m2) FROM bitmap5 "
+        "WHERE (a = 10 AND b IN (30, 70)) OR (c = 50 AND d <> 90 AND e BETWEEN 640 AND 1910)",
+        {}, 3, "config 3: inverted-index (Roaring) AND/OR/NOT filter + sorted range, SUM on 2 metric columns"),
 }
+
+
+def sorted_index_bytes(num_docs: int, card: int) -> bytes:
+    """Sorted column with dict id floor(doc * card / num_docs): (start, end inclusive) big-endian int32 pairs
+    (SortedIndexReaderImpl layout)."""
+    v = np.arange(card + 1, dtype=np.int64)
+    starts = (v * num_docs + card - 1) // card
+    pairs = np.stack([starts[:-1], starts[1:] - 1], axis=1).astype(">i4")
+    return pairs.tobytes()
 
 
 class SynthLib:
@@ -145,6 +169,23 @@ class SynthLib:
         self.lib.synth_sync.restype = C.c_int
         self.lib.synth_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         self.lib.synth_copy_to_host.restype = C.c_int
+        self.lib.synth_inverted_index.restype = C.c_int
+        self.lib.synth_inverted_index.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.c_int32,
+                                                  C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64)]
+        self.lib.synth_host_free.argtypes = [C.c_void_p]
+
+    def inverted(self, fwd: bytes, num_docs: int, bits: int, card: int) -> bytes:
+        """BitmapInvertedIndexWriter file of the dict ids in a fixed-bit forward index (host C builder)."""
+        buf = bytes(fwd) + b"\0" * 8  # the reader takes 5 bytes per value
+        out = C.POINTER(C.c_uint8)()
+        n = C.c_uint64()
+        rc = self.lib.synth_inverted_index(buf, num_docs, bits, card, C.byref(out), C.byref(n))
+        if rc != 0:
+            raise RuntimeError(f"synth_inverted_index failed ({rc})")
+        try:
+            return C.string_at(out, n.value)
+        finally:
+            self.lib.synth_host_free(out)
 
     def alloc(self, nbytes: int) -> int:
         p = self.lib.synth_alloc(nbytes)
@@ -171,12 +212,23 @@ def forward_index_bytes(num_docs: int, bits: int) -> int:
 def build_segment_cpu(w: Workload, segment: int, num_docs: int, pack: Callable) -> SegmentData:
     """Host-side twin of build_segment_gpu: `pack(ids, bits) -> bytes` is the caller's fixed-bit writer."""
     seg = SegmentData(f"{w.name}_{segment}", num_docs)
+    sl = None
     for c in w.columns:
         vals = c.values()
+        d = vals.astype(">i4").tobytes()
+        if c.index == "sorted":
+            seg.columns[c.name] = ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=d,
+                                                sorted_index=sorted_index_bytes(num_docs, c.cardinality))
+            continue
         cdf = zipf_cdf(c.cardinality, c.zipf_s) if c.dist == "zipf" else None
         ids = dict_ids_cpu(column_seed(w.seed, segment, c.name), num_docs, c.cardinality, cdf=cdf)
-        seg.columns[c.name] = ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=vals.astype(">i4").tobytes(),
-                                            forward=pack(ids, num_bits_per_value(c.cardinality - 1)))
+        bits = num_bits_per_value(c.cardinality - 1)
+        fwd = pack(ids, bits)
+        inv = None
+        if c.index == "inv":
+            sl = sl or SynthLib()
+            inv = sl.inverted(fwd, num_docs, bits, c.cardinality)
+        seg.columns[c.name] = ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=d, forward=fwd, inverted=inv)
     return seg
 
 
@@ -199,11 +251,18 @@ def build_segments_gpu(ctx: GpuContext, w: Workload, segment_ids: List[int], num
         for s in segment_ids:
             gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns))
             for c in w.columns:
+                if c.index == "sorted":
+                    gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],
+                                                sorted_index=sorted_index_bytes(num_docs, c.cardinality)))
+                    continue
                 bits = num_bits_per_value(c.cardinality - 1)
+                nbytes = forward_index_bytes(num_docs, bits)
                 sl.generate(scratch, num_docs, bits, c.cardinality, column_seed(w.seed, s, c.name), cdfs.get(c.name))
+                inv = None
+                if c.index == "inv":
+                    inv = sl.inverted(sl.to_host(scratch, nbytes), num_docs, bits, c.cardinality)
                 gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],
-                                            forward_device=scratch,
-                                            forward_device_bytes=forward_index_bytes(num_docs, bits)))
+                                            forward_device=scratch, forward_device_bytes=nbytes, inverted=inv))
                 gs.data.columns[c.name].forward_device = None  # the scratch buffer is reused by the next column
             gs.seal()
             out.append(gs)

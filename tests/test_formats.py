@@ -91,3 +91,22 @@ def test_inverted_index_file_and_sorted_index():
     pairs = np.frombuffer(sorted_index_bytes(s, 17), dtype=">i4").reshape(-1, 2)
     for d in range(17):
         assert pairs[d, 0] == np.searchsorted(s, d) and pairs[d, 1] == np.searchsorted(s, d, side="right") - 1
+
+
+@pytest.mark.parametrize("card,n,layout", [(4, 70_000, "uniform"), (16, 200_003, "uniform"), (64, 150_001, "uniform"),
+                                           (256, 131_072, "uniform"), (3, 5, "uniform"), (256, 300_000, "sorted"),
+                                           (16, 140_000, "blocks")])
+def test_synth_inverted_index_matches_oracle(card, n, layout):
+    """The bench's inverted-index builder (synth.hip, C++) writes the oracle's bytes exactly: offsets header,
+    cookies 12346 / 12347, array / bitmap / run containers chosen as RoaringBitmapWriter + runOptimize."""
+    from pinot_amd.synth import SynthLib
+    rng = np.random.default_rng(card * 7 + n)
+    if layout == "sorted":
+        ids = np.sort(rng.integers(0, card, n))
+    elif layout == "blocks":
+        ids = np.repeat(rng.integers(0, card, n // 700 + 1), 700)[:n]
+    else:
+        ids = rng.integers(0, card, n)
+    bits = bits_per_value(card)
+    fwd = pack_fixed_bit(ids, bits)
+    assert SynthLib().inverted(fwd, n, bits, card) == inverted_index_bytes(ids, card)

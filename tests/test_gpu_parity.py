@@ -352,3 +352,23 @@ def test_synth_segments_upload_d2d(gpu_ctx):
         _assert_same(res, ref)
         for g in gsegs:
             g.release()
+
+
+@pytest.mark.parametrize("wl", ["bitmap5", "adanalytics", "range_in"])
+def test_bench_workloads_vs_oracle(gpu_ctx, wl):
+    """The bench workloads' own segments (synth.py: forward indexes, Roaring inverted indexes from the C++ builder,
+    sorted columns) at 2 x 2^18 docs: the bench query and, for config 5, its looser variant."""
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import WORKLOADS, build_segment_cpu
+    w = WORKLOADS[wl]
+    segs = [build_segment_cpu(w, s, 1 << 18, pack_fixed_bit) for s in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    sqls = [w.sql] + ([w.sql.replace("accountId IN (123456789)", "accountId < 123456789")] if wl == "adanalytics" else [])
+    try:
+        for sql in sqls:
+            q = parse_sql(sql)
+            ref = engine.execute(q, segs)
+            _assert_same(_gpu(gpu_ctx, q, gs), ref)
+    finally:
+        for g in gs:
+            g.release()
