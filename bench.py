@@ -52,9 +52,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local %= max(1, torch.cuda.device_count())  # > 1 rank per GPU only in the gloo rehearsal
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # PGPU_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("PGPU_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
 
     from pinot_amd.combine import DistributedExecutor
@@ -94,7 +100,8 @@ def main():
         width = {0: 4, 1: 8, 2: 4, 3: 8}.get(segs[0].column(c).data_type, 4)
         full = sum(s.column(c).cardinality * width for s in segs)
         dict_bytes += min(full, 32 * st.num_docs_scanned)
-    out_bytes = 8 * max(1, len(r_stats.group_rows or [])) * (1 + len(q.aggregations))
+    ngroups = len(r_stats.group_rows or []) if r_stats is not None else 1  # ranks != 0 return no rows
+    out_bytes = 8 * max(1, ngroups) * (1 + len(q.aggregations))
     bitmap_bytes = inverted_bytes_read(q, segs)
     algo_bytes = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
 
@@ -107,20 +114,16 @@ def main():
     kernel_ms = []
     t_start = time.perf_counter()
     result = None
-    if world == 1 and args.inflight > 1:
-        # every step plans, launches and finishes one whole query; up to `inflight` are queued at once
-        pending = []
-        submitted = 0
-        for _ in range(args.steps):
-            while submitted < args.steps and len(pending) < args.inflight:
-                pending.append(pm.submit(q, segs))
-                submitted += 1
-            result = pm.collect(pending.pop(0))
-            kernel_ms.append(result.stats.kernel_ms)
-    else:
-        for _ in range(args.steps):
-            result = ex.execute(q, segs)
-            kernel_ms.append(ex.last_stats.kernel_ms)
+    # every step plans, launches, reduces (N > 1: RCCL all-reduce of the partial tables) and finishes one whole
+    # query; up to `inflight` are queued at once, so the host side of query i overlaps the GPU running query i+1
+    pending = []
+    submitted = 0
+    for _ in range(args.steps):
+        while submitted < args.steps and len(pending) < max(1, args.inflight):
+            pending.append(ex.submit(q, segs))
+            submitted += 1
+        result = ex.collect(pending.pop(0))
+        kernel_ms.append(ex.last_stats.kernel_ms)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -163,7 +166,7 @@ def main():
             "config": {"workload": args.workload, "description": w.description, "query": w.sql,
                        "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
                        "rows_per_gpu": rows_per_gpu, "total_rows": total_rows,
-                       "queries_in_flight": args.inflight if world == 1 else 1,
+                       "queries_in_flight": max(1, args.inflight),
                        "parallelism": f"segments sharded over {world} GPU(s); partial tables all-reduced over RCCL"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

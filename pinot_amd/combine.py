@@ -97,58 +97,85 @@ class DistributedExecutor:
             self._globals[key] = hit
         return hit
 
-    def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
+    def submit(self, query: QueryContext, segments: Sequence[GpuSegment]):
+        """Plan and launch this rank's part of the query without waiting (several may be in flight: the host
+        plans and reduces query i while the GPU runs query i+1)."""
         if self.world == 1:
-            # single GPU: no exchange step; launch, wait and compaction inside libpinotgpu (one synchronisation)
-            res = self.pm.execute(query, segments)
-            self.last_stats = res.stats
-            return res
+            return self.pm.submit(query, segments)
         import torch
         if query.group_by:
             self._global_dicts(query, segments)
         desc, keep, globals_ = self.pm.build_desc(query, segments)
         L = self.pm.layout(desc)
         n = int(L.num_sections * L.num_keys)
-        table = self._tables.get(n)
-        if table is None:
-            table = torch.empty(n, dtype=torch.int64, device=self.device)
-            self._tables[n] = table
-        # libpinotgpu runs on its own HIP runtime and stream (torch may bundle another runtime): the table
-        # memory is shared through the process's GPU address space and ordered by explicit synchronisation.
-        torch.cuda.current_stream(self.device).synchronize()
+        pool = self._tables.setdefault(n, [])
+        table = pool.pop() if pool else torch.empty(n, dtype=torch.int64, device=self.device)
+        # libpinotgpu runs on its own HIP stream: the table memory is shared through the process's GPU address
+        # space and ordered by explicit synchronisation (a pooled table's last reduce finished in collect)
         qh = C.c_void_p()
+        _lib.check(self.pm.ctx._lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
+                                                      C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
+        return _DistPending(query, len(segments), L, table, qh, globals_)
+
+    def collect(self, pending) -> Optional[QueryResult]:
+        """Wait for this rank's launch, all-reduce the partial table over RCCL; rank 0 compacts and finishes."""
+        if self.world == 1:
+            res = self.pm.collect(pending)
+            self.last_stats = res.stats
+            return res
+        import torch
+        import torch.distributed as dist
         lib = self.pm.ctx._lib
-        _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
-                                         C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
         st = QueryStats()
+        qh, pending.handle = pending.handle, None
         try:
             _lib.check(lib.pgpu_query_wait(qh, C.byref(st)))
         finally:
             lib.pgpu_query_release(qh)
         self.last_stats = st
-        if self.world > 1:
-            reduce_sections(table, L, self.group)
-            counts = torch.tensor([st.num_docs_scanned, st.num_total_docs], dtype=torch.int64, device=self.device)
-            import torch.distributed as dist
-            dist.all_reduce(counts, group=self.group)
-            docs_scanned, total_docs = (int(x) for x in counts.tolist())
-            torch.cuda.current_stream(self.device).synchronize()
-        else:
-            docs_scanned, total_docs = st.num_docs_scanned, st.num_total_docs
-        if self.rank != 0:
-            return None
-        cap = int(L.num_keys)
-        keys = np.empty(max(cap, 1), dtype=np.int64)
-        cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
-        ng = C.c_uint64()
-        _lib.check(lib.pgpu_table_compact(self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()),
-                                          None, keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                          cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(ng)))
-        gt = GroupTable(keys[: ng.value], cells[: ng.value], L)
-        stats = ExecutionStats(num_docs_scanned=docs_scanned,
-                               num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
-                               num_entries_scanned_post_filter=docs_scanned * len(query.projected_columns),
-                               num_total_docs=total_docs, num_segments_processed=len(segments) * self.world,
-                               kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
-                               dense_bytes=st.dense_bytes)
-        return finish(query, gt, [g[0] for g in globals_], stats)
+        L, table, query = pending.layout, pending.table, pending.query
+        reduce_sections(table, L, self.group)
+        counts = torch.tensor([st.num_docs_scanned, st.num_total_docs], dtype=torch.int64, device=self.device)
+        dist.all_reduce(counts, group=self.group)
+        docs_scanned, total_docs = (int(x) for x in counts.tolist())
+        torch.cuda.current_stream(self.device).synchronize()
+        try:
+            if self.rank != 0:
+                return None
+            cap = int(L.num_keys)
+            keys = np.empty(max(cap, 1), dtype=np.int64)
+            cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
+            ng = C.c_uint64()
+            _lib.check(lib.pgpu_table_compact(self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()),
+                                              None, keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                              cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(ng)))
+            gt = GroupTable(keys[: ng.value], cells[: ng.value], L)
+            stats = ExecutionStats(num_docs_scanned=docs_scanned,
+                                   num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
+                                   num_entries_scanned_post_filter=docs_scanned * len(query.projected_columns),
+                                   num_total_docs=total_docs, num_segments_processed=pending.num_segments * self.world,
+                                   kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
+                                   dense_bytes=st.dense_bytes)
+            return finish(query, gt, [g[0] for g in pending.globals_], stats)
+        finally:
+            self._tables.setdefault(int(table.numel()), []).append(table)
+
+    def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
+        return self.collect(self.submit(query, segments))
+
+
+class _DistPending:
+    """A launched, not yet collected multi-GPU query of this rank."""
+
+    def __init__(self, query, num_segments, layout, table, handle, globals_):
+        self.query, self.num_segments, self.layout = query, num_segments, layout
+        self.table, self.handle, self.globals_ = table, handle, globals_
+
+    def __del__(self):
+        if self.handle is not None and getattr(self.handle, "value", None):
+            try:
+                from . import _lib as L
+                L.load().pgpu_query_release(self.handle)
+            except Exception:
+                pass
+            self.handle = None

@@ -513,35 +513,56 @@ __device__ __noinline__ bool bitmap_contains(InvIndex c, uint32_t id, uint32_t d
 }
 
 // ---- Roaring containers / sorted ranges for a whole tile -------------------------------------------------------
+// Container of bitmap `id` holding key `key` (index into c.ct, -1 if none): uniform scalar loads; a bitmap that
+// has a container for every key (dense) is hit directly at first + key, others fall back to a binary search.
+FI int32_t find_container(const InvIndex& c, uint32_t id, uint32_t key) {
+  int32_t a = (int32_t)cld(c.dir + id), z = (int32_t)cld(c.dir + id + 1) - 1;
+  if (a > z) return -1;
+  const int32_t g = a + (int32_t)key;
+  if (g <= z && cld(&c.ct[g].key) == key) return g;
+  while (a <= z) {
+    const int32_t mid = (a + z) >> 1;
+    const uint32_t k = cld(&c.ct[mid].key);
+    if (k == key) return mid;
+    if (k < key) a = mid + 1; else z = mid - 1;
+  }
+  return -1;
+}
+// Number of values of the sorted uint16 array v[0, n) below x (n <= 4096), by two rounds of a 64-way wave
+// search instead of a 12-step chain of dependent loads: round 1 tests every step-th value (step = ceil(n / 64))
+// and a ballot finds the block holding the boundary; round 2 tests that block's values.
+FI int32_t lower_bound64(const uint16_t* v, int32_t n, uint32_t x) {
+  const int lane = lane_id();
+  const int32_t step = (n + 63) >> 6;
+  const int32_t p = lane * step;
+  const int c = __popcll(__ballot(p < n && (uint32_t)gld(v, p) < x));
+  if (c == 0) return 0;
+  const int32_t b = (c - 1) * step + 1;  // v[b - 1] < x; v[b + step - 1] >= x when that index exists
+  const int32_t q = b + lane;
+  return b + __popcll(__ballot(lane < step && q < n && (uint32_t)gld(v, q) < x));
+}
+
+// ---- Roaring containers / sorted ranges for a whole tile -------------------------------------------------------
 // Bits of the tile covered by one Roaring bitmap (dict id `id`), for this lane's 32 docs.
 __device__ __noinline__ uint32_t bitmap_word(InvIndex c, int32_t doc0, uint32_t id, uint32_t* lds_words) {
   const uint32_t key = (uint32_t)doc0 >> 16;
   const uint32_t lo16 = (uint32_t)doc0 & 0xFFFFu;  // multiple of 2048
   const int lane = lane_id();
-  int32_t a = (int32_t)c.dir[id], z = (int32_t)c.dir[id + 1] - 1;
-  int32_t ci = -1;
-  while (a <= z) {
-    const int32_t mid = (a + z) >> 1;
-    const uint32_t k = c.ct[mid].key;
-    if (k == key) { ci = mid; break; }
-    if (k < key) a = mid + 1; else z = mid - 1;
-  }
+  const int32_t ci = find_container(c, id, key);
   if (ci < 0) return 0u;
-  const DevContainer ct = c.ct[ci];
+  const uint32_t type = cld(&c.ct[ci].type), card = cld(&c.ct[ci].card), offset = cld(&c.ct[ci].offset);
   const uint32_t my0 = lo16 + 32u * lane;  // my first doc within the container
-  if (ct.type == PGPU_CT_BITMAP) {
-    return gld((const uint32_t*)(c.data + ct.offset), my0 >> 5);
-  }
-  if (ct.type == PGPU_CT_RUN) {
-    const uint16_t* r = (const uint16_t*)(c.data + ct.offset);
-    int32_t l = 0, h = (int32_t)ct.card;
+  if (type == PGPU_CT_BITMAP) return gld((const uint32_t*)(c.data + offset), my0 >> 5);
+  if (type == PGPU_CT_RUN) {
+    const uint16_t* r = (const uint16_t*)(c.data + offset);
+    int32_t l = 0, h = (int32_t)card;
     while (l < h) {  // first run whose end >= lo16
       const int32_t m = (l + h) >> 1;
-      if ((uint32_t)r[2 * m] + r[2 * m + 1] < lo16) l = m + 1; else h = m;
+      if ((uint32_t)gld(r, 2 * m) + gld(r, 2 * m + 1) < lo16) l = m + 1; else h = m;
     }
     uint32_t w = 0;
-    for (int32_t i = l; i < (int32_t)ct.card; ++i) {  // uniform loop over the runs overlapping the tile
-      const uint32_t s = r[2 * i], e = s + r[2 * i + 1];
+    for (int32_t i = l; i < (int32_t)card; ++i) {  // uniform loop over the runs overlapping the tile
+      const uint32_t s = gld(r, 2 * i), e = s + gld(r, 2 * i + 1);
       if (s >= lo16 + WT) break;
       if (e >= my0 && s <= my0 + 31) {
         const uint32_t bs = s > my0 ? s - my0 : 0u, be = e < my0 + 31 ? e - my0 : 31u;
@@ -551,16 +572,13 @@ __device__ __noinline__ uint32_t bitmap_word(InvIndex c, int32_t doc0, uint32_t 
     return w;
   }
   // ARRAY: values in [lo16, lo16 + WT) scattered to their owner lanes through LDS
-  const uint16_t* v = (const uint16_t*)(c.data + ct.offset);
-  int32_t l = 0, h = (int32_t)ct.card;
-  while (l < h) { const int32_t m = (l + h) >> 1; if (v[m] < lo16) l = m + 1; else h = m; }
-  const int32_t first = l;
-  h = (int32_t)ct.card;
-  while (l < h) { const int32_t m = (l + h) >> 1; if ((uint32_t)v[m] < lo16 + WT) l = m + 1; else h = m; }
+  const uint16_t* v = (const uint16_t*)(c.data + offset);
+  const int32_t first = lower_bound64(v, (int32_t)card, lo16);
+  const int32_t last = lower_bound64(v, (int32_t)card, lo16 + WT);
   lds_words[lane] = 0u;
   wave_sync();
-  for (int32_t i = first + lane; i < l; i += 64) {
-    const uint32_t off = (uint32_t)v[i] - lo16;
+  for (int32_t i = first + lane; i < last; i += 64) {
+    const uint32_t off = (uint32_t)gld(v, i) - lo16;
     atomicOr(&lds_words[off >> 5], 1u << (off & 31));
   }
   wave_sync();

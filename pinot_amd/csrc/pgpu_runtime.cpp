@@ -1290,7 +1290,15 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     release_ws(ctx, ws);
     return code;
   };
-  hipStream_t st = stream ? (hipStream_t)stream : ws->stream;
+  // NULL stream: the context's query stream (queries run back to back; each has its own completion event)
+  if (!stream) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->qstream) {
+      const hipError_t ce = hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking);
+      if (ce != hipSuccess) return bail(fail(PGPU_E_HIP, "query stream: %s", hipGetErrorString(ce)));
+    }
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->qstream;
 
   // arena: segs | instrs | cols | pool | remaps
   const size_t o_segs = 0;
@@ -1363,11 +1371,14 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
   if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, L.num_keys * L.num_sections, st);
+  // completion of this query alone (later queries may already be queued behind it on the same stream)
+  if (e == hipSuccess) e = hipEventRecord(ws->done, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
 
   auto* qq = new pgpu_query();
   qq->ctx = ctx;
   qq->ws = ws;
+  qq->done = ws->done;
   qq->stream = st;
   qq->params = p;
   qq->grid = grid;
@@ -1522,12 +1533,6 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   qq->tws = tws;
   qq->layout = L;
   qq->small = small;
-  e = hipEventRecord(tws->done, qq->stream);
-  if (e != hipSuccess) {
-    pgpu_query_release(qq);
-    return fail(PGPU_E_HIP, "event record: %s", hipGetErrorString(e));
-  }
-  qq->done = tws->done;
   *out_query = qq;
   return PGPU_OK;
 }
