@@ -255,6 +255,53 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
 int pgpu_query_collect(pgpu_query* query, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
                        uint64_t* out_num_groups, pgpu_query_stats* out_stats);
 
+/* ---- per-segment filter planning inside the library (numeric columns) ----------------------------------------
+ * The same query with the filter given once, as literals, instead of one dict-id program per segment: for every
+ * segment the library evaluates the predicates against that segment's (host copy of the) dictionary
+ * (<X>PredicateEvaluatorFactory, BaseImmutableDictionary.insertionIndexOf) and builds the physical filter as
+ * FilterPlanNode / FilterOperatorUtils do (EMPTY / MATCH_ALL folding, leaf choice sorted > inverted > scan,
+ * stable AND re-ordering) -- the host work of core/plan/FilterPlanNode.java:192-313 per segment, without a
+ * round trip per segment through the caller.  Expression nodes in prefix order:
+ *   PGPU_X_AND / PGPU_X_OR (num_children children follow), PGPU_X_NOT (one child follows), PGPU_X_PRED.
+ * PRED literals: EQ / NOT_EQ one value, IN / NOT_IN num_values values, RANGE [lower, upper] with unbounded /
+ * inclusive flags (a missing bound still occupies its slot).  Literal = the SQL literal parsed once:
+ * is_integral with i exact (integer columns compare exactly; a fractional literal is never equal and inserts
+ * by its double value), d for FLOAT (rounded to float) / DOUBLE columns.  A STRING column returns
+ * PGPU_E_UNSUPPORTED (the caller plans that query per segment itself).  segments[i].filter is ignored. */
+#define PGPU_X_PRED 0
+#define PGPU_X_AND 1
+#define PGPU_X_OR 2
+#define PGPU_X_NOT 3
+#define PGPU_P_EQ 0
+#define PGPU_P_NOT_EQ 1
+#define PGPU_P_IN 2
+#define PGPU_P_NOT_IN 3
+#define PGPU_P_RANGE 4
+
+typedef struct {
+  int64_t i;           /* exact value of an integral literal */
+  double d;            /* the literal as a double */
+  int32_t is_integral;
+  int32_t reserved;
+} pgpu_literal;
+
+typedef struct {
+  int32_t op;           /* PGPU_X_* */
+  int32_t num_children; /* AND / OR */
+  int32_t column;       /* PRED: query column index */
+  int32_t pred;         /* PRED: PGPU_P_* */
+  int32_t lower_unbounded, upper_unbounded, lower_inclusive, upper_inclusive; /* RANGE */
+  int32_t num_values;
+  int32_t reserved;
+  const pgpu_literal* values;
+} pgpu_expr_node;
+
+int pgpu_query_submit_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                           int32_t num_nodes, pgpu_query** out_query);
+int pgpu_query_launch_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                           int32_t num_nodes, void* stream, void* dev_table, uint64_t table_bytes,
+                           pgpu_query** out_query);
+
 /* Convenience: submit + collect. */
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
                        uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);

@@ -78,6 +78,21 @@ class QueryStats(C.Structure):
                 ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double)]
 
 
+PGPU_X_PRED, PGPU_X_AND, PGPU_X_OR, PGPU_X_NOT = range(4)
+PGPU_P_EQ, PGPU_P_NOT_EQ, PGPU_P_IN, PGPU_P_NOT_IN, PGPU_P_RANGE = range(5)
+
+
+class Literal(C.Structure):
+    _fields_ = [("i", C.c_int64), ("d", C.c_double), ("is_integral", C.c_int32), ("reserved", C.c_int32)]
+
+
+class ExprNode(C.Structure):
+    _fields_ = [("op", C.c_int32), ("num_children", C.c_int32), ("column", C.c_int32), ("pred", C.c_int32),
+                ("lower_unbounded", C.c_int32), ("upper_unbounded", C.c_int32), ("lower_inclusive", C.c_int32),
+                ("upper_inclusive", C.c_int32), ("num_values", C.c_int32), ("reserved", C.c_int32),
+                ("values", C.POINTER(Literal))]
+
+
 # exported symbols and their signatures: (name, restype, argtypes)
 _P = C.c_void_p
 SIGNATURES = [
@@ -104,6 +119,9 @@ SIGNATURES = [
     ("pgpu_query_submit", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(_P)]),
     ("pgpu_query_collect", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
                                      C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
+    ("pgpu_query_submit_expr", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(ExprNode), C.c_int32, C.POINTER(_P)]),
+    ("pgpu_query_launch_expr", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(ExprNode), C.c_int32, _P, _P,
+                                         C.c_uint64, C.POINTER(_P)]),
     ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_decode_minmax_key", C.c_double, [C.c_int64, C.c_int32]),

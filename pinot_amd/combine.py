@@ -105,7 +105,8 @@ class DistributedExecutor:
         import torch
         if query.group_by:
             self._global_dicts(query, segments)
-        desc, keep, globals_ = self.pm.build_desc(query, segments)
+        expr = self.pm.filter_expr(query, segments)
+        desc, keep, globals_ = self.pm.build_desc(query, segments, plan_filters=expr is None)
         L = self.pm.layout(desc)
         n = int(L.num_sections * L.num_keys)
         pool = self._tables.setdefault(n, [])
@@ -113,8 +114,13 @@ class DistributedExecutor:
         # libpinotgpu runs on its own HIP stream: the table memory is shared through the process's GPU address
         # space and ordered by explicit synchronisation (a pooled table's last reduce finished in collect)
         qh = C.c_void_p()
-        _lib.check(self.pm.ctx._lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
-                                                      C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
+        lib = self.pm.ctx._lib
+        if expr is None:
+            _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
+                                             C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
+        else:
+            _lib.check(lib.pgpu_query_launch_expr(self.pm.ctx.handle, C.byref(desc), expr[0], expr[1], None,
+                                                  C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
         return _DistPending(query, len(segments), L, table, qh, globals_)
 
     def collect(self, pending) -> Optional[QueryResult]:

@@ -182,6 +182,7 @@ struct HostColumn {
   uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
+  std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
 };
 
 }  // namespace
@@ -456,6 +457,7 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
+  c.hdict = std::move(le);
   return PGPU_OK;
 }
 
@@ -1493,6 +1495,333 @@ int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const
   return rc;
 }
 
+}  // extern "C"
+
+// ---- per-segment filter planning from literal predicates (pgpu_query_*_expr) --------------------------------------
+// The host-side work the reference does per segment before any doc is touched, restated in C++ for numeric
+// columns (pinot_amd/plan.py + predicate.py are the same rules in Python, used for STRING columns):
+//   dictionary predicate evaluators (core/operator/filter/predicate/<X>PredicateEvaluatorFactory.java; literal
+//     lookups = BaseImmutableDictionary.insertionIndexOf, seglocal/.../BaseImmutableDictionary.java:125-270),
+//   FilterPlanNode.constructPhysicalOperator (core/plan/FilterPlanNode.java:192-313) and FilterOperatorUtils
+//     (EMPTY / MATCH_ALL folding, leaf choice sorted > inverted > scan, stable AND re-ordering by priority;
+//     core/operator/filter/FilterOperatorUtils.java:42-221).
+namespace {
+
+struct Leaf {
+  int kind;  // 0 EMPTY, 1 ALL, 2 SCAN, 3 INV, 4 SORTED
+  bool exclusive = false;
+  bool range = false;  // RANGE evaluator [start, end)
+  int32_t start = 0, end = 0;
+  std::vector<int32_t> ids;  // SET evaluator: matching ids, or non-matching ids for exclusive predicates
+};
+
+struct PlanNode {
+  int kind;  // 0 EMPTY, 1 ALL, 2 SCAN, 3 INV, 4 SORTED, 5 AND, 6 OR, 7 NOT
+  int column = -1;
+  Leaf leaf;
+  std::vector<PlanNode> kids;
+  int priority() const {
+    switch (kind) {
+      case 4: return 0;
+      case 3: return 1;
+      case 5: return 3;
+      case 6: return 4;
+      case 7: return kids[0].priority();
+      default: return 5;
+    }
+  }
+};
+
+// BaseImmutableDictionary.insertionIndexOf: >= 0 exact match index, else -(insertion point + 1)
+int64_t insertion_index(const HostColumn& c, const pgpu_literal& lit) {
+  const int32_t n = c.dict_card;
+  const uint8_t* d = c.hdict.data();
+  int64_t lo = 0, hi = n;
+  if (c.dict_type == PGPU_INT || c.dict_type == PGPU_LONG) {
+    auto at = [&](int64_t i) -> int64_t {
+      if (c.dict_type == PGPU_INT) { int32_t v; memcpy(&v, d + 4 * i, 4); return v; }
+      int64_t v; memcpy(&v, d + 8 * i, 8); return v;
+    };
+    if (lit.is_integral) {
+      while (lo < hi) { const int64_t m = (lo + hi) / 2; if (at(m) < lit.i) lo = m + 1; else hi = m; }
+      return lo < n && at(lo) == lit.i ? lo : -(lo + 1);
+    }
+    // a fractional literal on an integer dictionary is never equal; its insertion point compares as double
+    while (lo < hi) { const int64_t m = (lo + hi) / 2; if ((double)at(m) < lit.d) lo = m + 1; else hi = m; }
+    return -(lo + 1);
+  }
+  double key = lit.d;
+  if (c.dict_type == PGPU_FLOAT) key = (double)(float)lit.d;
+  auto at = [&](int64_t i) -> double {
+    if (c.dict_type == PGPU_FLOAT) { float v; memcpy(&v, d + 4 * i, 4); return v; }
+    double v; memcpy(&v, d + 8 * i, 8); return v;
+  };
+  while (lo < hi) { const int64_t m = (lo + hi) / 2; if (at(m) < key) lo = m + 1; else hi = m; }
+  return lo < n && at(lo) == key ? lo : -(lo + 1);
+}
+
+// PredicateEvaluatorProvider.getPredicateEvaluator for dictionary-encoded columns
+Leaf evaluate(const HostColumn& c, const pgpu_expr_node& x) {
+  Leaf l;
+  const int32_t card = c.dict_card;
+  auto index_of = [&](const pgpu_literal& v) -> int32_t {
+    const int64_t i = insertion_index(c, v);
+    return i >= 0 ? (int32_t)i : -1;
+  };
+  auto id_set = [&]() {
+    std::vector<int32_t> ids;
+    for (int k = 0; k < x.num_values; ++k) {
+      const int32_t i = index_of(x.values[k]);
+      if (i >= 0) ids.push_back(i);
+    }
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    return ids;
+  };
+  switch (x.pred) {
+    case PGPU_P_EQ: {
+      const int32_t i = x.num_values > 0 ? index_of(x.values[0]) : -1;
+      if (i < 0) { l.kind = 0; return l; }
+      l.kind = card == 1 ? 1 : 2;
+      l.ids = {i};
+      return l;
+    }
+    case PGPU_P_NOT_EQ: {
+      const int32_t i = x.num_values > 0 ? index_of(x.values[0]) : -1;
+      if (i < 0) { l.kind = 1; return l; }
+      l.kind = card == 1 ? 0 : 2;
+      l.exclusive = true;
+      l.ids = {i};
+      return l;
+    }
+    case PGPU_P_IN:
+      l.ids = id_set();
+      l.kind = l.ids.empty() ? 0 : ((int32_t)l.ids.size() == card ? 1 : 2);
+      return l;
+    case PGPU_P_NOT_IN:
+      l.ids = id_set();
+      l.exclusive = true;
+      l.kind = l.ids.empty() ? 1 : ((int32_t)l.ids.size() == card ? 0 : 2);
+      return l;
+    default: {  // RANGE
+      int64_t start = 0, end = card;
+      if (!x.lower_unbounded) {
+        const int64_t ins = insertion_index(c, x.values[0]);
+        start = ins < 0 ? -(ins + 1) : (x.lower_inclusive ? ins : ins + 1);
+      }
+      if (!x.upper_unbounded) {
+        const int64_t ins = insertion_index(c, x.values[x.num_values - 1]);
+        end = ins < 0 ? -(ins + 1) : (x.upper_inclusive ? ins + 1 : ins);
+      }
+      l.range = true;
+      l.start = (int32_t)start;
+      l.end = (int32_t)end;
+      const int64_t n = end - start;
+      l.kind = n <= 0 ? 0 : (n == card ? 1 : 2);
+      return l;
+    }
+  }
+}
+
+struct ExprPlanner {
+  const pgpu_query_desc* q;
+  const pgpu_segment_plan* sp;
+  const pgpu_segment* seg;
+  const pgpu_expr_node* x;
+  int n;
+  int err = PGPU_OK;
+
+  const HostColumn* column(int qc) {
+    if (qc < 0 || qc >= q->num_columns) { err = fail(PGPU_E_INVALID, "expression column %d", qc); return nullptr; }
+    const int32_t slot = sp->column_map[qc];
+    if (slot < 0 || slot >= (int32_t)seg->cols.size()) { err = fail(PGPU_E_INVALID, "expression column slot"); return nullptr; }
+    const HostColumn& c = seg->cols[slot];
+    if (c.dict_type < PGPU_INT || c.dict_type > PGPU_DOUBLE || c.hdict.empty()) {
+      err = fail(PGPU_E_UNSUPPORTED, "expression on a non-numeric column (plan it on the host)");
+      return nullptr;
+    }
+    return &c;
+  }
+
+  // FilterPlanNode.constructPhysicalOperator over the subtree starting at node i; *next = first node after it
+  PlanNode build(int i, int* next) {
+    PlanNode out;
+    out.kind = 0;
+    if (i >= n) { err = fail(PGPU_E_INVALID, "malformed filter expression"); *next = n; return out; }
+    const pgpu_expr_node& e = x[i];
+    if (e.op == PGPU_X_AND || e.op == PGPU_X_OR) {
+      const bool is_and = e.op == PGPU_X_AND;
+      int j = i + 1;
+      std::vector<PlanNode> kids;
+      bool empty = false, all = false;
+      for (int k = 0; k < e.num_children && !err; ++k) {
+        PlanNode ch = build(j, &j);
+        if (is_and) {
+          if (ch.kind == 0) empty = true;
+          else if (ch.kind != 1) kids.push_back(std::move(ch));
+        } else {
+          if (ch.kind == 1) all = true;
+          else if (ch.kind != 0) kids.push_back(std::move(ch));
+        }
+      }
+      *next = j;
+      if (is_and ? empty : all) { out.kind = is_and ? 0 : 1; return out; }
+      if (kids.empty()) { out.kind = is_and ? 1 : 0; return out; }
+      if (kids.size() == 1) return std::move(kids[0]);
+      if (is_and)
+        std::stable_sort(kids.begin(), kids.end(),
+                         [](const PlanNode& a, const PlanNode& b) { return a.priority() < b.priority(); });
+      out.kind = is_and ? 5 : 6;
+      out.kids = std::move(kids);
+      return out;
+    }
+    if (e.op == PGPU_X_NOT) {
+      PlanNode ch = build(i + 1, next);
+      if (ch.kind == 1) { out.kind = 0; return out; }
+      if (ch.kind == 0) { out.kind = 1; return out; }
+      out.kind = 7;
+      out.kids.push_back(std::move(ch));
+      return out;
+    }
+    *next = i + 1;
+    const HostColumn* c = column(e.column);
+    if (!c) return out;
+    Leaf l = evaluate(*c, e);
+    out.column = e.column;
+    if (l.kind == 0 || l.kind == 1) { out.kind = l.kind; return out; }
+    if (c->kind == PGPU_COL_SORTED) out.kind = 4;
+    else if (e.pred != PGPU_P_RANGE && c->inv_card > 0) out.kind = 3;
+    else out.kind = 2;
+    out.leaf = std::move(l);
+    return out;
+  }
+
+  // emit the prefix-order pgpu_filter_node program; id lists go to `pool` (offsets patched afterwards)
+  void emit(const PlanNode& o, std::vector<pgpu_filter_node>& nodes, std::vector<int32_t>& pool,
+            std::vector<std::pair<int, int>>& id_at) {
+    pgpu_filter_node nd;
+    memset(&nd, 0, sizeof(nd));
+    auto with_ids = [&](const std::vector<int32_t>& v, int count) {
+      id_at.emplace_back((int)nodes.size(), (int)pool.size());
+      pool.insert(pool.end(), v.begin(), v.end());
+      nd.num_ids = count;
+    };
+    switch (o.kind) {
+      case 0: case 1:
+        nd.op = o.kind == 0 ? PGPU_F_EMPTY : PGPU_F_MATCH_ALL;
+        nodes.push_back(nd);
+        return;
+      case 2: {
+        const Leaf& l = o.leaf;
+        nd.op = PGPU_F_SCAN;
+        nd.column = o.column;
+        nd.negate = l.exclusive ? 1 : 0;
+        if (l.range) {
+          nd.pred = PGPU_PRED_RANGE; nd.lo = l.start; nd.hi = l.end;
+        } else if (!l.ids.empty() && l.ids.back() - l.ids.front() + 1 == (int32_t)l.ids.size()) {
+          nd.pred = PGPU_PRED_RANGE; nd.lo = l.ids.front(); nd.hi = l.ids.back() + 1;
+        } else {
+          nd.pred = PGPU_PRED_SET;
+          with_ids(l.ids, (int)l.ids.size());
+        }
+        nodes.push_back(nd);
+        return;
+      }
+      case 3: {  // INV: matching ids, or the non-matching ids of an exclusive predicate (flipped)
+        const Leaf& l = o.leaf;
+        nd.op = PGPU_F_INVERTED;
+        nd.column = o.column;
+        nd.negate = l.exclusive ? 1 : 0;
+        with_ids(l.ids, (int)l.ids.size());
+        nodes.push_back(nd);
+        return;
+      }
+      case 4: {  // SORTED: doc ranges of the (non-)matching ids, adjacent ranges merged
+        const Leaf& l = o.leaf;
+        const HostColumn& c = seg->cols[sp->column_map[o.column]];
+        std::vector<int32_t> flat;
+        if (l.range) {
+          flat = {c.sorted_pairs[2 * l.start], c.sorted_pairs[2 * (l.end - 1) + 1]};
+        } else {
+          for (int32_t id : l.ids) {
+            const int32_t s0 = c.sorted_pairs[2 * id], e0 = c.sorted_pairs[2 * id + 1];
+            if (!flat.empty() && s0 == flat.back() + 1) flat.back() = e0;
+            else { flat.push_back(s0); flat.push_back(e0); }
+          }
+        }
+        nd.op = PGPU_F_SORTED;
+        nd.column = o.column;
+        nd.negate = (l.exclusive && !l.range) ? 1 : 0;
+        with_ids(flat, (int)flat.size() / 2);
+        nodes.push_back(nd);
+        return;
+      }
+      case 5: case 6: {
+        const bool a = o.kind == 5;
+        nd.op = a ? PGPU_F_AND_BEGIN : PGPU_F_OR_BEGIN;
+        nodes.push_back(nd);
+        for (const PlanNode& ch : o.kids) {
+          emit(ch, nodes, pool, id_at);
+          pgpu_filter_node ce;
+          memset(&ce, 0, sizeof(ce));
+          ce.op = a ? PGPU_F_AND_CHILD_END : PGPU_F_OR_CHILD_END;
+          nodes.push_back(ce);
+        }
+        pgpu_filter_node en;
+        memset(&en, 0, sizeof(en));
+        en.op = a ? PGPU_F_AND_END : PGPU_F_OR_END;
+        nodes.push_back(en);
+        return;
+      }
+      default:
+        nd.op = PGPU_F_NOT;
+        nodes.push_back(nd);
+        emit(o.kids[0], nodes, pool, id_at);
+        return;
+    }
+  }
+};
+
+// Descriptor copy whose segment plans carry the filter programs planned from `expr`.
+struct PlannedDesc {
+  pgpu_query_desc q;
+  std::vector<pgpu_segment_plan> plans;
+  std::vector<std::vector<pgpu_filter_node>> nodes;
+  std::vector<std::vector<int32_t>> pools;
+};
+
+int plan_expr(const pgpu_query_desc* q, const pgpu_expr_node* expr, int32_t num_nodes, PlannedDesc& out) {
+  if (!q || (!expr && num_nodes > 0) || num_nodes < 0) return fail(PGPU_E_INVALID, "null argument");
+  out.q = *q;
+  out.plans.assign(q->segments, q->segments + q->num_segments);
+  out.nodes.resize(q->num_segments);
+  out.pools.resize(q->num_segments);
+  for (int s = 0; s < q->num_segments; ++s) {
+    pgpu_segment_plan& sp = out.plans[s];
+    sp.filter = nullptr;
+    sp.num_filter_nodes = 0;
+    if (num_nodes == 0) continue;
+    if (!sp.segment || !sp.column_map) return fail(PGPU_E_INVALID, "segment %d plan", s);
+    ExprPlanner pl{q, &sp, sp.segment, expr, num_nodes};
+    int next = 0;
+    PlanNode root = pl.build(0, &next);
+    if (pl.err) return pl.err;
+    if (next != num_nodes) return fail(PGPU_E_INVALID, "filter expression has %d trailing nodes", num_nodes - next);
+    if (root.kind == 1) continue;  // match all: no program
+    std::vector<std::pair<int, int>> id_at;
+    pl.emit(root, out.nodes[s], out.pools[s], id_at);
+    for (const auto& ia : id_at) out.nodes[s][ia.first].ids = out.pools[s].data() + ia.second;
+    sp.filter = out.nodes[s].data();
+    sp.num_filter_nodes = (int32_t)out.nodes[s].size();
+  }
+  out.q.segments = out.plans.data();
+  return PGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** out_query) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   pgpu_table_layout L;
@@ -1566,6 +1895,25 @@ int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, ui
   }
   pgpu_query_release(qq);
   return rc;
+}
+
+int pgpu_query_submit_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                           int32_t num_nodes, pgpu_query** out_query) {
+  if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
+  PlannedDesc pd;
+  const int rc = plan_expr(q, expr, num_nodes, pd);
+  if (rc) return rc;
+  return pgpu_query_submit(ctx, &pd.q, out_query);  // the descriptor is copied by the submit
+}
+
+int pgpu_query_launch_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                           int32_t num_nodes, void* stream, void* dev_table, uint64_t table_bytes,
+                           pgpu_query** out_query) {
+  if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
+  PlannedDesc pd;
+  const int rc = plan_expr(q, expr, num_nodes, pd);
+  if (rc) return rc;
+  return pgpu_query_launch(ctx, &pd.q, stream, dev_table, table_bytes, out_query);
 }
 
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,

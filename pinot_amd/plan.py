@@ -23,18 +23,19 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+from fractions import Fraction
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _lib
-from ._lib import (PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX, PGPU_AGG_MIN, PGPU_AGG_SUM, PGPU_DOUBLE,
+from ._lib import (ExprNode, Literal, PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX, PGPU_AGG_MIN, PGPU_AGG_SUM, PGPU_DOUBLE,
                    PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64,
                    PGPU_RED_SUM_I64, PGPU_STRING, Agg, FilterNode, QueryDesc, QueryStats, SegmentPlan, TableLayout,
                    UnsupportedPlanError)
 from .predicate import DictPredicateEvaluator, SortedDictionary, get_predicate_evaluator
-from .query import FilterContext, QueryContext
+from .query import UNBOUNDED, FilterContext, QueryContext
 from .segment import GpuContext, GpuSegment
 
 AGG_FN = {"COUNT": PGPU_AGG_COUNT, "SUM": PGPU_AGG_SUM, "MIN": PGPU_AGG_MIN, "MAX": PGPU_AGG_MAX,
@@ -314,8 +315,11 @@ class GpuPlanMaker:
 
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
-                 collect_stats: bool = False, query_flags: int = 0):
+                 collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False):
         self.ctx = ctx
+        # host_planning: plan every segment's filter in Python (SegmentFilterPlanner) even when the library could
+        # (numeric columns: pgpu_query_submit_expr plans all segments in C++ from the literals)
+        self.host_planning = host_planning
         self.query_flags = query_flags   # extra PGPU_Q_* flags (strategy overrides for tests / tuning)
         self.num_groups_limit = num_groups_limit
         self.max_init_group_holder_capacity = max_init_group_holder_capacity
@@ -369,9 +373,75 @@ class GpuPlanMaker:
                                    f"segment {seg.name}: group key space {prod} exceeds numGroupsLimit "
                                    f"{self.num_groups_limit}; first-seen truncation is served by the CPU plan")
 
-    def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment]):
+    def filter_expr(self, query: QueryContext, segments: Sequence[GpuSegment]):
+        """The query's filter as a pgpu_expr_node program (planned per segment inside the library), or None when
+        it must be planned here: STRING columns, literals that are not numbers, or host_planning."""
+        f = query.filter
+        if f is None or self.host_planning or not segments:
+            return None
+        col_index = {c: i for i, c in enumerate(query.columns)}
+        seg0 = segments[0]
+        nodes: list = []
+        lits: list = []
+
+        def lit(v: str):
+            try:
+                i = int(v)
+                return (i, float(i), 1) if -(1 << 63) <= i < (1 << 63) else None
+            except ValueError:
+                pass
+            try:
+                fr = Fraction(v)
+            except (ValueError, ZeroDivisionError):
+                return None
+            if fr.denominator == 1:
+                i = int(fr)
+                return (i, float(fr), 1) if -(1 << 63) <= i < (1 << 63) else None
+            return (0, float(fr), 0)
+
+        def rec(fc) -> bool:
+            if fc.type in ("AND", "OR"):
+                nodes.append([_lib.PGPU_X_AND if fc.type == "AND" else _lib.PGPU_X_OR, len(fc.children)])
+                return all(rec(ch) for ch in fc.children)
+            if fc.type == "NOT":
+                nodes.append([_lib.PGPU_X_NOT, 1])
+                return rec(fc.children[0])
+            p = fc.predicate
+            if seg0.column(p.column).data_type == PGPU_STRING:
+                return False
+            kind = {"EQ": _lib.PGPU_P_EQ, "NOT_EQ": _lib.PGPU_P_NOT_EQ, "IN": _lib.PGPU_P_IN,
+                    "NOT_IN": _lib.PGPU_P_NOT_IN, "RANGE": _lib.PGPU_P_RANGE}[p.type]
+            if p.type == "RANGE":
+                vals = [p.lower if p.lower != UNBOUNDED else "0", p.upper if p.upper != UNBOUNDED else "0"]
+            else:
+                vals = list(p.values)
+            parsed = [lit(v) for v in vals]
+            if any(x is None for x in parsed):
+                return False
+            nodes.append([_lib.PGPU_X_PRED, 0, col_index[p.column], kind, int(p.lower == UNBOUNDED),
+                          int(p.upper == UNBOUNDED), int(p.lower_inclusive), int(p.upper_inclusive), len(parsed),
+                          len(lits)])
+            lits.extend(parsed)
+            return True
+
+        if not rec(f):
+            return None
+        la = (Literal * max(1, len(lits)))(*[Literal(i, d, ig, 0) for i, d, ig in lits])
+        arr = (ExprNode * len(nodes))()
+        for k, nd in enumerate(nodes):
+            e = arr[k]
+            e.op, e.num_children = nd[0], nd[1]
+            if nd[0] == _lib.PGPU_X_PRED:
+                (e.column, e.pred, e.lower_unbounded, e.upper_unbounded, e.lower_inclusive, e.upper_inclusive,
+                 e.num_values) = nd[2:9]
+                e.values = C.cast(C.byref(la, nd[9] * C.sizeof(Literal)), C.POINTER(Literal))
+        return arr, len(nodes), la
+
+    def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment], plan_filters: bool = True):
         """Build the pgpu_query_desc.  Returns (desc, keep, globals_): `keep` owns every buffer the descriptor
-        points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array)."""
+        points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array).
+        plan_filters=False leaves the per-segment filter programs empty (the library plans them from
+        filter_expr)."""
         columns = query.columns
         col_index = {c: i for i, c in enumerate(columns)}
         nseg = len(segments)
@@ -380,7 +450,7 @@ class GpuPlanMaker:
         ids: list = []
         starts = []
         cmaps = []
-        flt = query.filter
+        flt = query.filter if plan_filters else None
         for seg in segments:
             if query.group_by:
                 self._check_group_limit(query, seg)
@@ -433,10 +503,15 @@ class GpuPlanMaker:
     def submit(self, query: QueryContext, segments: Sequence[GpuSegment]) -> "PendingQuery":
         """Plan the query and enqueue it on the GPU without waiting (pgpu_query_submit).  Several queries may be
         in flight: the host plans the next one while the GPU runs this one."""
-        desc, keep, globals_ = self.build_desc(query, segments)
+        expr = self.filter_expr(query, segments)
+        desc, keep, globals_ = self.build_desc(query, segments, plan_filters=expr is None)
         L = self.layout(desc)
         h = C.c_void_p()
-        _lib.check(self.ctx._lib.pgpu_query_submit(self.ctx.handle, C.byref(desc), C.byref(h)))
+        if expr is None:
+            _lib.check(self.ctx._lib.pgpu_query_submit(self.ctx.handle, C.byref(desc), C.byref(h)))
+        else:
+            _lib.check(self.ctx._lib.pgpu_query_submit_expr(self.ctx.handle, C.byref(desc), expr[0], expr[1],
+                                                            C.byref(h)))
         return PendingQuery(self, query, len(segments), h, L, globals_)
 
     def collect(self, pending: "PendingQuery") -> QueryResult:

@@ -372,3 +372,19 @@ def test_bench_workloads_vs_oracle(gpu_ctx, wl):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.parametrize("host_planning", [True, False], ids=["python_planner", "library_planner"])
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_both_filter_planners_vs_oracle(gpu_ctx, qi, host_planning):
+    """Per-segment filter planning in Python (SegmentFilterPlanner) and inside the library from literals
+    (pgpu_query_submit_expr) give the oracle's results, with and without inverted indexes loaded."""
+    rng = np.random.default_rng(4242 + qi)
+    segs = [_random_segment(rng, 30_001, f"h{i}", inverted=["b", "d", "e"] if i else ()) for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(QUERIES[qi])
+        _assert_same(_gpu(gpu_ctx, q, gs, host_planning=host_planning), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
