@@ -32,7 +32,8 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="adanalytics")
-    ap.add_argument("--segments", type=int, default=30, help="segments per GPU")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="segments per GPU (0 = the workload's BASELINE size: 30, or 60 for groupby1m = 2B rows)")
     ap.add_argument("--docs", type=int, default=1 << 25, help="docs per segment")
     ap.add_argument("--cpu-sample-segments", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much time")
@@ -70,6 +71,8 @@ def main():
     from pinot_amd.synth import WORKLOADS, build_segments_gpu
 
     w = WORKLOADS[args.workload]
+    if args.segments <= 0:
+        args.segments = w.segments
     log = (lambda *a: print(f"[bench rank {rank}]", *a, file=sys.stderr, flush=True))
     ctx = GpuContext(local)
     seg_ids = list(range(rank * args.segments, (rank + 1) * args.segments))

@@ -96,6 +96,7 @@ class Workload:
     options: Dict
     seed: int
     description: str
+    segments: int = 30      # segments per GPU in bench.py (2^25 docs each): BASELINE.json configs' row counts
 
 
 def _days():
@@ -130,7 +131,7 @@ WORKLOADS: Dict[str, Workload] = {
         [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
-        {"num_groups_limit": 2_000_000}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT"),
+        {"num_groups_limit": 2_000_000}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
     "bitmap5": Workload(
         "bitmap5", "bitmap5",
         [SynthColumn("a", 4, lambda: np.arange(4, dtype=np.int32) * 10, index="inv"),

@@ -20,6 +20,8 @@ for step in "$@"; do
     bench) run bench 600 python -u bench.py --steps 10 --warmup 2 ;;
     bench_range) run bench_range 600 python -u bench.py --steps 10 --warmup 2 --workload range_in ;;
     bench_gb) run bench_gb 600 python -u bench.py --steps 5 --warmup 1 --workload groupby1m ;;
+    bench_bm) run bench_bm 600 python -u bench.py --steps 10 --warmup 2 --workload bitmap5 ;;
+    round_prof) run round_prof 900 bash scripts/profile_round.sh "${PROF_TAG:-prof}" ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-check ;;
   esac
 done
