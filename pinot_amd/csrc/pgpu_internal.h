@@ -43,6 +43,7 @@
 #define PGPU_DOC_U 4            // candidate docs per lane per flush round
 #define PGPU_LDS_LIMIT 163840   // gfx950 LDS per CU
 #define PGPU_LDS_TABLE_BYTES (32 * 1024)
+#define PGPU_SLICE_RANGES 4       // dict-id ranges per bit-sliced fast leaf (RANGE = 1; small IN sets = runs)
 #define PGPU_MAX_STAGE_INSTRS 31  // DMA instructions per tile (so two tiles always fit the 6-bit vmcnt)
 
 // per-consumer LDS area: mask rows | list (candidate queue; DENSE: also the key / value lists) | accumulators
@@ -77,6 +78,7 @@ struct DevColumn {
   const uint32_t* inv_dir;        // card+1 container indexes
   const DevContainer* inv_ct;     // containers
   const uint8_t* inv_data;        // Roaring payload bytes
+  const uint32_t* sliced;         // FIXED_BIT: bit-sliced copy (pgpu_bitslice_kernel), nullptr = none
   int32_t kind;                   // PGPU_COL_*
   int32_t bits;
   int32_t card;
@@ -107,6 +109,12 @@ struct DevSeg {
   int32_t stage_col[PGPU_MAX_STAGE];   // query column of staged column j
   int32_t stage_off[PGPU_MAX_STAGE];   // byte offset of its region in a ring slot
   int32_t fast_ins[2];            // the fast leaves: instruction index within the dense program
+  int32_t stage_sliced;           // bit j: staged column j is streamed from its bit-sliced copy
+  // fast leaf j evaluated on bit planes (staged sliced): f_nr[j] ranges [lo, hi) of dict ids, OR-ed, then
+  // negated when f_sneg[j] (0 ranges = the leaf decodes the packed layout)
+  int32_t f_nr[2];
+  int32_t f_sneg[2];
+  uint32_t f_rng[2][PGPU_SLICE_RANGES][2];
 };
 
 // Filter instruction with statically resolved mask slots.
@@ -245,5 +253,10 @@ inline uint32_t pgpu_lds_bytes(int dense, int ring_slots, int slot_bytes, int lt
 
 // Bytes of one staged column's region in a ring slot and its DMA instruction count.  Widths that are multiples of
 // 8 bits get 16 B of padding per lane record so the consumers' ds_read_b128 are bank-conflict free.
-inline int pgpu_stage_region_bytes(int bits) { return (bits % 8 == 0) ? 64 * (4 * bits + 16) : 256 * bits; }
-inline int pgpu_stage_instrs(int bits) { return (bits % 8 == 0) ? bits / 4 + 1 : (bits + 3) / 4; }
+// A bit-sliced column is staged as its plain 256*b tile bytes (b planes x 64 lane words: no padding needed).
+inline int pgpu_stage_region_bytes(int bits, bool sliced = false) {
+  return (bits % 8 == 0 && !sliced) ? 64 * (4 * bits + 16) : 256 * bits;
+}
+inline int pgpu_stage_instrs(int bits, bool sliced = false) {
+  return (bits % 8 == 0 && !sliced) ? bits / 4 + 1 : (bits + 3) / 4;
+}

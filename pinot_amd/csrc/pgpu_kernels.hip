@@ -673,6 +673,7 @@ FI bool cursor_advance(const DevParams& p, Cursor& c, int k) {
 struct StageCache {
   int nst;
   int instrs;
+  int lin;  // bit j: column j is bit-sliced (plain 256*b tile copy)
   const char* fwd[PGPU_MAX_STAGE];
   int bits[PGPU_MAX_STAGE];
   int off[PGPU_MAX_STAGE];
@@ -681,12 +682,13 @@ FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
   const DevSeg* sg = p.segs + seg;
   sc.nst = cld(&sg->nstage);
   sc.instrs = cld(&sg->stage_instrs);
+  sc.lin = cld(&sg->stage_sliced);
   const DevColumn* cols = p.cols + cld(&sg->col_begin);
 #pragma unroll
   for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
     if (j < sc.nst) {
       const int qc = cld(&sg->stage_col[j]);
-      sc.fwd[j] = (const char*)cld(&cols[qc].fwd);
+      sc.fwd[j] = (sc.lin >> j) & 1 ? (const char*)cld(&cols[qc].sliced) : (const char*)cld(&cols[qc].fwd);
       sc.bits[j] = cld(&cols[qc].bits);
       sc.off[j] = cld(&sg->stage_off[j]);
     } else {
@@ -707,7 +709,7 @@ FI void issue_tile(const StageCache& sc, int tile_in_seg, unsigned char* slot) {
     const int b = sc.bits[j];
     const char* src = sc.fwd[j] + (size_t)tile_in_seg * 256 * b;
     unsigned char* dst = slot + sc.off[j];
-    if (b % 8 != 0) {
+    if (b % 8 != 0 || ((sc.lin >> j) & 1)) {
       const int ninstr = (b + 3) >> 2;
       const char* ls = src + 16 * lane;
       for (int k = 0; k < ninstr; ++k) {
@@ -804,6 +806,7 @@ struct SegState {
   // fast dense program (DevSeg::fast): per leaf bit width, staged offset, predicate kind / lo / span, negate
   int32_t fast;
   int32_t f_bits[2], f_off[2], f_kind[2], f_neg[2];
+  int32_t f_nr[2];  // bit-sliced leaf: number of dict-id ranges (0 = packed layout)
   uint32_t f_lo[2], f_span[2];
 };
 FI void load_seg(const DevParams& p, int seg, SegState& ss) {
@@ -826,7 +829,9 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   for (int j = 0; j < 2; ++j) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
     ss.f_lo[j] = ss.f_span[j] = 0;
+    ss.f_nr[j] = 0;
     if (j < ss.fast) {
+      ss.f_nr[j] = cld(&sg->f_nr[j]);
       const DevInstr* in = p.instrs + ss.prog_begin + cld(&sg->fast_ins[j]);
       ss.f_bits[j] = cld(&in->bits);
       ss.f_off[j] = cld(&in->stage_off);
@@ -976,6 +981,41 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
 // Fast dense program (SegState::fast leaves ANDed, RANGE / MASK predicates on staged columns): evaluated in
 // registers -- no instruction fetch, no mask-row LDS round trips.  Same result and scan accounting as
 // run_program on the equivalent AND program (a leaf is evaluated only while some doc of the wave survives).
+// ---- bit-sliced predicates ----------------------------------------------------------------------------------------
+// Bit-sliced tile layout (pgpu_bitslice_kernel): plane k of lane l = bit k of the dict ids of docs [32l, 32l+32),
+// doc 32l+i in bit i, at dword k*64 + l of the tile's 256*b bytes.  x < c for a wave-uniform constant c is the
+// borrow out of x - c, carried LSB -> MSB through the planes: borrow' = maj(~x_k, c_k, borrow), one v_bitop3 per
+// plane for 32 docs (the packed layout needs an extract + compare + pack per doc).  x_k sits in the middle operand,
+// so the table (0xB2) is symmetric in the outer two and does not depend on the operand-order convention.
+template <int B>
+FI uint32_t sliced_lt(const uint32_t (&x)[B], uint32_t c) {
+  if (c >> B) return ~0u;  // c = 2^B: past the largest id
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) br = __builtin_amdgcn_bitop3_b32((uint32_t)-(int32_t)((c >> k) & 1u), x[k], br, 0xB2);
+  return br;
+}
+template <int B>
+FI uint32_t sliced_ranges_b(const uint32_t* region, const DevSeg* sg, int j, int nr) {
+  const LAS uint32_t* src = (const LAS uint32_t*)region + opaque_lane();
+  uint32_t x[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) x[k] = src[64 * k];
+  uint32_t m = 0;
+  for (int r = 0; r < nr; ++r) {
+    const uint32_t lo = cld(&sg->f_rng[j][r][0]), hi = cld(&sg->f_rng[j][r][1]);
+    m |= sliced_lt<B>(x, hi) & ~sliced_lt<B>(x, lo);
+  }
+  return m;
+}
+FI uint32_t sliced_ranges(int bits, const uint32_t* region, const DevSeg* sg, int j, int nr) {
+  uint32_t m = 0;
+#define SL_CALL(B) m = sliced_ranges_b<B>(region, sg, j, nr)
+  PGPU_DISPATCH_B(bits, SL_CALL)
+#undef SL_CALL
+  return m;
+}
+
 FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) {
   uint32_t m = t.valid;
 #pragma unroll 1
@@ -989,6 +1029,13 @@ FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) 
     const uint32_t lo = j ? ss.f_lo[1] : ss.f_lo[0];
     const uint32_t span = j ? ss.f_span[1] : ss.f_span[0];
     const bool neg = (j ? ss.f_neg[1] : ss.f_neg[0]) != 0;
+    const int nr = j ? ss.f_nr[1] : ss.f_nr[0];
+    if (nr > 0) {
+      // bit-sliced leaf: OR of dict-id ranges evaluated on the lane's bit planes (32 docs per word op)
+      const uint32_t r = sliced_ranges(bits, (const uint32_t*)(t.slot + off), ss.sg, j, nr);
+      m &= cld(&ss.sg->f_sneg[j]) ? ~r : r;
+      continue;
+    }
     uint32_t ids[32];
     decode_ids(bits, (const uint32_t*)(t.slot + off), nullptr, t.tile_in_seg, ids);
     uint32_t r = 0;
@@ -1876,6 +1923,42 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 #define PGPU_ALL_QUERY_KERNELS(X)                                                                          \
   X(PGPU_MODE_AGG, 0) X(PGPU_MODE_LDS, 0) X(PGPU_MODE_GLOBAL, 0) X(PGPU_MODE_PART, 0) X(PGPU_MODE_AGG, 1) \
   X(PGPU_MODE_LDS, 1) X(PGPU_MODE_GLOBAL, 1) X(PGPU_MODE_PART, 1)
+
+// Bit-sliced copy of a fixed-bit forward index (built once per column at segment seal): thread (tile, lane) unpacks
+// its 32 dict ids from the big-endian packed words and writes plane k = bit k of each id (doc 32l+i in bit i) at
+// dword (tile * b + k) * 64 + lane.  Same bytes per tile as the packed stream, so staging costs are unchanged.
+template <int B>
+__device__ void bitslice_b(const uint32_t* fwd, uint32_t* out, int64_t tile, int lane) {
+  uint32_t w[B], ids[32];
+  const uint32_t* src = fwd + ((size_t)tile * 64 + lane) * B;
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(src[k]);
+  unpack_b<B>(w, ids);
+  uint32_t* dst = out + (size_t)tile * B * 64 + lane;
+#pragma unroll
+  for (int k = 0; k < B; ++k) {
+    uint32_t pl = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) pl |= ((ids[i] >> k) & 1u) << i;
+    dst[(size_t)k * 64] = pl;
+  }
+}
+__global__ __launch_bounds__(256) void bitslice_kernel(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tile = g >> 6;
+  const int lane = (int)(g & 63);
+  if (tile >= ntiles) return;
+#define BS_CALL(B) bitslice_b<B>(fwd, out, tile, lane)
+  PGPU_DISPATCH_B(bits, BS_CALL)
+#undef BS_CALL
+}
+
+hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  const int64_t blocks = (ntiles * 64 + 255) / 256;
+  hipLaunchKernelGGL(bitslice_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fwd, out, bits, ntiles);
+  return hipGetLastError();
+}
 
 hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
   hipError_t e = hipSuccess;

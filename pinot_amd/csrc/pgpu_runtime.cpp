@@ -33,6 +33,7 @@ hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
+hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st);
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
                                 bool init_table, hipStream_t st);
 hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
@@ -179,6 +180,7 @@ struct HostColumn {
   int32_t dict_card = 0;
   int32_t inv_card = 0;
   DevMem fwd, sorted, dict, inv_dir, inv_ct, inv_data;
+  DevMem sliced;                       // bit-sliced copy of fwd (built at seal; PGPU_NO_SLICE=1 skips it)
   uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
@@ -516,9 +518,19 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
 int pgpu_segment_seal(pgpu_segment* seg) {
   if (!seg) return fail(PGPU_E_INVALID, "null segment");
   seg->dev.resize(seg->cols.size());
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  static const bool no_slice = getenv("PGPU_NO_SLICE") && atoi(getenv("PGPU_NO_SLICE")) != 0;
   for (size_t i = 0; i < seg->cols.size(); ++i) {
     HostColumn& c = seg->cols[i];
+    if (c.kind == PGPU_COL_FIXED_BIT && !no_slice && !c.sliced.p) {
+      // bit planes of every 2048-doc tile of the padded stream (same byte count as the packed copy)
+      const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
+      HIP_TRY(c.sliced.alloc(c.fwd.n));
+      HIP_TRY(hipMemset(c.sliced.p, 0, c.sliced.n));
+      HIP_TRY(pgpu_launch_bitslice((const uint32_t*)c.fwd.p, (uint32_t*)c.sliced.p, c.bits, ntiles, nullptr));
+    }
     DevColumn d{};
+    d.sliced = (const uint32_t*)c.sliced.p;
     d.fwd = (const uint32_t*)c.fwd.p;
     d.sorted = (const int32_t*)c.sorted.p;
     d.dict = c.dict.p;
@@ -535,7 +547,6 @@ int pgpu_segment_seal(pgpu_segment* seg) {
                   c.fwd_card);
     seg->dev[i] = d;
   }
-  HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(hipDeviceSynchronize());
   seg->sealed = true;
   return PGPU_OK;
@@ -545,7 +556,7 @@ int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes) {
   if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
   uint64_t t = 0;
   for (const HostColumn& c : seg->cols)
-    t += c.fwd.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n;
+    t += c.fwd.n + c.sliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n;
   *out_bytes = t;
   return PGPU_OK;
 }
@@ -1056,41 +1067,15 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   int rc = convert_filter(q, sp, dn.data(), (int)dn.size(), seg, pk);
   if (rc) return rc;
   ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
-  std::vector<int> stage_offs;
-  {
-    int o = 0;
-    for (int qc : staged) {
-      stage_offs.push_back(o);
-      o += pgpu_stage_region_bytes(v.dev(qc)->bits);
-    }
-  }
-  for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
-    DevInstr& in = pk.instrs[i];
-    if (in.op != PGPU_I_SCAN) continue;
-    for (size_t j = 0; j < staged.size(); ++j)
-      if (staged[j] == in.col) in.stage_off = stage_offs[j];
-  }
   ds.rprog_begin = (int32_t)pk.instrs.size();
   rc = convert_filter(q, sp, rn.data(), (int)rn.size(), seg, pk);
   if (rc) return rc;
   ds.rprog_len = (int32_t)pk.instrs.size() - ds.rprog_begin;
-  // staging layout
-  ds.nstage = (int32_t)staged.size();
-  ds.stage_instrs = 0;
-  int off = 0;
-  for (size_t j = 0; j < staged.size(); ++j) {
-    const int b = v.dev(staged[j])->bits;
-    ds.stage_col[j] = staged[j];
-    ds.stage_off[j] = off;
-    off += pgpu_stage_region_bytes(b);
-    ds.stage_instrs += pgpu_stage_instrs(b);
-  }
-  pk.slot_bytes = std::max(pk.slot_bytes, off);
-  pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
-  int64_t tb = 0;
-  for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
-  pk.tile_bytes = std::max(pk.tile_bytes, tb);
-  pk.est_matched += rho * seg->num_docs;
+  auto stage_index = [&](int qc) {
+    for (size_t j = 0; j < staged.size(); ++j)
+      if (staged[j] == qc) return (int)j;
+    return -1;
+  };
   // fast dense program: one staged SCAN leaf, or AND_BEGIN (SCAN AND_CHILD){2} AND_END, RANGE / MASK predicates
   ds.fast = 0;
   ds.fast_ins[0] = ds.fast_ins[1] = -1;
@@ -1100,7 +1085,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     for (int i = 0; i < ds.prog_len && ok; ++i) {
       const DevInstr& in = pk.instrs[ds.prog_begin + i];
       if (in.op == PGPU_I_SCAN) {
-        ok = nscan < 2 && in.kind == PGPU_COL_FIXED_BIT && in.stage_off >= 0 && (in.pred == 0 || in.pred == 3);
+        ok = nscan < 2 && in.kind == PGPU_COL_FIXED_BIT && stage_index(in.col) >= 0 && (in.pred == 0 || in.pred == 3);
         if (ok) ds.fast_ins[nscan++] = i;
       } else if (in.op == PGPU_I_AND_BEGIN) {
         ok = ++nand == 1 && i == 0;
@@ -1110,6 +1095,80 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     }
     if (ok && nscan >= 1 && (nand == 0 ? ds.prog_len == 1 : ds.prog_len == 2 * nscan + 2)) ds.fast = nscan;
   }
+  // bit-sliced fast leaves (kernel sliced_ranges): the column has a bit-sliced copy, only the dense filter reads
+  // its staged tiles (it is not an aggregation / group column decoded from the slot, nor the other fast leaf's
+  // column), and the predicate is a RANGE or a 64-id MASK whose ids (or their complement) form <= 4 runs
+  ds.stage_sliced = 0;
+  for (int j = 0; j < 2; ++j) {
+    ds.f_nr[j] = ds.f_sneg[j] = 0;
+    for (int r = 0; r < PGPU_SLICE_RANGES; ++r) ds.f_rng[j][r][0] = ds.f_rng[j][r][1] = 0;
+  }
+  for (int j = 0; j < ds.fast; ++j) {
+    const DevInstr& in = pk.instrs[ds.prog_begin + ds.fast_ins[j]];
+    const DevColumn* dc = v.dev(in.col);
+    if (!dc->sliced || dc->bits < 1 || dc->bits > 31) continue;
+    if (agg_mode == PGPU_AM_DENSE && std::find(aggcols.begin(), aggcols.end(), in.col) != aggcols.end()) continue;
+    if (ds.fast == 2 && pk.instrs[ds.prog_begin + ds.fast_ins[1 - j]].col == in.col) continue;
+    const uint64_t top = 1ull << dc->bits;
+    std::vector<std::pair<uint32_t, uint32_t>> rng;
+    bool neg = in.negate != 0;
+    if (in.pred == 0) {
+      if (in.lo < 0 || in.hi < 0 || (uint64_t)in.lo > top || (uint64_t)in.hi > top) continue;
+      rng.emplace_back((uint32_t)in.lo, (uint32_t)in.hi);
+    } else {
+      const uint64_t mask = (uint64_t)(uint32_t)in.lo | ((uint64_t)(uint32_t)in.hi << 32);
+      const int n = (int)std::min<uint64_t>(64, top);
+      auto runs = [&](bool bit) {
+        std::vector<std::pair<uint32_t, uint32_t>> out;
+        for (int i = 0; i < n;) {
+          if (((mask >> i) & 1u) != (uint64_t)bit) { ++i; continue; }
+          int e = i;
+          while (e < n && ((mask >> e) & 1u) == (uint64_t)bit) ++e;
+          out.emplace_back((uint32_t)i, (uint32_t)e);
+          i = e;
+        }
+        return out;
+      };
+      auto set = runs(true), clr = runs(false);
+      if (set.size() <= clr.size()) rng = set;
+      else { rng = clr; neg = !neg; }
+      if (rng.empty()) rng.emplace_back(0u, 0u);  // matches no id
+      if ((int)rng.size() > PGPU_SLICE_RANGES) continue;
+    }
+    ds.f_nr[j] = (int32_t)rng.size();
+    ds.f_sneg[j] = neg ? 1 : 0;
+    for (size_t r = 0; r < rng.size(); ++r) {
+      ds.f_rng[j][r][0] = rng[r].first;
+      ds.f_rng[j][r][1] = rng[r].second;
+    }
+    ds.stage_sliced |= 1 << stage_index(in.col);
+  }
+  // staging layout
+  std::vector<int> stage_offs;
+  ds.nstage = (int32_t)staged.size();
+  ds.stage_instrs = 0;
+  int off = 0;
+  for (size_t j = 0; j < staged.size(); ++j) {
+    const int b = v.dev(staged[j])->bits;
+    const bool sl = (ds.stage_sliced >> j) & 1;
+    ds.stage_col[j] = staged[j];
+    ds.stage_off[j] = off;
+    stage_offs.push_back(off);
+    off += pgpu_stage_region_bytes(b, sl);
+    ds.stage_instrs += pgpu_stage_instrs(b, sl);
+  }
+  for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+    DevInstr& in = pk.instrs[i];
+    if (in.op != PGPU_I_SCAN) continue;
+    const int j = stage_index(in.col);
+    if (j >= 0) in.stage_off = stage_offs[j];
+  }
+  pk.slot_bytes = std::max(pk.slot_bytes, off);
+  pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
+  int64_t tb = 0;
+  for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
+  pk.tile_bytes = std::max(pk.tile_bytes, tb);
+  pk.est_matched += rho * seg->num_docs;
   ds.agg_mode = agg_mode;
   ds.nreg = -1;
   ds.reg_col[0] = ds.reg_col[1] = -1;
