@@ -217,7 +217,10 @@ struct DevParams {
   int32_t pcol;                   // query column carried in the records (-1: COUNT only)
   int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
   int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
-  int32_t pad1;
+  int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)
+  int32_t dslots;                 // direct: LDS slots per wave (dslots - 1 tiles in flight while one is filtered)
+  int32_t min_instrs;             // direct: fewest DMA instructions of any segment's tile (counted vmcnt waits)
+  int32_t pad2;
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];

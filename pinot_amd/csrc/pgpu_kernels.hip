@@ -807,6 +807,8 @@ struct SegState {
   int32_t fast;
   int32_t f_bits[2], f_off[2], f_kind[2], f_neg[2];
   int32_t f_nr[2];  // bit-sliced leaf: number of dict-id ranges (0 = packed layout)
+  uint32_t f_r0lo[2], f_r0hi[2];  // its first range (the only one of a RANGE leaf), kept in SGPRs
+  int32_t f_sneg[2];
   uint32_t f_lo[2], f_span[2];
 };
 FI void load_seg(const DevParams& p, int seg, SegState& ss) {
@@ -830,8 +832,13 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
     ss.f_lo[j] = ss.f_span[j] = 0;
     ss.f_nr[j] = 0;
+    ss.f_r0lo[j] = ss.f_r0hi[j] = 0;
+    ss.f_sneg[j] = 0;
     if (j < ss.fast) {
       ss.f_nr[j] = cld(&sg->f_nr[j]);
+      ss.f_r0lo[j] = cld(&sg->f_rng[j][0][0]);
+      ss.f_r0hi[j] = cld(&sg->f_rng[j][0][1]);
+      ss.f_sneg[j] = cld(&sg->f_sneg[j]);
       const DevInstr* in = p.instrs + ss.prog_begin + cld(&sg->fast_ins[j]);
       ss.f_bits[j] = cld(&in->bits);
       ss.f_off[j] = cld(&in->stage_off);
@@ -996,21 +1003,22 @@ FI uint32_t sliced_lt(const uint32_t (&x)[B], uint32_t c) {
   return br;
 }
 template <int B>
-FI uint32_t sliced_ranges_b(const uint32_t* region, const DevSeg* sg, int j, int nr) {
+FI uint32_t sliced_ranges_b(const uint32_t* region, const DevSeg* sg, int j, int nr, uint32_t lo0, uint32_t hi0) {
   const LAS uint32_t* src = (const LAS uint32_t*)region + opaque_lane();
   uint32_t x[B];
 #pragma unroll
   for (int k = 0; k < B; ++k) x[k] = src[64 * k];
-  uint32_t m = 0;
-  for (int r = 0; r < nr; ++r) {
+  uint32_t m = sliced_lt<B>(x, hi0) & ~sliced_lt<B>(x, lo0);
+  for (int r = 1; r < nr; ++r) {
     const uint32_t lo = cld(&sg->f_rng[j][r][0]), hi = cld(&sg->f_rng[j][r][1]);
     m |= sliced_lt<B>(x, hi) & ~sliced_lt<B>(x, lo);
   }
   return m;
 }
-FI uint32_t sliced_ranges(int bits, const uint32_t* region, const DevSeg* sg, int j, int nr) {
+FI uint32_t sliced_ranges(int bits, const uint32_t* region, const DevSeg* sg, int j, int nr, uint32_t lo0,
+                          uint32_t hi0) {
   uint32_t m = 0;
-#define SL_CALL(B) m = sliced_ranges_b<B>(region, sg, j, nr)
+#define SL_CALL(B) m = sliced_ranges_b<B>(region, sg, j, nr, lo0, hi0)
   PGPU_DISPATCH_B(bits, SL_CALL)
 #undef SL_CALL
   return m;
@@ -1032,8 +1040,9 @@ FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) 
     const int nr = j ? ss.f_nr[1] : ss.f_nr[0];
     if (nr > 0) {
       // bit-sliced leaf: OR of dict-id ranges evaluated on the lane's bit planes (32 docs per word op)
-      const uint32_t r = sliced_ranges(bits, (const uint32_t*)(t.slot + off), ss.sg, j, nr);
-      m &= cld(&ss.sg->f_sneg[j]) ? ~r : r;
+      const uint32_t r = sliced_ranges(bits, (const uint32_t*)(t.slot + off), ss.sg, j, nr,
+                                       j ? ss.f_r0lo[1] : ss.f_r0lo[0], j ? ss.f_r0hi[1] : ss.f_r0hi[0]);
+      m &= (j ? ss.f_sneg[1] : ss.f_sneg[0]) ? ~r : r;
       continue;
     }
     uint32_t ids[32];
@@ -1048,6 +1057,24 @@ FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) 
       for (int i = 31; i >= 0; --i) r = (r << 1) | (uint32_t)((ids[i] - lo) < span);
     }
     m &= neg ? ~r : r;
+  }
+  return m;
+}
+
+// Direct-kernel form of fast_filter: the scanned-entries count stays per lane (reduced once per wave at the end)
+// and the empty-tile exit is a ballot, so a tile costs no cross-lane reduction.
+FI uint32_t fast_filter_lean(const SegState& ss, const TileCtx& t, uint32_t& lane_scanned) {
+  uint32_t m = t.valid;
+#pragma unroll 1
+  for (int j = 0; j < ss.fast; ++j) {
+    if (j > 0 && __builtin_amdgcn_ballot_w64(m != 0) == 0) return 0u;
+    lane_scanned += __popc(m);
+    const int bits = j ? ss.f_bits[1] : ss.f_bits[0];
+    const int off = j ? ss.f_off[1] : ss.f_off[0];
+    const int nr = j ? ss.f_nr[1] : ss.f_nr[0];
+    const uint32_t r = sliced_ranges(bits, (const uint32_t*)(t.slot + off), ss.sg, j, nr,
+                                     j ? ss.f_r0lo[1] : ss.f_r0lo[0], j ? ss.f_r0hi[1] : ss.f_r0hi[0]);
+    m &= (j ? ss.f_sneg[1] : ss.f_sneg[0]) ? ~r : r;
   }
   return m;
 }
@@ -1253,6 +1280,9 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
     }
     if (nm && ss.agg_mode == PGPU_AM_SPARSE) sparse_agg<MODE>(p, L, cv, la, ss, d.doc, m);
   }
+  // a wait hipcc sees: its scoreboard then holds no pending gather, so it does not guard the next tile's LDS reads
+  // with vmcnt(0) (which would also drain the direct kernel's prefetched tiles)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   wave_sync();
 }
 
@@ -1639,6 +1669,264 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   return s;
 }
 
+// ================================================================================================================
+// DIRECT (self-loading) variant: every staged column is a bit-sliced fast leaf and no segment aggregates densely
+// (PGPU_AM_COUNT / PGPU_AM_SPARSE).  Such tiles are small (256 * b bytes) and their filter is a handful of VALU ops
+// per 32 docs, so the loader -> ring -> consumer hand-off (flag polls, per-tile cursor work on a shared scalar unit)
+// would dominate.  Here each wave streams its own tiles: it DMAs tile i+1 into one of two private LDS slots, waits
+// for tile i with a counted vmcnt and filters it; 256-thread workgroups, several per CU.  The DMAs are issued from
+// inline asm so that hipcc does not guard the wave's other LDS accesses with vmcnt(0) (in-order completion keeps
+// hipcc's own counted waits conservative).
+// ================================================================================================================
+#define PGPU_DIRECT_THREADS 256
+#define PGPU_DIRECT_WAVES (PGPU_DIRECT_THREADS / 64)
+
+// saddr form: wave-uniform base in an SGPR pair + this lane's byte offset (a VGPR that lives for the whole kernel),
+// so no VGPR is written right before the DMA -- a freshly written address VGPR draws a conservative vmcnt(0) from
+// hipcc, which would drain this wave's prefetches.
+FI void glds16_asm(uint32_t voff, const void* sbase, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst));
+}
+FI const void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = (uint32_t)sgpr((int)(uint32_t)v), hi = (uint32_t)sgpr((int)(uint32_t)(v >> 32));
+  return (const void*)(((uint64_t)hi << 32) | lo);
+}
+// The tile's staged (bit-sliced, linear) regions into `slot`: 16 B per lane, 1 KiB per instruction.
+FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* slot, uint32_t voff16) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
+    if (j >= sc.nst) break;
+    const int b = sc.bits[j];
+    const char* base = sc.fwd[j] + (size_t)tile_in_seg * 256 * b;
+    const uint32_t dst = sgpr((int)lds_off(slot + sc.off[j]));
+    const int ninstr = (b + 3) >> 2;
+    for (int k = 0; k < ninstr; ++k) {
+      if (64 * k + lane < 16 * b) glds16_asm(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
+    }
+  }
+}
+
+template <int MODE>
+FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NW = PGPU_DIRECT_WAVES;
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  const int S = p.slot_bytes;
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  unsigned char* slots = L.ring + (size_t)cidx * p.dslots * S;
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  uint32_t lane_scanned = 0, lane_matched = 0;  // per-lane counts (< 2^32 per lane), reduced at the end
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int qn = 0, qt = 0;
+  SegState ss;
+  int cseg = -1;
+  if (cidx < ntiles) {
+    // issue cursor `ci` runs up to D - 1 of this wave's tiles ahead of the processing cursor `cur`
+    const int D = p.dslots;
+    const int own = (ntiles - cidx + NW - 1) / NW;  // this wave's tiles: cidx, cidx + NW, ...
+    Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
+    StageCache sc;
+    load_stage(p, ci.seg, sc);
+    int issued = 0, islot = 0, pslot = 0;
+    uint32_t voff16;
+    asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(voff16) : "v"(opaque_lane()));  // lane * 16, kept live
+    for (int k = 0; k < own; ++k) {
+      while (issued < own && issued < k + D) {
+        if (issued > 0 && cursor_advance(p, ci, NW)) load_stage(p, ci.seg, sc);
+        issue_tile_direct(sc, ci.tile_in_seg, slots + (size_t)islot * S, voff16);
+        ++issued;
+        if (++islot == D) islot = 0;
+      }
+      const int next_instrs = (issued - k - 1) * p.min_instrs;  // lower bound of the DMAs issued after tile k
+      if (k > 0) cursor_advance(p, cur, NW);
+      if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES || cur.seg != cseg)) {
+        const int64_t tq = now(pf);
+        flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+        PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+        qn = qt = 0;
+      }
+      if (cur.seg != cseg) {
+        cseg = cur.seg;
+        load_seg(p, cseg, ss);
+      }
+      const int64_t tw = now(pf);
+      wait_vmcnt(next_instrs);  // this tile's DMAs have landed (later tiles' may still be in flight)
+      PROF_ADD(pf, PGPU_P_C_FULL, tw);
+      const int64_t tf = now(pf);
+#ifdef PGPU_PROFILE_BUILD
+      if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+#endif
+      TileCtx t;
+      t.ss = &ss;
+      t.slot = slots + (size_t)pslot * S;
+      if (++pslot == D) pslot = 0;
+      t.tile_in_seg = cur.tile_in_seg;
+      t.doc0 = cur.tile_in_seg * WT;
+      t.lane_doc0 = t.doc0 + 32 * lane;
+      {
+        const int ndocs = min(WT, ss.num_docs - t.doc0);
+        const int rem = ndocs - 32 * lane;
+        t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+        if (p.flags & PGPU_FLAG_STATS)
+          for (int j = 0; j < ss.nstage; ++j) {
+            const int b = col_of(ss, cld(&ss.sg->stage_col[j])).bits;
+            if (lane == 0) dense_bytes += ((int64_t)ndocs * b + 7) / 8;
+          }
+      }
+      const uint32_t mm = fast_filter_lean(ss, t, lane_scanned);
+      // the slot's planes have been read (lgkmcnt): it is rewritten by the issue of tile k + D, after this point
+      PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+      const int64_t ta = now(pf);
+      if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
+        lane_matched += __popc(mm);
+      } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
+        const int cnt = __popc(mm);
+        const int ex = wave_excl_scan(cnt);
+        const int nm = __builtin_amdgcn_readlane(ex + cnt, 63);
+        if (qn + nm <= PGPU_CQ_CAP) {
+          if (lane == 0) cv.qtiles[qt] = cur.tile_in_seg;
+          const uint32_t tag = (uint32_t)qt << 11;
+          ++qt;
+          int q = qn + ex;
+          for (uint32_t left = mm; left; left &= left - 1)
+            cv.queue[q++] = (uint16_t)(tag | (uint32_t)(32 * lane + __builtin_ctz(left)));
+          qn += nm;
+        } else {
+          if (qn) {
+            flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+            qn = qt = 0;
+          }
+          if (lane == 0) cv.qtiles[0] = cur.tile_in_seg;
+          for (int half = 0; half < 2; ++half) {
+            const uint32_t mh = (lane >> 5) == half ? mm : 0u;
+            const int nh = wave_sum_i32(__popc(mh));
+            if (nh == 0) continue;
+            int q = wave_excl_scan(__popc(mh));
+            for (uint32_t left = mh; left; left &= left - 1) cv.queue[q++] = (uint16_t)(32 * lane + __builtin_ctz(left));
+            flush_queue<MODE, NW>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
+          }
+        }
+      }
+      PROF_ADD(pf, PGPU_P_C_AGG, ta);
+    }
+    if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  {
+    const int64_t ls = wave_sum_i64((int64_t)lane_scanned), lm = wave_sum_i64((int64_t)lane_matched);
+    if (lane == 0) {
+      scanned += ls;
+      matched += lm;
+    }
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  if (MODE == PGPU_MODE_AGG) {
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  }
+  Stats st;
+  st.matched = matched;
+  st.scanned = scanned;
+  st.sector_bytes = sector_bytes;
+  st.dense_bytes = dense_bytes;
+  return st;
+}
+
+// LDS of the direct kernel: consumer areas | group table / partition cursors | two slots per wave.
+FI Lds carve_direct(unsigned char* base, const DevParams& p) {
+  Lds L;
+  L.full = L.freef = L.icnt = nullptr;
+  L.cons = base;
+  L.ltab = (int64_t*)(L.cons + PGPU_DIRECT_WAVES * p.cons_bytes);
+  L.ring = (unsigned char*)L.ltab + ((p.ltab_bytes + 15) & ~15);
+  return L;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_direct(DevParams p) {
+  constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  if (MODE == PGPU_MODE_LDS) {
+    const int n = p.nsec * (int)p.G;
+    for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+  }
+  if (MODE == PGPU_MODE_PART)
+    for (int i = threadIdx.x; i < p.nparts; i += NT) ((uint32_t*)L.ltab)[i] = 0u;
+  __syncthreads();
+  // contiguous tile range per workgroup, one contiguous run of workgroups per XCD (see query_kernel)
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const Stats st = direct_consumer<MODE>(p, L, wave, t0, t1 - t0, pf);
+  const size_t w = (size_t)blockIdx.x * NWAVES + wave;
+#ifdef PGPU_PROFILE_BUILD
+  if (pf.on && lane == 0) {
+    int64_t* o = p.prof + w * PGPU_NPROF;
+#pragma unroll
+    for (int k = 0; k < PGPU_NPROF; ++k) o[k] = pf.t[k];
+  }
+#endif
+  if (lane == 0) {
+    int64_t* o = p.stats + w * PGPU_NSTATS;
+    o[PGPU_STAT_MATCHED] = st.matched;
+    o[PGPU_STAT_SCANNED] = st.scanned;
+    o[PGPU_STAT_SECTOR_BYTES] = st.sector_bytes;
+    o[PGPU_STAT_DENSE_BYTES] = st.dense_bytes;
+  }
+  if (MODE == PGPU_MODE_AGG) {
+    int64_t* slab = p.slab + w * p.nsec;
+    if (lane == 0) slab[0] = st.matched;
+    if (lane < p.nagg && p.aggs[lane].fn != PGPU_AGG_COUNT) {
+      const int64_t* acc = (const int64_t*)(L.cons + (size_t)wave * p.cons_bytes + p.mask_rows * 256 +
+                                            PGPU_CONS_LIST_BYTES_OF(0));
+      slab[p.aggs[lane].sec] = acc[lane];
+    }
+  } else if (MODE == PGPU_MODE_LDS) {
+    __syncthreads();
+    const int G = (int)p.G;
+    for (int key = threadIdx.x; key < G; key += NT) {
+      const int64_t cnt = L.ltab[key];
+      if (cnt == 0) continue;
+      atomicAdd((unsigned long long*)&p.table[key], (unsigned long long)cnt);
+      for (int s = 1; s < p.nsec; ++s) cell_atomic(&p.table[(size_t)s * p.G + key], p.sec_op[s], L.ltab[s * G + key]);
+    }
+  } else if (MODE == PGPU_MODE_PART) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < p.nparts; q += NT) {
+      const uint32_t n = ((const uint32_t*)L.ltab)[q];
+      p.rcount[(size_t)q * gridDim.x + blockIdx.x] = n < (uint32_t)p.rcap ? n : (uint32_t)p.rcap;
+    }
+  }
+}
+
 // ---- the query kernel ----------------------------------------------------------------------------------------------
 template <int MODE, int DENSE>
 __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams p) {
@@ -1974,6 +2262,12 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
                             PGPU_PART_LDS_BYTES);
   PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
 #undef PART_ATTR
+#define DIRECT_ATTR(M)                                                                                      \
+  if (e == hipSuccess)                                                                                      \
+    e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)lds_bytes);
+  DIRECT_ATTR(PGPU_MODE_AGG) DIRECT_ATTR(PGPU_MODE_LDS) DIRECT_ATTR(PGPU_MODE_GLOBAL) DIRECT_ATTR(PGPU_MODE_PART)
+#undef DIRECT_ATTR
   return e;
 }
 
@@ -2008,6 +2302,18 @@ hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipS
   }
   PGPU_ALL_QUERY_KERNELS(LAUNCH)
 #undef LAUNCH
+  return hipErrorInvalidValue;
+}
+
+// Direct variant (p.direct): PGPU_DIRECT_THREADS per workgroup, several workgroups per CU.
+hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+#define LAUNCH_D(M)                                                                                        \
+  if (p.mode == M) {                                                                                       \
+    hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+    return hipGetLastError();                                                                              \
+  }
+  LAUNCH_D(PGPU_MODE_AGG) LAUNCH_D(PGPU_MODE_LDS) LAUNCH_D(PGPU_MODE_GLOBAL) LAUNCH_D(PGPU_MODE_PART)
+#undef LAUNCH_D
   return hipErrorInvalidValue;
 }
 

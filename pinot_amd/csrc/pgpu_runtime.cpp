@@ -31,6 +31,7 @@
 hipError_t pgpu_prepare_query_kernels(size_t lds_bytes);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
+hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
 hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st);
@@ -1290,7 +1291,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t fixed = pgpu_lds_fixed_bytes(p.dense, 0, p.mask_rows);
   // LDS-privatised table only when it fits next to >= 4 ring slots and enough docs are expected to match to pay
   // for initialising and flushing one table copy per workgroup
-  const int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
+  int grid = std::max(1, std::min(ctx->num_cus, p.total_tiles));
   const bool many = pk.est_matched > 4.0 * (double)L.num_keys * grid;
   // partitioned group-by (PGPU_MODE_PART): large key spaces, at most one aggregated column of a 4-byte type
   bool part_ok = q->num_group_columns > 0 &&
@@ -1335,7 +1336,45 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     const int64_t by_bytes = (64 * 1024 + nload * pk.tile_bytes - 1) / (nload * pk.tile_bytes);
     p.inflight = (int32_t)std::max<int64_t>(1, std::min(by_ring, by_bytes));
   }
-  const size_t dyn = pgpu_lds_bytes(p.dense, p.ring_slots, S, p.ltab_bytes, p.mask_rows);
+  size_t dyn = pgpu_lds_bytes(p.dense, p.ring_slots, S, p.ltab_bytes, p.mask_rows);
+  // direct (self-loading) variant: every segment's staged columns are its bit-sliced fast leaves and no segment
+  // aggregates densely; each wave streams its own tiles through two private LDS slots (query_kernel_direct)
+  static const bool no_direct = getenv("PGPU_NO_DIRECT") && atoi(getenv("PGPU_NO_DIRECT")) != 0;
+  p.direct = 0;
+  if (!no_direct && !p.dense && p.mode != PGPU_MODE_PART && pk.tile_bytes > 0) {
+    bool ok = true;
+    for (const DevSeg& ds : pk.segs)
+      ok &= ds.ntiles == 0 || (ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1 &&
+                               (ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE));
+    // up to five 4-wave workgroups per CU (more waves hide the per-tile latency better than deeper prefetch, which
+    // measured flat); each wave keeps D - 1 tiles in flight, aiming at ~12 KiB (HBM latency
+    // x per-CU bandwidth), within the 6-bit vmcnt and the LDS
+    int max_instrs = 1, min_instrs = 64;
+    for (const DevSeg& ds : pk.segs)
+      if (ds.ntiles) {
+        max_instrs = std::max(max_instrs, ds.stage_instrs);
+        min_instrs = std::min(min_instrs, ds.stage_instrs);
+      }
+    int D = (int)std::max<int64_t>(2, std::min<int64_t>(8, 1 + (12 * 1024 + pk.tile_bytes - 1) / std::max<int64_t>(1, pk.tile_bytes)));
+    D = std::min(D, 1 + 63 / max_instrs);
+    static const int env_slots = getenv("PGPU_DIRECT_SLOTS") ? atoi(getenv("PGPU_DIRECT_SLOTS")) : 0;
+    static const int env_wgs = getenv("PGPU_DIRECT_WGS") ? atoi(getenv("PGPU_DIRECT_WGS")) : 0;  // per CU
+    if (env_slots >= 2) D = std::min(env_slots, 1 + 63 / max_instrs);
+    const int wgs = env_wgs >= 1 ? env_wgs : 5;  // as many 4-wave workgroups as LDS and VGPRs allow (<= 20 waves)
+    auto ddyn_of = [&](int d) { return (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + (size_t)4 * d * S; };
+    while (D > 2 && wgs * ddyn_of(D) > PGPU_LDS_LIMIT) --D;
+    const size_t ddyn = ddyn_of(D);
+    if (ok && D >= 2 && ddyn <= PGPU_LDS_LIMIT) {
+      const int per_cu = (int)std::min<size_t>(wgs, PGPU_LDS_LIMIT / ddyn);
+      int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
+      if (g >= 8) g &= ~7;
+      p.direct = 1;
+      p.dslots = D;
+      p.min_instrs = std::max(1, min_instrs);
+      grid = std::max(1, g);
+      dyn = ddyn;
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->lds_ready) {
@@ -1343,7 +1382,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       ctx->lds_ready = true;
     }
   }
-  const int nwaves = grid * PGPU_WAVES_OF(p.dense);
+  const int nwaves = grid * (p.direct ? 4 : PGPU_WAVES_OF(p.dense));
 
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
@@ -1427,7 +1466,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
-  if (e == hipSuccess) e = pgpu_launch_query(p, grid, dyn, st);
+  if (e == hipSuccess) e = p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st);
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
@@ -1471,13 +1510,13 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
   if (qq->params.flags & PGPU_FLAG_PROFILE) {
-    const int nw = qq->grid * PGPU_WAVES_OF(qq->params.dense);
+    const int nw = qq->grid * (qq->params.direct ? 4 : PGPU_WAVES_OF(qq->params.dense));
     std::vector<int64_t> pr((size_t)nw * PGPU_NPROF);
     HIP_TRY(hipMemcpy(pr.data(), qq->params.prof, pr.size() * 8, hipMemcpyDeviceToHost));
     double sum[PGPU_NPROF] = {0};
     int nl = 0, nc = 0;
     for (int w = 0; w < nw; ++w) {
-      const bool ld = (w % PGPU_WAVES_OF(qq->params.dense)) < PGPU_NLOAD_OF(qq->params.dense);
+      const bool ld = !qq->params.direct && (w % PGPU_WAVES_OF(qq->params.dense)) < PGPU_NLOAD_OF(qq->params.dense);
       ld ? ++nl : ++nc;
       for (int k = 0; k < PGPU_NPROF; ++k) sum[k] += (double)pr[(size_t)w * PGPU_NPROF + k];
     }
