@@ -1024,13 +1024,14 @@ FI uint32_t sliced_ranges(int bits, const uint32_t* region, const DevSeg* sg, in
   return m;
 }
 
-FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) {
+// The scanned-entries count stays per lane (reduced once per wave at the end) and the empty-tile exit is a ballot:
+// a tile costs no cross-lane reduction here.
+FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, uint32_t& lane_scanned) {
   uint32_t m = t.valid;
 #pragma unroll 1
   for (int j = 0; j < ss.fast; ++j) {
-    const int n = wave_sum_i32(__popc(m));
-    if (n == 0) return 0u;
-    if (lane_id() == 0) scanned += n;
+    if (j > 0 && __builtin_amdgcn_ballot_w64(m != 0) == 0) return 0u;
+    lane_scanned += __popc(m);
     const int bits = j ? ss.f_bits[1] : ss.f_bits[0];
     const int off = j ? ss.f_off[1] : ss.f_off[0];
     const int kind = j ? ss.f_kind[1] : ss.f_kind[0];
@@ -1057,24 +1058,6 @@ FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, int64_t& scanned) 
       for (int i = 31; i >= 0; --i) r = (r << 1) | (uint32_t)((ids[i] - lo) < span);
     }
     m &= neg ? ~r : r;
-  }
-  return m;
-}
-
-// Direct-kernel form of fast_filter: the scanned-entries count stays per lane (reduced once per wave at the end)
-// and the empty-tile exit is a ballot, so a tile costs no cross-lane reduction.
-FI uint32_t fast_filter_lean(const SegState& ss, const TileCtx& t, uint32_t& lane_scanned) {
-  uint32_t m = t.valid;
-#pragma unroll 1
-  for (int j = 0; j < ss.fast; ++j) {
-    if (j > 0 && __builtin_amdgcn_ballot_w64(m != 0) == 0) return 0u;
-    lane_scanned += __popc(m);
-    const int bits = j ? ss.f_bits[1] : ss.f_bits[0];
-    const int off = j ? ss.f_off[1] : ss.f_off[0];
-    const int nr = j ? ss.f_nr[1] : ss.f_nr[0];
-    const uint32_t r = sliced_ranges(bits, (const uint32_t*)(t.slot + off), ss.sg, j, nr,
-                                     j ? ss.f_r0lo[1] : ss.f_r0lo[0], j ? ss.f_r0hi[1] : ss.f_r0hi[0]);
-    m &= (j ? ss.f_sneg[1] : ss.f_sneg[0]) ? ~r : r;
   }
   return m;
 }
@@ -1505,6 +1488,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
   wave_sync();
   int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  uint32_t lane_scanned = 0;  // fast-path scanned entries, per lane (reduced at the end)
   LaneAcc la;
 #pragma unroll
   for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
@@ -1586,7 +1570,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
         }
     }
     uint32_t mm = t.valid;
-    if (ss.fast) mm = fast_filter(ss, t, scanned);
+    if (ss.fast) mm = fast_filter(ss, t, lane_scanned);
     else if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
     const int nm = wave_sum_i32(__popc(mm));
     PROF_ADD(pf, PGPU_P_C_FILTER, tf);
@@ -1656,6 +1640,10 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     PROF_ADD(pf, PGPU_P_C_AGG, ta);
   }
   PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  {
+    const int64_t ls = wave_sum_i64((int64_t)lane_scanned);
+    if (lane == 0) scanned += ls;
+  }
   if (MODE == PGPU_MODE_AGG) {
 #pragma unroll
     for (int a = 0; a < NREG_ACC; ++a)
@@ -1791,7 +1779,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
             if (lane == 0) dense_bytes += ((int64_t)ndocs * b + 7) / 8;
           }
       }
-      const uint32_t mm = fast_filter_lean(ss, t, lane_scanned);
+      const uint32_t mm = fast_filter(ss, t, lane_scanned);
       // the slot's planes have been read (lgkmcnt): it is rewritten by the issue of tile k + D, after this point
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);
