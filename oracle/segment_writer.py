@@ -285,3 +285,70 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
             col.inverted = inverted_index_bytes(ids, card, allow_runs)
         seg.columns[cname] = col
     return seg
+
+
+# ---- on-disk segment directories (test infrastructure: feeds pinot_amd.loader) ---------------------------------
+_TYPE_NAME = {PGPU_INT: "INT", PGPU_LONG: "LONG", PGPU_FLOAT: "FLOAT", PGPU_DOUBLE: "DOUBLE", PGPU_STRING: "STRING"}
+_MAGIC = 0xDEADBEEFDEAFBEAD
+
+
+def string_dictionary_bytes(values: Sequence[str], pad: bytes = b"\0"):
+    """Fixed-width STRING dictionary: every value padded to the longest UTF-8 length
+    (SegmentDictionaryCreator.java:92-156 with the segment's padding character)."""
+    enc = [v.encode("utf-8") for v in values]
+    width = max([len(b) for b in enc] + [1])
+    return b"".join(b + pad * (width - len(b)) for b in enc), width
+
+
+def write_segment_dir(seg: SegmentData, path: str, version: str = "v3", pad_char: str = "\0") -> str:
+    """Write `seg` as a Pinot segment directory: metadata.properties plus either v1 files per index
+    (V1Constants.Indexes extensions) or v3 columns.psf + index_map, each index behind the 8-byte magic marker
+    (SingleFileIndexDirectory.allocNewBufferInternal :164-184, persistIndexMap :446-465).  Returns the
+    directory holding metadata.properties."""
+    import os
+    os.makedirs(path, exist_ok=True)
+    root = os.path.join(path, "v3") if version == "v3" else path
+    os.makedirs(root, exist_ok=True)
+    pad = pad_char.encode("utf-8")
+    pad_text = "\\\\u0000" if pad_char == "\0" else pad_char
+    meta = [f"segment.name = {seg.name}", "segment.table.name = testTable", f"segment.total.docs = {seg.num_docs}",
+            f"segment.padding.character = {pad_text}", f"segment.index.version = {version}"]
+    indexes = []  # (column, index name, v1 extension, bytes)
+    for c in seg.columns.values():
+        if c.data_type == PGPU_STRING:
+            dbytes, width = string_dictionary_bytes(list(c.dictionary), pad)
+        else:
+            dbytes, width = bytes(c.dictionary), 0
+        sorted_col = c.sorted_index is not None
+        meta += [f"column.{c.name}.cardinality = {c.cardinality}", f"column.{c.name}.totalDocs = {seg.num_docs}",
+                 f"column.{c.name}.dataType = {_TYPE_NAME[c.data_type]}",
+                 f"column.{c.name}.bitsPerElement = {bits_per_value(c.cardinality)}",
+                 f"column.{c.name}.lengthOfEachEntry = {width}",
+                 f"column.{c.name}.isSorted = {'true' if sorted_col else 'false'}",
+                 f"column.{c.name}.hasDictionary = true",
+                 f"column.{c.name}.hasInvertedIndex = {'true' if c.inverted is not None else 'false'}",
+                 f"column.{c.name}.isSingleValues = true"]
+        indexes.append((c.name, "dictionary", ".dict", dbytes))
+        if sorted_col:
+            indexes.append((c.name, "forward_index", ".sv.sorted.fwd", bytes(c.sorted_index)))
+        else:
+            indexes.append((c.name, "forward_index", ".sv.unsorted.fwd", bytes(c.forward)))
+        if c.inverted is not None:
+            indexes.append((c.name, "inverted_index", ".bitmap.inv", bytes(c.inverted)))
+    with open(os.path.join(root, "metadata.properties"), "w") as f:
+        f.write("\n".join(meta) + "\n")
+    if version == "v3":
+        off, lines = 0, []
+        with open(os.path.join(root, "columns.psf"), "wb") as f:
+            for col, idx, _, data in indexes:
+                f.write(struct.pack(">Q", _MAGIC))
+                f.write(data)
+                lines += [f"{col}.{idx}.startOffset = {off}", f"{col}.{idx}.size = {len(data) + 8}"]
+                off += len(data) + 8
+        with open(os.path.join(root, "index_map"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+    else:
+        for col, _, ext, data in indexes:
+            with open(os.path.join(root, col + ext), "wb") as f:
+                f.write(data)
+    return root

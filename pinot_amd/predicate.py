@@ -44,12 +44,22 @@ def _key(value: str, data_type: int):
 
 class SortedDictionary:
     """Sorted dictionary values with the reference's binary-search contract (numpy searchsorted for numeric
-    dictionaries, bisect for strings)."""
+    dictionaries, bisect for strings).
 
-    def __init__(self, values: Union[np.ndarray, Sequence[str]], data_type: int):
+    STRING dictionaries of segments written with a non-zero padding character (the legacy '%') are searched on
+    padded values with the literal padded the same way, as BaseImmutableDictionary.binarySearch / padString do
+    (seglocal/segment/index/readers/BaseImmutableDictionary.java:211-285); with '\\0' padding the unpadded values
+    are compared directly."""
+
+    def __init__(self, values: Union[np.ndarray, Sequence[str]], data_type: int, pad_char: str = "\0",
+                 entry_width: int = 0):
         self.data_type = data_type
+        self._pad = None
         if data_type == PGPU_STRING:
             self.values = list(values)
+            if pad_char != "\0" and entry_width > 0:
+                self._pad = (pad_char.encode("utf-8")[:1], entry_width)
+                self._search = [self._padded(v) for v in self.values]
         elif data_type in (PGPU_INT, PGPU_LONG):
             self.values = np.asarray(values, dtype=np.int64)
         else:
@@ -59,12 +69,20 @@ class SortedDictionary:
     def __len__(self) -> int:
         return self._n
 
+    def _padded(self, v: str) -> str:
+        pad, width = self._pad
+        b = v.encode("utf-8")
+        return (b + pad * (width - len(b))).decode("utf-8") if len(b) < width else v
+
     def insertion_index_of(self, literal: str) -> int:
         """>= 0: index of an exact match; < 0: -(insertion point + 1)."""
         k = _key(literal, self.data_type)
         if self.data_type == PGPU_STRING:
-            i = bisect.bisect_left(self.values, k)
-            found = i < self._n and self.values[i] == k
+            vals = self.values
+            if self._pad is not None:
+                vals, k = self._search, self._padded(k)
+            i = bisect.bisect_left(vals, k)
+            found = i < self._n and vals[i] == k
         elif isinstance(k, Fraction):  # fractional literal on an integer dictionary: never equal
             i = int(self.values.searchsorted(float(k), side="left"))
             found = False

@@ -50,6 +50,8 @@ class ColumnIndexes:
     inverted: Optional[bytes] = None
     forward_device: Optional[int] = None     # device pointer alternative to `forward` (PGPU_MEM_DEVICE)
     forward_device_bytes: int = 0
+    pad_char: str = "\0"                    # STRING dictionaries: segment.padding.character (legacy '%')
+    entry_width: int = 0                     # STRING dictionaries: lengthOfEachEntry (bytes per padded value)
 
     @property
     def bits_per_value(self) -> int:
@@ -213,7 +215,9 @@ class GpuSegment:
         d = cache.get(name)
         if d is None:
             from .predicate import SortedDictionary
-            d = SortedDictionary(self.dictionaries[name], self.column(name).data_type)
+            col = self.column(name)
+            d = SortedDictionary(self.dictionaries[name], col.data_type, pad_char=col.pad_char,
+                                 entry_width=col.entry_width)
             cache[name] = d
         return d
 
