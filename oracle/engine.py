@@ -597,6 +597,8 @@ class OracleResult:
 def execute(query: QueryContext, segments: Sequence[SegmentData], num_groups_limit: int = 100_000,
             max_init_group_holder_capacity: int = 10_000, iterator_stats: bool = False) -> OracleResult:
     """All segments of one server + the broker reduce (no group trimming)."""
+    if query.has_filtered_aggregations:
+        return _execute_filtered(query, segments, num_groups_limit, max_init_group_holder_capacity, iterator_stats)
     fns = [a.function for a in query.aggregations]
     out = OracleResult()
     decoded: Dict[int, DecodedSegment] = {}
@@ -632,4 +634,27 @@ def execute(query: QueryContext, segments: Sequence[SegmentData], num_groups_lim
     for r in ordered:
         sel.append(tuple(r[names.index(s if isinstance(s, str) else s.result_name)] for s in query.select))
     out.rows = sel
+    return out
+
+
+def _execute_filtered(query: QueryContext, segments, num_groups_limit, max_init, iterator_stats) -> OracleResult:
+    """FilteredAggregationOperator (core/operator/query/FilteredAggregationOperator.java:62-95) over the passes of
+    AggregationPlanNode.buildFilterOperatorInternal (:102-145): one per FILTER clause (main AND clause), then the
+    main filter; per-segment sums equal the sums over all segments, so the passes run server-wide."""
+    from pinot_amd.query import split_filtered_aggregations
+    out = OracleResult()
+    n = len(query.aggregations)
+    fin, inter = [None] * n, [None] * n
+    for sq, idx in split_filtered_aggregations(query):
+        r = execute(sq, segments, num_groups_limit, max_init, iterator_stats)
+        for j, i in enumerate(idx):
+            fin[i] = r.aggregation_result[j]
+            inter[i] = r.intermediate[()][j]
+        out.num_docs_scanned += r.num_docs_scanned
+        out.num_entries_scanned_in_filter += r.num_entries_scanned_in_filter
+        out.num_entries_scanned_post_filter += r.num_entries_scanned_post_filter
+        out.num_total_docs = r.num_total_docs
+    out.aggregation_result = fin
+    out.intermediate = {(): inter}
+    out.rows = [tuple(fin[query.aggregations.index(s)] for s in query.select)]
     return out

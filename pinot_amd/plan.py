@@ -35,7 +35,7 @@ from ._lib import (ExprNode, Literal, PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX
                    PGPU_RED_SUM_I64, PGPU_STRING, Agg, FilterNode, QueryDesc, QueryStats, SegmentPlan, TableLayout,
                    UnsupportedPlanError)
 from .predicate import DictPredicateEvaluator, SortedDictionary, get_predicate_evaluator
-from .query import UNBOUNDED, FilterContext, QueryContext
+from .query import UNBOUNDED, FilterContext, QueryContext, split_filtered_aggregations
 from .segment import GpuContext, GpuSegment
 
 AGG_FN = {"COUNT": PGPU_AGG_COUNT, "SUM": PGPU_AGG_SUM, "MIN": PGPU_AGG_MIN, "MAX": PGPU_AGG_MAX,
@@ -503,6 +503,9 @@ class GpuPlanMaker:
     def submit(self, query: QueryContext, segments: Sequence[GpuSegment]) -> "PendingQuery":
         """Plan the query and enqueue it on the GPU without waiting (pgpu_query_submit).  Several queries may be
         in flight: the host plans the next one while the GPU runs this one."""
+        if query.has_filtered_aggregations:
+            raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                            "filtered aggregations run one pass per FILTER clause: use execute()")
         expr = self.filter_expr(query, segments)
         desc, keep, globals_ = self.build_desc(query, segments, plan_filters=expr is None)
         L = self.layout(desc)
@@ -537,6 +540,10 @@ class GpuPlanMaker:
         return finish(query, table, [g[0] for g in pending.globals_], stats)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
+        if query.has_filtered_aggregations:
+            parts = split_filtered_aggregations(query)
+            pending = [self.submit(sq, segments) for sq, _ in parts]  # all in flight, then collected in order
+            return merge_filtered(query, parts, [self.collect(pq) for pq in pending])
         return self.collect(self.submit(query, segments))
 
 
@@ -591,6 +598,29 @@ def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats
     cols = GroupColumns(query, table, global_dicts)
     res._columns = cols
     res.rows = [to_select_order(query, r) for r in cols.rows(cols.order_and_limit())]
+    return res
+
+
+def merge_filtered(query: QueryContext, parts, results: Sequence[QueryResult]) -> QueryResult:
+    """FilteredAggregationOperator.getNextBlock (core/operator/query/FilteredAggregationOperator.java:62-95):
+    results placed back in aggregation order; docs scanned and entries scanned summed over every filter pass
+    (the main pass included); numTotalDocs once."""
+    res = QueryResult(query=query, stats=ExecutionStats())
+    fin: List = [None] * len(query.aggregations)
+    inter: List = [None] * len(query.aggregations)
+    st = res.stats
+    for (_, idx), r in zip(parts, results):
+        for j, i in enumerate(idx):
+            fin[i] = r.aggregation_result[j]
+            inter[i] = r.intermediate[()][j]
+        for f in ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
+                  "kernel_ms", "sparse_sector_bytes", "dense_bytes"):
+            setattr(st, f, getattr(st, f) + getattr(r.stats, f))
+    st.num_total_docs = results[-1].stats.num_total_docs
+    st.num_segments_processed = results[-1].stats.num_segments_processed
+    res.aggregation_result = fin
+    res._intermediate = {(): inter}
+    res.rows = [to_select_order(query, tuple(fin))]
     return res
 
 

@@ -48,10 +48,12 @@ class FilterContext:
 class AggregationSpec:
     function: str        # COUNT, SUM, MIN, MAX, AVG
     column: Optional[str]  # None for COUNT(*)
+    filter_key: Optional[str] = None  # FILTER(WHERE ...) clause text; its FilterContext is QueryContext.agg_filters
 
     @property
     def result_name(self) -> str:
-        return f"{self.function.lower()}({self.column if self.column else '*'})"
+        name = f"{self.function.lower()}({self.column if self.column else '*'})"
+        return name if self.filter_key is None else f"{name} FILTER(WHERE {self.filter_key})"
 
 
 @dataclass(frozen=True)
@@ -70,6 +72,12 @@ class QueryContext:
     order_by: List[OrderByExpr] = field(default_factory=list)
     limit: int = 10
     options: dict = field(default_factory=dict)
+    agg_filters: dict = field(default_factory=dict)  # filter_key -> FilterContext (QueryContext._filteredAggregations)
+
+    @property
+    def has_filtered_aggregations(self) -> bool:
+        """QueryContext.isHasFilteredAggregations (core/query/request/context/QueryContext.java)."""
+        return any(a.filter_key is not None for a in self.aggregations)
 
     @property
     def columns(self) -> List[str]:
@@ -89,6 +97,8 @@ class QueryContext:
                 walk(ch)
 
         walk(self.filter)
+        for f in self.agg_filters.values():
+            walk(f)
         for a in self.aggregations:
             add(a.column)
         for g in self.group_by:
@@ -133,6 +143,7 @@ class _Parser:
             self.toks.append((kind, val))
             pos = m.end()
         self.i = 0
+        self.agg_filters: dict = {}
 
     def peek(self, k=0):
         j = self.i + k
@@ -187,7 +198,17 @@ class _Parser:
             self.expect_op(")")
             if fn != "COUNT" and col is None:
                 raise SqlError(f"{fn}(*) is not supported")
-            return AggregationSpec(fn, None if fn == "COUNT" else col)
+            key = None
+            if self.kw("FILTER"):  # AGG(col) FILTER(WHERE <filter>)
+                self.expect_op("(")
+                self.expect_kw("WHERE")
+                start = self.i
+                f = self.bool_expr()
+                key = " ".join(v if k != "str" else "'" + v.replace("'", "''") + "'"
+                               for k, v in self.toks[start:self.i])
+                self.expect_op(")")
+                self.agg_filters[key] = f
+            return AggregationSpec(fn, None if fn == "COUNT" else col, key)
         return self.ident()
 
     def order_item(self) -> OrderByExpr:
@@ -316,5 +337,36 @@ def parse_sql(sql: str, **options) -> QueryContext:
     for s in select:
         if isinstance(s, str) and s not in group_by:
             raise SqlError(f"column {s} must appear in GROUP BY")
+    if p.agg_filters and group_by:
+        # filtered aggregations are planned by AggregationPlanNode only (AggregationPlanNode.java:81-145)
+        raise SqlError("FILTER(WHERE ...) aggregations are supported for aggregation-only queries")
     return QueryContext(table=table, select=select, aggregations=aggs, filter=filt, group_by=group_by,
-                        order_by=order_by, limit=limit, options=dict(options))
+                        order_by=order_by, limit=limit, options=dict(options), agg_filters=dict(p.agg_filters))
+
+
+def split_filtered_aggregations(q: QueryContext) -> List[Tuple[QueryContext, List[int]]]:
+    """One sub-query per distinct FILTER clause (WHERE = main AND clause, the CombinedFilterOperator), then the
+    main-filter query holding the non-filtered aggregations -- always run, even when it holds none, since its
+    matched docs count in numDocsScanned (AggregationPlanNode.buildFilterOperatorInternal :102-145,
+    FilteredAggregationOperator.getNextBlock :62-95).  Returns (sub-query, indices into q.aggregations)."""
+    groups: dict = {}
+    plain: List[int] = []
+    for i, a in enumerate(q.aggregations):
+        if a.filter_key is None:
+            plain.append(i)
+        else:
+            groups.setdefault(a.filter_key, []).append(i)
+
+    def sub(filt, idx):
+        aggs = [AggregationSpec(q.aggregations[i].function, q.aggregations[i].column) for i in idx]
+        if not aggs:
+            aggs = [AggregationSpec("COUNT", None)]
+        return QueryContext(table=q.table, select=list(aggs), aggregations=aggs, filter=filt, limit=q.limit,
+                            options=dict(q.options))
+
+    out = []
+    for key, idx in groups.items():
+        f = q.agg_filters[key]
+        out.append((sub(f if q.filter is None else FilterContext("AND", [q.filter, f]), idx), idx))
+    out.append((sub(q.filter, plain), plain))
+    return out
