@@ -22,8 +22,8 @@ import numpy as np
 from . import _lib
 from ._lib import (PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, QueryStats,
                    TableLayout)
-from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, finish
-from .query import QueryContext
+from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, finish, merge_filtered
+from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
 
@@ -167,6 +167,12 @@ class DistributedExecutor:
             self._tables.setdefault(int(table.numel()), []).append(table)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
+        if query.has_filtered_aggregations:
+            # one reduced pass per FILTER clause plus the main pass (FilteredAggregationOperator), merged on rank 0
+            parts = split_filtered_aggregations(query)
+            pending = [self.submit(sq, segments) for sq, _ in parts]
+            results = [self.collect(pq) for pq in pending]
+            return None if results[0] is None else merge_filtered(query, parts, results)
         return self.collect(self.submit(query, segments))
 
 

@@ -142,8 +142,10 @@ def _partial_table(query, rows, glob, L):
     from pinot_amd.query import UNBOUNDED
     x = rows["x"][1]
     mask = np.ones(len(x), dtype=bool)
-    f = query.filter
-    preds = [f] if f.type == "PREDICATE" else f.children
+    def leaves(f):  # conjunctions of range predicates on x (filtered-aggregation passes nest one AND)
+        return [f] if f.type == "PREDICATE" else [x for c in f.children for x in leaves(c)]
+
+    preds = leaves(query.filter) if query.filter is not None else []
     for p in preds:
         pr = p.predicate
         lo = -np.inf if pr.lower == UNBOUNDED else float(pr.lower)
@@ -242,3 +244,43 @@ def _e2e_worker(rank, sql):
 @pytest.mark.parametrize("sql", [SQL_GB, SQL_AGG], ids=["groupby", "aggregation"])
 def test_partial_tables_merge_like_reference_combine(sql):
     _spawn(_e2e_worker, sql)
+
+
+SQL_FILTERED = ("SELECT SUM(m) FILTER(WHERE x < 40), COUNT(*) FILTER(WHERE x >= 70), MAX(d), SUM(d) "
+                "FROM t WHERE x > 10")
+
+
+def _filtered_worker(rank, sql):
+    """Filtered aggregations across ranks: every pass (FILTER clauses, then the main filter) is reduced like the
+    unfiltered combine, then merged as FilteredAggregationOperator does -- DistributedExecutor.execute's shape."""
+    from oracle import engine
+    from oracle.segment_writer import build_segment
+    from pinot_amd.combine import reduce_sections
+    from pinot_amd.plan import ExecutionStats, GroupTable, finish, merge_filtered
+    from pinot_amd.query import parse_sql, split_filtered_aggregations
+    from tests.helpers import close
+
+    q = parse_sql(sql)
+    rows = _rank_rows(rank)
+    parts = split_filtered_aggregations(q)
+    results = []
+    for sq, _ in parts:
+        L = _layout_for(sq, 1)
+        t = torch.from_numpy(_partial_table(sq, rows, None, L).reshape(-1).copy())
+        reduce_sections(t, L)
+        cells = t.numpy().reshape(L.num_sections, 1).T
+        gt = GroupTable(np.array([0], dtype=np.int64), np.ascontiguousarray(cells), L)
+        results.append(finish(sq, gt, [], ExecutionStats(num_docs_scanned=int(cells[0, 0]), num_total_docs=3000 * WORLD)))
+    res = merge_filtered(q, parts, results)
+    if rank != 0:
+        return
+    segs = [build_segment(f"seg{r}", _rank_rows(r)) for r in range(WORLD)]
+    ref = engine.execute(q, segs)
+    assert all(close(u, v) for u, v in zip(res.aggregation_result, ref.aggregation_result)), \
+        (res.aggregation_result, ref.aggregation_result)
+    assert res.stats.num_docs_scanned == ref.num_docs_scanned
+    assert res.stats.num_total_docs == ref.num_total_docs
+
+
+def test_filtered_aggregations_merge_across_ranks():
+    _spawn(_filtered_worker, SQL_FILTERED)

@@ -174,3 +174,15 @@ def test_filtered_submit_rejected(gpu_ctx, gsegs):
     from pinot_amd.plan import GpuPlanMaker
     with pytest.raises(UnsupportedPlanError):
         GpuPlanMaker(gpu_ctx).submit(parse_sql(PAIRS[0][0]), gsegs)
+
+
+@pytest.mark.gpu
+def test_filtered_aggregations_distributed_executor_gpu(gpu_ctx, segs, gsegs):
+    """DistributedExecutor (world size 1 here; the N-rank merge is covered by test_combine_gloo)."""
+    from pinot_amd.combine import DistributedExecutor
+    from pinot_amd.plan import GpuPlanMaker
+    sql = MIXED[3][0]
+    res = DistributedExecutor(GpuPlanMaker(gpu_ctx)).execute(parse_sql(sql), gsegs)
+    ref = engine.execute(parse_sql(sql), segs)
+    _same_values(_vals(res), _vals(ref))
+    assert res.stats.num_docs_scanned == ref.num_docs_scanned
