@@ -521,6 +521,14 @@ def final(fn: str, v):
     return float(v)
 
 
+def fits_non_scan(query: QueryContext, num_docs: int) -> bool:
+    """AggregationPlanNode.isFitForNonScanBasedPlan (core/plan/AggregationPlanNode.java:234-262) for the functions
+    this path serves: aggregation-only, no FILTER clauses, only COUNT / MIN / MAX (dictionary-encoded columns).
+    Empty segments are left to the scan plan (their dictionaries hold no min / max)."""
+    return (not query.group_by and not query.has_filtered_aggregations and num_docs > 0
+            and all(a.function in ("COUNT", "MIN", "MAX") for a in query.aggregations))
+
+
 @dataclass
 class SegmentResult:
     aggregation: Optional[list] = None               # intermediate values (aggregation only)
@@ -537,6 +545,17 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
     ds = seg if isinstance(seg, DecodedSegment) else DecodedSegment(seg)
     n = ds.num_docs
     op = build_physical(ds, query.filter)
+    if op.kind == "ALL" and fits_non_scan(query, n):
+        # NonScanBasedAggregationOperator (core/operator/query/NonScanBasedAggregationOperator.java:85-101,253-256):
+        # COUNT from metadata, MIN / MAX from the dictionary's first / last value; stats (total, 0, 0, total)
+        agg = []
+        for a in query.aggregations:
+            if a.function == "COUNT":
+                agg.append(n)
+            else:
+                d = ds.dictionary(a.column)
+                agg.append(float(d[0] if a.function == "MIN" else d[-1]))
+        return SegmentResult(aggregation=agg, num_docs_scanned=n, num_total_docs=n)
     mask = eval_mask(op, n)
     docs = np.flatnonzero(mask)
     res = SegmentResult(num_docs_scanned=len(docs), num_total_docs=n, matched=docs)

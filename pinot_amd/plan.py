@@ -544,7 +544,22 @@ class GpuPlanMaker:
             parts = split_filtered_aggregations(query)
             pending = [self.submit(sq, segments) for sq, _ in parts]  # all in flight, then collected in order
             return merge_filtered(query, parts, [self.collect(pq) for pq in pending])
+        non_scan = self.non_scan_segments(query, segments)
+        if any(non_scan):
+            rest = [s for s, ns in zip(segments, non_scan) if not ns]
+            res = self.collect(self.submit(query, rest)) if rest else None
+            return merge_non_scan(query, res, [s for s, ns in zip(segments, non_scan) if ns])
         return self.collect(self.submit(query, segments))
+
+    def non_scan_segments(self, query: QueryContext, segments: Sequence[GpuSegment]) -> List[bool]:
+        """Per segment, AggregationPlanNode.buildNonFilteredAggOperator's choice (core/plan/AggregationPlanNode.java
+        :171-195): a filter that folds to match-all plus only COUNT / MIN / MAX is answered from segment metadata
+        and the dictionary, with no scan (NonScanBasedAggregationOperator)."""
+        q = query
+        if q.group_by or q.has_filtered_aggregations or any(a.function not in ("COUNT", "MIN", "MAX")
+                                                            for a in q.aggregations):
+            return [False] * len(segments)
+        return [s.num_docs > 0 and SegmentFilterPlanner(s).build(q.filter).kind == "ALL" for s in segments]
 
 
 @dataclass
@@ -598,6 +613,33 @@ def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats
     cols = GroupColumns(query, table, global_dicts)
     res._columns = cols
     res.rows = [to_select_order(query, r) for r in cols.rows(cols.order_and_limit())]
+    return res
+
+
+def merge_non_scan(query: QueryContext, scanned: Optional[QueryResult], segments: Sequence[GpuSegment]) -> QueryResult:
+    """Merge the scanned segments' result with the non-scan segments' metadata answers
+    (NonScanBasedAggregationOperator.java:85-101: COUNT = total docs, MIN / MAX = dictionary min / max as double;
+    statistics (numTotalDocs, 0, 0, numTotalDocs) per segment, :253-256)."""
+    res = QueryResult(query=query, stats=ExecutionStats() if scanned is None else scanned.stats)
+    vals = []
+    for ai, a in enumerate(query.aggregations):
+        v = {"COUNT": 0, "MIN": math.inf, "MAX": -math.inf}[a.function] if scanned is None else \
+            scanned.aggregation_result[ai]
+        for s in segments:
+            if a.function == "COUNT":
+                v += s.num_docs
+            else:
+                d = s.dictionaries[a.column]
+                v = min(v, float(d[0])) if a.function == "MIN" else max(v, float(d[-1]))
+        vals.append(v)
+    st = res.stats
+    for s in segments:
+        st.num_docs_scanned += s.num_docs
+        st.num_total_docs += s.num_docs
+        st.num_segments_processed += 1
+    res.aggregation_result = vals
+    res._intermediate = {(): list(vals)}
+    res.rows = [to_select_order(query, tuple(vals))]
     return res
 
 
