@@ -1296,6 +1296,26 @@ FI void dense_agg_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const Se
     if (ag.fn == PGPU_AGG_COUNT) continue;
     const bool r0 = ag.col == ss.reg_col0;
     const DevColumn c = col_of(ss, ag.col);
+    if (ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64) {
+      // dictionaries are sorted ascending and the MIN / MAX cell key is order-preserving, so the extreme value
+      // sits at the extreme dict id: reduce the ids in registers, then gather one value per lane
+      const bool is_min = ag.op == PGPU_RED_MIN_I64;
+      uint32_t best = is_min ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t id = r0 ? ra[i] : rb[i];
+        if (lane_bit(mm, i)) best = is_min ? min(best, id) : max(best, id);
+      }
+      int64_t part = sec_identity(ag.op);
+      if (mm) {  // lanes without survivors keep the identity (and never index with the sentinel id)
+        const uint32_t idx[1] = {best};
+        int64_t v[1];
+        gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+        part = v[0];
+      }
+      lacc_add(la, cv, a, ag.op, part);  // wave-uniform call: acc_commit reduces across the wave
+      continue;
+    }
     {
       int k = off;
 #pragma unroll

@@ -29,7 +29,7 @@ def main():
             r = pm.execute(q, segs)
             ks.append(r.stats.kernel_ms)
         k = sorted(ks)[len(ks) // 2]
-        print(f"{k:8.3f} ms  {rows / k / 1e6:8.1f} Grows/s  matched {r.stats.num_docs_scanned:>11}  | {sql}", flush=True)
+        print(f"{k:8.3f} ms  {rows / max(k, 1e-9) / 1e6:8.1f} Grows/s  matched {r.stats.num_docs_scanned:>11}  | {sql}", flush=True)
     ctx.close()
 
 
