@@ -91,10 +91,30 @@ def _lit(v: str, dt: int):
     return float(v)
 
 
-def _truth_on_dictionary(d, dt: int, p: Predicate) -> np.ndarray:
-    """Predicate truth per dictionary value, with SQL comparison semantics on the value."""
+def _padder(pad_char: str, width: int):
+    """BaseImmutableDictionary.padString (seglocal/segment/index/readers/BaseImmutableDictionary.java:272-285):
+    segments written with a non-zero padding character (legacy '%') compare padded values."""
+    if pad_char == "\0" or width <= 0:
+        return None
+    pb = pad_char.encode("utf-8")[:1]
+
+    def pad(v: str) -> str:
+        b = v.encode("utf-8")
+        return (b + pb * (width - len(b))).decode("utf-8") if len(b) < width else v
+    return pad
+
+
+def _truth_on_dictionary(d, dt: int, p: Predicate, pad=None) -> np.ndarray:
+    """Predicate truth per dictionary value, with SQL comparison semantics on the value (on padded values and
+    literals for legacy-padded STRING dictionaries, `pad`)."""
     if dt == PGPU_STRING:
         vals = list(d)
+        if pad is not None:
+            vals = [pad(v) for v in vals]
+            p = Predicate(p.type, p.column, tuple(pad(x) for x in p.values),
+                          lower=p.lower if p.lower == UNBOUNDED else pad(p.lower),
+                          upper=p.upper if p.upper == UNBOUNDED else pad(p.upper),
+                          lower_inclusive=p.lower_inclusive, upper_inclusive=p.upper_inclusive)
 
         def ok(v):
             if p.type == "EQ":
@@ -161,7 +181,8 @@ def predicate_mask(ds: DecodedSegment, p: Predicate) -> np.ndarray:
     """Boolean per doc: does the doc's value satisfy the predicate (truth per dictionary value, gathered by the
     doc's dict id — value semantics, since the dictionary holds the values)."""
     c = ds.seg.column(p.column)
-    return _truth_on_dictionary(ds.dictionary(p.column), c.data_type, p)[ds.ids(p.column)]
+    pad = _padder(c.pad_char, c.entry_width) if c.data_type == PGPU_STRING else None
+    return _truth_on_dictionary(ds.dictionary(p.column), c.data_type, p, pad)[ds.ids(p.column)]
 
 
 # ---- physical operator tree (restated FilterOperatorUtils) ------------------------------------------------------
@@ -212,7 +233,8 @@ def build_physical(ds: DecodedSegment, f: Optional[FilterContext]) -> POp:
     col = ds.seg.column(p.column)
     # alwaysTrue / alwaysFalse are decided on the dictionary (every dict value matches / none does)
     d = ds.dictionary(p.column)
-    truth_card = int(np.count_nonzero(_truth_on_dictionary(d, col.data_type, p)))
+    pad = _padder(col.pad_char, col.entry_width) if col.data_type == PGPU_STRING else None
+    truth_card = int(np.count_nonzero(_truth_on_dictionary(d, col.data_type, p, pad)))
     if truth_card == 0:
         return POp("EMPTY")
     if truth_card == len(d):

@@ -205,3 +205,42 @@ def test_loaded_segments_gpu_vs_oracle(gpu_ctx, tmp_path, version):
             assert res.stats.num_docs_scanned == ref.num_docs_scanned
         finally:
             g.release()
+
+
+# ---- queries over the real 5-doc padding segments (string predicates under both padding conventions) ------------
+PAD_QUERIES = ["SELECT COUNT(*), MAX(age), MIN(percent) FROM t WHERE name = 'lynda'",
+               "SELECT COUNT(*), SUM(age) FROM t WHERE name = 'lynda%'",
+               "SELECT COUNT(*), SUM(age) FROM t WHERE name IN ('lynda 2.0', 'lynda%%')",
+               "SELECT COUNT(*), SUM(outgoingName1) FROM t WHERE name > 'lynda'",
+               "SELECT name, COUNT(*), SUM(age) FROM t GROUP BY name ORDER BY name LIMIT 10"]
+
+
+@pytest.mark.parametrize("name", ["paddingNull", "paddingOld"])
+@pytest.mark.parametrize("sql", PAD_QUERIES)
+def test_padding_segment_queries_oracle(tmp_path, name, sql):
+    """The oracle's string predicates follow the segment's padding (padded compare for the legacy '%')."""
+    seg = load_segment(_padding_dir(tmp_path, name))
+    r = engine.execute(parse_sql(sql), [seg])
+    if sql == PAD_QUERIES[1]:
+        # LoaderTest: indexOf("lynda%") == 1 with '%' padding; with '\0' padding "lynda%" is not in the dictionary
+        assert r.num_docs_scanned == (0 if name == "paddingNull" else r.num_docs_scanned)
+        if name == "paddingOld":
+            assert r.num_docs_scanned == engine.execute(parse_sql(PAD_QUERIES[0]), [seg]).num_docs_scanned > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["paddingNull", "paddingOld", "paddingPercent"])
+def test_padding_segment_queries_gpu(gpu_ctx, tmp_path, name):
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    seg = load_segment(_padding_dir(tmp_path, name))
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        for sql in PAD_QUERIES:
+            q = parse_sql(sql)
+            res = GpuPlanMaker(gpu_ctx).execute(q, [g])
+            ref = engine.execute(q, [seg])
+            assert rows_close([list(r) for r in res.rows], [list(r) for r in ref.rows]), sql
+            assert res.stats.num_docs_scanned == ref.num_docs_scanned, sql
+    finally:
+        g.release()
