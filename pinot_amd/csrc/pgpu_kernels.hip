@@ -1174,6 +1174,23 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
     gather_ids(colref(c), doc, id);
 #pragma unroll
     for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
+    if (MODE == PGPU_MODE_AGG && (ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64)) {
+      // sorted dictionary + order-preserving cell key: one value gather per lane, at the extreme live id
+      const bool is_min = ag.op == PGPU_RED_MIN_I64;
+      uint32_t best = is_min ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if ((m >> u) & 1u) best = is_min ? min(best, id[u]) : max(best, id[u]);
+      int64_t part = sec_identity(ag.op);
+      if (m) {
+        const uint32_t idx[1] = {best};
+        int64_t v1[1];
+        gather_cells(c.dict, ag.vtype, ag.op, idx, v1);
+        part = v1[0];
+      }
+      lacc_add(la, cv, a, ag.op, part);
+      continue;
+    }
     int64_t v[U];
     gather_cells(c.dict, ag.vtype, ag.op, id, v);
     if (MODE == PGPU_MODE_AGG) {
