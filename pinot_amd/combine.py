@@ -167,6 +167,10 @@ class DistributedExecutor:
             self._tables.setdefault(int(table.numel()), []).append(table)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
+        if self.world == 1:  # single GPU: the plan maker's own plan choice (filtered passes, non-scan segments)
+            res = self.pm.execute(query, segments)
+            self.last_stats = res.stats
+            return res
         if query.has_filtered_aggregations:
             # one reduced pass per FILTER clause plus the main pass (FilteredAggregationOperator), merged on rank 0
             parts = split_filtered_aggregations(query)

@@ -82,3 +82,21 @@ def test_non_scan_kat_segment_gpu(gpu_ctx):
         assert a.stats.num_entries_scanned_post_filter == 0 and a.stats.num_docs_scanned == 2 * seg.num_docs
     finally:
         g.release()
+
+
+@pytest.mark.gpu
+def test_non_scan_distributed_executor_single_gpu(gpu_ctx):
+    from pinot_amd.combine import DistributedExecutor
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    segs = _two_segments()
+    g = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(MIXED)
+        res = DistributedExecutor(GpuPlanMaker(gpu_ctx)).execute(q, g)
+        ref = engine.execute(q, segs)
+        assert all(close(u, v) for u, v in zip(res.aggregation_result, ref.aggregation_result))
+        assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
+    finally:
+        for s in g:
+            s.release()
