@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 1
+#define PGPU_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -177,6 +177,10 @@ typedef struct {
   const int32_t* group_columns;       /* query column indexes, key = sum_j gid_j * prod_{k<j} card_k */
   const int32_t* group_cardinalities; /* global cardinality per group column */
   uint64_t flags;                     /* PGPU_Q_* */
+  /* Docs the partial table is reduced over (the whole node / cluster for a multi-GPU combine); 0 = the docs of
+   * this launch.  Bounds integer SUM cells: with max|dictionary value| x reduce_docs >= 2^62 an INT / LONG SUM
+   * is carried as three exact 21-bit-part sums (see pgpu_table_layout.agg_sum_parts). */
+  int64_t reduce_docs;
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
@@ -186,6 +190,9 @@ typedef struct {
  * partitioned path supports, and shrink its regions so that the spill path runs (tests and tuning). */
 #define PGPU_Q_PARTITION 2ull
 #define PGPU_Q_PART_SPILL 4ull
+/* Carry every INT / LONG SUM / AVG as three 21-bit-part sums whatever the bound says (multi-GPU callers set it
+ * on every rank when any rank's bound needs it, so that all ranks share one table layout). */
+#define PGPU_Q_SUM_SPLIT 8ull
 
 /* ---- partial-result table ----------------------------------------------------------------------------------
  * A query produces a dense table over G = prod(group_cardinalities) keys (G = 1 for aggregation only), laid out
@@ -193,12 +200,19 @@ typedef struct {
  *   section 0                : count      int64, SUM   (docs per key; COUNT(*) and the AVG count)
  *   one section per agg slot : SUM of INT/LONG column   -> int64   SUM (exact; == the reference's double sum
  *                                                                    while |partial sums| < 2^53)
+ *                              ... whose bound max|value| x docs reaches 2^62 (or PGPU_Q_SUM_SPLIT):
+ *                                  three int64 SUM sections s, s+1, s+2 holding the sums of bits [0,21),
+ *                                  [21,42) (unsigned parts) and [42,64) (arithmetic shift) of every value:
+ *                                  SUM = c[s] + c[s+1] * 2^21 + c[s+2] * 2^42, exact for < 2^42 docs
+ *                                  (SumAggregationFunction.java:55-92 adds doubles in doc order and never
+ *                                  wraps; an int64 cell would)
  *                              SUM of FLOAT/DOUBLE      -> float64 SUM
  *                              MIN / MAX                -> int64 MIN / MAX of an order-preserving key
  *                              AVG                      -> as SUM (count comes from section 0)
  *                              COUNT                    -> no section (section 0)
  * pgpu_table_layout describes it; pgpu_decode_minmax_key turns MIN/MAX keys back into doubles.
  */
+#define PGPU_MAX_SECTIONS 17 /* count + 16 value sections (a split SUM takes 3; more than 16 -> UNSUPPORTED) */
 #define PGPU_RED_SUM_I64 0
 #define PGPU_RED_SUM_F64 1
 #define PGPU_RED_MIN_I64 2
@@ -207,9 +221,10 @@ typedef struct {
 typedef struct {
   uint64_t num_keys;       /* G */
   int32_t num_sections;
-  int32_t section_op[17];  /* PGPU_RED_* per section (section 0 = count) */
+  int32_t section_op[PGPU_MAX_SECTIONS]; /* PGPU_RED_* per section (section 0 = count) */
   int32_t agg_section[16]; /* section of agg i, or 0 for COUNT */
   int32_t agg_value_type[16]; /* stored type of the agg column (PGPU_INT..), -1 for COUNT */
+  int32_t agg_sum_parts[16];  /* SUM / AVG of INT / LONG: 1 = one exact int64 section, 3 = 21-bit-part sections */
 } pgpu_table_layout;
 
 int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out);

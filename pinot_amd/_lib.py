@@ -29,7 +29,9 @@ PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
 PGPU_PRED_RANGE, PGPU_PRED_SET = 0, 1
 PGPU_AGG_COUNT, PGPU_AGG_SUM, PGPU_AGG_MIN, PGPU_AGG_MAX, PGPU_AGG_AVG = range(5)
 PGPU_RED_SUM_I64, PGPU_RED_SUM_F64, PGPU_RED_MIN_I64, PGPU_RED_MAX_I64 = range(4)
-PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL = 1, 2, 4
+PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT = 1, 2, 4, 8
+PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
+ABI_VERSION = 2
 
 
 class PinotGpuError(RuntimeError):
@@ -64,12 +66,13 @@ class QueryDesc(C.Structure):
     _fields_ = [("num_columns", C.c_int32), ("num_segments", C.c_int32), ("segments", C.POINTER(SegmentPlan)),
                 ("num_aggs", C.c_int32), ("num_group_columns", C.c_int32), ("aggs", C.POINTER(Agg)),
                 ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
-                ("flags", C.c_uint64)]
+                ("flags", C.c_uint64), ("reduce_docs", C.c_int64)]
 
 
 class TableLayout(C.Structure):
     _fields_ = [("num_keys", C.c_uint64), ("num_sections", C.c_int32), ("section_op", C.c_int32 * 17),
-                ("agg_section", C.c_int32 * 16), ("agg_value_type", C.c_int32 * 16)]
+                ("agg_section", C.c_int32 * 16), ("agg_value_type", C.c_int32 * 16),
+                ("agg_sum_parts", C.c_int32 * 16)]
 
 
 class QueryStats(C.Structure):
@@ -145,7 +148,7 @@ def load(path: str = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.pgpu_abi_version() != 1:
+    if lib.pgpu_abi_version() != ABI_VERSION:
         raise ImportError("libpinotgpu ABI version mismatch")
     _lib = lib
     return lib

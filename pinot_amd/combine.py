@@ -4,13 +4,22 @@ Replaces the host-side merge of the reference — ``AggregationOnlyCombineOperat
 (core/operator/combine/AggregationOnlyCombineOperator.java:47-57) and the ``GroupByOrderByCombineOperator``
 IndexedTable upserts (core/operator/combine/GroupByOrderByCombineOperator.java:127-248) — for segments sharded over
 the GPUs of one node (north_star).  Each rank runs ONE query launch over its own segments and leaves
-a dense partial table in HBM (layout: include/pinot_gpu.h, pgpu_table_layout).  Sections are reduced with one
-collective per reduction op (int64 SUM for counts and integer sums, float64 SUM for double sums, int64 MIN/MAX of
-order-preserving keys), then rank 0 compacts the non-empty keys and finishes ORDER BY / LIMIT.  Doc-id sets never
-leave their GPU; the only exchange is the table (G x sections x 8 bytes).
+a dense partial table in HBM (layout: include/pinot_gpu.h, pgpu_table_layout).  Then:
 
-Group keys must mean the same thing on every rank: each group column's global dictionary is the sorted union of
-every rank's segment dictionaries (``union_dictionaries``, one all_gather_object per query shape, cached).
+* small tables (aggregation only, or < 1 MiB): one ``all_reduce`` per reduction op (int64 SUM for counts and
+  integer sums, float64 SUM for double sums, int64 MIN / MAX of order-preserving keys); rank 0 compacts the
+  non-empty keys and finishes ORDER BY / LIMIT;
+* large group-by tables: one ``reduce_scatter`` per section, so each rank owns the FINAL cells of 1/world of the
+  key space; each rank compacts its slice and keeps its top ``max(5 * limit, 5000)`` rows by the ORDER BY
+  expressions (GroupByUtils.getTableCapacity, core/util/GroupByUtils.java:24-41 — exact here, because every kept
+  row's values are already merged over all ranks); rank 0 gathers the candidates and finishes.
+
+Doc-id sets never leave their GPU.  Segments that the reference answers without a scan
+(NonScanBasedAggregationOperator: match-all filter, only COUNT / MIN / MAX) are folded into the rank's G = 1 table
+from metadata and dictionaries, with the reference's statistics (numTotalDocs, 0, 0, numTotalDocs).
+
+Every decision that shapes a collective (global group dictionaries, the split-SUM table layout) is agreed by all
+ranks before the collective runs, so no rank can skip or reorder one.
 """
 from __future__ import annotations
 
@@ -20,19 +29,33 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, QueryStats,
-                   TableLayout)
-from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, finish, merge_filtered
+from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
+                   PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
+from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, finish, merge_filtered)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
+
+INT64_MAX = np.iinfo(np.int64).max
+INT64_MIN = np.iinfo(np.int64).min
 
 
 def section_ops(layout: TableLayout) -> List[int]:
     return [layout.section_op[s] for s in range(layout.num_sections)]
 
 
+def section_identity(op: int) -> int:
+    return INT64_MAX if op == PGPU_RED_MIN_I64 else (INT64_MIN if op == PGPU_RED_MAX_I64 else 0)
+
+
+def _dist_op(op: int):
+    import torch.distributed as dist
+    return {PGPU_RED_SUM_I64: dist.ReduceOp.SUM, PGPU_RED_SUM_F64: dist.ReduceOp.SUM,
+            PGPU_RED_MIN_I64: dist.ReduceOp.MIN, PGPU_RED_MAX_I64: dist.ReduceOp.MAX}[op]
+
+
 def reduce_sections(table, layout: TableLayout, group=None) -> None:
     """In-place all-reduce of a dense partial table (torch int64 tensor [nsec * G], CPU/gloo or GPU/RCCL)."""
+    import torch
     import torch.distributed as dist
     G = int(layout.num_keys)
     ops = section_ops(layout)
@@ -42,33 +65,115 @@ def reduce_sections(table, layout: TableLayout, group=None) -> None:
         idx = [s for s, o in enumerate(ops) if o == op]
         if not idx:
             continue
-        rop = {PGPU_RED_SUM_I64: dist.ReduceOp.SUM, PGPU_RED_SUM_F64: dist.ReduceOp.SUM,
-               PGPU_RED_MIN_I64: dist.ReduceOp.MIN, PGPU_RED_MAX_I64: dist.ReduceOp.MAX}[op]
         contiguous = idx == list(range(idx[0], idx[-1] + 1))
         buf = view[idx[0]: idx[-1] + 1] if contiguous else view[idx].contiguous()
         t = buf.view(-1)
         if op == PGPU_RED_SUM_F64:
-            t = t.view(__import__("torch").float64)
-        dist.all_reduce(t, op=rop, group=group)
+            t = t.view(torch.float64)
+        dist.all_reduce(t, op=_dist_op(op), group=group)
         if not contiguous:
             view[idx] = buf
 
 
-def union_dictionaries(local: Sequence, group=None):
-    """Sorted union of every rank's dictionary values for one group column."""
+def reduce_scatter_sections(table, layout: TableLayout, world: int, rank: int, group=None):
+    """Reduce-scatter a dense partial table: returns (chunk [nsec, K] int64 tensor, first key) where this rank's
+    K = ceil(G / world) keys hold cells reduced over every rank.  One collective per section."""
+    import torch
+    import torch.distributed as dist
+    G = int(layout.num_keys)
+    ops = section_ops(layout)
+    K = (G + world - 1) // world
+    view = table.view(len(ops), G)
+    out = torch.empty((len(ops), K), dtype=torch.int64, device=table.device)
+    for s, op in enumerate(ops):
+        src = torch.full((K * world,), section_identity(op), dtype=torch.int64, device=table.device)
+        src[:G] = view[s]
+        dst = out[s]
+        if op == PGPU_RED_SUM_F64:
+            src, dst = src.view(torch.float64), out[s].view(torch.float64)
+        if hasattr(dist, "reduce_scatter_tensor") and dist.get_backend(group) != "gloo":
+            dist.reduce_scatter_tensor(dst, src, op=_dist_op(op), group=group)
+        else:  # gloo has no reduce_scatter: all_reduce, keep this rank's slice
+            dist.all_reduce(src, op=_dist_op(op), group=group)
+            dst.copy_(src[rank * K:(rank + 1) * K])
+    return out, rank * K
+
+
+def _encode_dictionary(local) -> np.ndarray:
+    """A group dictionary as bytes for a tensor collective: int64 / float64 values, or length-prefixed UTF-8."""
+    if isinstance(local, list):
+        parts = []
+        for v in local:
+            b = v.encode("utf-8")
+            parts.append(len(b).to_bytes(4, "little") + b)
+        return np.frombuffer(b"".join(parts), dtype=np.uint8)
+    a = np.asarray(local)
+    a = a.astype(np.float64) if a.dtype.kind == "f" else a.astype(np.int64)
+    return a.view(np.uint8)
+
+
+def _decode_dictionary(raw: np.ndarray, kind: str):
+    if kind == "s":
+        out, b, i = [], raw.tobytes(), 0
+        while i < len(b):
+            n = int.from_bytes(b[i:i + 4], "little")
+            out.append(b[i + 4:i + 4 + n].decode("utf-8"))
+            i += 4 + n
+        return out
+    return raw.view(np.float64 if kind == "f" else np.int64)
+
+
+def union_dictionaries(local: Sequence, group=None, device=None):
+    """Sorted union of every rank's dictionary values for one group column, exchanged as byte tensors (sizes,
+    then one all_gather of padded payloads)."""
+    import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    parts: List = [None] * world
-    dist.all_gather_object(parts, list(local) if isinstance(local, list) else np.asarray(local).tolist(), group=group)
-    if any(isinstance(v, str) for p in parts for v in p[:1]):
+    dev = device if device is not None else torch.device("cpu")
+    kind = "s" if isinstance(local, list) else ("f" if np.asarray(local).dtype.kind == "f" else "i")
+    raw = _encode_dictionary(local)
+    n = torch.tensor([len(raw)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    pad = max(1, max(sizes))
+    mine = torch.zeros(pad, dtype=torch.uint8, device=dev)
+    if len(raw):
+        mine[: len(raw)] = torch.from_numpy(raw.copy()).to(dev)
+    bufs = [torch.zeros(pad, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(bufs, mine, group=group)
+    parts = [_decode_dictionary(b[:sz].cpu().numpy(), kind) for b, sz in zip(bufs, sizes)]
+    if kind == "s":
         return sorted(set().union(*[set(p) for p in parts]))
-    return np.unique(np.concatenate([np.asarray(p) for p in parts]))
+    vals = np.unique(np.concatenate(parts)) if parts else np.zeros(0)
+    if kind == "i":
+        return vals.astype(np.int64)
+    return vals
+
+
+def minmax_key(value: float, vtype: int) -> int:
+    """Order-preserving int64 key of a MIN / MAX value (the inverse of pgpu_decode_minmax_key)."""
+    if vtype in (PGPU_INT, PGPU_LONG):
+        return int(value)
+    b = int(np.float64(value).view(np.int64))
+    return b if b >= 0 else b ^ 0x7FFFFFFFFFFFFFFF
+
+
+STAT_FIELDS = ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
+               "num_total_docs", "num_segments_processed", "sparse_sector_bytes", "dense_bytes")
 
 
 class DistributedExecutor:
-    """Executes a query over this rank's GPU segments and merges every rank's partial table (rank 0 finishes)."""
+    """Executes a query over this rank's GPU segments and merges every rank's partial table (rank 0 finishes).
 
-    def __init__(self, plan_maker: GpuPlanMaker, group=None):
+    The local kernel step (``_prepare_local`` / ``_wait_local`` / ``_compact``) goes through libpinotgpu; the
+    collectives, agreements and finishing are backend-independent (the gloo tests drive them with a numpy
+    table producer)."""
+
+    SCATTER_MIN_BYTES = 1 << 20  # group-by tables from 1 MiB up are reduce-scattered (SURVEY.md §8e)
+    TOPK_MIN = 5000              # per-rank candidates: max(5 * limit, 5000) (GroupByUtils.java:24-41)
+
+    def __init__(self, plan_maker: Optional[GpuPlanMaker], group=None, device=None):
         import torch
         import torch.distributed as dist
         self.pm = plan_maker
@@ -76,95 +181,251 @@ class DistributedExecutor:
         self.dist = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(group) if self.dist else 0
         self.world = dist.get_world_size(group) if self.dist else 1
-        self.device = torch.device("cuda", plan_maker.ctx.device)
+        if device is None:
+            device = torch.device("cuda", plan_maker.ctx.device)
+        self.device = device
         self._globals: Dict[tuple, tuple] = {}
-        self._tables: Dict[int, object] = {}
-        self._cap_keys = None
+        self._docs: Dict[tuple, tuple] = {}
+        self._split: Dict[tuple, tuple] = {}
+        self._tables: Dict[int, list] = {}
         self.last_stats = None
 
+    # ---- collective helpers ------------------------------------------------------------------------------------
+    def _allreduce_i64(self, vals: Sequence[int], op: str = "sum") -> List[int]:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                               "min": dist.ReduceOp.MIN}[op], group=self.group)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def _agree(self, flag: bool) -> bool:
+        """True on every rank iff it is true on every rank (cache hits must be collective decisions)."""
+        return self._allreduce_i64([1 if flag else 0], "min")[0] == 1
+
+    @staticmethod
+    def _seg_key(segments: Sequence[GpuSegment]) -> tuple:
+        return tuple(s.uid for s in segments)
+
     def _global_dicts(self, query: QueryContext, segments: Sequence[GpuSegment]):
-        key = (tuple(query.group_by), tuple(id(s) for s in segments))
+        key = (tuple(query.group_by), self._seg_key(segments))
         hit = self._globals.get(key)
+        if not self._agree(hit is not None):
+            hit = None
         if hit is None:
-            hit = []
+            dicts = []
             for g in query.group_by:
                 local, _ = self.pm.global_dictionary(g, segments)
-                glob = union_dictionaries(local, self.group) if self.world > 1 else local
-                hit.append(glob)
-            # per-segment remap against the node-global dictionary
-            for g, glob in zip(query.group_by, hit):
+                dicts.append(union_dictionaries(local, self.group, self.device) if self.world > 1 else local)
+            for g, glob in zip(query.group_by, dicts):
                 self.pm.set_global_dictionary(g, segments, glob)
+            hit = (dicts, tuple(segments))
             self._globals[key] = hit
-        return hit
+        return hit[0]
 
+    def _reduce_docs(self, segments: Sequence[GpuSegment]) -> int:
+        """Docs over all ranks (the bound of integer SUM cells after the reduce)."""
+        key = self._seg_key(segments)
+        hit = self._docs.get(key)
+        if not self._agree(hit is not None):
+            hit = None
+        if hit is None:
+            hit = (self._allreduce_i64([sum(s.num_docs for s in segments)])[0], tuple(segments))
+            self._docs[key] = hit
+        return hit[0]
+
+    def _split_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int) -> int:
+        """PGPU_Q_SUM_SPLIT on every rank when any rank's integer-SUM bound needs the split layout."""
+        key = (tuple((a.function, a.column) for a in query.aggregations), self._seg_key(segments))
+        hit = self._split.get(key)
+        if not self._agree(hit is not None):
+            hit = None
+        if hit is None:
+            L = self._local_layout(query, segments, 0, reduce_docs)
+            need = any(L.agg_sum_parts[i] == 3 for i in range(len(query.aggregations)))
+            hit = (_lib.PGPU_Q_SUM_SPLIT if self._allreduce_i64([int(need)], "max")[0] else 0, tuple(segments))
+            self._split[key] = hit
+        return hit[0]
+
+    # ---- local kernel step (libpinotgpu) -------------------------------------------------------------------------
+    def _local_layout(self, query, segments, flags, reduce_docs) -> TableLayout:
+        return self._prepare_local(query, segments, flags, reduce_docs)[0]
+
+    def _alloc_table(self, n: int):
+        import torch
+        pool = self._tables.setdefault(n, [])
+        return pool.pop() if pool else torch.empty(n, dtype=torch.int64, device=self.device)
+
+    def _prepare_local(self, query, segments, flags, reduce_docs):
+        """(table layout, launch(table) -> handle) for this rank's scanned segments."""
+        expr = self.pm.filter_expr(query, segments)
+        desc, keep, _ = self.pm.build_desc(query, segments, plan_filters=expr is None, extra_flags=flags,
+                                           reduce_docs=reduce_docs)
+        L = self.pm.layout(desc)
+
+        def launch(table):
+            # libpinotgpu runs on its own HIP stream: the table memory is shared through the process's GPU address
+            # space and ordered by explicit synchronisation (pgpu_query_wait before any collective touches it)
+            _ = keep
+            qh = C.c_void_p()
+            lib = self.pm.ctx._lib
+            n = int(table.numel())
+            if expr is None:
+                _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
+                                                 C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
+            else:
+                _lib.check(lib.pgpu_query_launch_expr(self.pm.ctx.handle, C.byref(desc), expr[0], expr[1], None,
+                                                      C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
+            return qh
+        return L, launch
+
+    def _wait_local(self, handle) -> dict:
+        lib = self.pm.ctx._lib
+        st = QueryStats()
+        try:
+            _lib.check(lib.pgpu_query_wait(handle, C.byref(st)))
+        finally:
+            lib.pgpu_query_release(handle)
+        return {"num_docs_scanned": st.num_docs_scanned, "num_entries_scanned_in_filter":
+                st.num_entries_scanned_in_filter, "num_total_docs": st.num_total_docs,
+                "sparse_sector_bytes": st.sparse_sector_bytes, "dense_bytes": st.dense_bytes,
+                "kernel_ms": st.kernel_ms}
+
+    def _compact(self, L: TableLayout, table):
+        cap = int(L.num_keys)
+        keys = np.empty(max(cap, 1), dtype=np.int64)
+        cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
+        ng = C.c_uint64()
+        _lib.check(self.pm.ctx._lib.pgpu_table_compact(
+            self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()), None,
+            keys.ctypes.data_as(C.POINTER(C.c_int64)), cells.ctypes.data_as(C.POINTER(C.c_int64)), cap,
+            C.byref(ng)))
+        return keys[: ng.value], cells[: ng.value]
+
+    def _sync_device(self):
+        import torch
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    # ---- query ---------------------------------------------------------------------------------------------------
     def submit(self, query: QueryContext, segments: Sequence[GpuSegment]):
         """Plan and launch this rank's part of the query without waiting (several may be in flight: the host
         plans and reduces query i while the GPU runs query i+1)."""
         if self.world == 1:
             return self.pm.submit(query, segments)
         import torch
-        if query.group_by:
-            self._global_dicts(query, segments)
-        expr = self.pm.filter_expr(query, segments)
-        desc, keep, globals_ = self.pm.build_desc(query, segments, plan_filters=expr is None)
-        L = self.pm.layout(desc)
+        if not segments:
+            raise ValueError("every rank needs at least one segment")
+        globals_ = self._global_dicts(query, segments) if query.group_by else []
+        reduce_docs = self._reduce_docs(segments)
+        flags = self._split_flags(query, segments, reduce_docs)
+        non_scan = self.pm.non_scan_segments(query, segments)
+        scan = [s for s, ns in zip(segments, non_scan) if not ns]
+        # the layout is the same on every rank: group cardinalities are global, the split-SUM choice agreed
+        L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs)
         n = int(L.num_sections * L.num_keys)
-        pool = self._tables.setdefault(n, [])
-        table = pool.pop() if pool else torch.empty(n, dtype=torch.int64, device=self.device)
-        # libpinotgpu runs on its own HIP stream: the table memory is shared through the process's GPU address
-        # space and ordered by explicit synchronisation (a pooled table's last reduce finished in collect)
-        qh = C.c_void_p()
-        lib = self.pm.ctx._lib
-        if expr is None:
-            _lib.check(lib.pgpu_query_launch(self.pm.ctx.handle, C.byref(desc), None,
-                                             C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
-        else:
-            _lib.check(lib.pgpu_query_launch_expr(self.pm.ctx.handle, C.byref(desc), expr[0], expr[1], None,
-                                                  C.c_void_p(table.data_ptr()), 8 * n, C.byref(qh)))
-        return _DistPending(query, len(segments), L, table, qh, globals_)
+        table = self._alloc_table(n)
+        handle = None
+        if scan:
+            handle = launch(table)
+        else:  # every local segment is answered from metadata: start from the identity table
+            ops = section_ops(L)
+            table.view(len(ops), -1).copy_(torch.tensor([[section_identity(o)] for o in ops], dtype=torch.int64)
+                                           .expand(len(ops), int(L.num_keys)))
+        return _DistPending(query, L, table, handle, globals_,
+                            [s for s, ns in zip(segments, non_scan) if ns], len(segments))
+
+    def _fold_non_scan(self, p: "_DistPending", stats: dict) -> None:
+        """NonScanBasedAggregationOperator answers (NonScanBasedAggregationOperator.java:85-101,253-256) folded
+        into this rank's G = 1 table: COUNT = docs, MIN / MAX = the dictionary's first / last value."""
+        if not p.non_scan:
+            return
+        L, query = p.layout, p.query
+        view = p.table.view(L.num_sections, int(L.num_keys))
+        cnt = sum(s.num_docs for s in p.non_scan)
+        view[0, 0] += cnt
+        for ai, a in enumerate(query.aggregations):
+            if a.function not in ("MIN", "MAX"):
+                continue
+            sec, vt = L.agg_section[ai], L.agg_value_type[ai]
+            for s in p.non_scan:
+                d = s.dictionaries[a.column]
+                k = minmax_key(float(d[0] if a.function == "MIN" else d[-1]), vt)
+                cur = int(view[sec, 0].item())
+                view[sec, 0] = min(cur, k) if a.function == "MIN" else max(cur, k)
+        stats["num_docs_scanned"] += cnt
+        stats["num_total_docs"] += cnt
 
     def collect(self, pending) -> Optional[QueryResult]:
-        """Wait for this rank's launch, all-reduce the partial table over RCCL; rank 0 compacts and finishes."""
+        """Wait for this rank's launch, merge the partial tables over the collectives; rank 0 finishes."""
         if self.world == 1:
             res = self.pm.collect(pending)
             self.last_stats = res.stats
             return res
-        import torch
-        import torch.distributed as dist
-        lib = self.pm.ctx._lib
-        st = QueryStats()
-        qh, pending.handle = pending.handle, None
-        try:
-            _lib.check(lib.pgpu_query_wait(qh, C.byref(st)))
-        finally:
-            lib.pgpu_query_release(qh)
+        p = pending
+        stats = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
+                 "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
+        if p.handle is not None:
+            h, p.handle = p.handle, None
+            stats.update(self._wait_local(h))
+        self._fold_non_scan(p, stats)
+        query, L, table = p.query, p.layout, p.table
+        scan_docs = stats["num_docs_scanned"] - sum(s.num_docs for s in p.non_scan)
+        local = [stats["num_docs_scanned"], stats["num_entries_scanned_in_filter"],
+                 scan_docs * len(query.projected_columns), stats["num_total_docs"], p.num_segments,
+                 stats["sparse_sector_bytes"], stats["dense_bytes"]]
+        tot = dict(zip(STAT_FIELDS, self._allreduce_i64(local)))
+        st = ExecutionStats(kernel_ms=stats["kernel_ms"], **tot)  # kernel time of this rank's launch
         self.last_stats = st
-        L, table, query = pending.layout, pending.table, pending.query
-        reduce_sections(table, L, self.group)
-        counts = torch.tensor([st.num_docs_scanned, st.num_total_docs], dtype=torch.int64, device=self.device)
-        dist.all_reduce(counts, group=self.group)
-        docs_scanned, total_docs = (int(x) for x in counts.tolist())
-        torch.cuda.current_stream(self.device).synchronize()
         try:
+            big = query.group_by and 8 * int(table.numel()) >= self.SCATTER_MIN_BYTES
+            if big:
+                keys, cells = self._scatter_topk(p)
+            else:
+                reduce_sections(table, L, self.group)
+                self._sync_device()
+                if self.rank != 0:
+                    return None
+                keys, cells = self._compact(L, table)
             if self.rank != 0:
                 return None
-            cap = int(L.num_keys)
-            keys = np.empty(max(cap, 1), dtype=np.int64)
-            cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
-            ng = C.c_uint64()
-            _lib.check(lib.pgpu_table_compact(self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()),
-                                              None, keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                              cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(ng)))
-            gt = GroupTable(keys[: ng.value], cells[: ng.value], L)
-            stats = ExecutionStats(num_docs_scanned=docs_scanned,
-                                   num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
-                                   num_entries_scanned_post_filter=docs_scanned * len(query.projected_columns),
-                                   num_total_docs=total_docs, num_segments_processed=pending.num_segments * self.world,
-                                   kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
-                                   dense_bytes=st.dense_bytes)
-            return finish(query, gt, [g[0] for g in pending.globals_], stats)
+            order = np.argsort(keys, kind="stable")
+            return finish(query, GroupTable(keys[order], cells[order], L), p.globals_, st)
         finally:
             self._tables.setdefault(int(table.numel()), []).append(table)
+
+    def _scatter_topk(self, p: "_DistPending"):
+        """Large group-by table: reduce-scatter, per-rank compaction and top-K, gather of the candidates."""
+        import torch
+        import torch.distributed as dist
+        L, query = p.layout, p.query
+        chunk, key0 = reduce_scatter_sections(p.table, L, self.world, self.rank, self.group)
+        self._sync_device()
+        CL = TableLayout()
+        C.memmove(C.byref(CL), C.byref(L), C.sizeof(TableLayout))
+        CL.num_keys = int(chunk.shape[1])
+        keys, cells = self._compact(CL, chunk.reshape(-1).contiguous())
+        keys = keys + key0
+        cap = max(5 * query.limit, self.TOPK_MIN)  # GroupByUtils.getTableCapacity
+        if len(keys) > cap:
+            cols = GroupColumns(query, GroupTable(keys, cells, L), p.globals_)
+            idx = np.sort(cols.order_and_limit(limit=cap) if query.order_by else np.arange(cap))
+            keys, cells = keys[idx], cells[idx]
+        n = len(keys)
+        width = 1 + L.num_sections
+        sizes = self._allreduce_i64([n], "max")[0]
+        pad = max(1, sizes)
+        mine = torch.zeros((pad, width), dtype=torch.int64)
+        if n:
+            mine[:n, 0] = torch.from_numpy(keys.astype(np.int64))
+            mine[:n, 1:] = torch.from_numpy(np.ascontiguousarray(cells))
+        counts = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=self.device), group=self.group)
+        bufs = [torch.zeros((pad, width), dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        dist.all_gather(bufs, mine.to(self.device), group=self.group)
+        rows = np.concatenate([b[: int(c.item())].cpu().numpy() for b, c in zip(bufs, counts)]) if pad else \
+            np.zeros((0, width), np.int64)
+        return rows[:, 0].copy(), np.ascontiguousarray(rows[:, 1:])
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
         if self.world == 1:  # single GPU: the plan maker's own plan choice (filtered passes, non-scan segments)
@@ -183,15 +444,14 @@ class DistributedExecutor:
 class _DistPending:
     """A launched, not yet collected multi-GPU query of this rank."""
 
-    def __init__(self, query, num_segments, layout, table, handle, globals_):
-        self.query, self.num_segments, self.layout = query, num_segments, layout
-        self.table, self.handle, self.globals_ = table, handle, globals_
+    def __init__(self, query, layout, table, handle, globals_, non_scan, num_segments):
+        self.query, self.layout, self.table, self.handle = query, layout, table, handle
+        self.globals_, self.non_scan, self.num_segments = globals_, non_scan, num_segments
 
     def __del__(self):
         if self.handle is not None and getattr(self.handle, "value", None):
             try:
-                from . import _lib as L
-                L.load().pgpu_query_release(self.handle)
+                _lib.load().pgpu_query_release(self.handle)
             except Exception:
                 pass
             self.handle = None

@@ -161,7 +161,10 @@ struct DevAgg {
   int32_t op;       // PGPU_RED_* of the section
   int32_t vtype;    // dictionary type
   int32_t emit;     // PART mode: this aggregation's column is the one carried in the records (first such agg)
+  int32_t part;     // split integer SUM (pgpu_table_layout.agg_sum_parts == 3): 0 whole value, 1 bits [0,21),
+                    // 2 bits [21,42), 3 bits [42,64) (arithmetic) -- each a SUM_I64 section of its own
 };
+#define PGPU_PART_BITS 21
 
 #define PGPU_MODE_AGG 0
 #define PGPU_MODE_LDS 1
@@ -224,7 +227,7 @@ struct DevParams {
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];
-  int32_t sec_op[PGPU_MAX_AGGS + 1];
+  int32_t sec_op[PGPU_MAX_SECTIONS];
 };
 
 #define PGPU_FLAG_STATS 1

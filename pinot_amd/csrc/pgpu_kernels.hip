@@ -41,6 +41,15 @@
 #include "../../include/pinot_gpu.h"
 #include "pgpu_internal.h"
 
+// The file is compiled as several translation units in parallel (__graft_entry__.build): -DPGPU_TU=k keeps only
+// the kernels of one aggregation mode (0 AGG, 1 LDS, 2 GLOBAL, 3 PART, 4 HASH) or the common kernels and the
+// dispatchers (5).  Every query-kernel instantiation inlines all 31 bit widths, so one TU would take minutes.
+#ifndef PGPU_TU
+#define PGPU_TU -1  // everything
+#endif
+#define PGPU_TU_COMMON 5
+#define TU_HAS(k) (PGPU_TU < 0 || PGPU_TU == (k))
+
 #define WT PGPU_WT
 #define MAXS PGPU_MAX_SLOTS
 #define U PGPU_DOC_U
@@ -244,6 +253,20 @@ FI void gather_cells(const void* dict, int32_t vtype, int32_t op, const uint32_t
       for (int r = 0; r < N; ++r) out[r] = op == PGPU_RED_SUM_F64 ? raw[r] : key_of_double(__longlong_as_double(raw[r]));
     }
   }
+}
+// Split integer SUM (DevAgg::part): the agg's cell sums one 21-bit part of every value, so that no int64 cell can
+// wrap (pgpu_table_layout.agg_sum_parts).
+FI int64_t part_of(int64_t v, int32_t part) {
+  if (part == 1) return v & ((1ll << PGPU_PART_BITS) - 1);
+  if (part == 2) return (v >> PGPU_PART_BITS) & ((1ll << PGPU_PART_BITS) - 1);
+  if (part == 3) return v >> (2 * PGPU_PART_BITS);
+  return v;
+}
+template <int N>
+FI void apply_part(int64_t (&v)[N], int32_t part) {
+  if (part == 0) return;
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = part_of(v[r], part);
 }
 FI int64_t cell_combine(int32_t op, int64_t a, int64_t b) {
   if (op == PGPU_RED_SUM_I64) return a + b;
@@ -1193,6 +1216,7 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
     }
     int64_t v[U];
     gather_cells(c.dict, ag.vtype, ag.op, id, v);
+    apply_part(v, ag.part);
     if (MODE == PGPU_MODE_AGG) {
       int64_t part = sec_identity(ag.op);
 #pragma unroll
@@ -1350,6 +1374,7 @@ FI void dense_agg_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const Se
       }
       int64_t v[8];
       gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+      apply_part(v, ag.part);
 #pragma unroll
       for (int r = 0; r < 8; ++r)
         if (b0 + lane + 64 * r < nt) part = cell_combine(ag.op, part, v[r]);
@@ -1486,6 +1511,7 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
         }
         int64_t v[8];
         gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+        apply_part(v, ag.part);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int e = lane + 64 * (r0 + r);
@@ -2113,6 +2139,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   }
 }
 
+#if TU_HAS(PGPU_TU_COMMON)
 // Table init: count/sum sections 0, MIN +max, MAX -max.
 __global__ void table_init_kernel(int64_t* table, uint64_t G, int32_t nsec, DevParams p) {
   const uint64_t n = G * (uint64_t)nsec;
@@ -2230,12 +2257,79 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
   }
 }
 
+#endif  // TU_HAS(PGPU_TU_COMMON)
+
 }  // namespace
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
-#define PGPU_ALL_QUERY_KERNELS(X)                                                                          \
-  X(PGPU_MODE_AGG, 0) X(PGPU_MODE_LDS, 0) X(PGPU_MODE_GLOBAL, 0) X(PGPU_MODE_PART, 0) X(PGPU_MODE_AGG, 1) \
-  X(PGPU_MODE_LDS, 1) X(PGPU_MODE_GLOBAL, 1) X(PGPU_MODE_PART, 1)
+// Per aggregation mode (one translation unit each): launch the ring or direct query kernel, set its LDS attribute.
+#define PGPU_MODE_FUNCS(M, NAME)                                                                                  \
+  hipError_t pgpu_launch_query_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {          \
+    if (p.dense) hipLaunchKernelGGL((query_kernel<M, 1>), dim3(grid), dim3(PGPU_THREADS(1)), dyn_smem, st, p);   \
+    else hipLaunchKernelGGL((query_kernel<M, 0>), dim3(grid), dim3(PGPU_THREADS(0)), dyn_smem, st, p);           \
+    return hipGetLastError();                                                                                   \
+  }                                                                                                             \
+  hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
+    hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);       \
+    return hipGetLastError();                                                                                   \
+  }                                                                                                             \
+  hipError_t pgpu_prepare_##NAME(size_t lds_bytes) {                                                            \
+    hipError_t e = hipFuncSetAttribute((const void*)query_kernel<M, 0>,                                         \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);            \
+    if (e == hipSuccess)                                                                                        \
+      e = hipFuncSetAttribute((const void*)query_kernel<M, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                              (int)lds_bytes);                                                                  \
+    if (e == hipSuccess)                                                                                        \
+      e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                              (int)lds_bytes);                                                                  \
+    return e;                                                                                                   \
+  }
+#define PGPU_MODE_DECLS(NAME)                                                                   \
+  hipError_t pgpu_launch_query_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);  \
+  hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st); \
+  hipError_t pgpu_prepare_##NAME(size_t lds_bytes);
+PGPU_MODE_DECLS(agg) PGPU_MODE_DECLS(lds) PGPU_MODE_DECLS(global) PGPU_MODE_DECLS(part)
+
+#if TU_HAS(0)
+PGPU_MODE_FUNCS(PGPU_MODE_AGG, agg)
+#endif
+#if TU_HAS(1)
+PGPU_MODE_FUNCS(PGPU_MODE_LDS, lds)
+#endif
+#if TU_HAS(2)
+PGPU_MODE_FUNCS(PGPU_MODE_GLOBAL, global)
+#endif
+#if TU_HAS(3)
+PGPU_MODE_FUNCS(PGPU_MODE_PART, part)
+
+hipError_t pgpu_prepare_part_reduce() {
+  hipError_t e = hipSuccess;
+#define PART_ATTR(NS)                                                                                       \
+  if (e == hipSuccess)                                                                                      \
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            PGPU_PART_LDS_BYTES);
+  PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
+#undef PART_ATTR
+  return e;
+}
+
+hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
+  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
+  switch (p.nsec - 1) {
+#define PART_LAUNCH(NS)                                                                        \
+  case NS:                                                                                     \
+    hipLaunchKernelGGL(part_reduce_kernel<NS>, dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
+    return hipGetLastError();
+    PART_LAUNCH(0) PART_LAUNCH(1) PART_LAUNCH(2) PART_LAUNCH(3) PART_LAUNCH(4)
+#undef PART_LAUNCH
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+#endif  // TU_HAS(3)
+
+#if TU_HAS(PGPU_TU_COMMON)
+hipError_t pgpu_prepare_part_reduce();
 
 // Bit-sliced copy of a fixed-bit forward index (built once per column at segment seal): thread (tile, lane) unpacks
 // its 32 dict ids from the big-endian packed words and writes plane k = bit k of each id (doc 32l+i in bit i) at
@@ -2274,40 +2368,12 @@ hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, in
 }
 
 hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
-  hipError_t e = hipSuccess;
-#define SET_ATTR(M, D)                                                                                        \
-  if (e == hipSuccess)                                                                                        \
-    e = hipFuncSetAttribute((const void*)query_kernel<M, D>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            (int)lds_bytes);
-  PGPU_ALL_QUERY_KERNELS(SET_ATTR)
-#undef SET_ATTR
-#define PART_ATTR(NS)                                                                                       \
-  if (e == hipSuccess)                                                                                      \
-    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            PGPU_PART_LDS_BYTES);
-  PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
-#undef PART_ATTR
-#define DIRECT_ATTR(M)                                                                                      \
-  if (e == hipSuccess)                                                                                      \
-    e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            (int)lds_bytes);
-  DIRECT_ATTR(PGPU_MODE_AGG) DIRECT_ATTR(PGPU_MODE_LDS) DIRECT_ATTR(PGPU_MODE_GLOBAL) DIRECT_ATTR(PGPU_MODE_PART)
-#undef DIRECT_ATTR
+  hipError_t e = pgpu_prepare_agg(lds_bytes);
+  if (e == hipSuccess) e = pgpu_prepare_lds(lds_bytes);
+  if (e == hipSuccess) e = pgpu_prepare_global(lds_bytes);
+  if (e == hipSuccess) e = pgpu_prepare_part(lds_bytes);
+  if (e == hipSuccess) e = pgpu_prepare_part_reduce();
   return e;
-}
-
-hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
-  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
-  switch (p.nsec - 1) {
-#define PART_LAUNCH(NS)                                                                        \
-  case NS:                                                                                     \
-    hipLaunchKernelGGL(part_reduce_kernel<NS>, dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
-    return hipGetLastError();
-    PART_LAUNCH(0) PART_LAUNCH(1) PART_LAUNCH(2) PART_LAUNCH(3) PART_LAUNCH(4)
-#undef PART_LAUNCH
-    default:
-      return hipErrorInvalidValue;
-  }
 }
 
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {
@@ -2320,26 +2386,24 @@ hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st) {
 }
 
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
-#define LAUNCH(M, D)                                                                                \
-  if (p.mode == M && p.dense == D) {                                                                \
-    hipLaunchKernelGGL((query_kernel<M, D>), dim3(grid), dim3(PGPU_THREADS(D)), dyn_smem, st, p); \
-    return hipGetLastError();                                                                       \
+  switch (p.mode) {
+    case PGPU_MODE_AGG: return pgpu_launch_query_agg(p, grid, dyn_smem, st);
+    case PGPU_MODE_LDS: return pgpu_launch_query_lds(p, grid, dyn_smem, st);
+    case PGPU_MODE_GLOBAL: return pgpu_launch_query_global(p, grid, dyn_smem, st);
+    case PGPU_MODE_PART: return pgpu_launch_query_part(p, grid, dyn_smem, st);
+    default: return hipErrorInvalidValue;
   }
-  PGPU_ALL_QUERY_KERNELS(LAUNCH)
-#undef LAUNCH
-  return hipErrorInvalidValue;
 }
 
 // Direct variant (p.direct): PGPU_DIRECT_THREADS per workgroup, several workgroups per CU.
 hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
-#define LAUNCH_D(M)                                                                                        \
-  if (p.mode == M) {                                                                                       \
-    hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
-    return hipGetLastError();                                                                              \
+  switch (p.mode) {
+    case PGPU_MODE_AGG: return pgpu_launch_direct_agg(p, grid, dyn_smem, st);
+    case PGPU_MODE_LDS: return pgpu_launch_direct_lds(p, grid, dyn_smem, st);
+    case PGPU_MODE_GLOBAL: return pgpu_launch_direct_global(p, grid, dyn_smem, st);
+    case PGPU_MODE_PART: return pgpu_launch_direct_part(p, grid, dyn_smem, st);
+    default: return hipErrorInvalidValue;
   }
-  LAUNCH_D(PGPU_MODE_AGG) LAUNCH_D(PGPU_MODE_LDS) LAUNCH_D(PGPU_MODE_GLOBAL) LAUNCH_D(PGPU_MODE_PART)
-#undef LAUNCH_D
-  return hipErrorInvalidValue;
 }
 
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
@@ -2381,3 +2445,4 @@ hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, i
   }
   return hipGetLastError();
 }
+#endif  // TU_HAS(PGPU_TU_COMMON)

@@ -186,6 +186,7 @@ struct HostColumn {
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
+  double max_abs = 0;                  // numeric dictionary: largest |value| (integer SUM overflow bound)
 };
 
 }  // namespace
@@ -448,19 +449,42 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
                 (unsigned long long)num_bytes, (unsigned long long)w * cardinality);
   std::vector<uint8_t> le(num_bytes);
   const uint8_t* b = (const uint8_t*)bytes;
+  // Pinot dictionaries are sorted ascending (SegmentDictionaryCreator.java:92-156; BaseImmutableDictionary's
+  // binary searches rely on it), and so do the kernels' MIN / MAX-on-dict-id reductions: an unsorted numeric
+  // dictionary is malformed input.  Floating values compare by their order-preserving bit key (-0.0 < 0.0, as
+  // Float.compare / Double.compare order them).
+  auto order_key = [&](int32_t i) -> int64_t {
+    if (data_type == PGPU_INT) return (int64_t)(int32_t)be32(b + 4 * i);
+    if (data_type == PGPU_LONG) return (int64_t)be64(b + 8 * (size_t)i);
+    int64_t k = data_type == PGPU_FLOAT ? (int64_t)(int32_t)be32(b + 4 * i) : (int64_t)be64(b + 8 * (size_t)i);
+    if (data_type == PGPU_FLOAT) {  // widen the float bits' order to the int64 key space
+      const int32_t f = (int32_t)k;
+      return f >= 0 ? (int64_t)f : (int64_t)(f ^ 0x7FFFFFFF);
+    }
+    return k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
+  };
+  double max_abs = 0;
+  int64_t prev = 0;
   for (int32_t i = 0; i < cardinality; ++i) {
+    const int64_t k = order_key(i);
+    if (i > 0 && k <= prev)
+      return fail(PGPU_E_INVALID, "dictionary of column %d is not sorted ascending at id %d", column, i);
+    prev = k;
     if (w == 4) {
       uint32_t v = be32(b + 4 * i);
       memcpy(&le[4 * i], &v, 4);
+      if (data_type == PGPU_INT) max_abs = std::max(max_abs, std::fabs((double)(int32_t)v));
     } else {
       uint64_t v = be64(b + 8 * i);
       memcpy(&le[8 * (size_t)i], &v, 8);
+      if (data_type == PGPU_LONG) max_abs = std::max(max_abs, std::fabs((double)(int64_t)v));
     }
   }
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
   c.hdict = std::move(le);
+  c.max_abs = max_abs;
   return PGPU_OK;
 }
 
@@ -607,6 +631,10 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
   out->num_sections = 1;
   out->section_op[0] = PGPU_RED_SUM_I64;
   const pgpu_segment* s0 = q->segments[0].segment;
+  int64_t docs = 0;
+  for (int s = 0; s < q->num_segments; ++s)
+    if (q->segments[s].segment) docs += q->segments[s].segment->num_docs;
+  docs = std::max<int64_t>(docs, q->reduce_docs);
   for (int a = 0; a < q->num_aggs; ++a) {
     const pgpu_agg& ag = q->aggs[a];
     if (ag.fn < PGPU_AGG_COUNT || ag.fn > PGPU_AGG_AVG) return fail(PGPU_E_UNSUPPORTED, "aggregation fn %d", ag.fn);
@@ -625,9 +653,24 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
     if (ag.fn == PGPU_AGG_MIN) op = PGPU_RED_MIN_I64;
     else if (ag.fn == PGPU_AGG_MAX) op = PGPU_RED_MAX_I64;
     else op = (vt == PGPU_INT || vt == PGPU_LONG) ? PGPU_RED_SUM_I64 : PGPU_RED_SUM_F64;
+    // integer SUM: one int64 cell while max|value| x docs stays below 2^62, else three exact part sums
+    int parts = 1;
+    if (op == PGPU_RED_SUM_I64) {
+      double max_abs = 0;
+      for (int s = 0; s < q->num_segments; ++s) {
+        const pgpu_segment* sg = q->segments[s].segment;
+        const int32_t sl = q->segments[s].column_map ? q->segments[s].column_map[ag.column] : -1;
+        if (!sg || sl < 0 || sl >= (int32_t)sg->cols.size()) return fail(PGPU_E_INVALID, "agg %d column slot", a);
+        max_abs = std::max(max_abs, sg->cols[sl].max_abs);
+      }
+      if ((q->flags & PGPU_Q_SUM_SPLIT) || max_abs * (double)docs >= 4.611686018427388e18) parts = 3;
+    }
+    if (out->num_sections + parts > PGPU_MAX_SECTIONS)
+      return fail(PGPU_E_UNSUPPORTED, "more than %d value sections", PGPU_MAX_SECTIONS - 1);
     out->agg_section[a] = out->num_sections;
     out->agg_value_type[a] = vt;
-    out->section_op[out->num_sections++] = op;
+    out->agg_sum_parts[a] = parts;
+    for (int k = 0; k < parts; ++k) out->section_op[out->num_sections++] = op;
   }
   return PGPU_OK;
 }
@@ -1184,7 +1227,6 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
 int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_layout& L, Packer& pk, DevParams& p) {
   memset(&p, 0, sizeof(p));
   p.ncols = q->num_columns;
-  p.nagg = q->num_aggs;
   p.ngcols = q->num_group_columns;
   p.nsec = L.num_sections;
   p.G = L.num_keys;
@@ -1199,13 +1241,21 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     p.gstride[g] = stride;
     stride *= (uint32_t)q->group_cardinalities[g];
   }
+  // device aggregations: one per query aggregation, or one per part section of a split integer SUM
+  p.nagg = 0;
   for (int a = 0; a < q->num_aggs; ++a) {
-    p.aggs[a].fn = q->aggs[a].fn;
-    p.aggs[a].col = q->aggs[a].column;
-    p.aggs[a].sec = L.agg_section[a];
-    p.aggs[a].op = L.section_op[L.agg_section[a]];
-    p.aggs[a].vtype = L.agg_value_type[a];
-    p.aggs[a].emit = 0;
+    const int parts = q->aggs[a].fn == PGPU_AGG_COUNT ? 1 : std::max(1, L.agg_sum_parts[a]);
+    for (int k = 0; k < parts; ++k) {
+      if (p.nagg >= PGPU_MAX_AGGS) return fail(PGPU_E_UNSUPPORTED, "more than %d device aggregations", PGPU_MAX_AGGS);
+      DevAgg& d = p.aggs[p.nagg++];
+      d.fn = q->aggs[a].fn;
+      d.col = q->aggs[a].column;
+      d.sec = L.agg_section[a] + k;
+      d.op = L.section_op[d.sec];
+      d.vtype = L.agg_value_type[a];
+      d.emit = 0;
+      d.part = parts == 3 ? k + 1 : 0;
+    }
   }
   int64_t tiles = 0;
   for (int s = 0; s < q->num_segments; ++s) {
@@ -1297,12 +1347,13 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   bool part_ok = q->num_group_columns > 0 &&
                  (L.num_keys >= PGPU_PART_MIN_KEYS || (q->flags & PGPU_Q_PARTITION) != 0);
   int pcol = -1;
-  for (int a = 0; a < q->num_aggs && part_ok; ++a) {
-    if (q->aggs[a].fn == PGPU_AGG_COUNT) continue;
-    if (pcol >= 0 && q->aggs[a].column != pcol) part_ok = false;
-    if (L.agg_value_type[a] != PGPU_INT && L.agg_value_type[a] != PGPU_FLOAT) part_ok = false;
+  for (int a = 0; a < p.nagg && part_ok; ++a) {
+    if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+    if (pcol >= 0 && p.aggs[a].col != pcol) part_ok = false;
+    if (p.aggs[a].vtype != PGPU_INT && p.aggs[a].vtype != PGPU_FLOAT) part_ok = false;
+    if (p.aggs[a].part != 0) part_ok = false;  // records carry whole 4-byte values
     if (pcol < 0) {
-      pcol = q->aggs[a].column;
+      pcol = p.aggs[a].col;
       p.aggs[a].emit = 1;
     }
   }
@@ -1318,7 +1369,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   else if (part_ok) p.mode = PGPU_MODE_PART;
   else p.mode = PGPU_MODE_GLOBAL;
   if (p.mode != PGPU_MODE_PART)
-    for (int a = 0; a < q->num_aggs; ++a) p.aggs[a].emit = 0;
+    for (int a = 0; a < p.nagg; ++a) p.aggs[a].emit = 0;
   p.ltab_bytes = p.mode == PGPU_MODE_LDS ? (int32_t)tbytes : (p.mode == PGPU_MODE_PART ? (int32_t)(4 * nparts) : 0);
   const size_t avail = PGPU_LDS_LIMIT - fixed - align16(p.ltab_bytes);
   p.slot_bytes = S;

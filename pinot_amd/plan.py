@@ -22,6 +22,7 @@ reported as PGPU_E_UNSUPPORTED-equivalent (``UnsupportedPlanError``) so the serv
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
 import math
 from fractions import Fraction
 from dataclasses import dataclass, field
@@ -265,8 +266,17 @@ class QueryResult:
         return self._intermediate
 
 
+def join_parts(row_cells, sec: int, parts: int) -> int:
+    """Exact integer SUM of a cell split into 21-bit-part sections (pgpu_table_layout.agg_sum_parts == 3):
+    c[sec] + c[sec+1] * 2^21 + c[sec+2] * 2^42, as a Python int (rounded once, on conversion to double)."""
+    if parts != 3:
+        return int(row_cells[sec])
+    b = _lib.PGPU_PART_BITS
+    return int(row_cells[sec]) + (int(row_cells[sec + 1]) << b) + (int(row_cells[sec + 2]) << (2 * b))
+
+
 def final_value(fn: str, cell_count: int, cell: Optional[int], op: int, vtype: int):
-    """AggregationFunction.extractFinalResult on a merged cell."""
+    """AggregationFunction.extractFinalResult on a merged cell (an exact Python int for integer sums)."""
     if fn == "COUNT":
         return int(cell_count)
     if fn == "SUM":
@@ -309,6 +319,22 @@ def to_select_order(query: QueryContext, row: tuple) -> tuple:
     return tuple(out)
 
 
+def dictionary_digest(glob) -> str:
+    """Content digest of a global dictionary: remap tables are cached per (segment, column, digest), so two
+    different global dictionaries of the same length never share one."""
+    h = hashlib.blake2b(digest_size=16)
+    if isinstance(glob, list):
+        for v in glob:
+            b = str(v).encode("utf-8")
+            h.update(len(b).to_bytes(4, "little"))
+            h.update(b)
+    else:
+        a = np.ascontiguousarray(glob)
+        h.update(str(a.dtype).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
 # ---- plan maker ------------------------------------------------------------------------------------------------
 class GpuPlanMaker:
     """PlanMaker for the GPU path (core/plan/maker/PlanMaker.java:36-59): one launch per query per GPU."""
@@ -330,10 +356,10 @@ class GpuPlanMaker:
     def global_dictionary(self, column: str, segments: Sequence[GpuSegment]):
         """Global dictionary of a group column (sorted union of the segments' dictionaries unless a wider one was
         installed by set_global_dictionary) and per-segment remap buffers (None = identity)."""
-        key = (column, tuple(id(s) for s in segments))
+        key = (column, tuple(s.uid for s in segments))
         hit = self._global_dicts.get(key)
         if hit is not None:
-            return hit
+            return hit[:2]
         dicts = [s.dictionaries[column] for s in segments]
         first = dicts[0]
         if isinstance(first, list):
@@ -343,8 +369,9 @@ class GpuPlanMaker:
         return self.set_global_dictionary(column, segments, glob)
 
     def set_global_dictionary(self, column: str, segments: Sequence[GpuSegment], glob):
-        key = (column, tuple(id(s) for s in segments))
+        key = (column, tuple(s.uid for s in segments))
         remaps = []
+        digest = dictionary_digest(glob)
         if isinstance(glob, list):
             pos = {v: i for i, v in enumerate(glob)}
         for s in segments:
@@ -356,10 +383,10 @@ class GpuPlanMaker:
                 t = np.array([pos[v] for v in d], dtype=np.int32)
             else:
                 t = np.searchsorted(glob, d).astype(np.int32)
-            remaps.append(self.ctx.remap((s.name, id(s), column, len(glob)), t))
-        hit = (glob, remaps)
-        self._global_dicts[key] = hit
-        return hit
+            remaps.append(self.ctx.remap((s.uid, column, digest), t))
+        # the entry holds the segments themselves, so their uids stay theirs while it is cached
+        self._global_dicts[key] = (glob, remaps, tuple(segments))
+        return glob, remaps
 
     def _check_group_limit(self, query: QueryContext, seg: GpuSegment) -> None:
         prod = 1
@@ -437,7 +464,8 @@ class GpuPlanMaker:
                 e.values = C.cast(C.byref(la, nd[9] * C.sizeof(Literal)), C.POINTER(Literal))
         return arr, len(nodes), la
 
-    def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment], plan_filters: bool = True):
+    def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment], plan_filters: bool = True,
+                   extra_flags: int = 0, reduce_docs: int = 0):
         """Build the pgpu_query_desc.  Returns (desc, keep, globals_): `keep` owns every buffer the descriptor
         points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array).
         plan_filters=False leaves the per-segment filter programs empty (the library plans them from
@@ -492,7 +520,8 @@ class GpuPlanMaker:
                          segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
                          num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
                          group_columns=gcols, group_cardinalities=gcards,
-                         flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags)
+                         flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags | extra_flags,
+                         reduce_docs=reduce_docs)
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:
@@ -589,7 +618,7 @@ def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats
         fin, inter = [], []
         for ai, a in enumerate(aggs):
             sec = L.agg_section[ai]
-            cell = int(row_cells[sec]) if sec > 0 else None
+            cell = join_parts(row_cells, sec, L.agg_sum_parts[ai]) if sec > 0 else None
             op = L.section_op[sec]
             vt = L.agg_value_type[ai]
             fin.append(final_value(a.function, cnt, cell, op, vt))
@@ -693,6 +722,10 @@ class GroupColumns:
             s = None
             if fn == "COUNT":
                 f = cnt.astype(np.int64)
+            elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] == 3:
+                # split integer sum: join the parts exactly (Python ints), round once to double
+                s = np.array([float(join_parts(r, sec, 3)) for r in table.cells], dtype=np.float64)
+                f = s if fn == "SUM" else s / cnt
             elif fn in ("SUM", "AVG"):
                 s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)
                 f = s if fn == "SUM" else s / cnt  # compacted groups have count > 0
@@ -707,13 +740,15 @@ class GroupColumns:
     def __len__(self):
         return len(self.count)
 
-    def order_and_limit(self) -> np.ndarray:
+    def order_and_limit(self, limit: Optional[int] = None) -> np.ndarray:
         """Row indexes after ORDER BY / LIMIT: stable sort by each ORDER BY expression (GroupByDataTableReducer,
-        IndexedTable.finish), ties kept in ascending global-key order like ``order_and_limit``."""
+        IndexedTable.finish), ties kept in ascending global-key order like ``order_and_limit``.  `limit`
+        overrides the query's (a combine keeping its top max(5 * limit, 5000) candidates)."""
         q = self.query
         n = len(self)
+        lim = q.limit if limit is None else limit
         if not q.order_by:
-            return np.arange(min(n, q.limit))
+            return np.arange(min(n, lim))
         names = list(q.group_by) + [a.result_name for a in q.aggregations]
         columns = self.values + self.finals
         keys = []
@@ -724,12 +759,12 @@ class GroupColumns:
             else:
                 kk = np.unique(c, return_inverse=True)[1].astype(np.int64)
             keys.append(kk if ob.ascending else -kk)
-        if n > 4 * q.limit > 0:
+        if n > 4 * lim > 0:
             # only rows whose primary key is at least as good as the limit-th one can be in the result
-            kth = np.partition(keys[0], q.limit - 1)[q.limit - 1]
+            kth = np.partition(keys[0], lim - 1)[lim - 1]
             cand = np.flatnonzero(keys[0] <= kth)
-            return cand[np.lexsort([k[cand] for k in keys[::-1]])][: q.limit]
-        return np.lexsort(keys[::-1])[: q.limit]
+            return cand[np.lexsort([k[cand] for k in keys[::-1]])][: lim]
+        return np.lexsort(keys[::-1])[: lim]
 
     def rows(self, idx: Optional[np.ndarray] = None) -> List[tuple]:
         sel = (lambda a: a) if idx is None else (lambda a: a[idx])

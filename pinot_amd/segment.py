@@ -17,6 +17,7 @@ PredicateEvaluators do (core/operator/filter/predicate/PredicateEvaluatorProvide
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -137,12 +138,19 @@ class DeviceBuffer:
             self.handle = None
 
 
+_UIDS = itertools.count(1)
+
+
 class GpuSegment:
-    """An immutable segment resident in HBM plus the host-side dictionaries used for predicate evaluation."""
+    """An immutable segment resident in HBM plus the host-side dictionaries used for predicate evaluation.
+
+    ``uid`` is unique for the life of the process (never reused, unlike ``id()``): host-side caches of derived
+    per-segment state (global group dictionaries, remap tables) key on it."""
 
     def __init__(self, ctx: GpuContext, data: SegmentData, columns: Optional[Sequence[str]] = None,
                  _incremental: bool = False):
         self.ctx = ctx
+        self.uid = next(_UIDS)
         self.data = data
         self.name = data.name
         self.num_docs = data.num_docs

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_sizes():
     lib = _lib.load()
-    assert lib.pgpu_abi_version() == 1
+    assert lib.pgpu_abi_version() == _lib.ABI_VERSION
     assert C.sizeof(_lib.FilterNode) == 40
     assert C.sizeof(_lib.Agg) == 8
     assert C.sizeof(_lib.QueryStats) == 56
@@ -62,3 +62,31 @@ def test_minmax_key_decoding():
         b = struct.unpack("<q", struct.pack("<d", v))[0]
         key = b if b >= 0 else b ^ 0x7FFFFFFFFFFFFFFF
         assert lib.pgpu_decode_minmax_key(key, _lib.PGPU_DOUBLE) == v
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """Every ctypes struct mirrors include/pinot_gpu.h: sizeof and every field offset, checked by compiling the
+    header with gcc (the same layout the JNI stub in INTEGRATION.md sees)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"pgpu_filter_node": _lib.FilterNode, "pgpu_agg": _lib.Agg, "pgpu_segment_plan": _lib.SegmentPlan,
+               "pgpu_query_desc": _lib.QueryDesc, "pgpu_table_layout": _lib.TableLayout,
+               "pgpu_query_stats": _lib.QueryStats, "pgpu_literal": _lib.Literal, "pgpu_expr_node": _lib.ExprNode}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{ROOT}/include/pinot_gpu.h"', "int main(void){"]
+    for cname, ct in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in ct._fields_:
+            lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                        text=True).stdout.splitlines())
+    for cname, ct in structs.items():
+        assert int(out[cname]) == C.sizeof(ct), cname
+        for fname, _ in ct._fields_:
+            assert int(out[f"{cname}.{fname}"]) == getattr(ct, fname).offset, (cname, fname)
