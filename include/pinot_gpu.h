@@ -181,6 +181,14 @@ typedef struct {
    * this launch.  Bounds integer SUM cells: with max|dictionary value| x reduce_docs >= 2^62 an INT / LONG SUM
    * is carried as three exact 21-bit-part sums (see pgpu_table_layout.agg_sum_parts). */
   int64_t reduce_docs;
+  /* Group-key holder limits (InstancePlanMakerImplV2 num.groups.limit / max.init.group.holder.capacity,
+   * core/plan/maker/InstancePlanMakerImplV2.java:66-88).  A segment whose local cardinality product exceeds both
+   * can meet more than num_groups_limit distinct keys; the reference then keeps only the first-seen ones
+   * (DictionaryBasedGroupKeyGenerator.java:137-164, :384-463).  Such segments' distinct keys are counted on the
+   * GPU, and a segment that really exceeds the limit makes the query return PGPU_E_UNSUPPORTED (the server keeps
+   * the CPU plan, which reproduces the truncation).  0 = no limit. */
+  int32_t num_groups_limit;
+  int32_t array_based_threshold;
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
@@ -193,6 +201,15 @@ typedef struct {
 /* Carry every INT / LONG SUM / AVG as three 21-bit-part sums whatever the bound says (multi-GPU callers set it
  * on every rank when any rank's bound needs it, so that all ranks share one table layout). */
 #define PGPU_Q_SUM_SPLIT 8ull
+/* Group-by through the hash table (PGPU_KEYS_HASH) whatever the key space; chosen by default for key spaces
+ * above 2^31 keys, for sparse occupancy, and when a segment's distinct keys must be counted (num_groups_limit). */
+#define PGPU_Q_HASH 16ull
+/* numEntriesScannedInFilter exactly as the reference's iterators count it (see pgpu_filter_entries_scanned):
+ * every leaf of every segment's filter is also evaluated over all docs into a bitmap, and the iterator tree is
+ * replayed on the host in pgpu_query_wait.  Without it the statistic is the GPU's own count of evaluated
+ * forward-index entries, which equals the reference's except under leap-frogging iterators (an AND of several
+ * scan leaves, an OR / NOT advanced by a parent AND); pgpu_query_stats.filter_stats_exact tells which. */
+#define PGPU_Q_EXACT_FILTER_STATS 32ull
 
 /* ---- partial-result table ----------------------------------------------------------------------------------
  * A query produces a dense table over G = prod(group_cardinalities) keys (G = 1 for aggregation only), laid out
@@ -218,39 +235,57 @@ typedef struct {
 #define PGPU_RED_MIN_I64 2
 #define PGPU_RED_MAX_I64 3
 
+/* key_kind of a table layout */
+#define PGPU_KEYS_DENSE 0 /* cell index = global raw key: sum_j gid_j * prod_{k<j} card_k (< 2^31) */
+#define PGPU_KEYS_HASH 1  /* cell index = hash slot; the slot's key words follow the sections (below) */
+
 typedef struct {
-  uint64_t num_keys;       /* G */
+  uint64_t num_keys;       /* G: keys (dense) or hash slots (hash) */
   int32_t num_sections;
   int32_t section_op[PGPU_MAX_SECTIONS]; /* PGPU_RED_* per section (section 0 = count) */
   int32_t agg_section[16]; /* section of agg i, or 0 for COUNT */
   int32_t agg_value_type[16]; /* stored type of the agg column (PGPU_INT..), -1 for COUNT */
   int32_t agg_sum_parts[16];  /* SUM / AVG of INT / LONG: 1 = one exact int64 section, 3 = 21-bit-part sections */
+  /* Group keys.  Dense: the cell index is the key.  Hash: key_words int64 words per slot follow the sections
+   * (word w of slot i at int64 index (num_sections + w) * num_keys + i; an empty slot holds -1).  Word 0 is the
+   * mixed-radix key of group columns [0, key_split), word 1 (when key_words == 2, key spaces above 2^63, the
+   * reference's ArrayMapBasedHolder, DictionaryBasedGroupKeyGenerator.java:137-146) that of [key_split, n). */
+  int32_t key_kind;
+  int32_t key_words;
+  int32_t key_split;
+  int32_t reserved;
 } pgpu_table_layout;
+
+/* Bytes of the partial table of a layout: 8 * (num_sections [+ key_words when hash]) * num_keys. */
+uint64_t pgpu_table_bytes(const pgpu_table_layout* layout);
 
 int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out);
 
 typedef struct {
   int64_t num_docs_scanned;              /* docs matching the filter (AggregationOperator.java:82-87) */
-  int64_t num_entries_scanned_in_filter; /* forward-index entries the GPU filter evaluated */
+  int64_t num_entries_scanned_in_filter; /* GPU-evaluated forward-index entries, or the reference's count */
   int64_t num_total_docs;
   int64_t num_segments_matched;          /* reserved (0): per-segment match counts are not tracked */
   int64_t sparse_sector_bytes;           /* PGPU_Q_STATS: 32-B sectors touched by sparse reads * 32 */
   int64_t dense_bytes;                   /* forward-index bytes streamed in dense (staged) mode */
   double kernel_ms;                      /* main query kernel time (HIP events on the query stream) */
+  int64_t filter_stats_exact;            /* 1: num_entries_scanned_in_filter is the reference's figure */
 } pgpu_query_stats;
 
-/* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the dense partial
- * table in caller-provided device memory `dev_table` (table_bytes >= 8 * num_sections * G).  Does not
- * synchronize.  Used for multi-GPU combine: the caller RCCL-reduces the sections, then calls
- * pgpu_table_compact.  Stats become valid after pgpu_query_wait. */
+/* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the partial table in
+ * caller-provided device memory `dev_table` (table_bytes >= pgpu_table_bytes(layout)).  Does not synchronize.
+ * Used for multi-GPU combine: the caller RCCL-reduces the sections of a dense table (hash tables are compacted
+ * first and merged by key), then calls pgpu_table_compact.  Stats become valid after pgpu_query_wait, which
+ * returns PGPU_E_UNSUPPORTED when a segment met more distinct group keys than num_groups_limit. */
 typedef struct pgpu_query pgpu_query;
 int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
                       uint64_t table_bytes, pgpu_query** out_query);
 int pgpu_query_wait(pgpu_query* query, pgpu_query_stats* out_stats);
 int pgpu_query_release(pgpu_query* query);
 
-/* Compact a (reduced) dense table: copy every key with count > 0 to the host, ascending by key.
- *   out_keys  : int64[capacity]               (global raw key)
+/* Compact a (reduced) table: copy every key with count > 0 to the host (dense: ascending by key; hash: in slot
+ * order).
+ *   out_keys  : int64[capacity * key_words]   (global raw key words, row-major; key_words = 1 for dense)
  *   out_cells : int64[capacity * num_sections] row-major (section 0 = count, then sections in layout order;
  *               float64 sections are bit-cast into the int64 cells)
  * *out_num_groups receives the number of non-empty keys; if it exceeds capacity nothing beyond is written
@@ -320,6 +355,15 @@ int pgpu_query_launch_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pg
 /* Convenience: submit + collect. */
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
                        uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);
+
+/* ---- reference execution statistics ---------------------------------------------------------------------
+ * numEntriesScannedInFilter as the reference's iterators count it (SVScanDocIdIterator.java:57-98 under
+ * AndDocIdSet.java:60-146 / OrDocIdSet.java:58-110 and the And / Or / Not iterators): the segment's filter program
+ * (prefix order, as in pgpu_segment_plan) driven over host bitmaps of its leaves' matches -- leaf k in prefix order,
+ * doc d at bit d % 32 of leaf_bits[k][d / 32].  The query path computes the same figure itself when the query
+ * carries PGPU_Q_EXACT_FILTER_STATS (leaf bitmaps made on the GPU); this entry point is the host routine it uses. */
+int pgpu_filter_entries_scanned(const pgpu_filter_node* nodes, int32_t num_nodes, const uint32_t* const* leaf_bits,
+                                int32_t num_leaves, int32_t num_docs, int64_t* out);
 
 /* MIN/MAX order-preserving key -> double (value_type = stored type of the aggregated column). */
 double pgpu_decode_minmax_key(int64_t key, int32_t value_type);

@@ -29,7 +29,9 @@ PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
 PGPU_PRED_RANGE, PGPU_PRED_SET = 0, 1
 PGPU_AGG_COUNT, PGPU_AGG_SUM, PGPU_AGG_MIN, PGPU_AGG_MAX, PGPU_AGG_AVG = range(5)
 PGPU_RED_SUM_I64, PGPU_RED_SUM_F64, PGPU_RED_MIN_I64, PGPU_RED_MAX_I64 = range(4)
-PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT = 1, 2, 4, 8
+PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH = 1, 2, 4, 8, 16
+PGPU_Q_EXACT_FILTER_STATS = 32
+PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
 ABI_VERSION = 2
 
@@ -66,19 +68,22 @@ class QueryDesc(C.Structure):
     _fields_ = [("num_columns", C.c_int32), ("num_segments", C.c_int32), ("segments", C.POINTER(SegmentPlan)),
                 ("num_aggs", C.c_int32), ("num_group_columns", C.c_int32), ("aggs", C.POINTER(Agg)),
                 ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
-                ("flags", C.c_uint64), ("reduce_docs", C.c_int64)]
+                ("flags", C.c_uint64), ("reduce_docs", C.c_int64), ("num_groups_limit", C.c_int32),
+                ("array_based_threshold", C.c_int32)]
 
 
 class TableLayout(C.Structure):
     _fields_ = [("num_keys", C.c_uint64), ("num_sections", C.c_int32), ("section_op", C.c_int32 * 17),
                 ("agg_section", C.c_int32 * 16), ("agg_value_type", C.c_int32 * 16),
-                ("agg_sum_parts", C.c_int32 * 16)]
+                ("agg_sum_parts", C.c_int32 * 16), ("key_kind", C.c_int32), ("key_words", C.c_int32),
+                ("key_split", C.c_int32), ("reserved", C.c_int32)]
 
 
 class QueryStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_total_docs", C.c_int64), ("num_segments_matched", C.c_int64),
-                ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double)]
+                ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double),
+                ("filter_stats_exact", C.c_int64)]
 
 
 PGPU_X_PRED, PGPU_X_AND, PGPU_X_OR, PGPU_X_NOT = range(4)
@@ -114,6 +119,7 @@ SIGNATURES = [
     ("pgpu_remap_upload", C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),
     ("pgpu_buffer_release", C.c_int, [_P]),
     ("pgpu_table_layout_of", C.c_int, [C.POINTER(QueryDesc), C.POINTER(TableLayout)]),
+    ("pgpu_table_bytes", C.c_uint64, [C.POINTER(TableLayout)]),
     ("pgpu_query_launch", C.c_int, [_P, C.POINTER(QueryDesc), _P, _P, C.c_uint64, C.POINTER(_P)]),
     ("pgpu_query_wait", C.c_int, [_P, C.POINTER(QueryStats)]),
     ("pgpu_query_release", C.c_int, [_P]),
@@ -128,6 +134,8 @@ SIGNATURES = [
     ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_decode_minmax_key", C.c_double, [C.c_int64, C.c_int32]),
+    ("pgpu_filter_entries_scanned", C.c_int, [C.POINTER(FilterNode), C.c_int32, C.POINTER(C.POINTER(C.c_uint32)),
+                                             C.c_int32, C.c_int32, C.POINTER(C.c_int64)]),
     ("pgpu_kernel_geometry", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
 ]
 
@@ -167,6 +175,10 @@ def check(rc: int) -> None:
         if rc == PGPU_E_UNSUPPORTED:
             raise UnsupportedPlanError(rc, msg)
         raise PinotGpuError(rc, msg)
+
+
+def table_bytes(layout: TableLayout) -> int:
+    return int(load().pgpu_table_bytes(C.byref(layout)))
 
 
 def decode_minmax_key(key: int, value_type: int) -> float:

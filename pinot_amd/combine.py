@@ -31,7 +31,8 @@ import numpy as np
 from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
-from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, finish, merge_filtered)
+from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, finish, key_words_out,
+                   merge_filtered)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
@@ -159,6 +160,32 @@ def minmax_key(value: float, vtype: int) -> int:
     return b if b >= 0 else b ^ 0x7FFFFFFFFFFFFFFF
 
 
+def merge_rows(keys: np.ndarray, cells: np.ndarray, L: TableLayout):
+    """Rows with equal keys merged section by section (AggregationFunction.merge on the cells): count and
+    integer sums add, float sums add as doubles, MIN / MAX keys take the min / max."""
+    if len(keys) == 0:
+        return keys.reshape(0, keys.shape[1] if keys.ndim == 2 else 1), cells
+    k2 = keys.reshape(len(keys), -1)
+    uniq, inv = np.unique(k2, axis=0, return_inverse=True)
+    inv = np.asarray(inv).reshape(-1)
+    out = np.empty((len(uniq), cells.shape[1]), dtype=np.int64)
+    for s, op in enumerate(section_ops(L)):
+        col = cells[:, s]
+        if op == PGPU_RED_SUM_F64:
+            acc = np.zeros(len(uniq), dtype=np.float64)
+            np.add.at(acc, inv, col.view(np.float64))
+            out[:, s] = acc.view(np.int64)
+        elif op == PGPU_RED_SUM_I64:
+            acc = np.zeros(len(uniq), dtype=np.int64)
+            np.add.at(acc, inv, col)
+            out[:, s] = acc
+        else:
+            acc = np.full(len(uniq), section_identity(op), dtype=np.int64)
+            (np.minimum if op == PGPU_RED_MIN_I64 else np.maximum).at(acc, inv, col)
+            out[:, s] = acc
+    return uniq, out
+
+
 STAT_FIELDS = ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
                "num_total_docs", "num_segments_processed", "sparse_sector_bytes", "dense_bytes")
 
@@ -234,16 +261,20 @@ class DistributedExecutor:
             self._docs[key] = hit
         return hit[0]
 
-    def _split_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int) -> int:
-        """PGPU_Q_SUM_SPLIT on every rank when any rank's integer-SUM bound needs the split layout."""
-        key = (tuple((a.function, a.column) for a in query.aggregations), self._seg_key(segments))
+    def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int) -> int:
+        """Flags that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's integer-SUM bound
+        needs the split sections, PGPU_Q_HASH when any rank's key space takes the hash group-by."""
+        key = (tuple((a.function, a.column) for a in query.aggregations), tuple(query.group_by),
+               self._seg_key(segments))
         hit = self._split.get(key)
         if not self._agree(hit is not None):
             hit = None
         if hit is None:
             L = self._local_layout(query, segments, 0, reduce_docs)
-            need = any(L.agg_sum_parts[i] == 3 for i in range(len(query.aggregations)))
-            hit = (_lib.PGPU_Q_SUM_SPLIT if self._allreduce_i64([int(need)], "max")[0] else 0, tuple(segments))
+            split = any(L.agg_sum_parts[i] == 3 for i in range(len(query.aggregations)))
+            hashed = L.key_kind == _lib.PGPU_KEYS_HASH
+            s_any, h_any = self._allreduce_i64([int(split), int(hashed)], "max")
+            hit = ((_lib.PGPU_Q_SUM_SPLIT if s_any else 0) | (_lib.PGPU_Q_HASH if h_any else 0), tuple(segments))
             self._split[key] = hit
         return hit[0]
 
@@ -289,18 +320,20 @@ class DistributedExecutor:
         return {"num_docs_scanned": st.num_docs_scanned, "num_entries_scanned_in_filter":
                 st.num_entries_scanned_in_filter, "num_total_docs": st.num_total_docs,
                 "sparse_sector_bytes": st.sparse_sector_bytes, "dense_bytes": st.dense_bytes,
-                "kernel_ms": st.kernel_ms}
+                "kernel_ms": st.kernel_ms, "filter_stats_exact": st.filter_stats_exact}
 
     def _compact(self, L: TableLayout, table):
         cap = int(L.num_keys)
-        keys = np.empty(max(cap, 1), dtype=np.int64)
+        kw = key_words_out(L)
+        keys = np.empty(max(cap, 1) * kw, dtype=np.int64)
         cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
         ng = C.c_uint64()
         _lib.check(self.pm.ctx._lib.pgpu_table_compact(
             self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()), None,
             keys.ctypes.data_as(C.POINTER(C.c_int64)), cells.ctypes.data_as(C.POINTER(C.c_int64)), cap,
             C.byref(ng)))
-        return keys[: ng.value], cells[: ng.value]
+        n = ng.value
+        return (keys[: n * kw].reshape(n, kw) if kw > 1 else keys[:n]), cells[:n]
 
     def _sync_device(self):
         import torch
@@ -318,12 +351,12 @@ class DistributedExecutor:
             raise ValueError("every rank needs at least one segment")
         globals_ = self._global_dicts(query, segments) if query.group_by else []
         reduce_docs = self._reduce_docs(segments)
-        flags = self._split_flags(query, segments, reduce_docs)
+        flags = self._layout_flags(query, segments, reduce_docs)
         non_scan = self.pm.non_scan_segments(query, segments)
         scan = [s for s, ns in zip(segments, non_scan) if not ns]
         # the layout is the same on every rank: group cardinalities are global, the split-SUM choice agreed
         L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs)
-        n = int(L.num_sections * L.num_keys)
+        n = _lib.table_bytes(L) // 8 if L.key_kind == _lib.PGPU_KEYS_HASH else int(L.num_sections * L.num_keys)
         table = self._alloc_table(n)
         handle = None
         if scan:
@@ -373,13 +406,17 @@ class DistributedExecutor:
         scan_docs = stats["num_docs_scanned"] - sum(s.num_docs for s in p.non_scan)
         local = [stats["num_docs_scanned"], stats["num_entries_scanned_in_filter"],
                  scan_docs * len(query.projected_columns), stats["num_total_docs"], p.num_segments,
-                 stats["sparse_sector_bytes"], stats["dense_bytes"]]
-        tot = dict(zip(STAT_FIELDS, self._allreduce_i64(local)))
-        st = ExecutionStats(kernel_ms=stats["kernel_ms"], **tot)  # kernel time of this rank's launch
+                 stats["sparse_sector_bytes"], stats["dense_bytes"], 0 if stats.get("filter_stats_exact", 1) else 1]
+        sums = self._allreduce_i64(local)
+        tot = dict(zip(STAT_FIELDS, sums))
+        st = ExecutionStats(kernel_ms=stats["kernel_ms"], filter_stats_exact=sums[-1] == 0,  # this rank's kernel
+                            **tot)
         self.last_stats = st
         try:
             big = query.group_by and 8 * int(table.numel()) >= self.SCATTER_MIN_BYTES
-            if big:
+            if L.key_kind == _lib.PGPU_KEYS_HASH:
+                keys, cells = self._hash_merge_topk(p)
+            elif big:
                 keys, cells = self._scatter_topk(p)
             else:
                 reduce_sections(table, L, self.group)
@@ -389,10 +426,77 @@ class DistributedExecutor:
                 keys, cells = self._compact(L, table)
             if self.rank != 0:
                 return None
-            order = np.argsort(keys, kind="stable")
-            return finish(query, GroupTable(keys[order], cells[order], L), p.globals_, st)
+            if keys.ndim == 1:
+                order = np.argsort(keys, kind="stable")
+                keys, cells = keys[order], cells[order]
+            return finish(query, GroupTable.sorted(keys, cells, L), p.globals_, st)
         finally:
             self._tables.setdefault(int(table.numel()), []).append(table)
+
+    def _trim(self, query, L, keys, cells, globals_):
+        """This rank's candidate rows: its top max(5 * limit, TOPK_MIN) by the ORDER BY expressions (the rows'
+        values are final here), or that many smallest keys without ORDER BY."""
+        cap = max(5 * query.limit, self.TOPK_MIN)  # GroupByUtils.getTableCapacity
+        if len(keys) <= cap:
+            return keys, cells
+        t = GroupTable.sorted(keys, cells, L)
+        idx = np.sort(GroupColumns(query, t, globals_).order_and_limit(limit=cap)) if query.order_by else \
+            np.arange(cap)
+        return t.keys[idx], t.cells[idx]
+
+    def _gather_rows(self, keys, cells, L):
+        """All ranks' candidate rows (key words + cells) gathered on every rank (padded tensors)."""
+        import torch
+        import torch.distributed as dist
+        kw = 1 if keys.ndim == 1 else keys.shape[1]
+        n = len(keys)
+        width = kw + L.num_sections
+        pad = max(1, self._allreduce_i64([n], "max")[0])
+        mine = torch.zeros((pad, width), dtype=torch.int64)
+        if n:
+            mine[:n, :kw] = torch.from_numpy(np.ascontiguousarray(keys.reshape(n, kw), dtype=np.int64))
+            mine[:n, kw:] = torch.from_numpy(np.ascontiguousarray(cells))
+        counts = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=self.device), group=self.group)
+        bufs = [torch.zeros((pad, width), dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        dist.all_gather(bufs, mine.to(self.device), group=self.group)
+        rows = np.concatenate([b[: int(c.item())].cpu().numpy() for b, c in zip(bufs, counts)])
+        k = rows[:, 0].copy() if kw == 1 else np.ascontiguousarray(rows[:, :kw])
+        return k, np.ascontiguousarray(rows[:, kw:])
+
+    def _hash_merge_topk(self, p: "_DistPending"):
+        """Hash tables (slots differ per rank): compact locally, route every row to the rank owning its key
+        (hash of the key words), merge the partial rows by key there (the IndexedTable upsert of
+        GroupByOrderByCombineOperator.java:169-190), keep each rank's top-K, gather the candidates."""
+        import torch
+        import torch.distributed as dist
+        L, query = p.layout, p.query
+        keys, cells = self._compact(L, p.table)
+        kw = 1 if keys.ndim == 1 else keys.shape[1]
+        n = len(keys)
+        k2 = keys.reshape(n, kw).astype(np.uint64)
+        h = k2[:, 0].copy()
+        for w in range(1, kw):
+            h = h * np.uint64(0x9E3779B97F4A7C15) + k2[:, w]
+        h ^= h >> np.uint64(33)
+        h *= np.uint64(0xff51afd7ed558ccd)
+        h ^= h >> np.uint64(33)
+        dest = (h % np.uint64(self.world)).astype(np.int64)
+        order = np.argsort(dest, kind="stable")
+        width = kw + L.num_sections
+        rows = np.concatenate([keys.reshape(n, kw), cells], axis=1)[order] if n else np.zeros((0, width), np.int64)
+        send = np.bincount(dest, minlength=self.world).astype(np.int64)
+        send_t = torch.from_numpy(send).to(self.device)
+        recv_t = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(recv_t, send_t, group=self.group)
+        recv = recv_t.cpu().numpy()
+        out = torch.empty((int(recv.sum()), width), dtype=torch.int64, device=self.device)
+        dist.all_to_all_single(out, torch.from_numpy(np.ascontiguousarray(rows)).to(self.device),
+                               [int(x) for x in recv], [int(x) for x in send], group=self.group)
+        got = out.cpu().numpy()
+        mk, mc = merge_rows(got[:, :kw], got[:, kw:], L)
+        mk, mc = self._trim(query, L, mk[:, 0] if kw == 1 else mk, mc, p.globals_)
+        return self._gather_rows(mk, mc, L)
 
     def _scatter_topk(self, p: "_DistPending"):
         """Large group-by table: reduce-scatter, per-rank compaction and top-K, gather of the candidates."""
@@ -405,27 +509,8 @@ class DistributedExecutor:
         C.memmove(C.byref(CL), C.byref(L), C.sizeof(TableLayout))
         CL.num_keys = int(chunk.shape[1])
         keys, cells = self._compact(CL, chunk.reshape(-1).contiguous())
-        keys = keys + key0
-        cap = max(5 * query.limit, self.TOPK_MIN)  # GroupByUtils.getTableCapacity
-        if len(keys) > cap:
-            cols = GroupColumns(query, GroupTable(keys, cells, L), p.globals_)
-            idx = np.sort(cols.order_and_limit(limit=cap) if query.order_by else np.arange(cap))
-            keys, cells = keys[idx], cells[idx]
-        n = len(keys)
-        width = 1 + L.num_sections
-        sizes = self._allreduce_i64([n], "max")[0]
-        pad = max(1, sizes)
-        mine = torch.zeros((pad, width), dtype=torch.int64)
-        if n:
-            mine[:n, 0] = torch.from_numpy(keys.astype(np.int64))
-            mine[:n, 1:] = torch.from_numpy(np.ascontiguousarray(cells))
-        counts = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
-        dist.all_gather(counts, torch.tensor([n], dtype=torch.int64, device=self.device), group=self.group)
-        bufs = [torch.zeros((pad, width), dtype=torch.int64, device=self.device) for _ in range(self.world)]
-        dist.all_gather(bufs, mine.to(self.device), group=self.group)
-        rows = np.concatenate([b[: int(c.item())].cpu().numpy() for b, c in zip(bufs, counts)]) if pad else \
-            np.zeros((0, width), np.int64)
-        return rows[:, 0].copy(), np.ascontiguousarray(rows[:, 1:])
+        keys, cells = self._trim(query, L, keys + key0, cells, p.globals_)
+        return self._gather_rows(keys, cells, L)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Optional[QueryResult]:
         if self.world == 1:  # single GPU: the plan maker's own plan choice (filtered passes, non-scan segments)

@@ -32,7 +32,7 @@
 #define PGPU_NCONS_OF(dense) (PGPU_WAVES_OF(dense) - PGPU_NLOAD_OF(dense))
 #define PGPU_MAX_SLOTS 8        // per-consumer mask rows (filter slots + 1 scratch row)
 #define PGPU_MAX_AGGS 16
-#define PGPU_MAX_GCOLS 8
+#define PGPU_MAX_GCOLS 16
 #define PGPU_MAX_STAGE 6        // staged (LDS-streamed) columns per segment
 #define PGPU_RING_MAX 64        // ring slots (flag arrays are sized for this)
 #define PGPU_CQ_CAP 1280        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile):
@@ -115,6 +115,14 @@ struct DevSeg {
   int32_t f_nr[2];
   int32_t f_sneg[2];
   uint32_t f_rng[2][PGPU_SLICE_RANGES][2];
+  int32_t track;                  // HASH mode: 1 + row of this segment's distinct-key bitmap (0 = not counted)
+  // PGPU_Q_EXACT_FILTER_STATS: the leaves of the segment's whole (unsplit) filter program, in prefix order --
+  // instruction indexes at pool[leaf_begin, +leaf_len); leaf k's match bits at leaf_bits[leaf_bits_off +
+  // k * ntiles * 64 + tile * 64 + lane] (leafbits_kernel)
+  int32_t leaf_len;
+  int32_t leaf_begin;
+  int32_t pad_;
+  int64_t leaf_bits_off;
 };
 
 // Filter instruction with statically resolved mask slots.
@@ -177,6 +185,11 @@ struct DevAgg {
 #define PGPU_PART_LDS_BYTES (128 * 1024)   // phase-2 LDS table per partition (keys x sections x 8 B)
 #define PGPU_PART_MAX_PARTS 8192           // phase-1 LDS cursors (4 B each) must fit PGPU_LDS_TABLE_BYTES
 #define PGPU_PART_MAX_SECTIONS 5           // count + up to 4 value sections (part_reduce_kernel<NS>)
+// Hash group-by (PGPU_KEYS_HASH): the table's cells are indexed by an open-addressing slot (linear probing,
+// lock-free 64-bit CAS insert).  Keys of more than 63 bits are interned in two levels: word 0 (columns
+// [0, key_split)) gets a slot s0 in a first table, then the slot of (s0 << 32 | word 1) is the cell index.
+#define PGPU_MODE_HASH 4
+#define PGPU_HASH_EMPTY (~0ull)
 
 #define PGPU_STAT_MATCHED 0
 #define PGPU_STAT_SCANNED 1
@@ -224,11 +237,23 @@ struct DevParams {
   int32_t dslots;                 // direct: LDS slots per wave (dslots - 1 tiles in flight while one is filtered)
   int32_t min_instrs;             // direct: fewest DMA instructions of any segment's tile (counted vmcnt waits)
   int32_t pad2;
+  // HASH mode: key words follow the sections in `table` (word 0 at table + nsec * G; two-level keys: the
+  // interned word-0 values at + G); segmask = distinct-key bitmaps of the tracked segments ([rows][G / 32]);
+  // hflag[0] = a probe sequence ran out of slots (query fails)
+  uint32_t* segmask;
+  int32_t* hflag;
+  uint32_t* leaf_bits;            // PGPU_Q_EXACT_FILTER_STATS (see DevSeg::leaf_bits_off)
+  int32_t key_words;
+  int32_t key_split;
+  int32_t segmask_rows;
+  int32_t pad3;
+  uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
   uint32_t gstride[PGPU_MAX_GCOLS];
   int32_t sec_op[PGPU_MAX_SECTIONS];
 };
+static_assert(sizeof(DevParams) <= 4096, "DevParams is a kernel argument");
 
 #define PGPU_FLAG_STATS 1
 #define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)

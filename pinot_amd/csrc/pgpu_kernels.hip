@@ -498,6 +498,78 @@ FI void remap_ids(const int32_t* remap, uint32_t (&id)[N]) {
   for (int u = 0; u < N; ++u) id[u] = (uint32_t)gld(remap, id[u]);
 }
 
+// ---- hash group-by (PGPU_MODE_HASH) --------------------------------------------------------------------------------
+FI uint64_t hmix(uint64_t k) {  // 64-bit finaliser (murmur3 fmix64)
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+// Slot keys change once (empty -> key), by CAS; agent-scope loads see other XCDs' claims.  A stale empty read only
+// costs a failed CAS.
+FI uint64_t hload(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Slot of every live key in the open-addressing table `keys` (mask + 1 slots, linear probing): the slot already
+// holding the key, or the empty slot this lane claims with a 64-bit CAS.  Every first probe is issued before the
+// first compare.  A probe sequence that runs through the whole table sets hflag (the query fails, never hangs).
+template <int N>
+FI void hash_insert(uint64_t* keys, uint64_t mask, const uint64_t (&key)[N], uint32_t live, uint32_t (&slot)[N],
+                    int32_t* hflag) {
+  uint64_t h[N], cur[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    h[r] = hmix(key[r]) & mask;
+    cur[r] = ((live >> r) & 1u) ? hload(keys + h[r]) : 0ull;
+  }
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    slot[r] = 0;
+    if (!((live >> r) & 1u)) continue;
+    uint64_t hh = h[r], c = cur[r];
+    for (uint64_t it = 0;; ++it) {
+      if (c == key[r]) break;
+      if (c == PGPU_HASH_EMPTY) {
+        const uint64_t prev = atomicCAS((unsigned long long*)(keys + hh), (unsigned long long)PGPU_HASH_EMPTY,
+                                        (unsigned long long)key[r]);
+        if (prev == PGPU_HASH_EMPTY || prev == key[r]) break;
+      }
+      if (it >= mask) {
+        __hip_atomic_store(hflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hh = 0;
+        break;
+      }
+      hh = (hh + 1) & mask;
+      c = hload(keys + hh);
+    }
+    slot[r] = (uint32_t)hh;
+  }
+}
+// Cell slots of the live docs' group keys (words k0 / k1, see PGPU_MODE_HASH), then the segment's distinct-key bit.
+template <int N>
+FI void hash_slots(const DevParams& p, const uint64_t (&k0)[N], const uint64_t (&k1)[N], uint32_t live,
+                   int32_t track, uint32_t (&slot)[N]) {
+  uint64_t* w0 = (uint64_t*)(p.table + (size_t)p.nsec * p.G);
+  const uint64_t mask = p.G - 1;
+  if (p.key_words == 2) {
+    uint32_t s0[N];
+    hash_insert(w0 + p.G, mask, k0, live, s0, p.hflag);  // intern word 0
+    uint64_t c[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) c[r] = ((uint64_t)s0[r] << 32) | k1[r];
+    hash_insert(w0, mask, c, live, slot, p.hflag);
+  } else {
+    hash_insert(w0, mask, k0, live, slot, p.hflag);
+  }
+  if (track) {
+    uint32_t* row = p.segmask + (size_t)(track - 1) * (p.G >> 5);
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      if ((live >> r) & 1u) atomicOr(row + (slot[r] >> 5), 1u << (slot[r] & 31));
+  }
+}
+
 // Roaring probe for one doc (per-doc filter leaves): is `d` in the bitmap of dict id `id`?
 struct InvIndex {
   const uint32_t* dir;
@@ -823,6 +895,7 @@ struct Cons {
 // Scalars of the consumer's current segment (SGPRs); arrays stay behind `sg` and are read with cld.
 struct SegState {
   const DevSeg* sg;
+  int32_t track;  // HASH: distinct-key bitmap row + 1 (0 = not counted)
   const DevColumn* cols;
   const int32_t* const* remaps;
   int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
@@ -850,6 +923,7 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   ss.reg_col0 = cld(&sg->reg_col[0]);
   ss.reg_col1 = cld(&sg->reg_col[1]);
   ss.fast = cld(&sg->fast);
+  ss.track = cld(&sg->track);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
@@ -1157,7 +1231,30 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
   uint32_t key[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) key[u] = 0;
-  if (MODE != PGPU_MODE_AGG) {
+  if (MODE == PGPU_MODE_HASH) {
+    // 64-bit mixed-radix key words, then their hash slots: from here on the slot is the cell index
+    uint64_t k0[U], k1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) k0[u] = k1[u] = 0;
+    for (int g = 0; g < p.ngcols; ++g) {
+      const DevColumn c = col_of(ss, p.gcols[g]);
+      const int32_t* remap = cld(ss.remaps, g);
+      uint32_t id[U];
+      gather_ids(colref(c), doc, id);
+#pragma unroll
+      for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
+      remap_ids(remap, id);
+      const uint64_t st = p.gstride64[g];
+      if (g < p.key_split) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) k0[u] += (uint64_t)id[u] * st;
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) k1[u] += (uint64_t)id[u] * st;
+      }
+    }
+    hash_slots(p, k0, k1, m, ss.track, key);
+  } else if (MODE != PGPU_MODE_AGG) {
     for (int g = 0; g < p.ngcols; ++g) {
       const DevColumn c = col_of(ss, p.gcols[g]);
       const int32_t* remap = cld(ss.remaps, g);
@@ -1169,6 +1266,8 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
 #pragma unroll
       for (int u = 0; u < U; ++u) key[u] += id[u] * p.gstride[g];
     }
+  }
+  if (MODE != PGPU_MODE_AGG) {
     if (MODE == PGPU_MODE_PART) {
       uint32_t raw[U];
 #pragma unroll
@@ -2183,10 +2282,68 @@ __global__ __launch_bounds__(256) void prologue_kernel(const u32x4* __restrict__
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += ncopy * 256) dst[i] = src[i];
     return;
   }
+  // table sections (identities), then HASH key words (empty = -1; two-level keys: both tables), then the
+  // distinct-key bitmaps of the tracked segments
   const uint64_t n = p.G * (uint64_t)p.nsec;
+  const uint64_t nk = p.mode == PGPU_MODE_HASH ? p.G * (uint64_t)p.key_words : 0;
+  const uint64_t nm = p.segmask ? (uint64_t)p.segmask_rows * (p.G >> 5) : 0;
   const uint64_t nb = gridDim.x - ncopy;
-  for (uint64_t i = (blockIdx.x - ncopy) * 256ull + threadIdx.x; i < n; i += nb * 256)
-    p.table[i] = sec_identity(p.sec_op[i / p.G]);
+  for (uint64_t i = (blockIdx.x - ncopy) * 256ull + threadIdx.x; i < n + nk + nm; i += nb * 256) {
+    if (i < n) p.table[i] = sec_identity(p.sec_op[i / p.G]);
+    else if (i < n + nk) p.table[i] = -1;
+    else p.segmask[i - n - nk] = 0u;
+  }
+}
+
+// PGPU_Q_EXACT_FILTER_STATS: the match bits of every leaf of every segment's whole filter program over all its
+// docs (one wave per tile, leaves read straight from HBM), for the host replay of the reference's iterators
+// (pgpu_iterstats.cpp).
+__global__ __launch_bounds__(256) void leafbits_kernel(DevParams p) {
+  __shared__ uint32_t scratch[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = (int)blockIdx.x * 4 + wave;
+  if (tile >= p.total_tiles) return;
+  const Cursor c = cursor_at(p, tile);
+  SegState ss;
+  load_seg(p, c.seg, ss);
+  const int nleaf = cld(&ss.sg->leaf_len);
+  if (nleaf == 0) return;
+  const int leaf_begin = cld(&ss.sg->leaf_begin);
+  const int64_t off = cld(&ss.sg->leaf_bits_off);
+  TileCtx t;
+  t.ss = &ss;
+  t.slot = nullptr;
+  t.tile_in_seg = c.tile_in_seg;
+  t.doc0 = c.tile_in_seg * WT;
+  t.lane_doc0 = t.doc0 + 32 * lane;
+  {
+    const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+    t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+  }
+  int64_t dummy = 0;
+  for (int k = 0; k < nleaf; ++k) {
+    const DevInstr in = cld(p.instrs + cld(p.pool, leaf_begin + k));
+    uint32_t m = 0;
+    if (in.op == PGPU_I_SCAN) m = leaf_scan(p, t, in, t.valid, dummy);
+    else if (in.op == PGPU_I_INV) m = leaf_inv(p, t, in, scratch[wave]) & t.valid;
+    else if (in.op == PGPU_I_SORTED) m = leaf_sorted(p, t, in) & t.valid;
+    p.leaf_bits[off + (int64_t)k * c.ntiles * 64 + (int64_t)c.tile_in_seg * 64 + lane] = m;
+  }
+}
+
+// Distinct group keys of each tracked segment: popcount of its bitmap row (HASH mode, num_groups_limit).
+__global__ __launch_bounds__(256) void segcount_kernel(DevParams p, int64_t* out) {
+  const uint32_t* row = p.segmask + (size_t)blockIdx.x * (p.G >> 5);
+  int64_t c = 0;
+  for (uint64_t i = threadIdx.x; i < (p.G >> 5); i += 256) c += __popc(row[i]);
+  __shared__ int64_t red[256];
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 // Copy `words` int64 of a finished table into pinned host memory.
 __global__ __launch_bounds__(256) void export_kernel(const int64_t* __restrict__ src, int64_t* dst, uint64_t words) {
@@ -2227,8 +2384,26 @@ __global__ void compact_scan_kernel(int32_t* block_counts, int32_t nblocks, int6
   }
 }
 
-__global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t nsec, const int32_t* block_offsets,
-                                     int64_t* out_keys, int64_t* out_cells) {
+// Output keys: the cell index (dense), or the slot's key words (hash: kw = 1 plain; kw = 2 two-level, word 0
+// interned in the second key table).
+__device__ inline void write_key(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, uint64_t k,
+                                 int64_t* out) {
+  if (kw == 0) {
+    out[0] = (int64_t)k;
+    return;
+  }
+  const int64_t* w0 = table + (size_t)nsec * G;
+  if (kw == 1) {
+    out[0] = w0[k];
+    return;
+  }
+  const uint64_t c = (uint64_t)w0[k];
+  out[0] = w0[G + (c >> 32)];
+  out[1] = (int64_t)(c & 0xFFFFFFFFull);
+}
+
+__global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw,
+                                     const int32_t* block_offsets, int64_t* out_keys, int64_t* out_cells) {
   const uint64_t base = (uint64_t)blockIdx.x * CMP_PER_BLOCK;
   __shared__ int wbase[CMP_BLOCK / 64 + 1];
   __shared__ int running;
@@ -2250,7 +2425,7 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
     __syncthreads();
     if (f) {
       const int pos = wbase[wave] + below;
-      out_keys[pos] = (int64_t)k;
+      write_key(table, G, nsec, kw, k, out_keys + (size_t)pos * (kw > 1 ? kw : 1));
       for (int s = 0; s < nsec; ++s) out_cells[(size_t)pos * nsec + s] = table[(size_t)s * G + k];
     }
     __syncthreads();
@@ -2288,7 +2463,7 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
   hipError_t pgpu_launch_query_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);  \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st); \
   hipError_t pgpu_prepare_##NAME(size_t lds_bytes);
-PGPU_MODE_DECLS(agg) PGPU_MODE_DECLS(lds) PGPU_MODE_DECLS(global) PGPU_MODE_DECLS(part)
+PGPU_MODE_DECLS(agg) PGPU_MODE_DECLS(lds) PGPU_MODE_DECLS(global) PGPU_MODE_DECLS(part) PGPU_MODE_DECLS(hash)
 
 #if TU_HAS(0)
 PGPU_MODE_FUNCS(PGPU_MODE_AGG, agg)
@@ -2298,6 +2473,9 @@ PGPU_MODE_FUNCS(PGPU_MODE_LDS, lds)
 #endif
 #if TU_HAS(2)
 PGPU_MODE_FUNCS(PGPU_MODE_GLOBAL, global)
+#endif
+#if TU_HAS(4)
+PGPU_MODE_FUNCS(PGPU_MODE_HASH, hash)
 #endif
 #if TU_HAS(3)
 PGPU_MODE_FUNCS(PGPU_MODE_PART, part)
@@ -2372,6 +2550,7 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes) {
   if (e == hipSuccess) e = pgpu_prepare_lds(lds_bytes);
   if (e == hipSuccess) e = pgpu_prepare_global(lds_bytes);
   if (e == hipSuccess) e = pgpu_prepare_part(lds_bytes);
+  if (e == hipSuccess) e = pgpu_prepare_hash(lds_bytes);
   if (e == hipSuccess) e = pgpu_prepare_part_reduce();
   return e;
 }
@@ -2391,6 +2570,7 @@ hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipS
     case PGPU_MODE_LDS: return pgpu_launch_query_lds(p, grid, dyn_smem, st);
     case PGPU_MODE_GLOBAL: return pgpu_launch_query_global(p, grid, dyn_smem, st);
     case PGPU_MODE_PART: return pgpu_launch_query_part(p, grid, dyn_smem, st);
+    case PGPU_MODE_HASH: return pgpu_launch_query_hash(p, grid, dyn_smem, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2402,8 +2582,21 @@ hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_sme
     case PGPU_MODE_LDS: return pgpu_launch_direct_lds(p, grid, dyn_smem, st);
     case PGPU_MODE_GLOBAL: return pgpu_launch_direct_global(p, grid, dyn_smem, st);
     case PGPU_MODE_PART: return pgpu_launch_direct_part(p, grid, dyn_smem, st);
+    case PGPU_MODE_HASH: return pgpu_launch_direct_hash(p, grid, dyn_smem, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
+  if (p.total_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(leafbits_kernel, dim3((p.total_tiles + 3) / 4), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st) {
+  if (!p.segmask || p.segmask_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(segcount_kernel, dim3(p.segmask_rows), dim3(256), 0, st, p, out);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
@@ -2412,7 +2605,8 @@ hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void
   const int ncopy = std::max(1, std::min(16, (int)((n16 + 255) / 256)));
   int ninit = 0;
   if (init_table) {
-    const uint64_t n = p.G * (uint64_t)p.nsec;
+    const uint64_t n = p.G * (uint64_t)(p.nsec + (p.mode == PGPU_MODE_HASH ? p.key_words : 0)) +
+                       (p.segmask ? (uint64_t)p.segmask_rows * (p.G >> 5) : 0);
     ninit = (int)std::min<uint64_t>(4096, (n + 255) / 256);
     if (ninit < 1) ninit = 1;
   }
@@ -2432,7 +2626,7 @@ hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_o
   return hipGetLastError();
 }
 
-hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts,
+hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, int32_t* block_counts,
                                int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only,
                                hipStream_t st) {
   const int nb = (int)((G + CMP_PER_BLOCK - 1) / CMP_PER_BLOCK);
@@ -2440,7 +2634,7 @@ hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, i
     hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, block_counts);
     hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(64), 0, st, block_counts, nb, total);
   } else {
-    hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, nsec, block_counts,
+    hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, nsec, kw, block_counts,
                        out_keys, out_cells);
   }
   return hipGetLastError();

@@ -38,8 +38,14 @@ hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, in
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
                                 bool init_table, hipStream_t st);
 hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
-hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t* block_counts, int64_t* total,
-                               int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
+hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, int32_t* block_counts,
+                               int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
+hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
+hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
+// pgpu_iterstats.cpp
+int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
+                                  int num_leaves, int32_t num_docs);
+bool pgpu_filter_count_is_reference(const pgpu_filter_node* nodes, int num_nodes);
 
 namespace {
 
@@ -137,7 +143,9 @@ struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof, recs, rcount;
-  PinnedMem h_arena, h_stats, h_total, h_table;
+  DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
+  DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
+  PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
   bool busy = false;
   ~Workspace() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -210,6 +218,18 @@ struct pgpu_query {
   Workspace* tws = nullptr;
   pgpu_table_layout layout{};
   bool small = false;
+  // HASH mode: tracked segments (query segment index) whose distinct keys are checked against the limit
+  std::vector<int32_t> tracked;
+  int64_t groups_limit = 0;
+  // PGPU_Q_EXACT_FILTER_STATS: each segment's program (ids copied) and where its leaf bitmaps are
+  struct FilterReplay {
+    std::vector<pgpu_filter_node> nodes;
+    std::vector<std::vector<int32_t>> ids;
+    int32_t num_docs = 0, num_leaves = 0, ntiles = 0;
+    int64_t bits_off = 0;
+  };
+  std::vector<FilterReplay> replay;
+  bool exact_filter = false;
   hipEvent_t done = nullptr;  // submitted queries: recorded after the last copy of this query
 };
 
@@ -326,12 +346,97 @@ hipError_t upload(DevMem& m, const void* src, size_t bytes, size_t alloc_bytes, 
   return e;
 }
 
+// Local cardinality product of the group columns in segment plan `sp` (saturating at 2^126).
+unsigned __int128 local_key_space(const pgpu_query_desc* q, const pgpu_segment_plan& sp) {
+  unsigned __int128 P = 1;
+  for (int g = 0; g < q->num_group_columns; ++g) {
+    const int32_t slot = sp.column_map ? sp.column_map[q->group_columns[g]] : -1;
+    const pgpu_segment* sg = sp.segment;
+    const int32_t card = (sg && slot >= 0 && slot < (int32_t)sg->cols.size()) ? std::max(1, sg->cols[slot].card) : 1;
+    P *= (unsigned __int128)card;
+    if (P > ((unsigned __int128)1 << 126)) P = (unsigned __int128)1 << 126;
+  }
+  return P;
+}
+
+// DictionaryBasedGroupKeyGenerator's holder choice for one segment (DictionaryBasedGroupKeyGenerator.java:137-164):
+// a map-based holder (product above the array threshold) stops at num_groups_limit distinct keys, so such a
+// segment whose product also exceeds the limit must have its distinct keys counted.
+bool segment_needs_count(const pgpu_query_desc* q, const pgpu_segment_plan& sp) {
+  if (q->num_group_columns == 0 || q->num_groups_limit <= 0) return false;
+  const unsigned __int128 P = local_key_space(q, sp);
+  return P > (unsigned __int128)std::max(0, q->array_based_threshold) &&
+         P > (unsigned __int128)q->num_groups_limit;
+}
+
+// Table shape of the group keys: dense (cell = mixed-radix key) or hash slots (key words stored per slot).
+int group_key_space(const pgpu_query_desc* q, pgpu_table_layout* out) {
+  out->key_kind = PGPU_KEYS_DENSE;
+  out->key_words = 1;
+  out->key_split = q->num_group_columns;
+  out->num_keys = 1;
+  if (q->num_group_columns == 0) return PGPU_OK;
+  unsigned __int128 G = 1;
+  const unsigned __int128 cap126 = (unsigned __int128)1 << 126;
+  for (int i = 0; i < q->num_group_columns; ++i) {
+    const int32_t c = q->group_cardinalities ? q->group_cardinalities[i] : 0;
+    if (c < 1) return fail(PGPU_E_INVALID, "group column %d cardinality %d", i, c);
+    G *= (unsigned __int128)c;
+    if (G > cap126) G = cap126;
+  }
+  // distinct keys the launch can meet: per segment its local key space, bounded by the holder limit (a segment
+  // beyond it fails the query anyway) and by its docs
+  double est = 0;
+  bool track = false;
+  for (int s = 0; s < q->num_segments; ++s) {
+    const pgpu_segment_plan& sp = q->segments[s];
+    const double P = (double)local_key_space(q, sp);
+    double b = P;
+    if (q->num_groups_limit > 0 && P > (double)std::max(0, q->array_based_threshold)) b = std::min(P, (double)q->num_groups_limit);
+    b = std::min(b, (double)(sp.segment ? sp.segment->num_docs : 0));
+    est += b;
+    track |= segment_needs_count(q, sp);
+  }
+  est = std::min(est, (double)G);
+  const bool hash = (q->flags & PGPU_Q_HASH) || track || G > ((unsigned __int128)1 << 31) ||
+                    ((double)G >= 65536.0 && (double)G > 8.0 * est);
+  if (!hash) {
+    out->num_keys = (uint64_t)G;
+    return PGPU_OK;
+  }
+  uint64_t slots = 64;
+  while ((double)slots < 2.0 * est) slots <<= 1;
+  if (slots > (1ull << 31)) return fail(PGPU_E_UNSUPPORTED, "hash group-by table of %llu slots", (unsigned long long)slots);
+  out->key_kind = PGPU_KEYS_HASH;
+  out->num_keys = slots;
+  if (G < ((unsigned __int128)1 << 63)) return PGPU_OK;
+  // above 2^63 keys (the reference's ArrayMapBasedHolder): word 0 = the longest prefix of columns below 2^63,
+  // word 1 = the rest, which must stay below 2^32 (the second level packs (interned word-0 slot << 32 | word 1))
+  unsigned __int128 pre = 1;
+  int split = 0;
+  while (split < q->num_group_columns && pre * (unsigned __int128)q->group_cardinalities[split] < ((unsigned __int128)1 << 63))
+    pre *= (unsigned __int128)q->group_cardinalities[split++];
+  unsigned __int128 rest = 1;
+  for (int i = split; i < q->num_group_columns; ++i) rest *= (unsigned __int128)q->group_cardinalities[i];
+  if (split == 0 || rest >= ((unsigned __int128)1 << 32))
+    return fail(PGPU_E_UNSUPPORTED, "group key of more than 95 bits");
+  out->key_words = 2;
+  out->key_split = split;
+  return PGPU_OK;
+}
+
 }  // namespace
 
 // =============================================================================================================
 extern "C" {
 
 int pgpu_abi_version(void) { return PGPU_ABI_VERSION; }
+
+uint64_t pgpu_table_bytes(const pgpu_table_layout* L) {
+  if (!L) return 0;
+  const uint64_t words = (uint64_t)L->num_sections + (L->key_kind == PGPU_KEYS_HASH ? (uint64_t)L->key_words : 0);
+  return 8ull * words * L->num_keys;
+}
 
 int pgpu_last_error(char* buf, size_t len) {
   if (buf && len) {
@@ -620,14 +725,8 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
     return fail(PGPU_E_UNSUPPORTED, "%d group-by columns", q->num_group_columns);
   if (q->num_segments < 1 || !q->segments) return fail(PGPU_E_INVALID, "no segments");
   memset(out, 0, sizeof(*out));
-  uint64_t G = 1;
-  for (int i = 0; i < q->num_group_columns; ++i) {
-    const int32_t c = q->group_cardinalities ? q->group_cardinalities[i] : 0;
-    if (c < 1) return fail(PGPU_E_INVALID, "group column %d cardinality %d", i, c);
-    G *= (uint64_t)c;
-    if (G > (1ull << 31)) return fail(PGPU_E_UNSUPPORTED, "group key space %llu exceeds the dense-table limit", G);
-  }
-  out->num_keys = G;
+  const int rc = group_key_space(q, out);
+  if (rc) return rc;
   out->num_sections = 1;
   out->section_op[0] = PGPU_RED_SUM_I64;
   const pgpu_segment* s0 = q->segments[0].segment;
@@ -706,6 +805,8 @@ struct Packer {
   int32_t max_instrs = 0;   // most DMA instructions of one tile
   int64_t tile_bytes = 0;   // largest staged bytes of one tile
   double est_matched = 0;   // estimated matched docs (LDS-table decision)
+  std::vector<int32_t> tracked;  // HASH: query segments whose distinct keys are counted (bitmap row order)
+  int64_t leaf_words = 0;        // PGPU_Q_EXACT_FILTER_STATS: 32-bit words of all leaf bitmaps
 };
 
 // Convert one prefix-order filter program into slot-resolved device instructions appended to pk.instrs.
@@ -1065,7 +1166,8 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   } else if (residual) {
     agg_mode = PGPU_AM_SPARSE;
   } else {
-    bool dense = true;
+    // the hash group-by computes 64-bit keys and slots per doc in the candidate path only
+    bool dense = p.mode != PGPU_MODE_HASH;
     for (int qc : aggcols)
       dense &= v.dev(qc)->kind == PGPU_COL_FIXED_BIT && sector_touch(rho, v.dev(qc)->bits) >= kDenseTouch;
     agg_mode = dense ? PGPU_AM_DENSE : PGPU_AM_SPARSE;
@@ -1220,7 +1322,6 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     ds.nreg = (int32_t)aggcols.size();
     for (size_t j = 0; j < aggcols.size(); ++j) ds.reg_col[j] = aggcols[j];
   }
-  (void)p;
   return PGPU_OK;
 }
 
@@ -1234,12 +1335,19 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   if (profile_enabled()) p.flags |= PGPU_FLAG_PROFILE;
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
+  uint64_t stride64 = 1;
+  if (L.key_kind == PGPU_KEYS_HASH) p.mode = PGPU_MODE_HASH;  // final; plan_segment reads it
+  p.key_words = L.key_words;
+  p.key_split = L.key_split;
   for (int g = 0; g < q->num_group_columns; ++g) {
     if (q->group_columns[g] < 0 || q->group_columns[g] >= q->num_columns)
       return fail(PGPU_E_INVALID, "group column %d", q->group_columns[g]);
     p.gcols[g] = q->group_columns[g];
+    if (g == L.key_split) stride64 = 1;  // second key word
     p.gstride[g] = stride;
+    p.gstride64[g] = stride64;
     stride *= (uint32_t)q->group_cardinalities[g];
+    stride64 *= (uint64_t)q->group_cardinalities[g];
   }
   // device aggregations: one per query aggregation, or one per part section of a split integer SUM
   p.nagg = 0;
@@ -1294,6 +1402,26 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     }
     int rc = plan_segment(q, sp, seg, p, pk, ds);
     if (rc) return rc;
+    ds.track = 0;
+    if (p.mode == PGPU_MODE_HASH && segment_needs_count(q, sp)) {
+      pk.tracked.push_back(s);
+      ds.track = (int32_t)pk.tracked.size();
+    }
+    ds.leaf_len = ds.leaf_begin = 0;
+    ds.leaf_bits_off = pk.leaf_words;
+    if ((q->flags & PGPU_Q_EXACT_FILTER_STATS) && sp.num_filter_nodes > 0) {
+      // the whole program once more, for its leaves' match bitmaps (leafbits_kernel)
+      const int base = (int)pk.instrs.size();
+      rc = convert_filter(q, sp, sp.filter, sp.num_filter_nodes, seg, pk);
+      if (rc) return rc;
+      ds.leaf_begin = (int32_t)pk.pool.size();
+      for (int i = base; i < (int)pk.instrs.size(); ++i) {
+        const int op = pk.instrs[i].op;
+        if (op == PGPU_I_SCAN || op == PGPU_I_INV || op == PGPU_I_SORTED) pk.pool.push_back(i);
+      }
+      ds.leaf_len = (int32_t)pk.pool.size() - ds.leaf_begin;
+      pk.leaf_words += (int64_t)ds.leaf_len * ds.ntiles * 64;
+    }
     pk.segs.push_back(ds);
     tiles += ds.ntiles;
     if (tiles > INT32_MAX / 2) return fail(PGPU_E_UNSUPPORTED, "too many docs in one launch");
@@ -1317,7 +1445,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
   if (rc) return rc;
-  const uint64_t need = 8ull * L.num_sections * L.num_keys;
+  const uint64_t need = pgpu_table_bytes(&L);
   if (!dev_table || table_bytes < need)
     return fail(PGPU_E_INVALID, "table buffer %llu bytes < %llu needed", (unsigned long long)table_bytes,
                 (unsigned long long)need);
@@ -1363,6 +1491,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31) &&
             L.num_sections <= PGPU_PART_MAX_SECTIONS;
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
+  else if (L.key_kind == PGPU_KEYS_HASH) p.mode = PGPU_MODE_HASH;
   else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && !(q->flags & PGPU_Q_PARTITION) &&
            (PGPU_LDS_LIMIT - fixed - align16(tbytes)) / S >= 4)
     p.mode = PGPU_MODE_LDS;
@@ -1463,7 +1592,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
   if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
-  if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS);
+  if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS + 16);
   if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   if (p.mode == PGPU_MODE_PART) {
@@ -1491,6 +1620,22 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "group-by record buffers: %s", hipGetErrorString(e)));
     p.recs = (uint32_t*)ws->recs.p;
     p.rcount = (uint32_t*)ws->rcount.p;
+  }
+  if (pk.leaf_words > 0) {
+    e = ws->leafbits.ensure(4ull * pk.leaf_words);
+    if (e == hipSuccess) e = ws->h_leafbits.ensure(4ull * pk.leaf_words);
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "filter-statistics bitmaps: %s", hipGetErrorString(e)));
+    p.leaf_bits = (uint32_t*)ws->leafbits.p;
+  }
+  if (p.mode == PGPU_MODE_HASH) {
+    p.segmask_rows = (int32_t)pk.tracked.size();
+    e = ws->hflag.ensure(16);
+    if (e == hipSuccess && p.segmask_rows) e = ws->segmask.ensure((size_t)p.segmask_rows * (L.num_keys / 8) + 16);
+    if (e == hipSuccess && p.segmask_rows) e = ws->h_segcnt.ensure(8 * (size_t)p.segmask_rows);
+    if (e == hipSuccess) e = hipMemsetAsync(ws->hflag.p, 0, 16, st);
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "hash group-by buffers: %s", hipGetErrorString(e)));
+    p.hflag = (int32_t*)ws->hflag.p;
+    p.segmask = p.segmask_rows ? (uint32_t*)ws->segmask.p : nullptr;
   }
   char* h = (char*)ws->h_arena.p;
   memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
@@ -1521,7 +1666,20 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
-  if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, L.num_keys * L.num_sections, st);
+  if (e == hipSuccess && p.mode == PGPU_MODE_HASH) {
+    // probe-overflow flag and the tracked segments' distinct-key counts, into pinned host memory
+    void* h_cnt_dev = nullptr;
+    if (p.segmask_rows) {
+      e = hipHostGetDevicePointer(&h_cnt_dev, ws->h_segcnt.p, 0);
+      if (e == hipSuccess) e = pgpu_launch_segcount(p, (int64_t*)h_cnt_dev, st);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync((char*)ws->h_stats.p + 8 * PGPU_NSTATS, ws->hflag.p, 4, hipMemcpyDeviceToHost, st);
+  }
+  if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, pgpu_table_bytes(&L) / 8, st);
+  if (e == hipSuccess && pk.leaf_words > 0) {
+    e = pgpu_launch_leafbits(p, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(ws->h_leafbits.p, ws->leafbits.p, 4ull * pk.leaf_words, hipMemcpyDeviceToHost, st);
+  }
   // completion of this query alone (later queries may already be queued behind it on the same stream)
   if (e == hipSuccess) e = hipEventRecord(ws->done, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
@@ -1537,6 +1695,29 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   int64_t tot_docs = 0;
   for (int s = 0; s < q->num_segments; ++s) tot_docs += q->segments[s].segment->num_docs;
   qq->stats.num_total_docs = tot_docs;
+  qq->tracked = pk.tracked;
+  qq->groups_limit = q->num_groups_limit;
+  qq->exact_filter = pk.leaf_words > 0;
+  bool exact = true;
+  for (int s = 0; s < q->num_segments; ++s) {
+    const pgpu_segment_plan& sp = q->segments[s];
+    exact = exact && pgpu_filter_count_is_reference(sp.filter, sp.num_filter_nodes);
+    if (!qq->exact_filter) continue;
+    pgpu_query::FilterReplay r;
+    r.nodes.assign(sp.filter, sp.filter + sp.num_filter_nodes);
+    r.ids.resize(sp.num_filter_nodes);
+    for (int i = 0; i < sp.num_filter_nodes; ++i) {
+      const int k = sp.filter[i].op == PGPU_F_SORTED ? 2 * sp.filter[i].num_ids : sp.filter[i].num_ids;
+      if (sp.filter[i].ids && k > 0) r.ids[i].assign(sp.filter[i].ids, sp.filter[i].ids + k);
+      r.nodes[i].ids = nullptr;
+    }
+    r.num_docs = sp.segment->num_docs;
+    r.num_leaves = pk.segs[s].leaf_len;
+    r.ntiles = pk.segs[s].ntiles;
+    r.bits_off = pk.segs[s].leaf_bits_off;
+    qq->replay.push_back(std::move(r));
+  }
+  qq->stats.filter_stats_exact = exact ? 1 : 0;
   *out_query = qq;
   return PGPU_OK;
 }
@@ -1560,6 +1741,38 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
+  if (qq->exact_filter) {
+    // the reference's iterators replayed over the leaves' bitmaps (pgpu_iterstats.cpp)
+    const uint32_t* bits = (const uint32_t*)qq->ws->h_leafbits.p;
+    int64_t total = 0;
+    for (const pgpu_query::FilterReplay& r : qq->replay) {
+      std::vector<const uint32_t*> leaf(r.num_leaves);
+      for (int k = 0; k < r.num_leaves; ++k) leaf[k] = bits + r.bits_off + (int64_t)k * r.ntiles * 64;
+      const int64_t c = reference_entries_scanned(r.nodes.data(), (int)r.nodes.size(), leaf.data(), r.num_leaves,
+                                                  r.num_docs);
+      if (c < 0) return fail(PGPU_E_INVALID, "filter program cannot be replayed for statistics");
+      total += c;
+    }
+    qq->stats.num_entries_scanned_in_filter = total;
+    qq->stats.filter_stats_exact = 1;
+  }
+  if (qq->params.mode == PGPU_MODE_HASH) {
+    int32_t flag = 0;
+    memcpy(&flag, (const char*)qq->ws->h_stats.p + 8 * PGPU_NSTATS, 4);
+    if (flag) {
+      if (out_stats) *out_stats = qq->stats;
+      return fail(PGPU_E_UNSUPPORTED, "hash group-by table overflow (more distinct keys than the holder limits allow)");
+    }
+    const int64_t* cnt = (const int64_t*)qq->ws->h_segcnt.p;
+    for (size_t i = 0; i < qq->tracked.size(); ++i)
+      if (cnt[i] > qq->groups_limit) {
+        if (out_stats) *out_stats = qq->stats;
+        return fail(PGPU_E_UNSUPPORTED,
+                    "segment %d meets %lld distinct group keys > numGroupsLimit %lld: the reference keeps the "
+                    "first-seen keys only (DictionaryBasedGroupKeyGenerator); served by the CPU plan",
+                    qq->tracked[i], (long long)cnt[i], (long long)qq->groups_limit);
+      }
+  }
   if (qq->params.flags & PGPU_FLAG_PROFILE) {
     const int nw = qq->grid * (qq->params.direct ? 4 : PGPU_WAVES_OF(qq->params.dense));
     std::vector<int64_t> pr((size_t)nw * PGPU_NPROF);
@@ -1602,11 +1815,13 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
                  uint64_t* out_num_groups) {
   const uint64_t G = L->num_keys;
   const int nsec = L->num_sections;
+  const int kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;  // 0: the cell index is the key
+  const int okw = kw > 1 ? kw : 1;
   const uint64_t nb = (G + 4095) / 4096;
   HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16));
   HIP_TRY(ws->cmp_total.ensure(16));
   HIP_TRY(ws->h_total.ensure(16));
-  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, (int32_t*)ws->cmp_counts.p,
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p,
                               (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st));
   HIP_TRY(hipMemcpyAsync(ws->h_total.p, ws->cmp_total.p, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -1616,11 +1831,11 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
     return fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
                 (unsigned long long)capacity);
   if (n == 0) return PGPU_OK;
-  HIP_TRY(ws->cmp_keys.ensure(8 * n));
+  HIP_TRY(ws->cmp_keys.ensure(8 * n * okw));
   HIP_TRY(ws->cmp_cells.ensure(8 * n * nsec));
-  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, (int32_t*)ws->cmp_counts.p, nullptr,
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p, nullptr,
                               (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st));
-  HIP_TRY(hipMemcpyAsync(out_keys, ws->cmp_keys.p, 8 * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out_keys, ws->cmp_keys.p, 8 * n * okw, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(out_cells, ws->cmp_cells.p, 8 * n * nsec, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   (void)ctx;
@@ -1984,7 +2199,7 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   int err = 0;
   Workspace* tws = acquire_ws(ctx, &err);  // owns the partial table until pgpu_query_collect
   if (!tws) return err;
-  const uint64_t bytes = 8ull * L.num_sections * L.num_keys;
+  const uint64_t bytes = pgpu_table_bytes(&L);
   hipError_t e = tws->table.ensure(bytes);
   if (e != hipSuccess) {
     release_ws(ctx, tws);
@@ -2024,11 +2239,22 @@ int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, ui
     const int64_t* t = (const int64_t*)qq->tws->h_table.p;
     const uint64_t G = L.num_keys;
     const int nsec = L.num_sections;
+    const bool hash = L.key_kind == PGPU_KEYS_HASH;
+    const int okw = hash && L.key_words == 2 ? 2 : 1;
+    const int64_t* w0 = t + (size_t)nsec * G;
     uint64_t n = 0;
     for (uint64_t k = 0; k < G; ++k) {
       if (t[k] <= 0) continue;
       if (n < capacity) {
-        out_keys[n] = (int64_t)k;
+        if (!hash) {
+          out_keys[n] = (int64_t)k;
+        } else if (okw == 1) {
+          out_keys[n] = w0[k];
+        } else {  // two-level key: (interned word-0 slot << 32 | word 1)
+          const uint64_t c = (uint64_t)w0[k];
+          out_keys[2 * n] = w0[G + (c >> 32)];
+          out_keys[2 * n + 1] = (int64_t)(c & 0xFFFFFFFFull);
+        }
         for (int sc = 0; sc < nsec; ++sc) out_cells[n * nsec + sc] = t[(size_t)sc * G + k];
       }
       ++n;

@@ -15,9 +15,11 @@ Mirrors the reference's per-segment planning and hands the whole query to libpin
 * results -> final aggregation values (``AggregationFunction.extractFinalResult``) and the execution statistics
   (CombineOperatorUtils.setExecutionStatistics, core/operator/combine/CombineOperatorUtils.java:55-82).
 
-Group-count semantics: when a segment's key space can exceed ``numGroupsLimit`` in a map-based holder the
-reference keeps only the first-seen keys (DictionaryBasedGroupKeyGenerator.java:991-1016); that shape is
-reported as PGPU_E_UNSUPPORTED-equivalent (``UnsupportedPlanError``) so the server keeps its CPU plan.
+Group-count semantics: a segment whose map-based holder meets more than ``numGroupsLimit`` distinct keys keeps
+only the first-seen ones in the reference (DictionaryBasedGroupKeyGenerator.java:137-164, :991-1016).  The library
+counts the distinct keys of every segment whose key space could exceed the limit (hash group-by, include/
+pinot_gpu.h) and fails only a query where one really does, with PGPU_E_UNSUPPORTED (``UnsupportedPlanError``):
+the server keeps its CPU plan for it.
 """
 from __future__ import annotations
 
@@ -220,22 +222,36 @@ def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list
 @dataclass
 class ExecutionStats:
     num_docs_scanned: int = 0
-    num_entries_scanned_in_filter: int = 0   # GPU's own count of forward-index entries evaluated
+    num_entries_scanned_in_filter: int = 0   # the reference's count when filter_stats_exact, else the GPU's own
     num_entries_scanned_post_filter: int = 0
     num_total_docs: int = 0
     num_segments_processed: int = 0
     kernel_ms: float = 0.0
+    filter_stats_exact: bool = True          # num_entries_scanned_in_filter is the reference's figure
     sparse_sector_bytes: int = 0
     dense_bytes: int = 0
+
+
+def key_words_out(L: TableLayout) -> int:
+    """int64 words per compacted group key (pgpu_table_compact): 2 for two-word hash keys, else 1."""
+    return 2 if L.key_kind == _lib.PGPU_KEYS_HASH and L.key_words == 2 else 1
 
 
 @dataclass
 class GroupTable:
     """Compacted partial table: global keys + cells (section 0 = count, then one section per non-COUNT agg)."""
 
-    keys: np.ndarray          # int64 [n]
+    keys: np.ndarray          # int64 [n] (mixed-radix key) or [n, 2] (two key words, layout.key_split)
     cells: np.ndarray         # int64 [n, nsec]
     layout: TableLayout
+
+    @staticmethod
+    def sorted(keys: np.ndarray, cells: np.ndarray, layout: TableLayout) -> "GroupTable":
+        """Rows in ascending key order (hash tables compact in slot order; dense ones already are)."""
+        if layout.key_kind == _lib.PGPU_KEYS_HASH and len(keys):
+            order = np.lexsort((keys[:, 0], keys[:, 1])) if keys.ndim == 2 else np.argsort(keys, kind="stable")
+            keys, cells = keys[order], cells[order]
+        return GroupTable(keys, cells, layout)
 
 
 class QueryResult:
@@ -341,8 +357,12 @@ class GpuPlanMaker:
 
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
-                 collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False):
+                 collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False,
+                 exact_filter_stats: bool = False):
         self.ctx = ctx
+        # exact_filter_stats: numEntriesScannedInFilter as the reference's iterators count it, also where they
+        # leap-frog (PGPU_Q_EXACT_FILTER_STATS: one more pass over every filter leaf, replayed on the host)
+        self.exact_filter_stats = exact_filter_stats
         # host_planning: plan every segment's filter in Python (SegmentFilterPlanner) even when the library could
         # (numeric columns: pgpu_query_submit_expr plans all segments in C++ from the literals)
         self.host_planning = host_planning
@@ -387,18 +407,6 @@ class GpuPlanMaker:
         # the entry holds the segments themselves, so their uids stay theirs while it is cached
         self._global_dicts[key] = (glob, remaps, tuple(segments))
         return glob, remaps
-
-    def _check_group_limit(self, query: QueryContext, seg: GpuSegment) -> None:
-        prod = 1
-        for g in query.group_by:
-            prod *= seg.column(g).cardinality
-        if prod <= self.max_init_group_holder_capacity:
-            return  # ArrayBasedHolder: no limit
-        if prod <= self.num_groups_limit:
-            return  # map-based holder can never reach the limit
-        raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
-                                   f"segment {seg.name}: group key space {prod} exceeds numGroupsLimit "
-                                   f"{self.num_groups_limit}; first-seen truncation is served by the CPU plan")
 
     def filter_expr(self, query: QueryContext, segments: Sequence[GpuSegment]):
         """The query's filter as a pgpu_expr_node program (planned per segment inside the library), or None when
@@ -480,8 +488,6 @@ class GpuPlanMaker:
         cmaps = []
         flt = query.filter if plan_filters else None
         for seg in segments:
-            if query.group_by:
-                self._check_group_limit(query, seg)
             slots = seg.slots
             cmaps.append([slots[c] for c in columns] if columns else [0])
             starts.append(len(nodes))
@@ -520,8 +526,10 @@ class GpuPlanMaker:
                          segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
                          num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
                          group_columns=gcols, group_cardinalities=gcards,
-                         flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags | extra_flags,
-                         reduce_docs=reduce_docs)
+                         flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags | extra_flags |
+                         (_lib.PGPU_Q_EXACT_FILTER_STATS if self.exact_filter_stats else 0),
+                         reduce_docs=reduce_docs, num_groups_limit=self.num_groups_limit,
+                         array_based_threshold=self.max_init_group_holder_capacity)
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:
@@ -550,7 +558,8 @@ class GpuPlanMaker:
         """Wait for a submitted query and finish it (pgpu_query_collect + ORDER BY / LIMIT on the host)."""
         L = pending.layout
         cap = int(min(L.num_keys, 1 << 26))
-        keys = np.empty(max(cap, 1), dtype=np.int64)
+        kw = key_words_out(L)
+        keys = np.empty(max(cap, 1) * kw, dtype=np.int64)
         cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
         n = C.c_uint64()
         st = QueryStats()
@@ -558,14 +567,15 @@ class GpuPlanMaker:
         _lib.check(self.ctx._lib.pgpu_query_collect(h, keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                                     cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
                                                     C.byref(st)))
-        table = GroupTable(keys[: n.value], cells[: n.value], L)
+        table = GroupTable.sorted(keys[: n.value * kw].reshape(-1, kw) if kw > 1 else keys[: n.value],
+                                  cells[: n.value], L)
         query = pending.query
         stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
                                num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
                                num_total_docs=st.num_total_docs, num_segments_processed=pending.num_segments,
                                kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
-                               dense_bytes=st.dense_bytes)
+                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact))
         return finish(query, table, [g[0] for g in pending.globals_], stats)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
@@ -687,6 +697,7 @@ def merge_filtered(query: QueryContext, parts, results: Sequence[QueryResult]) -
         for f in ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
                   "kernel_ms", "sparse_sector_bytes", "dense_bytes"):
             setattr(st, f, getattr(st, f) + getattr(r.stats, f))
+        st.filter_stats_exact = st.filter_stats_exact and r.stats.filter_stats_exact
     st.num_total_docs = results[-1].stats.num_total_docs
     st.num_segments_processed = results[-1].stats.num_segments_processed
     res.aggregation_result = fin
@@ -702,10 +713,13 @@ class GroupColumns:
     def __init__(self, query: QueryContext, table: GroupTable, global_dicts: Sequence):
         self.query = query
         L = table.layout
-        k = table.keys.astype(np.int64, copy=True)
+        keys = np.asarray(table.keys, dtype=np.int64)
+        words = [keys[:, 0].copy(), keys[:, 1].copy()] if keys.ndim == 2 else [keys.copy()]
+        split = L.key_split if keys.ndim == 2 else len(global_dicts)
         self.values = []
-        for g in global_dicts:
+        for gi, g in enumerate(global_dicts):
             card = len(g)
+            k = words[0 if gi < split else 1]
             gid = k % card
             k //= card
             arr = np.asarray(g, dtype=object) if isinstance(g, list) else np.asarray(g)

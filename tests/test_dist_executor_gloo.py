@@ -117,63 +117,78 @@ def _layout(query, segments, flags, reduce_docs, globs):
 
 def _numpy_executor(pm):
     from oracle import engine
+    from pinot_amd._lib import PGPU_KEYS_HASH, PGPU_Q_HASH
     from pinot_amd.combine import DistributedExecutor, minmax_key, section_identity
 
     class NumpyExecutor(DistributedExecutor):
-        """The local kernel step in numpy (what pgpu_query_launch leaves in HBM)."""
+        """The local kernel step in numpy: the table pgpu_query_launch leaves in HBM (dense cells indexed by the
+        mixed-radix key, or -- PGPU_Q_HASH -- slots whose key words follow the sections)."""
 
         def _prepare_local(self, query, segments, flags, reduce_docs):
+            flags |= self.pm.query_flags
             globs = self._globals_of(query, segments)
             L = _layout(query, segments, flags, reduce_docs, globs)
+            ops = [L.section_op[k] for k in range(L.num_sections)]
+            st = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
+                  "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
+            per_seg = []
+            for s in segments:
+                ds = engine.DecodedSegment(s.data)
+                op = engine.build_physical(ds, query.filter)
+                docs = np.flatnonzero(engine.eval_mask(op, s.num_docs))
+                st["num_docs_scanned"] += len(docs)
+                st["num_total_docs"] += s.num_docs
+                st["num_entries_scanned_in_filter"] += engine.entries_scanned_in_filter(op, s.num_docs)[0]
+                key = np.zeros(len(docs), dtype=np.int64)
+                stride = 1
+                for g in query.group_by:
+                    glob = globs[g]
+                    vals = ds.values(g)
+                    if isinstance(glob, list):
+                        pos = {v: i for i, v in enumerate(glob)}
+                        gid = np.array([pos[vals[d]] for d in docs], dtype=np.int64)
+                    else:
+                        gid = np.searchsorted(glob, np.asarray(vals)[docs])
+                    key += gid * stride
+                    stride *= len(glob)
+                per_seg.append((ds, docs, key))
+            hashed = bool(query.group_by) and bool(flags & PGPU_Q_HASH)
+            if hashed:  # slots: the distinct keys, in a table of a power-of-two slot count
+                uniq = np.unique(np.concatenate([k for _, _, k in per_seg]))
+                slots = 64
+                while slots < 2 * len(uniq):
+                    slots *= 2
+                L.key_kind, L.key_words, L.num_keys = PGPU_KEYS_HASH, 1, slots
+            G = int(L.num_keys)
+            t = np.array([[section_identity(o)] * G for o in ops] + ([[-1] * G] if hashed else []), dtype=np.int64)
+            if hashed:
+                t[len(ops), : len(uniq)] = uniq
+            for ds, docs, key in per_seg:
+                cell = np.searchsorted(uniq, key) if hashed else key
+                np.add.at(t[0], cell, 1)
+                for i, a in enumerate(query.aggregations):
+                    sec = L.agg_section[i]
+                    if sec == 0:
+                        continue
+                    v = np.asarray(ds.values(a.column))[docs]
+                    o = L.section_op[sec]
+                    if o == PGPU_RED_SUM_I64:
+                        v = v.astype(np.int64)
+                        if L.agg_sum_parts[i] == 3:
+                            m = (1 << PGPU_PART_BITS) - 1
+                            for k, part in enumerate((v & m, (v >> PGPU_PART_BITS) & m, v >> (2 * PGPU_PART_BITS))):
+                                np.add.at(t[sec + k], cell, part)
+                        else:
+                            np.add.at(t[sec], cell, v)
+                    elif o == PGPU_RED_SUM_F64:
+                        np.add.at(t[sec].view(np.float64), cell, v.astype(np.float64))
+                    else:
+                        kv = np.array([minmax_key(float(x), L.agg_value_type[i]) for x in v], dtype=np.int64)
+                        (np.minimum if o == PGPU_RED_MIN_I64 else np.maximum).at(t[sec], cell, kv)
 
             def launch(table):
-                G, ops = int(L.num_keys), [L.section_op[k] for k in range(L.num_sections)]
-                t = np.array([[section_identity(o)] * G for o in ops], dtype=np.int64)
-                st = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
-                      "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
-                for s in segments:
-                    ds = engine.DecodedSegment(s.data)
-                    op = engine.build_physical(ds, query.filter)
-                    docs = np.flatnonzero(engine.eval_mask(op, s.num_docs))
-                    st["num_docs_scanned"] += len(docs)
-                    st["num_total_docs"] += s.num_docs
-                    st["num_entries_scanned_in_filter"] += engine.entries_scanned_in_filter(op, s.num_docs)[0]
-                    key = np.zeros(len(docs), dtype=np.int64)
-                    stride = 1
-                    for g in query.group_by:
-                        glob = globs[g]
-                        vals = ds.values(g)
-                        if isinstance(glob, list):
-                            pos = {v: i for i, v in enumerate(glob)}
-                            gid = np.array([pos[vals[d]] for d in docs], dtype=np.int64)
-                        else:
-                            gid = np.searchsorted(glob, np.asarray(vals)[docs])
-                        key += gid * stride
-                        stride *= len(glob)
-                    np.add.at(t[0], key, 1)
-                    for i, a in enumerate(query.aggregations):
-                        sec = L.agg_section[i]
-                        if sec == 0:
-                            continue
-                        v = np.asarray(ds.values(a.column))[docs]
-                        o = L.section_op[sec]
-                        if o == PGPU_RED_SUM_I64:
-                            v = v.astype(np.int64)
-                            if L.agg_sum_parts[i] == 3:
-                                m = (1 << PGPU_PART_BITS) - 1
-                                for k, part in enumerate((v & m, (v >> PGPU_PART_BITS) & m,
-                                                          v >> (2 * PGPU_PART_BITS))):
-                                    np.add.at(t[sec + k], key, part)
-                            else:
-                                np.add.at(t[sec], key, v)
-                        elif o == PGPU_RED_SUM_F64:
-                            acc = t[sec].view(np.float64)
-                            np.add.at(acc, key, v.astype(np.float64))
-                        else:
-                            kv = np.array([minmax_key(float(x), L.agg_value_type[i]) for x in v], dtype=np.int64)
-                            (np.minimum if o == PGPU_RED_MIN_I64 else np.maximum).at(t[sec], key, kv)
                 table.copy_(torch.from_numpy(t.reshape(-1)))
-                return st
+                return dict(st)
             return L, launch
 
         def _globals_of(self, query, segments):
@@ -183,9 +198,11 @@ def _numpy_executor(pm):
             return handle
 
         def _compact(self, L, table):
-            t = table.cpu().numpy().reshape(L.num_sections, int(L.num_keys))
-            keys = np.flatnonzero(t[0] > 0)
-            return keys.astype(np.int64), np.ascontiguousarray(t[:, keys].T)
+            rows = L.num_sections + (1 if L.key_kind == PGPU_KEYS_HASH else 0)
+            t = table.cpu().numpy()[: rows * int(L.num_keys)].reshape(rows, int(L.num_keys))
+            live = np.flatnonzero(t[0] > 0)
+            keys = t[L.num_sections, live] if L.key_kind == PGPU_KEYS_HASH else live
+            return keys.astype(np.int64), np.ascontiguousarray(t[: L.num_sections, live].T)
 
     return NumpyExecutor(pm, device=torch.device("cpu"))
 
@@ -309,3 +326,27 @@ def _union_worker(rank):
 
 def test_union_dictionaries_tensor_collectives():
     _spawn(_union_worker)
+
+
+def _hash_worker(rank, qi, force_on):
+    """Hash tables merged across ranks by key ownership (all_to_all) and top-K; `force_on` = the ranks whose own
+    flags ask for the hash layout -- the layout must still be the same on every rank."""
+    from oracle import engine
+    from pinot_amd._lib import PGPU_Q_HASH
+    from pinot_amd.query import parse_sql
+    q = parse_sql(QUERIES[qi])
+    segs = [HostSegment(s) for s in _rank_segments(rank)]
+    pm = _plan_maker()
+    if rank in force_on:
+        pm.query_flags = PGPU_Q_HASH
+    ex = _numpy_executor(pm)
+    ex.TOPK_MIN = 40
+    res = ex.execute(q, segs)
+    if rank == 0:
+        _check(res, engine.execute(q, _all_segments()), q)
+
+
+@pytest.mark.parametrize("force_on", [(0, 1), (1,)], ids=["all_ranks", "one_rank"])
+@pytest.mark.parametrize("qi", [0, 2, 5])
+def test_hash_tables_merge_by_key_ownership(qi, force_on):
+    _spawn(_hash_worker, qi, force_on)

@@ -34,6 +34,8 @@ def _gpu(gpu_ctx, q, segs, **kw):
 
 
 def _assert_same(res, ref, rel=1e-9):
+    """Results, and the four execution statistics: numEntriesScannedInFilter whenever the GPU reports it as the
+    reference's figure (the oracle must then have run with iterator_stats=True)."""
     if res.aggregation_result is not None:
         assert len(res.aggregation_result) == len(ref.aggregation_result)
         for a, b in zip(res.aggregation_result, ref.aggregation_result):
@@ -47,6 +49,14 @@ def _assert_same(res, ref, rel=1e-9):
     assert res.stats.num_docs_scanned == ref.num_docs_scanned
     assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
     assert res.stats.num_total_docs == ref.num_total_docs
+    if res.stats.filter_stats_exact and getattr(ref, "_iterator_stats", False):
+        assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
+
+
+def _oracle(q, segs, **kw):
+    ref = engine.execute(q, segs, iterator_stats=True, **kw)
+    ref._iterator_stats = True
+    return ref
 
 
 # ---- reference KATs ---------------------------------------------------------------------------------------------
@@ -55,15 +65,13 @@ def test_inner_segment_kat_gpu(gpu_ctx, sv, case):
     seg, g = sv
     sql = KAT["inner_segment"]["aggregation_query"] + (KAT["filter"] if case["filter"] else "") + case["group_by"]
     q = parse_sql(sql)
-    if len(q.group_by) >= 5:
-        # LongMapBased / ArrayMapBased key spaces (> 2^31 raw keys) are served by the CPU plan in this build
-        with pytest.raises(UnsupportedPlanError):
-            _gpu(gpu_ctx, q, [g])
-        return
-    res = _gpu(gpu_ctx, q, [g])
+    # 5 and 9 group columns: LongMapBasedHolder / ArrayMapBasedHolder key spaces (> 2^31, > 2^63 raw keys) run in
+    # the hash group-by (one and two key words)
+    res = _gpu(gpu_ctx, q, [g], exact_filter_stats=True)
     st = res.stats
-    assert [st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs] == \
-        [case["stats"][0], case["stats"][2], case["stats"][3]]
+    assert st.filter_stats_exact
+    assert [st.num_docs_scanned, st.num_entries_scanned_in_filter, st.num_entries_scanned_post_filter,
+            st.num_total_docs] == case["stats"]
     v = res.intermediate[tuple(case["group"])] if case["group_by"] else res.intermediate[()]
     got = [v[0], int(v[1]), int(v[2]), int(v[3]), int(v[4][0]), v[4][1]]
     assert got == case["result"]
@@ -73,10 +81,10 @@ def test_inner_segment_kat_gpu(gpu_ctx, sv, case):
 def test_inter_segment_kat_gpu(gpu_ctx, sv, case):
     seg, g = sv
     q = parse_sql(case["sql"].replace("{FILTER}", KAT["filter"]))
-    res = _gpu(gpu_ctx, q, [g] * 4)
+    res = _gpu(gpu_ctx, q, [g] * 4, exact_filter_stats=True)
     st = res.stats
-    assert [st.num_docs_scanned, st.num_entries_scanned_post_filter, st.num_total_docs] == \
-        [case["stats"][0], case["stats"][2], case["stats"][3]]
+    assert [st.num_docs_scanned, st.num_entries_scanned_in_filter, st.num_entries_scanned_post_filter,
+            st.num_total_docs] == case["stats"]
     assert rows_close([list(x) for x in res.rows], case["rows"], rel=case.get("delta", 1e-12))
 
 
@@ -179,8 +187,10 @@ def test_random_segments_vs_oracle(gpu_ctx, n, qi):
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         q = parse_sql(QUERIES[qi])
-        res = _gpu(gpu_ctx, q, gs)
-        ref = engine.execute(q, segs)
+        ref = _oracle(q, segs)
+        _assert_same(_gpu(gpu_ctx, q, gs), ref)  # the GPU's own filter count where it is the reference's
+        res = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+        assert res.stats.filter_stats_exact
         _assert_same(res, ref)
     finally:
         for g in gs:
@@ -209,7 +219,7 @@ def test_inverted_leaves_vs_oracle(gpu_ctx, qi):
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         q = parse_sql(QUERIES[qi])
-        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+        _assert_same(_gpu(gpu_ctx, q, gs, exact_filter_stats=True), _oracle(q, segs))
     finally:
         for g in gs:
             g.release()
@@ -367,8 +377,9 @@ def test_bench_workloads_vs_oracle(gpu_ctx, wl):
     try:
         for sql in sqls:
             q = parse_sql(sql)
-            ref = engine.execute(q, segs)
+            ref = _oracle(q, segs)
             _assert_same(_gpu(gpu_ctx, q, gs), ref)
+            _assert_same(_gpu(gpu_ctx, q, gs, exact_filter_stats=True), ref)
     finally:
         for g in gs:
             g.release()
@@ -384,7 +395,7 @@ def test_both_filter_planners_vs_oracle(gpu_ctx, qi, host_planning):
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         q = parse_sql(QUERIES[qi])
-        _assert_same(_gpu(gpu_ctx, q, gs, host_planning=host_planning), engine.execute(q, segs))
+        _assert_same(_gpu(gpu_ctx, q, gs, host_planning=host_planning), _oracle(q, segs))
     finally:
         for g in gs:
             g.release()
@@ -421,7 +432,7 @@ def test_bit_sliced_leaves_vs_oracle(gpu_ctx, qi):
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         q = parse_sql(SLICED_QUERIES[qi])
-        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+        _assert_same(_gpu(gpu_ctx, q, gs), _oracle(q, segs))
     finally:
         for g in gs:
             g.release()
