@@ -352,6 +352,22 @@ int pgpu_query_launch_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pg
                            int32_t num_nodes, void* stream, void* dev_table, uint64_t table_bytes,
                            pgpu_query** out_query);
 
+/* ---- node-level combine: one process, several GPUs, RCCL inside the library ------------------------------------
+ * For a server that drives all GPUs of a node from one process (a JVM): contexts for the given HIP ordinals and
+ * one RCCL communicator clique over them (RCCL is loaded on first use).  Segments are uploaded through each
+ * device's context (pgpu_node_context).  pgpu_node_query runs descs[i] (device i's segments, the same aggregations,
+ * group columns and global group cardinalities on every device) on every device, merges the partial tables --
+ * dense: grouped ncclReduce per section to device 0 over xGMI; hash: per-device compaction merged by key -- and
+ * compacts the result like pgpu_query_collect (out_layout receives the layout the cells follow).  Replaces the
+ * host-side combine (AggregationOnlyCombineOperator.java:47-57, GroupByOrderByCombineOperator.java:127-248). */
+typedef struct pgpu_node pgpu_node;
+int pgpu_node_init(const int32_t* device_ordinals, int32_t num_devices, pgpu_node** out_node);
+int pgpu_node_context(pgpu_node* node, int32_t index, pgpu_context** out_ctx);
+int pgpu_node_shutdown(pgpu_node* node);
+int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_t* out_keys, int64_t* out_cells,
+                    uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
+                    pgpu_table_layout* out_layout);
+
 /* Convenience: submit + collect. */
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,
                        uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);

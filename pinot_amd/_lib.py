@@ -134,6 +134,11 @@ SIGNATURES = [
     ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_decode_minmax_key", C.c_double, [C.c_int64, C.c_int32]),
+    ("pgpu_node_init", C.c_int, [C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),
+    ("pgpu_node_context", C.c_int, [_P, C.c_int32, C.POINTER(_P)]),
+    ("pgpu_node_shutdown", C.c_int, [_P]),
+    ("pgpu_node_query", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                  C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats), C.POINTER(TableLayout)]),
     ("pgpu_filter_entries_scanned", C.c_int, [C.POINTER(FilterNode), C.c_int32, C.POINTER(C.POINTER(C.c_uint32)),
                                              C.c_int32, C.c_int32, C.POINTER(C.c_int64)]),
     ("pgpu_kernel_geometry", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

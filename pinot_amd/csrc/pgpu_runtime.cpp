@@ -428,6 +428,15 @@ int group_key_space(const pgpu_query_desc* q, pgpu_table_layout* out) {
 }  // namespace
 
 // =============================================================================================================
+// pgpu_node.cpp's access to the thread's error message and to segment sizes
+int pgpu_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+int64_t pgpu_desc_docs(const pgpu_query_desc* q) {
+  int64_t d = 0;
+  for (int s = 0; q && s < q->num_segments; ++s)
+    if (q->segments[s].segment) d += q->segments[s].segment->num_docs;
+  return d;
+}
+
 extern "C" {
 
 int pgpu_abi_version(void) { return PGPU_ABI_VERSION; }

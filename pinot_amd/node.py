@@ -1,0 +1,95 @@
+"""One process, several GPUs: the node-level combine inside libpinotgpu (pgpu_node_*, include/pinot_gpu.h).
+
+The shape of a Pinot server that keeps one JVM for all GPUs of a node: segments are uploaded through each device's
+context, a query is planned per device (the same aggregations, group columns and node-global group dictionaries on
+every device) and ``pgpu_node_query`` launches every device and merges the partial tables with RCCL over xGMI
+inside the library -- the combine the reference runs on the host (AggregationOnlyCombineOperator.java:47-57,
+GroupByOrderByCombineOperator.java:127-248).  (``combine.DistributedExecutor`` is the one-process-per-GPU form.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import QueryDesc, QueryStats, TableLayout
+from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, finish, key_words_out
+from .query import QueryContext
+from .segment import GpuContext, GpuSegment
+
+
+def union_dictionary(column: str, segments: Sequence[GpuSegment]):
+    """Sorted union of the segments' dictionaries of one group column (host data only)."""
+    dicts = [s.dictionaries[column] for s in segments]
+    if isinstance(dicts[0], list):
+        return sorted(set().union(*[set(d) for d in dicts]))
+    return np.unique(np.concatenate([np.asarray(d) for d in dicts]))
+
+
+class GpuNode:
+    """pgpu_node: contexts for `devices` and one RCCL clique over them."""
+
+    def __init__(self, devices: Sequence[int], **plan_options):
+        self._lib = _lib.load()
+        arr = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        _lib.check(self._lib.pgpu_node_init(arr, len(devices), C.byref(h)))
+        self.handle = h
+        self.contexts: List[GpuContext] = []
+        for i, d in enumerate(devices):
+            ch = C.c_void_p()
+            _lib.check(self._lib.pgpu_node_context(h, i, C.byref(ch)))
+            self.contexts.append(GpuContext(d, _handle=ch))
+        self.planners = [GpuPlanMaker(c, **plan_options) for c in self.contexts]
+
+    def close(self) -> None:
+        if self.handle:
+            for c in self.contexts:
+                c.close()
+            self._lib.pgpu_node_shutdown(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def execute(self, query: QueryContext, segments_by_device: Sequence[Sequence[GpuSegment]]) -> QueryResult:
+        """One query over every device's segments, merged inside the library."""
+        if len(segments_by_device) != len(self.contexts):
+            raise ValueError("one segment list per device")
+        everything = [s for segs in segments_by_device for s in segs]
+        globs = [union_dictionary(g, everything) for g in query.group_by]
+        keep, descs = [], []
+        for pm, segs in zip(self.planners, segments_by_device):
+            for g, glob in zip(query.group_by, globs):
+                pm.set_global_dictionary(g, segs, glob)
+            desc, k, _ = pm.build_desc(query, segs)
+            keep.append((desc, k))
+            descs.append(desc)
+        arr = (C.POINTER(QueryDesc) * len(descs))(*[C.pointer(d) for d in descs])
+        L0 = self.planners[0].layout(descs[0])
+        cap = int(min(max(L0.num_keys * len(descs), 1), 1 << 26))
+        kw = 2  # enough for either key width
+        keys = np.empty(cap * kw, dtype=np.int64)
+        cells = np.empty((cap, 64), dtype=np.int64)
+        n = C.c_uint64()
+        st = QueryStats()
+        L = TableLayout()
+        _lib.check(self._lib.pgpu_node_query(self.handle, arr, keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                             cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
+                                             C.byref(st), C.byref(L)))
+        kw = key_words_out(L)
+        ng = n.value
+        k = keys[: ng * kw].reshape(ng, kw) if kw > 1 else keys[:ng]
+        c = cells.reshape(-1)[: ng * L.num_sections].reshape(ng, L.num_sections)
+        stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
+                               num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
+                               num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
+                               num_total_docs=st.num_total_docs, num_segments_processed=len(everything),
+                               kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
+                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact))
+        return finish(query, GroupTable.sorted(k, c, L), globs, stats)

@@ -84,11 +84,13 @@ class SegmentData:
 class GpuContext:
     """One HIP device (one process per GPU); wraps pgpu_init / pgpu_shutdown."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, _handle: Optional[C.c_void_p] = None):
         self._lib = _lib.load()
-        h = C.c_void_p()
-        _lib.check(self._lib.pgpu_init(device, C.byref(h)))
-        self.handle = h
+        self.owned = _handle is None  # a node's contexts are shut down by pgpu_node_shutdown
+        if _handle is None:
+            _handle = C.c_void_p()
+            _lib.check(self._lib.pgpu_init(device, C.byref(_handle)))
+        self.handle = _handle
         self.device = device
         self._remap_cache: Dict[tuple, "DeviceBuffer"] = {}
 
@@ -97,7 +99,8 @@ class GpuContext:
             for b in self._remap_cache.values():
                 b.release()
             self._remap_cache.clear()
-            self._lib.pgpu_shutdown(self.handle)
+            if self.owned:
+                self._lib.pgpu_shutdown(self.handle)
             self.handle = None
 
     def __enter__(self):
