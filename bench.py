@@ -5,12 +5,14 @@ weak scaling: config 5 "AdAnalytics ... 8B rows sharded across 8xMI355X" at N=8)
 packing, the query kernel, the RCCL all-reduce of the partial group-by tables (N>1) and rank 0's compaction to
 host results.  Segments are generated in HBM before timing (synthetic data, seeded; see pinot_amd/synth.py).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|range_in|groupby1m]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload adanalytics|range_in|groupby1m|bitmap5|...]
   torchrun --nproc-per-node N bench.py --gpus N ...       (one process per GPU, RCCL over xGMI)
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (query_kernel: algorithmic bytes per
 launch / its HIP-event time) and the CPU baseline (oracle/pinot_cpu.c, Pinot's per-segment operators restated,
-timed on a bounded sample on this host).
+timed on a bounded sample on this host).  The default N=1 run also measures BASELINE.json configs 2-4 and the
+SURVEY.md 8(d) variants (Zipf keys, inverted-indexed accountId) into a `workloads` sub-object, each with its own
+ms/step, roofline and CPU baseline.
 """
 from __future__ import annotations
 
@@ -42,7 +44,135 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = Pinot default min(#seg, min(10, nproc/2))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip the small GPU-vs-oracle check of this workload")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="measure the headline workload only (default N=1 run: also configs 2-4 and variants)")
     return ap.parse_args()
+
+
+def available_cores() -> int:
+    """CPU cores this process may use: its affinity set, capped by OMP_NUM_THREADS when the box sets a share."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
+
+
+def measure(ex, q, segs, steps, warmup, inflight, world, barrier):
+    """Time `steps` whole queries (plan, launch, reduce, finish) with up to `inflight` in flight at N = 1;
+    returns (ms_per_step over the max of ranks, average HIP-event kernel ms, last result)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        ex.execute(q, segs)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    t_start = time.perf_counter()
+    result = None
+    pending = []
+    submitted = 0
+    for _ in range(steps):
+        while submitted < steps and len(pending) < max(1, inflight):
+            pending.append(ex.submit(q, segs))
+            submitted += 1
+        result = ex.collect(pending.pop(0))
+        kernel_ms.append(ex.last_stats.kernel_ms)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed * 1000.0 / steps, sum(kernel_ms) / len(kernel_ms), result
+
+
+def algorithmic_bytes(ex, pm, q, segs):
+    """forward-index bytes (dense tiles + 32-B sectors of sparse reads, exact from the kernel's
+    stats pass) + dictionary bytes read once per segment per query (bounded by one 32-B sector per matched doc when
+    few docs match) + inverted-index bitmap bytes + output bytes."""
+    pm.collect_stats = True
+    r = ex.execute(q, segs)
+    st = ex.last_stats
+    pm.collect_stats = False
+    dict_bytes = 0
+    for c in sorted(set(a.column for a in q.aggregations if a.column)):
+        width = {0: 4, 1: 8, 2: 4, 3: 8}.get(segs[0].column(c).data_type, 4)
+        full = sum(s.column(c).cardinality * width for s in segs)
+        dict_bytes += min(full, 32 * st.num_docs_scanned)
+    ngroups = len(r.group_rows or []) if r is not None else 1  # ranks != 0 return no rows
+    out_bytes = 8 * max(1, ngroups) * (1 + len(q.aggregations))
+    bitmap_bytes = inverted_bytes_read(q, segs)
+    total = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
+    return total, st, {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
+                       "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes, "output": out_bytes}
+
+
+def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier):
+    """Generate the workload's segments in HBM, measure it, time the CPU baseline beside it; returns the fields
+    of one result (the headline line or an entry of `workloads`)."""
+    import torch
+    from pinot_amd.combine import DistributedExecutor
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.query import parse_sql
+    from pinot_amd.synth import WORKLOADS, build_segments_gpu
+
+    w = WORKLOADS[name]
+    nseg = segments or w.segments
+    seg_ids = list(range(rank * nseg, (rank + 1) * nseg))
+    t0 = time.time()
+    segs = build_segments_gpu(ctx, w, seg_ids, args.docs)
+    torch.cuda.synchronize()
+    gen_s = time.time() - t0
+    log(f"{name}: generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
+    opts = dict(w.options)
+    q = parse_sql(w.sql)
+    pm = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000))
+    ex = DistributedExecutor(pm)
+    try:
+        algo_bytes, st, breakdown = algorithmic_bytes(ex, pm, q, segs)
+        log(f"{name}: stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, "
+            f"{st.kernel_ms:.3f} ms")
+        ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight, world, barrier)
+        rows_per_gpu = nseg * args.docs
+        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        log(f"{name}: timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
+        cpu = check = None
+        if rank == 0 and not args.no_cpu_baseline:
+            cpu, check = cpu_baseline(ctx, w, q, opts, args, cpu_seconds)
+        traffic, traffic_src = _pmc_traffic(name)
+        return {
+            "value": rows_per_gpu * world / (ms_per_step * 1e-3),
+            "ms_per_step": ms_per_step,
+            "steps": steps,
+            "config": {"workload": name, "description": w.description, "query": w.sql,
+                       "segments_per_gpu": nseg, "docs_per_segment": args.docs, "rows_per_gpu": rows_per_gpu,
+                       "total_rows": rows_per_gpu * world, "queries_in_flight": max(1, args.inflight),
+                       "parallelism": f"segments sharded over {world} GPU(s); partial tables merged over RCCL"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel_ms_avg": avg_kernel_ms, "bytes_breakdown": breakdown},
+            "cpu_baseline": cpu,
+            "result": {"matched_docs_per_gpu": st.num_docs_scanned,
+                       "groups": (len(result.group_rows) if result and result.group_rows is not None else None),
+                       "rows": [list(r) for r in (result.rows[:3] if result else [])]},
+            "parity_check": check,
+            "setup_s": round(gen_s, 1),
+        }
+    finally:
+        for s in segs:
+            s.release()
+
+
+# Secondary workloads measured after the headline in the default run (BASELINE.json configs 2-4 and the SURVEY 8(d)
+# variants): (name, steps, warmup, segments per GPU or 0 = the workload's own, CPU sample seconds)
+SECONDARY = [("range_in", 10, 2, 0, 3.0), ("groupby1m", 5, 1, 0, 3.0), ("bitmap5", 10, 2, 0, 3.0),
+             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 8, 3.0)]
 
 
 def main():
@@ -64,127 +194,48 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
 
-    from pinot_amd.combine import DistributedExecutor
-    from pinot_amd.plan import GpuPlanMaker
-    from pinot_amd.query import parse_sql
     from pinot_amd.segment import GpuContext
-    from pinot_amd.synth import WORKLOADS, build_segments_gpu
 
-    w = WORKLOADS[args.workload]
-    if args.segments <= 0:
-        args.segments = w.segments
     log = (lambda *a: print(f"[bench rank {rank}]", *a, file=sys.stderr, flush=True))
     ctx = GpuContext(local)
-    seg_ids = list(range(rank * args.segments, (rank + 1) * args.segments))
-    t0 = time.time()
-    segs = build_segments_gpu(ctx, w, seg_ids, args.docs)
-    torch.cuda.synchronize()
-    gen_s = time.time() - t0
-    log(f"generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
-    opts = dict(w.options)
-    q = parse_sql(w.sql)
-    pm = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000))
-    ex = DistributedExecutor(pm)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    # algorithmic bytes of one launch (stats pass: dense tile bytes + touched 32-B sectors of sparse reads)
-    pm.collect_stats = True
-    r_stats = ex.execute(q, segs)
-    st = ex.last_stats
-    pm.collect_stats = False
-    # forward-index bytes (dense tiles + 32-B sectors of sparse reads, exact from the kernel's
-    # stats) + dictionary bytes read once per segment per query (bounded by one 32-B sector per matched doc
-    # when few docs match) + output bytes
-    dict_bytes = 0
-    for c in sorted(set(a.column for a in q.aggregations if a.column)):
-        width = {0: 4, 1: 8, 2: 4, 3: 8}.get(segs[0].column(c).data_type, 4)
-        full = sum(s.column(c).cardinality * width for s in segs)
-        dict_bytes += min(full, 32 * st.num_docs_scanned)
-    ngroups = len(r_stats.group_rows or []) if r_stats is not None else 1  # ranks != 0 return no rows
-    out_bytes = 8 * max(1, ngroups) * (1 + len(q.aggregations))
-    bitmap_bytes = inverted_bytes_read(q, segs)
-    algo_bytes = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
-
-    log(f"stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, {st.kernel_ms:.3f} ms")
-    for _ in range(args.warmup):
-        ex.execute(q, segs)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    kernel_ms = []
-    t_start = time.perf_counter()
-    result = None
-    # every step plans, launches, reduces (N > 1: RCCL all-reduce of the partial tables) and finishes one whole
-    # query; up to `inflight` are queued at once, so the host side of query i overlaps the GPU running query i+1
-    pending = []
-    submitted = 0
-    for _ in range(args.steps):
-        while submitted < args.steps and len(pending) < max(1, args.inflight):
-            pending.append(ex.submit(q, segs))
-            submitted += 1
-        result = ex.collect(pending.pop(0))
-        kernel_ms.append(ex.last_stats.kernel_ms)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed * 1000.0 / args.steps
-    rows_per_gpu = args.segments * args.docs
-    total_rows = rows_per_gpu * world
-    value = total_rows / (elapsed / args.steps)
-
-    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-
-    # small parity check of the same workload against the oracle (2 x 2^18-doc segments)
-    log(f"timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
-    # the CPU leg (the only one that touches oracle/): Pinot's operators restated on the CPU, timed on this host,
-    # and a GPU-vs-CPU check of the same workload on small segments
-    check = cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu, check = cpu_baseline(ctx, w, q, opts, args)
-
+    head = run_workload(args.workload, ctx, args, world, rank, args.steps, args.warmup, args.segments,
+                        args.cpu_seconds, log, barrier)
+    workloads = {}
+    if args.secondary and world == 1 and args.workload == "adanalytics":
+        for name, steps, warmup, nseg, cpu_s in SECONDARY:
+            try:
+                workloads[name] = run_workload(name, ctx, args, world, rank, steps, warmup, nseg, cpu_s, log, barrier)
+            except Exception as e:  # a secondary workload never hides the headline line
+                log(f"{name}: failed: {e!r}")
+                workloads[name] = {"error": repr(e)}
     if rank == 0:
-        traffic = _pmc_traffic(args.workload)
         line = {
             "metric": "rows/sec for filtered GROUP BY SUM at 1/8 GPUs + achieved HBM GB/s vs peak",
-            "value": value,
+            "value": head["value"],
             "unit": "rows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded dict ids generated in HBM; dictionaries per BASELINE.md section 3)",
-            "config": {"workload": args.workload, "description": w.description, "query": w.sql,
-                       "segments_per_gpu": args.segments, "docs_per_segment": args.docs,
-                       "rows_per_gpu": rows_per_gpu, "total_rows": total_rows,
-                       "queries_in_flight": max(1, args.inflight),
-                       "parallelism": f"segments sharded over {world} GPU(s); partial tables all-reduced over RCCL"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
-                         "kernel_ms_avg": avg_kernel_ms,
-                         "bytes_breakdown": {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
-                                             "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes,
-                                             "output": out_bytes}},
-            "cpu_baseline": cpu,
-            "result": {"matched_docs_per_gpu": st.num_docs_scanned, "groups": (len(result.group_rows)
-                       if result and result.group_rows is not None else None),
-                       "rows": [list(r) for r in (result.rows[:3] if result else [])]},
-            "parity_check": check,
-            "setup_s": round(gen_s, 1),
+            "config": head["config"],
+            "roofline": head["roofline"],
+            "cpu_baseline": head["cpu_baseline"],
+            "result": head["result"],
+            "parity_check": head["parity_check"],
+            "setup_s": head["setup_s"],
         }
+        if workloads:
+            line["workloads"] = workloads
         print(json.dumps(line, default=float), flush=True)
     ctx.close()
     if world > 1:
@@ -192,16 +243,18 @@ def main():
 
 
 def _pmc_traffic(workload):
-    """HBM bytes per launch measured by rocprofv3 PMC (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), when a
-    committed measurement for this workload exists under profiles/."""
+    """HBM bytes per launch measured by rocprofv3 PMC (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) from the
+    committed measurement of this workload under profiles/, and where / at which commit it was measured (so a
+    figure that predates a kernel change is visibly stale).  (None, None) when there is none."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if os.path.exists(p):
         try:
             with open(p) as f:
-                return json.load(f).get("hbm_bytes_per_launch")
+                d = json.load(f)
+            return d.get("hbm_bytes_per_launch"), f"profiles/pmc_{workload}.json @ {d.get('commit', 'unknown')}"
         except Exception:
-            return None
-    return None
+            return None, None
+    return None, None
 
 
 def inverted_bytes_read(q, segs):
@@ -265,22 +318,24 @@ def parity_check(ctx, w, q, opts):
             g.release()
 
 
-def cpu_baseline(ctx, w, q, opts, args):
+def cpu_baseline(ctx, w, q, opts, args, seconds):
     """The CPU leg: (1) Pinot's per-segment operators restated in C (oracle/pinot_cpu.c) timed on this host,
-    the sample's segments queried repeatedly until ~args.cpu_seconds of wall time with Pinot's default task
-    count; filters the C port does not cover (OR / NOT / index leaves) time the numpy restatement
-    (oracle/engine.py) instead; (2) the GPU-vs-oracle parity check (parity_check)."""
+    the sample's segments queried repeatedly until ~`seconds` of wall time, at Pinot's default task count and
+    with every available core; filters the C port does not cover (OR / NOT / index leaves) time the numpy
+    restatement (oracle/engine.py) instead; (2) the GPU-vs-oracle parity check (parity_check)."""
     check = None if args.no_check else parity_check(ctx, w, q, opts)
     from oracle import cpu as ocpu
 
     try:
         ocpu._leaves(q.filter)
+        if any(c.dist != "uniform" or c.index != "fwd" for c in w.columns):
+            raise ValueError("the C port's generator covers uniform forward-index columns")
     except ValueError:
-        return engine_baseline(w, q, opts, args), check
-    return c_baseline(w, q, args), check
+        return engine_baseline(w, q, opts, args, seconds), check
+    return c_baseline(w, q, args, seconds), check
 
 
-def engine_baseline(w, q, opts, args):
+def engine_baseline(w, q, opts, args, seconds):
     from oracle import engine
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.synth import build_segment_cpu
@@ -288,7 +343,7 @@ def engine_baseline(w, q, opts, args):
     nseg, n = 2, 1 << 21
     segs = [build_segment_cpu(w, s, n, pack_fixed_bit) for s in range(nseg)]
     total, runs = 0.0, 0
-    while runs == 0 or total < args.cpu_seconds:
+    while runs == 0 or total < seconds:
         t = time.perf_counter()
         engine.execute(q, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
         total += time.perf_counter() - t
@@ -300,7 +355,7 @@ def engine_baseline(w, q, opts, args):
             "seconds": total}
 
 
-def c_baseline(w, q, args):
+def c_baseline(w, q, args, seconds):
     from oracle.cpu import CpuBaseline, synth_segment
 
     nseg = args.cpu_sample_segments
@@ -308,16 +363,27 @@ def c_baseline(w, q, args):
     nproc = os.cpu_count() or 1
     threads = args.cpu_threads or max(1, min(nseg, min(10, nproc // 2)))
     cb = CpuBaseline(q, segs)
-    total, runs = 0.0, 0
-    while runs == 0 or total < args.cpu_seconds:
-        dt, matched, _, _, _ = cb.run(threads)
-        total += dt
-        runs += 1
-    return {"value": runs * nseg * args.docs / total, "unit": "rows/s", "cores": threads, "kind": "port",
+
+    def timed(th, budget):
+        total, runs = 0.0, 0
+        while runs == 0 or total < budget:
+            dt, matched, _, _, _ = cb.run(th)
+            total += dt
+            runs += 1
+        return runs * nseg * args.docs / total, runs, total
+
+    value, runs, total = timed(threads, seconds)
+    # the same operators with every core this process may use (one task per segment, so
+    # at most #segments of them run at once)
+    cores = available_cores()
+    all_value, all_runs, all_total = timed(cores, max(1.0, seconds / 2))
+    return {"value": value, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload, "
                       f"oracle/pinot_cpu.c (AndDocIdIterator over SVScanDocIdIterators, 10k-doc blocks, double SUM), "
                       f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
-            "seconds": total}
+            "seconds": total,
+            "all_cores": {"value": all_value, "cores": min(cores, nseg), "available_cores": cores,
+                          "runs": all_runs, "seconds": all_total}}
 
 
 if __name__ == "__main__":

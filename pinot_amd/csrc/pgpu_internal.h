@@ -231,6 +231,9 @@ struct DevParams {
   int32_t rcap;
   int32_t rw;
   int32_t pcol;                   // query column carried in the records (-1: COUNT only)
+  int32_t rec_idbits;             // > 0: one-word records ((key & partition mask) << rec_idbits | dict id) -- every
+                                  // segment shares pcol's dictionary (pdict); 0: {key, raw 4-byte value} records
+  const void* pdict;              // rec_idbits > 0: the shared dictionary of pcol
   int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
   int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
   int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)

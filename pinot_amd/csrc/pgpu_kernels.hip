@@ -1191,6 +1191,7 @@ FI int64_t* table_base(const DevParams& p, const Lds& L) {
 // partition.  All N slot reservations (LDS cursor atomics) are issued before the first store.  A full region
 // spills the doc straight into the HBM table with atomics: correct, only slower.
 FI void part_spill(const DevParams& p, uint32_t key, uint32_t raw) {
+  if (p.rec_idbits) raw = gld((const uint32_t*)p.pdict, raw);  // one-word records carry the dict id
   atomicAdd((unsigned long long*)&p.table[key], 1ull);
   for (int a = 0; a < p.nagg; ++a) {
     const DevAgg ag = p.aggs[a];
@@ -1211,7 +1212,8 @@ FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], co
     if (!((live >> r) & 1u)) continue;
     if (slot[r] < cap) {
       const size_t rec = ((size_t)(key[r] >> p.pshift) * gridDim.x + blockIdx.x) * (size_t)cap + slot[r];
-      if (p.rw == 1) p.recs[rec] = key[r];
+      if (p.rw == 1)
+        p.recs[rec] = p.rec_idbits ? ((key[r] & ((1u << p.pshift) - 1)) << p.rec_idbits) | raw[r] : key[r];
       else *(u32x2*)(p.recs + 2 * rec) = u32x2{key[r], raw[r]};
     } else {
       spill |= 1u << r;
@@ -1278,7 +1280,12 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
         gather_ids(colref(c), doc, id);
 #pragma unroll
         for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
-        gather_raw(c.dict, id, raw);
+        if (p.rec_idbits) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) raw[u] = id[u];
+        } else {
+          gather_raw(c.dict, id, raw);
+        }
       }
       part_emit(p, L, key, raw, m);
       return;
@@ -1586,7 +1593,12 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
             const int e = lane + 64 * (r0 + r);
             idx[r] = e < nh ? (uint32_t)vlist[e] : 0u;
           }
-          gather_raw(c.dict, idx, raw);
+          if (p.rec_idbits) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) raw[r] = idx[r];
+          } else {
+            gather_raw(c.dict, idx, raw);
+          }
           uint32_t kk[8], live = 0;
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
@@ -2176,6 +2188,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NS + 1) * K; i += blockDim.x)
     ptab[i] = sec_identity(p.sec_op[i >> p.pshift]);
   __syncthreads();
+  // one-word records: (in-partition key << idbits | dict id) over the shared dictionary; MIN / MAX sections reduce
+  // the dict ids (sorted dictionary) and are turned into cell keys when folded into the HBM table
+  const int idbits = p.rec_idbits;
+  const uint32_t idmask = idbits ? (1u << idbits) - 1u : 0u;
   constexpr int R = 8;
   for (int w = 0; w < nwg; ++w) {
     const uint32_t n = p.rcount[(size_t)q * nwg + w];
@@ -2190,13 +2206,27 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
         k[r] = (uint32_t)key0;
         raw[r] = 0;
         if (ok[r]) {
-          if (NS == 0) {
-            k[r] = gld(p.recs, base + i);
+          if (NS == 0 || idbits) {
+            const uint32_t v = gld(p.recs, base + i);
+            k[r] = idbits ? (uint32_t)key0 + (v >> idbits) : v;
+            raw[r] = v & idmask;
           } else {
             const u32x2 v = gld((const u32x2*)p.recs, base + i);
             k[r] = v.x;
             raw[r] = v.y;
           }
+        }
+      }
+      uint32_t val[R];  // the record's 4-byte dictionary value (SUM sections)
+#pragma unroll
+      for (int r = 0; r < R; ++r) val[r] = raw[r];
+      if (idbits) {
+        bool need = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) need |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
+        if (need) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) val[r] = ok[r] ? gld((const uint32_t*)p.pdict, raw[r]) : 0u;
         }
       }
 #pragma unroll
@@ -2210,16 +2240,16 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
         if (op[s] == PGPU_RED_SUM_I64) {
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (ok[r]) atomicAdd((unsigned long long*)&sec[k[r]], (unsigned long long)(int64_t)(int32_t)raw[r]);
+            if (ok[r]) atomicAdd((unsigned long long*)&sec[k[r]], (unsigned long long)(int64_t)(int32_t)val[r]);
         } else if (op[s] == PGPU_RED_SUM_F64) {
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (ok[r]) atomicAdd((double*)&sec[k[r]], (double)__uint_as_float(raw[r]));
+            if (ok[r]) atomicAdd((double*)&sec[k[r]], (double)__uint_as_float(val[r]));
         } else {
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             if (!ok[r]) continue;
-            const int64_t c = raw_to_cell(raw[r], vt, op[s]);
+            const int64_t c = idbits ? (int64_t)raw[r] : raw_to_cell(raw[r], vt, op[s]);
             if (op[s] == PGPU_RED_MIN_I64) atomicMin((long long*)&sec[k[r]], (long long)c);
             else atomicMax((long long*)&sec[k[r]], (long long)c);
           }
@@ -2233,7 +2263,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
 #pragma unroll
     for (int s = 0; s <= NS; ++s) {
       int64_t* cell = &p.table[(size_t)s * p.G + key0 + k];
-      *cell = cell_combine(p.sec_op[s], *cell, ptab[(size_t)s * K + k]);
+      int64_t v = ptab[(size_t)s * K + k];
+      if (idbits && s > 0 && (p.sec_op[s] == PGPU_RED_MIN_I64 || p.sec_op[s] == PGPU_RED_MAX_I64))
+        v = raw_to_cell(gld((const uint32_t*)p.pdict, (uint32_t)v), vt, p.sec_op[s]);  // id -> cell key
+      *cell = cell_combine(p.sec_op[s], *cell, v);
     }
   }
 }

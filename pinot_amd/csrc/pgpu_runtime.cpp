@@ -195,6 +195,7 @@ struct HostColumn {
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
   double max_abs = 0;                  // numeric dictionary: largest |value| (integer SUM overflow bound)
+  uint64_t dict_hash[2] = {0, 0};      // two independent 64-bit hashes of the dictionary bytes (shared-dict checks)
 };
 
 }  // namespace
@@ -597,6 +598,14 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
+  uint64_t h1 = 1469598103934665603ull, h2 = 0x9E3779B97F4A7C15ull;  // FNV-1a, and a multiply-xorshift mix
+  for (uint8_t x : le) {
+    h1 = (h1 ^ x) * 1099511628211ull;
+    h2 = (h2 + x + 1) * 0xBF58476D1CE4E5B9ull;
+    h2 ^= h2 >> 29;
+  }
+  c.dict_hash[0] = h1;
+  c.dict_hash[1] = h2;
   c.hdict = std::move(le);
   c.max_abs = max_abs;
   return PGPU_OK;
@@ -1611,18 +1620,43 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.nparts = (int32_t)nparts;
     p.pcol = pcol;
     p.rw = pcol >= 0 ? 2 : 1;
+    p.rec_idbits = 0;
+    p.pdict = nullptr;
+    if (pcol >= 0) {
+      // one-word records (in-partition key, dict id) when every segment holds the same dictionary for the
+      // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
+      const HostColumn* h0 = &q->segments[0].segment->cols[q->segments[0].column_map[pcol]];
+      bool shared = h0->dict_card > 0 && !h0->hdict.empty();
+      for (int s = 1; s < q->num_segments && shared; ++s) {
+        const HostColumn* h = &q->segments[s].segment->cols[q->segments[s].column_map[pcol]];
+        shared = h->dict_card == h0->dict_card && h->dict_type == h0->dict_type && h->dict_hash[0] == h0->dict_hash[0] &&
+                 h->dict_hash[1] == h0->dict_hash[1];
+      }
+      int idbits = 1;
+      while (idbits < 31 && (1ll << idbits) < h0->dict_card) ++idbits;
+      if (shared && pshift + idbits <= 32 && !(q->flags & PGPU_Q_PART_SPILL)) {
+        p.rw = 1;
+        p.rec_idbits = idbits;
+        p.pdict = h0->dict.p;
+      }
+    }
     const double per = pk.est_matched / ((double)grid * (double)nparts);
     uint64_t cap = (uint64_t)(1.25 * per) + 32;
     if (q->flags & PGPU_Q_PART_SPILL) cap = 16;
-    cap = (cap + 15) & ~15ull;
+    // regions of an odd number of 128-B lines: the active (partially written) line of every region then falls on
+    // a different L2 set instead of all regions' cursors sharing a few sets, so lines stay resident until full
+    const uint64_t per_line = 32 / p.rw;
+    uint64_t lines = (cap + per_line - 1) / per_line;
+    if (!(q->flags & PGPU_Q_PART_SPILL) && (lines & 1) == 0) ++lines;
+    cap = lines * per_line;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
     const uint64_t regions = nparts * (uint64_t)grid;
     const uint64_t have = ws->recs.n;
     const uint64_t budget = std::max<uint64_t>(have, (uint64_t)free_b / 2);
     const uint64_t max_cap = budget / (regions * 4ull * p.rw);
-    if (cap > max_cap) cap = max_cap & ~15ull;
-    if (cap > (uint64_t)INT32_MAX) cap = (uint64_t)INT32_MAX & ~15ull;
+    if (cap > max_cap) cap = max_cap / per_line * per_line;
+    if (cap > (uint64_t)INT32_MAX) cap = (uint64_t)INT32_MAX / per_line * per_line;
     p.rcap = (int32_t)std::max<uint64_t>(cap, 16);
     e = ws->recs.ensure(regions * (uint64_t)p.rcap * 4ull * p.rw);
     if (e == hipSuccess) e = ws->rcount.ensure(4ull * regions);

@@ -144,6 +144,23 @@ WORKLOADS: Dict[str, Workload] = {
         "SELECT SUM(m1), SUM(m2) FROM bitmap5 "
         "WHERE (a = 10 AND b IN (30, 70)) OR (c = 50 AND d <> 90 AND e BETWEEN 640 AND 1910)",
         {}, 3, "config 3: inverted-index (Roaring) AND/OR/NOT filter + sorted range, SUM on 2 metric columns"),
+    # SURVEY.md 8(d) variants: config 4 with Zipf(1.1)-skewed keys, config 5 with accountId inverted-indexed
+    "groupby1m_zipf": Workload(
+        "groupby1m_zipf", "synth",
+        [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3, dist="zipf", zipf_s=1.1),
+         SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
+        "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
+        {"num_groups_limit": 2_000_000}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+    "adanalytics_inv": Workload(
+        "adanalytics_inv", "adAnalytics",
+        [SynthColumn("daysSinceEpoch", 1024, _days),
+         SynthColumn("accountId", 1 << 20, _accounts, index="inv"),
+         SynthColumn("clicks", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 11)),
+         SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
+        "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
+        "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
+        "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
+        {}, 5, "config 5, accountId inverted-indexed: the IN leaf is a Roaring bitmap"),
 }
 
 

@@ -436,3 +436,35 @@ def test_bit_sliced_leaves_vs_oracle(gpu_ctx, qi):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.parametrize("mtype", [PGPU_INT, PGPU_FLOAT])
+@pytest.mark.parametrize("sql", [
+    "SELECT k, SUM(m), MIN(m), MAX(m), AVG(m), COUNT(*) FROM t GROUP BY k",
+    "SELECT k, MAX(m), COUNT(*) FROM t WHERE f < 30 GROUP BY k ORDER BY MAX(m) DESC LIMIT 20",
+    "SELECT k, COUNT(*) FROM t WHERE f >= 50 GROUP BY k",
+])
+def test_partitioned_groupby_shared_dictionary(gpu_ctx, sql, mtype):
+    """Segments sharing the aggregated column's dictionary: the partitioned group-by writes one-word records
+    (in-partition key, dict id) and phase 2 resolves values / MIN / MAX through the shared dictionary."""
+    from pinot_amd._lib import PGPU_Q_PARTITION
+    rng = np.random.default_rng(77 + len(sql))
+    values = np.sort(rng.choice(np.arange(-3000, 50_000), 4000, replace=False))
+    if mtype == PGPU_FLOAT:
+        values = values.astype(np.float32) * np.float32(0.5)
+    segs = []
+    for i in range(3):
+        n = 90_001
+        m = np.concatenate([values, values[rng.integers(0, len(values), n - len(values))]])
+        k = rng.integers(0, 70_000, n).astype(np.int32)
+        f = rng.integers(0, 100, n).astype(np.int32)
+        segs.append(build_segment(f"sd{i}", {"k": (PGPU_INT, k), "m": (mtype, m), "f": (PGPU_INT, f)}))
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(sql)
+        for flags in (0, PGPU_Q_PARTITION):
+            res = _gpu(gpu_ctx, q, gs, num_groups_limit=1_000_000, query_flags=flags)
+            _assert_same(res, engine.execute(q, segs, num_groups_limit=1_000_000))
+    finally:
+        for g in gs:
+            g.release()
