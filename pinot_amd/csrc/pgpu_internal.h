@@ -185,6 +185,7 @@ struct DevAgg {
 #define PGPU_PART_LDS_BYTES (128 * 1024)   // phase-2 LDS table per partition (keys x sections x 8 B)
 #define PGPU_PART_MAX_PARTS 8192           // phase-1 LDS cursors (4 B each) must fit PGPU_LDS_TABLE_BYTES
 #define PGPU_PART_MAX_SECTIONS 5           // count + up to 4 value sections (part_reduce_kernel<NS>)
+#define PGPU_PSCAN_MAX_PARTS 512           // part_scan_kernel: per-wave histograms of at most this many partitions
 // Hash group-by (PGPU_KEYS_HASH): the table's cells are indexed by an open-addressing slot (linear probing,
 // lock-free 64-bit CAS insert).  Keys of more than 63 bits are interned in two levels: word 0 (columns
 // [0, key_split)) gets a slot s0 in a first table, then the slot of (s0 << 32 | word 1) is the cell index.
@@ -234,6 +235,8 @@ struct DevParams {
   int32_t rec_idbits;             // > 0: one-word records ((key & partition mask) << rec_idbits | dict id) -- every
                                   // segment shares pcol's dictionary (pdict); 0: {key, raw 4-byte value} records
   const void* pdict;              // rec_idbits > 0: the shared dictionary of pcol
+  int32_t pscan;                  // phase 1 by part_scan_kernel (dense filter programs, <= 2 group columns)
+  int32_t pscan_wave_bytes;       // its per-wave LDS area
   int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
   int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
   int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)

@@ -2167,6 +2167,176 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
   }
 }
 
+// ---- PART mode, phase 1 without the ring: part_scan_kernel ------------------------------------------------------
+// Used when every segment's filter is a dense program (no candidate queue) and at most two group columns: each
+// wave reads its tiles' columns straight from HBM (lane l's b consecutive words of each column: the whole tile is
+// one contiguous read per column) and emits the matched docs' records SORTED by key partition: per half tile a
+// wave-local counting sort in LDS (rank within the partition by an LDS atomic on a per-wave histogram, one cursor
+// reservation per non-empty partition on the workgroup's region cursors), then lanes store consecutive records of
+// a partition run to consecutive addresses -- coalesced runs instead of one scattered 4-B store per record.
+#define PGPU_PSCAN_THREADS 256
+#define PGPU_PSCAN_WAVES (PGPU_PSCAN_THREADS / 64)
+
+__global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int np = p.nparts;
+  uint32_t* cursor = (uint32_t*)dyn_smem;  // [np] this workgroup's region fill (records)
+  unsigned char* wb = dyn_smem + ((4 * np + 15) & ~15) + (size_t)wave * p.pscan_wave_bytes;
+  uint32_t* hist = (uint32_t*)wb;  // [np] records per partition in this half tile, then their ranks
+  uint32_t* start = hist + np;     // [np] run start in the sorted staging area
+  uint32_t* base = start + np;     // [np] run start in the region (reserved on `cursor`)
+  uint32_t* srec = base + np;      // [1024 * rw] staging: records sorted by partition
+  uint16_t* spart = (uint16_t*)(srec + 1024 * p.rw);  // [1024] partition of each staged record
+  Cons cv;
+  cv.masks = (uint32_t*)(spart + 1024);  // filter mask rows
+  cv.queue = nullptr;
+  cv.klist = cv.vlist = nullptr;
+  cv.acc = nullptr;
+  cv.qtiles = nullptr;
+  for (int i = threadIdx.x; i < np; i += PGPU_PSCAN_THREADS) cursor[i] = 0u;
+  __syncthreads();
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  const uint32_t cap = (uint32_t)p.rcap, pmask = (1u << p.pshift) - 1u;
+  const int idbits = p.rec_idbits;
+  int64_t matched = 0, scanned = 0, dense_bytes = 0;
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = false;
+#endif
+  SegState ss;
+  int cseg = -1;
+  for (int tile = t0 + wave; tile < t1; tile += PGPU_PSCAN_WAVES) {
+    const Cursor cu = cursor_at(p, tile);
+    if (cu.seg != cseg) {
+      cseg = cu.seg;
+      load_seg(p, cseg, ss);
+    }
+    TileCtx t;
+    t.ss = &ss;
+    t.slot = nullptr;
+    t.tile_in_seg = cu.tile_in_seg;
+    t.doc0 = cu.tile_in_seg * WT;
+    t.lane_doc0 = t.doc0 + 32 * lane;
+    const int ndocs = min(WT, ss.num_docs - t.doc0);
+    {
+      const int rem = ndocs - 32 * lane;
+      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+    }
+    uint32_t mm = t.valid;
+    if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
+    const int nm = wave_sum_i32(__popc(mm));
+    if (lane == 0) matched += nm;
+    if (nm == 0) continue;
+    // group keys (mixed radix of remapped ids) and the carried value / dict id, in registers
+    uint32_t key[32], val[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) key[i] = val[i] = 0;
+    for (int g = 0; g < p.ngcols; ++g) {
+      const DevColumn c = col_of(ss, p.gcols[g]);
+      if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
+      uint32_t ids[32];
+      decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, ids);
+      const int32_t* remap = cld(ss.remaps, g);
+      if (remap) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) ids[i] = lane_bit(mm, i) ? (uint32_t)gld(remap, ids[i]) : 0u;
+      }
+      const uint32_t st = p.gstride[g];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) key[i] += ids[i] * st;
+    }
+    if (p.pcol >= 0) {
+      const DevColumn c = col_of(ss, p.pcol);
+      if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
+      decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, val);
+      if (!idbits) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
+      }
+    }
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t hm = (mm >> (16 * h)) & 0xFFFFu;
+      const int nh = wave_sum_i32(__popc(hm));
+      if (nh == 0) continue;
+      for (int i = lane; i < np; i += 64) hist[i] = 0u;
+      wave_sync();
+      uint32_t rank[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t k = h ? key[16 + i] : key[i];
+        rank[i] = lane_bit(hm, i) ? atomicAdd(&hist[k >> p.pshift], 1u) : 0u;
+      }
+      wave_sync();
+      // run starts (exclusive scan of the histogram) and region reservations, 8 partitions per lane
+      {
+        uint32_t c8[8], tot = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int q = lane * 8 + j;
+          c8[j] = q < np ? hist[q] : 0u;
+          tot += c8[j];
+        }
+        uint32_t run = (uint32_t)wave_excl_scan((int)tot);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int q = lane * 8 + j;
+          if (q < np) {
+            start[q] = run;
+            base[q] = c8[j] ? atomicAdd(&cursor[q], c8[j]) : 0u;
+          }
+          run += c8[j];
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (!lane_bit(hm, i)) continue;
+        const uint32_t k = h ? key[16 + i] : key[i];
+        const uint32_t v = h ? val[16 + i] : val[i];
+        const uint32_t q = k >> p.pshift;
+        const uint32_t j = start[q] + rank[i];
+        if (p.rw == 1) srec[j] = idbits ? ((k & pmask) << idbits) | v : k;
+        else *(u32x2*)(srec + 2 * j) = u32x2{k, v};
+        spart[j] = (uint16_t)q;
+      }
+      wave_sync();
+      for (int j = lane; j < nh; j += 64) {
+        const uint32_t q = spart[j];
+        const uint32_t off = base[q] + (uint32_t)j - start[q];
+        const size_t region = ((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap;
+        if (off < cap) {
+          if (p.rw == 1) p.recs[region + off] = srec[j];
+          else *(u32x2*)(p.recs + 2 * (region + off)) = *(const u32x2*)(srec + 2 * j);
+        } else if (p.rw == 1) {  // region full: this record goes straight into the HBM table
+          const uint32_t r = srec[j];
+          if (idbits) part_spill(p, (q << p.pshift) | (r >> idbits), r & ((1u << idbits) - 1u));
+          else part_spill(p, r, 0u);
+        } else {
+          const u32x2 r = *(const u32x2*)(srec + 2 * j);
+          part_spill(p, r.x, r.y);
+        }
+      }
+      wave_sync();
+    }
+  }
+  const size_t w = (size_t)blockIdx.x * PGPU_PSCAN_WAVES + wave;
+  if (lane == 0) {
+    int64_t* o = p.stats + w * PGPU_NSTATS;
+    o[PGPU_STAT_MATCHED] = matched;
+    o[PGPU_STAT_SCANNED] = scanned;
+    o[PGPU_STAT_SECTOR_BYTES] = 0;
+    o[PGPU_STAT_DENSE_BYTES] = dense_bytes;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
+    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = cursor[q] < cap ? cursor[q] : cap;
+}
+
 // PART mode, phase 2: workgroup q aggregates the records of key partition q (from every query workgroup's
 // region) into an LDS table [nsec][K], then folds it into the HBM table, which holds the identities plus the
 // phase-1 spills.  NS = value sections (all reduce the records' one value column); R records per thread per
@@ -2521,7 +2691,15 @@ hipError_t pgpu_prepare_part_reduce() {
                             PGPU_PART_LDS_BYTES);
   PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
 #undef PART_ATTR
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)part_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PGPU_LDS_LIMIT);
   return e;
+}
+
+hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+  hipLaunchKernelGGL(part_scan_kernel, dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {

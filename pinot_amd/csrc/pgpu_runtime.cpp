@@ -42,6 +42,7 @@ hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, i
                                int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
+hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 // pgpu_iterstats.cpp
 int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
                                   int num_leaves, int32_t num_docs);
@@ -1573,6 +1574,26 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       dyn = ddyn;
     }
   }
+  // partitioned group-by whose segments need no candidate queue: phase 1 by part_scan_kernel (self-loading waves,
+  // records emitted in partition-sorted runs)
+  static const bool no_pscan = getenv("PGPU_NO_PSCAN") && atoi(getenv("PGPU_NO_PSCAN")) != 0;
+  p.pscan = 0;
+  if (!no_pscan && p.mode == PGPU_MODE_PART && nparts <= PGPU_PSCAN_MAX_PARTS && pk.tile_bytes >= 0) {
+    bool ok = true;
+    for (const DevSeg& ds : pk.segs) ok &= ds.rprog_len == 0;
+    if (ok) {
+      const int rw = pcol >= 0 ? 2 : 1;  // worst case; the one-word decision below only shrinks the area
+      p.pscan_wave_bytes = (int32_t)align16(12 * nparts + 1024 * 4 * rw + 2048 + 256 * p.mask_rows);
+      const size_t pdyn = align16(4 * nparts) + 4 * (size_t)p.pscan_wave_bytes;
+      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(3, PGPU_LDS_LIMIT / pdyn));
+      int g = (int)std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 4));
+      if (g >= 8) g &= ~7;
+      p.pscan = 1;
+      p.direct = 0;
+      grid = std::max(1, g);
+      dyn = pdyn;
+    }
+  }
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!ctx->lds_ready) {
@@ -1580,7 +1601,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       ctx->lds_ready = true;
     }
   }
-  const int nwaves = grid * (p.direct ? 4 : PGPU_WAVES_OF(p.dense));
+  const int nwaves = grid * (p.direct || p.pscan ? 4 : PGPU_WAVES_OF(p.dense));
 
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
@@ -1705,7 +1726,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
-  if (e == hipSuccess) e = p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st);
+  if (e == hipSuccess)
+    e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
+                : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
@@ -1817,13 +1840,14 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
       }
   }
   if (qq->params.flags & PGPU_FLAG_PROFILE) {
-    const int nw = qq->grid * (qq->params.direct ? 4 : PGPU_WAVES_OF(qq->params.dense));
+    const int nw = qq->grid * (qq->params.direct || qq->params.pscan ? 4 : PGPU_WAVES_OF(qq->params.dense));
     std::vector<int64_t> pr((size_t)nw * PGPU_NPROF);
     HIP_TRY(hipMemcpy(pr.data(), qq->params.prof, pr.size() * 8, hipMemcpyDeviceToHost));
     double sum[PGPU_NPROF] = {0};
     int nl = 0, nc = 0;
     for (int w = 0; w < nw; ++w) {
-      const bool ld = !qq->params.direct && (w % PGPU_WAVES_OF(qq->params.dense)) < PGPU_NLOAD_OF(qq->params.dense);
+      const bool ld = !qq->params.direct && !qq->params.pscan &&
+                      (w % PGPU_WAVES_OF(qq->params.dense)) < PGPU_NLOAD_OF(qq->params.dense);
       ld ? ++nl : ++nc;
       for (int k = 0; k < PGPU_NPROF; ++k) sum[k] += (double)pr[(size_t)w * PGPU_NPROF + k];
     }
