@@ -235,8 +235,9 @@ struct DevParams {
   int32_t rec_idbits;             // > 0: one-word records ((key & partition mask) << rec_idbits | dict id) -- every
                                   // segment shares pcol's dictionary (pdict); 0: {key, raw 4-byte value} records
   const void* pdict;              // rec_idbits > 0: the shared dictionary of pcol
-  int32_t pscan;                  // phase 1 by part_scan_kernel (dense filter programs, <= 2 group columns)
-  int32_t pscan_wave_bytes;       // its per-wave LDS area
+  int32_t pscan;                  // > 0: phase 1 by part_scan_kernel (dense filter programs) with LDS rings of
+                                  // this many records per partition (a power of two, >= two 128-B lines)
+  int32_t pscan_wave_bytes;       // its per-wave LDS area (filter mask rows)
   int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
   int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
   int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)

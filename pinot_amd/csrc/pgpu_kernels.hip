@@ -2168,33 +2168,123 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
 }
 
 // ---- PART mode, phase 1 without the ring: part_scan_kernel ------------------------------------------------------
-// Used when every segment's filter is a dense program (no candidate queue) and at most two group columns: each
-// wave reads its tiles' columns straight from HBM (lane l's b consecutive words of each column: the whole tile is
-// one contiguous read per column) and emits the matched docs' records SORTED by key partition: per half tile a
-// wave-local counting sort in LDS (rank within the partition by an LDS atomic on a per-wave histogram, one cursor
-// reservation per non-empty partition on the workgroup's region cursors), then lanes store consecutive records of
-// a partition run to consecutive addresses -- coalesced runs instead of one scattered 4-B store per record.
+// Used when every segment's filter is a dense program (no candidate queue): each wave reads its tiles' columns
+// straight from HBM (lane l's b consecutive words of each column: the whole tile is one contiguous read per column)
+// and appends the matched docs' records to its workgroup's region of each key partition through an LDS
+// write-combining ring per partition (p.pscan records, >= two 128-B lines).  Steps are workgroup-synchronous:
+//   insert  every wave takes a slot per record on the partition's LDS tail (the slot IS the record's position in
+//           the region) and writes the record into the ring, or straight to HBM when the ring is full;
+//   flush   the ring's complete 128-B lines (all of them at the end) are written out, two lines per store
+//           instruction (lanes 0-31 / 32-63) -- HBM sees whole lines instead of one 4-B store per record.
+#if TU_HAS(3)
 #define PGPU_PSCAN_THREADS 256
 #define PGPU_PSCAN_WAVES (PGPU_PSCAN_THREADS / 64)
+
+// one record to its region position `slot`, or into the HBM table when the region is full
+FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, uint32_t r0, uint32_t r1) {
+  if (slot < cap) {
+    const size_t at = ((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap + slot;
+    if (p.rw == 1) p.recs[at] = r0;
+    else *(u32x2*)(p.recs + 2 * at) = u32x2{r0, r1};
+  } else if (p.rw == 2) {
+    part_spill(p, r0, r1);
+  } else if (p.rec_idbits) {
+    part_spill(p, (q << p.pshift) | (r0 >> p.rec_idbits), r0 & ((1u << p.rec_idbits) - 1u));
+  } else {
+    part_spill(p, r0, 0u);
+  }
+}
+
+struct PscanChunk {  // records [s0, s0 + len) of partition q's ring, within one 128-B line of the region
+  int32_t q;
+  uint32_t s0, len;
+};
+
+// Store two chunks with one wave: lanes 0-31 write chunk a, lanes 32-63 chunk b (len 0 = none); lane j of a half
+// writes dword j of its chunk.
+FI void pscan_store(const DevParams& p, const uint32_t* ring, uint32_t RC, uint32_t cap, PscanChunk a, PscanChunk b) {
+  const int lane = lane_id(), j = lane & 31;
+  const bool hi = lane >= 32;
+  const int32_t q = hi ? b.q : a.q;
+  const uint32_t s0 = hi ? b.s0 : a.s0, len = hi ? b.len : a.len;
+  if (p.rw == 1) {
+    if ((uint32_t)j < len) {
+      const uint32_t slot = s0 + j;
+      pscan_put(p, q, slot, cap, ring[(size_t)q * RC + (slot & (RC - 1))], 0u);
+    }
+  } else {
+    const uint32_t r = (uint32_t)j >> 1;
+    if (r < len) {
+      const uint32_t slot = s0 + r;
+      const uint32_t* src = ring + 2 * ((size_t)q * RC + (slot & (RC - 1)));
+      if (slot < cap) {
+        p.recs[2 * (((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap + slot) + (j & 1)] = src[j & 1];
+      } else if ((j & 1) == 0) {
+        part_spill(p, src[0], src[1]);
+      }
+    }
+  }
+}
+
+// Flush this wave's share of the partitions: complete lines (every record when `final`), pairing chunks.
+FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring, uint32_t RC,
+                    uint32_t cap, int wave, bool final) {
+  const int lane = lane_id(), np = p.nparts;
+  const uint32_t line = 32u / (uint32_t)p.rw;  // records per 128-B line
+  PscanChunk pend{0, 0, 0};
+  for (int qb = wave * 64; qb < np; qb += 64 * PGPU_PSCAN_WAVES) {
+    const int q = qb + lane;
+    uint32_t H = 0, E = 0;
+    if (q < np) {
+      H = head[q];
+      const uint32_t T = tail[q];
+      if (T - H > RC) {  // the ring overflowed this step: it holds [H, H + RC), the rest went straight to HBM
+        E = H + RC;
+        head[q] = T;
+      } else {
+        E = final ? T : (T & ~(line - 1u));
+        if (E < H) E = H;
+        head[q] = E;
+      }
+    }
+    uint64_t todo = __ballot(E > H);
+    while (todo) {
+      const int l = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int32_t qq = qb + l;
+      uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)H, l);
+      const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)E, l);
+      while (h < e) {
+        const uint32_t ce = min(e, (h | (line - 1u)) + 1u);
+        const PscanChunk c{qq, h, ce - h};
+        if (pend.len) {
+          pscan_store(p, ring, RC, cap, pend, c);
+          pend.len = 0;
+        } else {
+          pend = c;
+        }
+        h = ce;
+      }
+    }
+  }
+  if (pend.len) pscan_store(p, ring, RC, cap, pend, PscanChunk{0, 0, 0});
+}
 
 __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int np = p.nparts;
-  uint32_t* cursor = (uint32_t*)dyn_smem;  // [np] this workgroup's region fill (records)
-  unsigned char* wb = dyn_smem + ((4 * np + 15) & ~15) + (size_t)wave * p.pscan_wave_bytes;
-  uint32_t* hist = (uint32_t*)wb;  // [np] records per partition in this half tile, then their ranks
-  uint32_t* start = hist + np;     // [np] run start in the sorted staging area
-  uint32_t* base = start + np;     // [np] run start in the region (reserved on `cursor`)
-  uint32_t* srec = base + np;      // [1024 * rw] staging: records sorted by partition
-  uint16_t* spart = (uint16_t*)(srec + 1024 * p.rw);  // [1024] partition of each staged record
+  const uint32_t RC = (uint32_t)p.pscan;  // ring records per partition (power of two)
+  uint32_t* head = (uint32_t*)dyn_smem;   // [np] first slot not yet written out
+  uint32_t* tail = head + np;             // [np] slots taken (= records of this workgroup in the partition)
+  uint32_t* ring = tail + np;             // [np][RC * rw]
   Cons cv;
-  cv.masks = (uint32_t*)(spart + 1024);  // filter mask rows
+  cv.masks = (uint32_t*)((unsigned char*)(ring + (size_t)np * RC * p.rw) + (size_t)wave * p.pscan_wave_bytes);
   cv.queue = nullptr;
   cv.klist = cv.vlist = nullptr;
   cv.acc = nullptr;
   cv.qtiles = nullptr;
-  for (int i = threadIdx.x; i < np; i += PGPU_PSCAN_THREADS) cursor[i] = 0u;
+  for (int i = threadIdx.x; i < 2 * np; i += PGPU_PSCAN_THREADS) head[i] = 0u;
   __syncthreads();
   const int nb = gridDim.x, b = blockIdx.x;
   const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
@@ -2209,121 +2299,81 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams
 #endif
   SegState ss;
   int cseg = -1;
-  for (int tile = t0 + wave; tile < t1; tile += PGPU_PSCAN_WAVES) {
-    const Cursor cu = cursor_at(p, tile);
-    if (cu.seg != cseg) {
-      cseg = cu.seg;
-      load_seg(p, cseg, ss);
-    }
-    TileCtx t;
-    t.ss = &ss;
-    t.slot = nullptr;
-    t.tile_in_seg = cu.tile_in_seg;
-    t.doc0 = cu.tile_in_seg * WT;
-    t.lane_doc0 = t.doc0 + 32 * lane;
-    const int ndocs = min(WT, ss.num_docs - t.doc0);
-    {
-      const int rem = ndocs - 32 * lane;
-      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
-    }
-    uint32_t mm = t.valid;
-    if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
-    const int nm = wave_sum_i32(__popc(mm));
-    if (lane == 0) matched += nm;
-    if (nm == 0) continue;
-    // group keys (mixed radix of remapped ids) and the carried value / dict id, in registers
-    uint32_t key[32], val[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) key[i] = val[i] = 0;
-    for (int g = 0; g < p.ngcols; ++g) {
-      const DevColumn c = col_of(ss, p.gcols[g]);
-      if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
-      uint32_t ids[32];
-      decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, ids);
-      const int32_t* remap = cld(ss.remaps, g);
-      if (remap) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) ids[i] = lane_bit(mm, i) ? (uint32_t)gld(remap, ids[i]) : 0u;
+  const int nsteps = (t1 - t0 + PGPU_PSCAN_WAVES - 1) / PGPU_PSCAN_WAVES;
+  for (int step = 0; step < nsteps; ++step) {
+    const int tile = t0 + step * PGPU_PSCAN_WAVES + wave;
+    if (tile < t1) {
+      const Cursor cu = cursor_at(p, tile);
+      if (cu.seg != cseg) {
+        cseg = cu.seg;
+        load_seg(p, cseg, ss);
       }
-      const uint32_t st = p.gstride[g];
-#pragma unroll
-      for (int i = 0; i < 32; ++i) key[i] += ids[i] * st;
-    }
-    if (p.pcol >= 0) {
-      const DevColumn c = col_of(ss, p.pcol);
-      if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
-      decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, val);
-      if (!idbits) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
-      }
-    }
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-      const uint32_t hm = (mm >> (16 * h)) & 0xFFFFu;
-      const int nh = wave_sum_i32(__popc(hm));
-      if (nh == 0) continue;
-      for (int i = lane; i < np; i += 64) hist[i] = 0u;
-      wave_sync();
-      uint32_t rank[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t k = h ? key[16 + i] : key[i];
-        rank[i] = lane_bit(hm, i) ? atomicAdd(&hist[k >> p.pshift], 1u) : 0u;
-      }
-      wave_sync();
-      // run starts (exclusive scan of the histogram) and region reservations, 8 partitions per lane
+      TileCtx t;
+      t.ss = &ss;
+      t.slot = nullptr;
+      t.tile_in_seg = cu.tile_in_seg;
+      t.doc0 = cu.tile_in_seg * WT;
+      t.lane_doc0 = t.doc0 + 32 * lane;
+      const int ndocs = min(WT, ss.num_docs - t.doc0);
       {
-        uint32_t c8[8], tot = 0;
+        const int rem = ndocs - 32 * lane;
+        t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+      }
+      uint32_t mm = t.valid;
+      if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
+      const int nm = wave_sum_i32(__popc(mm));
+      if (lane == 0) matched += nm;
+      if (nm) {
+        // group keys (mixed radix of remapped ids) and the carried value / dict id, in registers
+        uint32_t key[32], val[32];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int q = lane * 8 + j;
-          c8[j] = q < np ? hist[q] : 0u;
-          tot += c8[j];
-        }
-        uint32_t run = (uint32_t)wave_excl_scan((int)tot);
+        for (int i = 0; i < 32; ++i) key[i] = val[i] = 0;
+        for (int g = 0; g < p.ngcols; ++g) {
+          const DevColumn c = col_of(ss, p.gcols[g]);
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
+          uint32_t ids[32];
+          decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, ids);
+          const int32_t* remap = cld(ss.remaps, g);
+          if (remap) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int q = lane * 8 + j;
-          if (q < np) {
-            start[q] = run;
-            base[q] = c8[j] ? atomicAdd(&cursor[q], c8[j]) : 0u;
+            for (int i = 0; i < 32; ++i) ids[i] = lane_bit(mm, i) ? (uint32_t)gld(remap, ids[i]) : 0u;
           }
-          run += c8[j];
-        }
-      }
-      wave_sync();
+          const uint32_t st = p.gstride[g];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (!lane_bit(hm, i)) continue;
-        const uint32_t k = h ? key[16 + i] : key[i];
-        const uint32_t v = h ? val[16 + i] : val[i];
-        const uint32_t q = k >> p.pshift;
-        const uint32_t j = start[q] + rank[i];
-        if (p.rw == 1) srec[j] = idbits ? ((k & pmask) << idbits) | v : k;
-        else *(u32x2*)(srec + 2 * j) = u32x2{k, v};
-        spart[j] = (uint16_t)q;
-      }
-      wave_sync();
-      for (int j = lane; j < nh; j += 64) {
-        const uint32_t q = spart[j];
-        const uint32_t off = base[q] + (uint32_t)j - start[q];
-        const size_t region = ((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap;
-        if (off < cap) {
-          if (p.rw == 1) p.recs[region + off] = srec[j];
-          else *(u32x2*)(p.recs + 2 * (region + off)) = *(const u32x2*)(srec + 2 * j);
-        } else if (p.rw == 1) {  // region full: this record goes straight into the HBM table
-          const uint32_t r = srec[j];
-          if (idbits) part_spill(p, (q << p.pshift) | (r >> idbits), r & ((1u << idbits) - 1u));
-          else part_spill(p, r, 0u);
-        } else {
-          const u32x2 r = *(const u32x2*)(srec + 2 * j);
-          part_spill(p, r.x, r.y);
+          for (int i = 0; i < 32; ++i) key[i] += ids[i] * st;
+        }
+        if (p.pcol >= 0) {
+          const DevColumn c = col_of(ss, p.pcol);
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
+          decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, val);
+          if (!idbits) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
+          }
+        }
+        // slots first (all LDS atomics in flight together), then the ring writes
+        uint32_t slot[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) slot[i] = lane_bit(mm, i) ? atomicAdd(&tail[key[i] >> p.pshift], 1u) : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          if (!lane_bit(mm, i)) continue;
+          const uint32_t q = key[i] >> p.pshift;
+          const uint32_t r0 = p.rw == 1 ? (idbits ? ((key[i] & pmask) << idbits) | val[i] : key[i]) : key[i];
+          if (slot[i] - head[q] < RC) {
+            if (p.rw == 1) ring[(size_t)q * RC + (slot[i] & (RC - 1))] = r0;
+            else *(u32x2*)(ring + 2 * ((size_t)q * RC + (slot[i] & (RC - 1)))) = u32x2{r0, val[i]};
+          } else {
+            pscan_put(p, q, slot[i], cap, r0, val[i]);
+          }
         }
       }
-      wave_sync();
     }
+    __syncthreads();
+    pscan_flush(p, head, tail, ring, RC, cap, wave, false);
+    __syncthreads();
   }
+  pscan_flush(p, head, tail, ring, RC, cap, wave, true);
   const size_t w = (size_t)blockIdx.x * PGPU_PSCAN_WAVES + wave;
   if (lane == 0) {
     int64_t* o = p.stats + w * PGPU_NSTATS;
@@ -2332,23 +2382,25 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams
     o[PGPU_STAT_SECTOR_BYTES] = 0;
     o[PGPU_STAT_DENSE_BYTES] = dense_bytes;
   }
-  __syncthreads();
   for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
-    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = cursor[q] < cap ? cursor[q] : cap;
+    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = tail[q] < cap ? tail[q] : cap;
 }
+#endif  // TU_HAS(3)
 
-// PART mode, phase 2: workgroup q aggregates the records of key partition q (from every query workgroup's
+// PART mode, phase 2: workgroup q aggregates the records of key partition q (from every phase-1 workgroup's
 // region) into an LDS table [nsec][K], then folds it into the HBM table, which holds the identities plus the
-// phase-1 spills.  NS = value sections (all reduce the records' one value column); R records per thread per
-// round, all loads issued before the first LDS atomic; section ops are uniform, so each round runs one
-// branch-free atomic loop per section.
-template <int NS>
+// phase-1 spills.  NS = value sections (all reduce the records' one value column); ONE = one-word records.  Each
+// wave walks its own regions in chunks of R x 64 records: the loads are unconditional (clamped indices), so a
+// chunk's R loads -- and then its R dictionary gathers -- are in flight together; section ops are uniform, so
+// each chunk runs one branch-free atomic loop per section.
+template <int NS, bool ONE>
 __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
   const uint32_t K = 1u << p.pshift;
   const uint32_t q = blockIdx.x;
   const uint64_t key0 = (uint64_t)q * K;
   const uint32_t nk = (uint32_t)min((uint64_t)K, p.G - key0);
+  const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   int32_t op[NS > 0 ? NS : 1];
 #pragma unroll
   for (int s = 0; s < NS; ++s) op[s] = p.sec_op[1 + s];
@@ -2360,47 +2412,40 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   __syncthreads();
   // one-word records: (in-partition key << idbits | dict id) over the shared dictionary; MIN / MAX sections reduce
   // the dict ids (sorted dictionary) and are turned into cell keys when folded into the HBM table
-  const int idbits = p.rec_idbits;
+  const int idbits = ONE ? p.rec_idbits : 0;
   const uint32_t idmask = idbits ? (1u << idbits) - 1u : 0u;
-  constexpr int R = 8;
-  for (int w = 0; w < nwg; ++w) {
+  bool need_val = false;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) need_val |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
+  constexpr int R = 16;
+  for (int w = wave; w < nwg; w += nwaves) {
     const uint32_t n = p.rcount[(size_t)q * nwg + w];
     const size_t base = ((size_t)q * nwg + w) * (size_t)p.rcap;
-    for (uint32_t i0 = 0; i0 < n; i0 += R * blockDim.x) {
+    for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
       uint32_t k[R], raw[R];
       bool ok[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const uint32_t i = i0 + r * blockDim.x + threadIdx.x;
+        const uint32_t i = i0 + r * 64 + lane;
         ok[r] = i < n;
-        k[r] = (uint32_t)key0;
-        raw[r] = 0;
-        if (ok[r]) {
-          if (NS == 0 || idbits) {
-            const uint32_t v = gld(p.recs, base + i);
-            k[r] = idbits ? (uint32_t)key0 + (v >> idbits) : v;
-            raw[r] = v & idmask;
-          } else {
-            const u32x2 v = gld((const u32x2*)p.recs, base + i);
-            k[r] = v.x;
-            raw[r] = v.y;
-          }
+        const size_t at = base + (ok[r] ? i : n - 1);
+        if (ONE) {
+          const uint32_t v = gld(p.recs, at);
+          k[r] = idbits ? v >> idbits : v - (uint32_t)key0;
+          raw[r] = v & idmask;
+        } else {
+          const u32x2 v = gld((const u32x2*)p.recs, at);
+          k[r] = v.x - (uint32_t)key0;
+          raw[r] = v.y;
         }
       }
       uint32_t val[R];  // the record's 4-byte dictionary value (SUM sections)
 #pragma unroll
       for (int r = 0; r < R; ++r) val[r] = raw[r];
-      if (idbits) {
-        bool need = false;
+      if (idbits && need_val) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) need |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
-        if (need) {
-#pragma unroll
-          for (int r = 0; r < R; ++r) val[r] = ok[r] ? gld((const uint32_t*)p.pdict, raw[r]) : 0u;
-        }
+        for (int r = 0; r < R; ++r) val[r] = gld((const uint32_t*)p.pdict, raw[r]);
       }
-#pragma unroll
-      for (int r = 0; r < R; ++r) k[r] -= (uint32_t)key0;
 #pragma unroll
       for (int r = 0; r < R; ++r)
         if (ok[r]) atomicAdd((unsigned long long*)&ptab[k[r]], 1ull);
@@ -2685,10 +2730,13 @@ PGPU_MODE_FUNCS(PGPU_MODE_PART, part)
 
 hipError_t pgpu_prepare_part_reduce() {
   hipError_t e = hipSuccess;
-#define PART_ATTR(NS)                                                                                       \
-  if (e == hipSuccess)                                                                                      \
-    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                            PGPU_PART_LDS_BYTES);
+#define PART_ATTR(NS)                                                                                  \
+  if (e == hipSuccess)                                                                                 \
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, true>,                                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_PART_LDS_BYTES);          \
+  if (e == hipSuccess)                                                                                 \
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, false>,                               \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_PART_LDS_BYTES);
   PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
 #undef PART_ATTR
   if (e == hipSuccess)
@@ -2705,9 +2753,10 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
   const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
   switch (p.nsec - 1) {
-#define PART_LAUNCH(NS)                                                                        \
-  case NS:                                                                                     \
-    hipLaunchKernelGGL(part_reduce_kernel<NS>, dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
+#define PART_LAUNCH(NS)                                                                                  \
+  case NS:                                                                                               \
+    if (p.rw == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true>), dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
+    else hipLaunchKernelGGL((part_reduce_kernel<NS, false>), dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
     return hipGetLastError();
     PART_LAUNCH(0) PART_LAUNCH(1) PART_LAUNCH(2) PART_LAUNCH(3) PART_LAUNCH(4)
 #undef PART_LAUNCH

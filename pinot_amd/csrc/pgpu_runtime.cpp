@@ -1574,24 +1574,50 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       dyn = ddyn;
     }
   }
+  // one-word PART records (in-partition key, dict id) when every segment holds the same dictionary for the
+  // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
+  int part_idbits = 0;
+  const void* part_pdict = nullptr;
+  if (p.mode == PGPU_MODE_PART && pcol >= 0) {
+    const HostColumn* h0 = &q->segments[0].segment->cols[q->segments[0].column_map[pcol]];
+    bool shared = h0->dict_card > 0 && !h0->hdict.empty();
+    for (int s = 1; s < q->num_segments && shared; ++s) {
+      const HostColumn* h = &q->segments[s].segment->cols[q->segments[s].column_map[pcol]];
+      shared = h->dict_card == h0->dict_card && h->dict_type == h0->dict_type && h->dict_hash[0] == h0->dict_hash[0] &&
+               h->dict_hash[1] == h0->dict_hash[1];
+    }
+    int idbits = 1;
+    while (idbits < 31 && (1ll << idbits) < h0->dict_card) ++idbits;
+    if (shared && pshift + idbits <= 32 && !(q->flags & PGPU_Q_PART_SPILL)) {
+      part_idbits = idbits;
+      part_pdict = h0->dict.p;
+    }
+  }
+  const int part_rw = pcol >= 0 && !part_idbits ? 2 : 1;
   // partitioned group-by whose segments need no candidate queue: phase 1 by part_scan_kernel (self-loading waves,
-  // records emitted in partition-sorted runs)
+  // records written through per-partition LDS rings of >= two 128-B lines); two workgroups per CU when the rings
+  // fit, else one
   static const bool no_pscan = getenv("PGPU_NO_PSCAN") && atoi(getenv("PGPU_NO_PSCAN")) != 0;
   p.pscan = 0;
-  if (!no_pscan && p.mode == PGPU_MODE_PART && nparts <= PGPU_PSCAN_MAX_PARTS && pk.tile_bytes >= 0) {
+  if (!no_pscan && p.mode == PGPU_MODE_PART && nparts <= PGPU_PSCAN_MAX_PARTS) {
     bool ok = true;
     for (const DevSeg& ds : pk.segs) ok &= ds.rprog_len == 0;
-    if (ok) {
-      const int rw = pcol >= 0 ? 2 : 1;  // worst case; the one-word decision below only shrinks the area
-      p.pscan_wave_bytes = (int32_t)align16(12 * nparts + 1024 * 4 * rw + 2048 + 256 * p.mask_rows);
-      const size_t pdyn = align16(4 * nparts) + 4 * (size_t)p.pscan_wave_bytes;
-      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(3, PGPU_LDS_LIMIT / pdyn));
+    const size_t wave_bytes = 256 * (size_t)p.mask_rows;
+    const size_t fixed_b = 8 * nparts + 4 * wave_bytes;
+    const uint64_t min_rc = 64 / part_rw;
+    for (int per_cu = 2; ok && per_cu >= 1 && !p.pscan; --per_cu) {
+      const size_t budget = PGPU_LDS_LIMIT / per_cu;
+      if (budget <= fixed_b) continue;
+      uint64_t rc = 1;
+      while (rc < 1024 && fixed_b + 4ull * nparts * part_rw * (rc * 2) <= budget) rc *= 2;
+      if (rc < min_rc) continue;
+      p.pscan = (int32_t)rc;
+      p.pscan_wave_bytes = (int32_t)wave_bytes;
       int g = (int)std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 4));
       if (g >= 8) g &= ~7;
-      p.pscan = 1;
       p.direct = 0;
       grid = std::max(1, g);
-      dyn = pdyn;
+      dyn = align16(fixed_b + 4ull * nparts * part_rw * rc);
     }
   }
   {
@@ -1640,27 +1666,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.pshift = pshift;
     p.nparts = (int32_t)nparts;
     p.pcol = pcol;
-    p.rw = pcol >= 0 ? 2 : 1;
-    p.rec_idbits = 0;
-    p.pdict = nullptr;
-    if (pcol >= 0) {
-      // one-word records (in-partition key, dict id) when every segment holds the same dictionary for the
-      // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
-      const HostColumn* h0 = &q->segments[0].segment->cols[q->segments[0].column_map[pcol]];
-      bool shared = h0->dict_card > 0 && !h0->hdict.empty();
-      for (int s = 1; s < q->num_segments && shared; ++s) {
-        const HostColumn* h = &q->segments[s].segment->cols[q->segments[s].column_map[pcol]];
-        shared = h->dict_card == h0->dict_card && h->dict_type == h0->dict_type && h->dict_hash[0] == h0->dict_hash[0] &&
-                 h->dict_hash[1] == h0->dict_hash[1];
-      }
-      int idbits = 1;
-      while (idbits < 31 && (1ll << idbits) < h0->dict_card) ++idbits;
-      if (shared && pshift + idbits <= 32 && !(q->flags & PGPU_Q_PART_SPILL)) {
-        p.rw = 1;
-        p.rec_idbits = idbits;
-        p.pdict = h0->dict.p;
-      }
-    }
+    p.rw = part_rw;
+    p.rec_idbits = part_idbits;
+    p.pdict = part_pdict;
     const double per = pk.est_matched / ((double)grid * (double)nparts);
     uint64_t cap = (uint64_t)(1.25 * per) + 32;
     if (q->flags & PGPU_Q_PART_SPILL) cap = 16;
