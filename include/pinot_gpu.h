@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 2
+#define PGPU_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -40,6 +40,14 @@ extern "C" {
 #define PGPU_E_HIP (-2)         /* HIP runtime failure (out of memory, launch failure, ...) */
 #define PGPU_E_UNSUPPORTED (-3) /* plan shape this build does not run on the GPU: caller keeps the CPU plan */
 #define PGPU_E_NOT_FOUND (-4)
+/* The query passed its deadline (pgpu_query_desc.deadline_ms) before it finished: the reference's combine stops
+ * polling for results blocks and answers QueryException.EXECUTION_TIMEOUT_ERROR
+ * (core/operator/combine/BaseCombineOperator.java:194-203).  Its kernels are told to stop (as by
+ * pgpu_query_cancel) and have drained when the call returns; the context stays usable. */
+#define PGPU_E_TIMEOUT (-5)
+/* pgpu_query_cancel was called before the query finished (the reference cancels the segment tasks' futures,
+ * BaseCombineOperator.getNextBlock); results and stats are partial and must be discarded. */
+#define PGPU_E_CANCELLED (-6)
 
 /* ---- stored data types (spi/data/FieldSpec.java DataType, stored type) -------------------------------------- */
 #define PGPU_INT 0
@@ -189,6 +197,11 @@ typedef struct {
    * the CPU plan, which reproduces the truncation).  0 = no limit. */
   int32_t num_groups_limit;
   int32_t array_based_threshold;
+  /* End time in milliseconds since the Unix epoch (QueryContext.getEndTimeMs: the broker's timeoutMs from the
+   * query's arrival, System.currentTimeMillis clock); 0 = none.  Passed when the query is waited for (or already
+   * at launch), the query is cancelled and pgpu_query_wait / _collect / _execute / pgpu_node_query return
+   * PGPU_E_TIMEOUT. */
+  int64_t deadline_ms;
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
@@ -282,6 +295,12 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
                       uint64_t table_bytes, pgpu_query** out_query);
 int pgpu_query_wait(pgpu_query* query, pgpu_query_stats* out_stats);
 int pgpu_query_release(pgpu_query* query);
+/* Ask a launched / submitted query to stop (thread-safe; returns at once, from any thread, also while another
+ * thread blocks in pgpu_query_wait / _collect).  Every kernel of the query polls the flag per range of tiles
+ * (the ring kernel's loaders, the self-loading waves, the partitioned group-by's phase-1 steps and phase-2
+ * regions) and skips the rest of its work; the wait then returns PGPU_E_CANCELLED (PGPU_E_TIMEOUT when the
+ * deadline fired it), and the query must still be released / collected. */
+int pgpu_query_cancel(pgpu_query* query);
 
 /* Compact a (reduced) table: copy every key with count > 0 to the host (dense: ascending by key; hash: in slot
  * order).

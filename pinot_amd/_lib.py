@@ -20,6 +20,9 @@ PGPU_OK = 0
 PGPU_E_INVALID = -1
 PGPU_E_HIP = -2
 PGPU_E_UNSUPPORTED = -3
+PGPU_E_NOT_FOUND = -4
+PGPU_E_TIMEOUT = -5
+PGPU_E_CANCELLED = -6
 
 PGPU_INT, PGPU_LONG, PGPU_FLOAT, PGPU_DOUBLE, PGPU_STRING = range(5)
 PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
@@ -33,7 +36,7 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class PinotGpuError(RuntimeError):
@@ -46,6 +49,15 @@ class PinotGpuError(RuntimeError):
 
 class UnsupportedPlanError(PinotGpuError):
     """PGPU_E_UNSUPPORTED: the server keeps the reference CPU plan for this query."""
+
+
+class QueryTimeoutError(PinotGpuError):
+    """PGPU_E_TIMEOUT: the query passed its deadline (QueryException.EXECUTION_TIMEOUT_ERROR,
+    BaseCombineOperator.java:194-203)."""
+
+
+class QueryCancelledError(PinotGpuError):
+    """PGPU_E_CANCELLED: pgpu_query_cancel stopped the query."""
 
 
 # ---- structs -------------------------------------------------------------------------------------------------
@@ -69,7 +81,7 @@ class QueryDesc(C.Structure):
                 ("num_aggs", C.c_int32), ("num_group_columns", C.c_int32), ("aggs", C.POINTER(Agg)),
                 ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
                 ("flags", C.c_uint64), ("reduce_docs", C.c_int64), ("num_groups_limit", C.c_int32),
-                ("array_based_threshold", C.c_int32)]
+                ("array_based_threshold", C.c_int32), ("deadline_ms", C.c_int64)]
 
 
 class TableLayout(C.Structure):
@@ -123,6 +135,7 @@ SIGNATURES = [
     ("pgpu_query_launch", C.c_int, [_P, C.POINTER(QueryDesc), _P, _P, C.c_uint64, C.POINTER(_P)]),
     ("pgpu_query_wait", C.c_int, [_P, C.POINTER(QueryStats)]),
     ("pgpu_query_release", C.c_int, [_P]),
+    ("pgpu_query_cancel", C.c_int, [_P]),
     ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_query_submit", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(_P)]),
@@ -179,6 +192,10 @@ def check(rc: int) -> None:
         msg = last_error()
         if rc == PGPU_E_UNSUPPORTED:
             raise UnsupportedPlanError(rc, msg)
+        if rc == PGPU_E_TIMEOUT:
+            raise QueryTimeoutError(rc, msg)
+        if rc == PGPU_E_CANCELLED:
+            raise QueryCancelledError(rc, msg)
         raise PinotGpuError(rc, msg)
 
 

@@ -185,7 +185,7 @@ struct DevAgg {
 #define PGPU_PART_LDS_BYTES (128 * 1024)   // phase-2 LDS table per partition (keys x sections x 8 B)
 #define PGPU_PART_MAX_PARTS 8192           // phase-1 LDS cursors (4 B each) must fit PGPU_LDS_TABLE_BYTES
 #define PGPU_PART_MAX_SECTIONS 5           // count + up to 4 value sections (part_reduce_kernel<NS>)
-#define PGPU_PSCAN_MAX_PARTS 512           // part_scan_kernel: per-wave histograms of at most this many partitions
+#define PGPU_PSCAN_MAX_PARTS 2048          // part_scan_kernel: LDS rings of at most this many partitions
 // Hash group-by (PGPU_KEYS_HASH): the table's cells are indexed by an open-addressing slot (linear probing,
 // lock-free 64-bit CAS insert).  Keys of more than 63 bits are interned in two levels: word 0 (columns
 // [0, key_split)) gets a slot s0 in a first table, then the slot of (s0 << 32 | word 1) is the cell index.
@@ -197,6 +197,9 @@ struct DevAgg {
 #define PGPU_STAT_SECTOR_BYTES 2
 #define PGPU_STAT_DENSE_BYTES 3
 #define PGPU_NSTATS 4
+// a ring slot's FULL flag with this bit: the loader saw the query cancelled and loaded nothing -- skip the tile
+#define PGPU_SLOT_SKIP 0x40000000
+#define PGPU_CANCEL_POLL 16   // tiles (per loader / self-loading wave) or phase-1 steps between polls
 
 struct DevParams {
   const DevSeg* segs;
@@ -224,7 +227,7 @@ struct DevParams {
   int32_t max_instrs;             // max DMA instructions of one tile (loader vmcnt budget)
   int32_t dense;                  // kernel variant (PGPU_THREADS)
   // PART mode: records of rw uint32 words {global key[, raw 4-byte dictionary value of column pcol]}; region of
-  // (partition q, workgroup w) = records [(q * grid + w) * rcap, +rcap); rcount[q * grid + w] = records written
+  // (partition q, workgroup w) = records [(w * nparts + q) * rcap, +rcap); rcount[q * grid + w] = records written
   uint32_t* recs;
   uint32_t* rcount;
   int32_t pshift;                 // keys per partition = 1 << pshift
@@ -243,13 +246,18 @@ struct DevParams {
   int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)
   int32_t dslots;                 // direct: LDS slots per wave (dslots - 1 tiles in flight while one is filtered)
   int32_t min_instrs;             // direct: fewest DMA instructions of any segment's tile (counted vmcnt waits)
-  int32_t pad2;
+  // PART with one-word records: ldict = phase 2 reads SUM values from pdict copied into LDS beside its table
+  // (1 << slice_shift >= pdict_n entries)
+  int32_t slice_shift;
+  int32_t ldict;
+  uint32_t pdict_n;               // pdict entries
   // HASH mode: key words follow the sections in `table` (word 0 at table + nsec * G; two-level keys: the
   // interned word-0 values at + G); segmask = distinct-key bitmaps of the tracked segments ([rows][G / 32]);
   // hflag[0] = a probe sequence ran out of slots (query fails)
   uint32_t* segmask;
   int32_t* hflag;
   uint32_t* leaf_bits;            // PGPU_Q_EXACT_FILTER_STATS (see DevSeg::leaf_bits_off)
+  const int32_t* cancel;          // != 0: stop (pgpu_query_cancel / deadline); pinned host word, polled per tile range
   int32_t key_words;
   int32_t key_split;
   int32_t segmask_rows;

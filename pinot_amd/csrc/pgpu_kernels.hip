@@ -185,6 +185,12 @@ FI void loader_flag_store(int* p, int v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
 }
 
+// The query's cancel word (pinned host memory, written by pgpu_query_cancel): one uncached system-scope load.
+FI bool query_cancelled(const DevParams& p) {
+  if (!p.cancel) return false;
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0;
+}
+
 // s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the immediate must be a constant).
 FI void wait_vmcnt(int n) {
 #define VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
@@ -850,9 +856,13 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
     while (pslot >= R) pslot -= R;
     if (pub < ntiles && cursor_advance(p, cp, NLOAD)) cp_instrs = cld(&p.segs[cp.seg].stage_instrs);
   };
+  bool cx = false;  // cancelled: publish the remaining tiles as skipped, load nothing
   for (;;) {
     while (nunpub > 0 && (nunpub > P || pend > budget || seq >= ntiles)) publish_one();
     if (seq >= ntiles) break;
+    if (!cx && ((seq - li) / NLOAD) % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p)) cx = true;
+    if (cx)
+      while (nunpub > 0) publish_one();
     if (seq >= R) {
       // the slot's previous tile must have been consumed; publish what is in flight while waiting
       const int64_t t0f = now(pf);
@@ -866,6 +876,13 @@ FI void loader(const DevParams& p, const Lds& L, int li, int t0, int ntiles, Pro
         }
       }
       PROF_ADD(pf, PGPU_P_L_FREE, t0f);
+    }
+    if (cx) {
+      loader_flag_store(&L.full[slot], (seq + 1) | PGPU_SLOT_SKIP);
+      seq += NLOAD;
+      slot += NLOAD;
+      while (slot >= R) slot -= R;
+      continue;
     }
     const int64_t t0i = now(pf);
     issue_tile(sc, ci.tile_in_seg, L.ring + (size_t)slot * S);
@@ -1187,6 +1204,10 @@ FI int64_t* table_base(const DevParams& p, const Lds& L) {
   return MODE == PGPU_MODE_LDS ? L.ltab : p.table;
 }
 
+// PART mode: region of (partition q, phase-1 workgroup w): a workgroup's regions are contiguous, so its record
+// streams stay within a few pages (one region per partition would put every store on a different page)
+FI size_t part_region(const DevParams& p, uint32_t q, uint32_t w) { return (size_t)w * p.nparts + q; }
+
 // PART mode: append the records {key[, raw]} of the live entries to this workgroup's region of each key's
 // partition.  All N slot reservations (LDS cursor atomics) are issued before the first store.  A full region
 // spills the doc straight into the HBM table with atomics: correct, only slower.
@@ -1211,7 +1232,7 @@ FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], co
   for (int r = 0; r < N; ++r) {
     if (!((live >> r) & 1u)) continue;
     if (slot[r] < cap) {
-      const size_t rec = ((size_t)(key[r] >> p.pshift) * gridDim.x + blockIdx.x) * (size_t)cap + slot[r];
+      const size_t rec = part_region(p, key[r] >> p.pshift, blockIdx.x) * (size_t)cap + slot[r];
       if (p.rw == 1)
         p.recs[rec] = p.rec_idbits ? ((key[r] & ((1u << p.pshift) - 1)) << p.rec_idbits) | raw[r] : key[r];
       else *(u32x2*)(p.recs + 2 * rec) = u32x2{key[r], raw[r]};
@@ -1714,7 +1735,8 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     unsigned char* slot = L.ring + (size_t)slot_i * S;
     const int64_t tw = now(pf);
     // poll with back-off: the scalar ALU is shared by every wave of the CU
-    for (int nap = 0; flag_load(&L.full[slot_i]) != seq + 1; nap = nap < 3 ? nap + 1 : 3) {
+    int fl;
+    for (int nap = 0; ((fl = flag_load(&L.full[slot_i])) & ~PGPU_SLOT_SKIP) != seq + 1; nap = nap < 3 ? nap + 1 : 3) {
       if (nap == 0) __builtin_amdgcn_s_sleep(1);
       else if (nap == 1) __builtin_amdgcn_s_sleep(2);
       else if (nap == 2) __builtin_amdgcn_s_sleep(4);
@@ -1722,6 +1744,10 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     PROF_ADD(pf, PGPU_P_C_FULL, tw);
+    if (fl & PGPU_SLOT_SKIP) {  // cancelled: nothing was loaded into the slot; hand it back
+      if (lane == 0) flag_store(&L.freef[slot_i], seq + 1);
+      continue;
+    }
     const int64_t tf = now(pf);
 #ifdef PGPU_PROFILE_BUILD
     if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
@@ -1917,6 +1943,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
         ++issued;
         if (++islot == D) islot = 0;
       }
+      if (k % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p)) break;  // in-flight DMAs drain below
       const int next_instrs = (issued - k - 1) * p.min_instrs;  // lower bound of the DMAs issued after tile k
       if (k > 0) cursor_advance(p, cur, NW);
       if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES || cur.seg != cseg)) {
@@ -2183,7 +2210,7 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
 // one record to its region position `slot`, or into the HBM table when the region is full
 FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, uint32_t r0, uint32_t r1) {
   if (slot < cap) {
-    const size_t at = ((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap + slot;
+    const size_t at = part_region(p, q, blockIdx.x) * (size_t)cap + slot;
     if (p.rw == 1) p.recs[at] = r0;
     else *(u32x2*)(p.recs + 2 * at) = u32x2{r0, r1};
   } else if (p.rw == 2) {
@@ -2195,43 +2222,16 @@ FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, u
   }
 }
 
-struct PscanChunk {  // records [s0, s0 + len) of partition q's ring, within one 128-B line of the region
-  int32_t q;
-  uint32_t s0, len;
-};
-
-// Store two chunks with one wave: lanes 0-31 write chunk a, lanes 32-63 chunk b (len 0 = none); lane j of a half
-// writes dword j of its chunk.
-FI void pscan_store(const DevParams& p, const uint32_t* ring, uint32_t RC, uint32_t cap, PscanChunk a, PscanChunk b) {
-  const int lane = lane_id(), j = lane & 31;
-  const bool hi = lane >= 32;
-  const int32_t q = hi ? b.q : a.q;
-  const uint32_t s0 = hi ? b.s0 : a.s0, len = hi ? b.len : a.len;
-  if (p.rw == 1) {
-    if ((uint32_t)j < len) {
-      const uint32_t slot = s0 + j;
-      pscan_put(p, q, slot, cap, ring[(size_t)q * RC + (slot & (RC - 1))], 0u);
-    }
-  } else {
-    const uint32_t r = (uint32_t)j >> 1;
-    if (r < len) {
-      const uint32_t slot = s0 + r;
-      const uint32_t* src = ring + 2 * ((size_t)q * RC + (slot & (RC - 1)));
-      if (slot < cap) {
-        p.recs[2 * (((size_t)q * gridDim.x + blockIdx.x) * (size_t)cap + slot) + (j & 1)] = src[j & 1];
-      } else if ((j & 1) == 0) {
-        part_spill(p, src[0], src[1]);
-      }
-    }
-  }
-}
-
-// Flush this wave's share of the partitions: complete lines (every record when `final`), pairing chunks.
+// Flush this wave's share of the partitions (64 per pass): every complete 128-B line of a ring (every record when
+// `final`).  A lane first settles its partition's range [H, E) and head.  Whole lines below the region's end go
+// out eight partitions per step: 8 lanes per line, one 16-B ds_read_b128 / global_store_dwordx4 each, offsets in
+// 32 bits from the workgroup's region block.  The rest -- a line's head or tail piece (after a ring overflow, and
+// at the end) and records past a full region -- take a per-record walk, two partitions per step.
 FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring, uint32_t RC,
                     uint32_t cap, int wave, bool final) {
-  const int lane = lane_id(), np = p.nparts;
-  const uint32_t line = 32u / (uint32_t)p.rw;  // records per 128-B line
-  PscanChunk pend{0, 0, 0};
+  const int lane = lane_id(), np = p.nparts, half = lane >> 5, j = lane & 31, g = lane >> 3, sub = lane & 7;
+  const uint32_t rw = (uint32_t)p.rw, lsh = rw == 1 ? 5u : 4u, line = 1u << lsh;  // records per 128-B line
+  uint32_t* wrec = p.recs + (size_t)blockIdx.x * (size_t)np * cap * rw;  // part_region(p, q, blockIdx.x) = this + q
   for (int qb = wave * 64; qb < np; qb += 64 * PGPU_PSCAN_WAVES) {
     const int q = qb + lane;
     uint32_t H = 0, E = 0;
@@ -2247,44 +2247,73 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
         head[q] = E;
       }
     }
-    uint64_t todo = __ballot(E > H);
-    while (todo) {
-      const int l = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const int32_t qq = qb + l;
-      uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)H, l);
-      const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)E, l);
-      while (h < e) {
-        const uint32_t ce = min(e, (h | (line - 1u)) + 1u);
-        const PscanChunk c{qq, h, ce - h};
-        if (pend.len) {
-          pscan_store(p, ring, RC, cap, pend, c);
-          pend.len = 0;
-        } else {
-          pend = c;
-        }
-        h = ce;
+    if (!__ballot(E > H)) continue;
+    // whole lines [FL, LL) (line numbers) inside the region
+    const uint32_t FL = (H + line - 1u) >> lsh;
+    uint32_t LL = min(E, cap) >> lsh;
+    if (LL < FL) LL = FL;
+    const bool rest = E > H && ((FL << lsh) != H || (LL << lsh) != E);
+#pragma unroll 2
+    for (int pb = 0; pb < 64; pb += 8) {
+      const int src = pb + g;
+      const uint32_t fl = (uint32_t)__shfl((int)FL, src, 64), ll = (uint32_t)__shfl((int)LL, src, 64);
+      const uint32_t qq = (uint32_t)(qb + src);
+      for (uint32_t l = fl; l < ll; ++l) {
+        const uint32_t s = l << lsh;
+        const u32x4 v = *(const u32x4*)(ring + (qq * RC + (s & (RC - 1))) * rw + 4 * sub);
+        *(u32x4*)(wrec + (qq * cap + s) * rw + 4 * sub) = v;
       }
     }
+    if (!__ballot(rest)) continue;
+    // head / tail pieces and records past the region's end: lane j of a half takes dword j of a line
+    bool spill = false;
+    for (int pp = 0; pp < 32; ++pp) {
+      const int src = 2 * pp + half;
+      const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
+      const uint32_t lo = (uint32_t)__shfl((int)FL, src, 64) << lsh, hi = (uint32_t)__shfl((int)LL, src, 64) << lsh;
+      const uint32_t qq = (uint32_t)(qb + src);
+      for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
+        const uint32_t s = s0 + j / rw;
+        if (s < h || s >= e || (s >= lo && s < hi)) continue;
+        if (s < cap) wrec[(qq * cap + s) * rw + (j & (rw - 1))] = ring[(qq * RC + (s & (RC - 1))) * rw + (j & (rw - 1))];
+        else spill = true;
+      }
+    }
+    // region full (rare): the same walk again, HBM-table atomics for the records past the region's end
+    if (__ballot(spill)) {
+      for (int pp = 0; pp < 32; ++pp) {
+        const int src = 2 * pp + half;
+        const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
+        const uint32_t qq = (uint32_t)(qb + src);
+        for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
+          const uint32_t s = s0 + j / rw;
+          if (s < h || s >= e || s < cap || (j & (rw - 1))) continue;
+          const uint32_t* r = ring + (qq * RC + (s & (RC - 1))) * rw;
+          pscan_put(p, qq, s, cap, r[0], rw == 2 ? r[1] : 0u);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // nothing of this rare path stays pending into the store loops above
+    }
   }
-  if (pend.len) pscan_store(p, ring, RC, cap, pend, PscanChunk{0, 0, 0});
 }
 
-__global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams p) {
+__global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int np = p.nparts;
   const uint32_t RC = (uint32_t)p.pscan;  // ring records per partition (power of two)
-  uint32_t* head = (uint32_t*)dyn_smem;   // [np] first slot not yet written out
-  uint32_t* tail = head + np;             // [np] slots taken (= records of this workgroup in the partition)
-  uint32_t* ring = tail + np;             // [np][RC * rw]
+  // [np + 64]: first slot not yet written out; the 64 lanes' dummy partitions follow the real ones
+  const int npad = (np + 64 + 2) & ~1;   // + the cancel word; keeps the ring 16-B aligned
+  uint32_t* head = (uint32_t*)dyn_smem;
+  uint32_t* tail = head + npad;           // [np + 64] slots taken (= records of this workgroup in the partition)
+  uint32_t* ring = tail + npad;           // [np][RC * rw], then one dummy record per lane
   Cons cv;
-  cv.masks = (uint32_t*)((unsigned char*)(ring + (size_t)np * RC * p.rw) + (size_t)wave * p.pscan_wave_bytes);
+  cv.masks = (uint32_t*)((unsigned char*)(ring + ((size_t)np * RC + 64) * p.rw) + (size_t)wave * p.pscan_wave_bytes);
   cv.queue = nullptr;
   cv.klist = cv.vlist = nullptr;
   cv.acc = nullptr;
   cv.qtiles = nullptr;
-  for (int i = threadIdx.x; i < 2 * np; i += PGPU_PSCAN_THREADS) head[i] = 0u;
+  for (int i = threadIdx.x; i < 2 * npad; i += PGPU_PSCAN_THREADS) head[i] = 0u;
   __syncthreads();
   const int nb = gridDim.x, b = blockIdx.x;
   const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
@@ -2295,14 +2324,19 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams
   int64_t matched = 0, scanned = 0, dense_bytes = 0;
   Prof pf;
 #ifdef PGPU_PROFILE_BUILD
-  pf.on = false;
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
+  const int64_t t_all = now(pf);
   SegState ss;
   int cseg = -1;
   const int nsteps = (t1 - t0 + PGPU_PSCAN_WAVES - 1) / PGPU_PSCAN_WAVES;
   for (int step = 0; step < nsteps; ++step) {
     const int tile = t0 + step * PGPU_PSCAN_WAVES + wave;
+    int64_t tp = now(pf);
     if (tile < t1) {
+      if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
       const Cursor cu = cursor_at(p, tile);
       if (cu.seg != cseg) {
         cseg = cu.seg;
@@ -2351,30 +2385,79 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams
             for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
           }
         }
-        // slots first (all LDS atomics in flight together), then the ring writes
-        uint32_t slot[32];
+        PROF_ADD(pf, PGPU_P_C_FILTER, tp);  // loads, filter, decode
+        tp = now(pf);
+        // slots first (all LDS atomics in flight together), then the ring writes.  Branch-free per doc: a doc
+        // that does not match takes its slot on the lane's own dummy partition (np + lane) and writes the
+        // lane's dummy ring entry; only records whose ring is full (rare) take the branch to an HBM store
+        const uint32_t dq = (uint32_t)(np + lane);
+        uint32_t spm = 0;  // docs whose region is full
+        // eight docs at a time: their slots and the partitions' heads come back in one LDS round trip
 #pragma unroll
-        for (int i = 0; i < 32; ++i) slot[i] = lane_bit(mm, i) ? atomicAdd(&tail[key[i] >> p.pshift], 1u) : 0u;
+        for (int g8 = 0; g8 < 4; ++g8) {
+          uint32_t qq[8], slot[8], hd[8];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          if (!lane_bit(mm, i)) continue;
-          const uint32_t q = key[i] >> p.pshift;
-          const uint32_t r0 = p.rw == 1 ? (idbits ? ((key[i] & pmask) << idbits) | val[i] : key[i]) : key[i];
-          if (slot[i] - head[q] < RC) {
-            if (p.rw == 1) ring[(size_t)q * RC + (slot[i] & (RC - 1))] = r0;
-            else *(u32x2*)(ring + 2 * ((size_t)q * RC + (slot[i] & (RC - 1)))) = u32x2{r0, val[i]};
-          } else {
-            pscan_put(p, q, slot[i], cap, r0, val[i]);
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * g8 + j;
+            qq[j] = lane_bit(mm, i) ? (key[i] >> p.pshift) : dq;
           }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) slot[j] = atomicAdd(&tail[qq[j]], 1u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hd[j] = head[qq[j]];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = 8 * g8 + j;
+            const bool live = lane_bit(mm, i);
+            const bool in = live && slot[j] - hd[j] < RC;
+            const uint32_t r0 = p.rw == 1 ? (idbits ? ((key[i] & pmask) << idbits) | val[i] : key[i]) : key[i];
+            const uint32_t at = in ? qq[j] * RC + (slot[j] & (RC - 1)) : (uint32_t)np * RC + lane;
+            if (p.rw == 1) ring[at] = r0;
+            else *(u32x2*)(ring + 2 * at) = u32x2{r0, val[i]};
+            if (live && !in) {  // the partition's ring is full: straight to the region (a store, nothing to wait on)
+              if (slot[j] < cap) {
+                const size_t rec = part_region(p, qq[j], blockIdx.x) * (size_t)cap + slot[j];
+                if (p.rw == 1) p.recs[rec] = r0;
+                else *(u32x2*)(p.recs + 2 * rec) = u32x2{r0, val[i]};
+              } else {
+                spm |= 1u << i;
+              }
+            }
+          }
+        }
+        // region full (rare): HBM-table atomics, kept out of the loops above so that their dictionary loads put
+        // no vmcnt waits on the stores there
+        if (__ballot(spm != 0)) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i)
+            if ((spm >> i) & 1u) part_spill(p, key[i], p.pcol >= 0 ? val[i] : 0u);
+          __builtin_amdgcn_s_waitcnt(0);
         }
       }
     }
+    PROF_ADD(pf, PGPU_P_C_AGG, tp);  // inserts (0 when the tile had no match)
+    tp = now(pf);
     __syncthreads();
+    PROF_ADD(pf, PGPU_P_C_FULL, tp);  // barrier waits
+    tp = now(pf);
     pscan_flush(p, head, tail, ring, RC, cap, wave, false);
+    if (wave == 0 && step % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p) && lane == 0) head[np + 64] = 1u;
+    PROF_ADD(pf, PGPU_P_C_FLUSH, tp);
+    tp = now(pf);
     __syncthreads();
+    PROF_ADD(pf, PGPU_P_C_FULL, tp);
+    if (head[np + 64]) break;  // cancelled: the workgroup stops together (the word was set before the barrier)
   }
   pscan_flush(p, head, tail, ring, RC, cap, wave, true);
   const size_t w = (size_t)blockIdx.x * PGPU_PSCAN_WAVES + wave;
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_all);
+#ifdef PGPU_PROFILE_BUILD
+  if (pf.on && lane == 0) {
+    int64_t* o = p.prof + w * PGPU_NPROF;
+#pragma unroll
+    for (int k = 0; k < PGPU_NPROF; ++k) o[k] = pf.t[k];
+  }
+#endif
   if (lane == 0) {
     int64_t* o = p.stats + w * PGPU_NSTATS;
     o[PGPU_STAT_MATCHED] = matched;
@@ -2389,13 +2472,48 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS) void part_scan_kernel(DevParams
 
 // PART mode, phase 2: workgroup q aggregates the records of key partition q (from every phase-1 workgroup's
 // region) into an LDS table [nsec][K], then folds it into the HBM table, which holds the identities plus the
-// phase-1 spills.  NS = value sections (all reduce the records' one value column); ONE = one-word records.  Each
-// wave walks its own regions in chunks of R x 64 records: the loads are unconditional (clamped indices), so a
-// chunk's R loads -- and then its R dictionary gathers -- are in flight together; section ops are uniform, so
-// each chunk runs one branch-free atomic loop per section.
-template <int NS, bool ONE>
+// phase-1 spills.  NS = value sections (all reduce the records' one value column); ONE = one-word records.
+// SUM values of one-word records come from the shared dictionary (pdict), per LDM:
+//   0  gathered from L2 -- one 128-B line per 4-B lookup (~300 G lookups/s chip-wide for a 256-KiB dictionary,
+//      tools/gather_bench.hip), the bound of this kernel when the dictionary is large;
+//   1  the whole dictionary copied into LDS beside the table (~3,200 G lookups/s).
+// Each wave walks its own regions in chunks of R x 64 records; loads are unconditional (clamped indices), so a
+// chunk's R loads are in flight together; section ops are uniform, so a chunk runs one branch-free atomic loop
+// per section.
+template <int NS, int R>
+FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS : 1], int32_t vt, int idbits,
+                          const uint32_t (&k)[R], const uint32_t (&raw)[R], const uint32_t (&val)[R],
+                          const bool (&ok)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (ok[r]) atomicAdd((unsigned long long*)&ptab[k[r]], 1ull);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int64_t* sec = ptab + (size_t)(1 + s) * K;
+    if (op[s] == PGPU_RED_SUM_I64) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (ok[r]) atomicAdd((unsigned long long*)&sec[k[r]], (unsigned long long)(int64_t)(int32_t)val[r]);
+    } else if (op[s] == PGPU_RED_SUM_F64) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (ok[r]) atomicAdd((double*)&sec[k[r]], (double)__uint_as_float(val[r]));
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (!ok[r]) continue;
+        const int64_t c = idbits ? (int64_t)raw[r] : raw_to_cell(raw[r], vt, op[s]);
+        if (op[s] == PGPU_RED_MIN_I64) atomicMin((long long*)&sec[k[r]], (long long)c);
+        else atomicMax((long long*)&sec[k[r]], (long long)c);
+      }
+    }
+  }
+}
+
+template <int NS, bool ONE, int LDM>
 __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
+  uint32_t* sdict = (uint32_t*)(ptab + (size_t)(NS + 1) * (1u << p.pshift));  // LDM 1: [1 << slice_shift]
   const uint32_t K = 1u << p.pshift;
   const uint32_t q = blockIdx.x;
   const uint64_t key0 = (uint64_t)q * K;
@@ -2409,6 +2527,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
     if (p.aggs[a].fn != PGPU_AGG_COUNT) vt = p.aggs[a].vtype;
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NS + 1) * K; i += blockDim.x)
     ptab[i] = sec_identity(p.sec_op[i >> p.pshift]);
+  const uint32_t slice = 1u << p.slice_shift;
+  if (LDM == 1)
+    for (uint32_t i = threadIdx.x; i < slice; i += blockDim.x)
+      sdict[i] = i < p.pdict_n ? gld((const uint32_t*)p.pdict, i) : 0u;
   __syncthreads();
   // one-word records: (in-partition key << idbits | dict id) over the shared dictionary; MIN / MAX sections reduce
   // the dict ids (sorted dictionary) and are turned into cell keys when folded into the HBM table
@@ -2417,58 +2539,37 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   bool need_val = false;
 #pragma unroll
   for (int s = 0; s < NS; ++s) need_val |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
-  constexpr int R = 16;
-  for (int w = wave; w < nwg; w += nwaves) {
-    const uint32_t n = p.rcount[(size_t)q * nwg + w];
-    const size_t base = ((size_t)q * nwg + w) * (size_t)p.rcap;
-    for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
-      uint32_t k[R], raw[R];
-      bool ok[R];
+  {
+    constexpr int R = 16;
+    for (int w = wave; w < nwg; w += nwaves) {
+      if (((w - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
+      const uint32_t n = p.rcount[(size_t)q * nwg + w];
+      const size_t base = part_region(p, q, w) * (size_t)p.rcap;
+      for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
+        uint32_t k[R], raw[R], val[R];
+        bool ok[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint32_t i = i0 + r * 64 + lane;
-        ok[r] = i < n;
-        const size_t at = base + (ok[r] ? i : n - 1);
-        if (ONE) {
-          const uint32_t v = gld(p.recs, at);
-          k[r] = idbits ? v >> idbits : v - (uint32_t)key0;
-          raw[r] = v & idmask;
-        } else {
-          const u32x2 v = gld((const u32x2*)p.recs, at);
-          k[r] = v.x - (uint32_t)key0;
-          raw[r] = v.y;
-        }
-      }
-      uint32_t val[R];  // the record's 4-byte dictionary value (SUM sections)
-#pragma unroll
-      for (int r = 0; r < R; ++r) val[r] = raw[r];
-      if (idbits && need_val) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) val[r] = gld((const uint32_t*)p.pdict, raw[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (ok[r]) atomicAdd((unsigned long long*)&ptab[k[r]], 1ull);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        int64_t* sec = ptab + (size_t)(1 + s) * K;
-        if (op[s] == PGPU_RED_SUM_I64) {
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (ok[r]) atomicAdd((unsigned long long*)&sec[k[r]], (unsigned long long)(int64_t)(int32_t)val[r]);
-        } else if (op[s] == PGPU_RED_SUM_F64) {
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (ok[r]) atomicAdd((double*)&sec[k[r]], (double)__uint_as_float(val[r]));
-        } else {
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            if (!ok[r]) continue;
-            const int64_t c = idbits ? (int64_t)raw[r] : raw_to_cell(raw[r], vt, op[s]);
-            if (op[s] == PGPU_RED_MIN_I64) atomicMin((long long*)&sec[k[r]], (long long)c);
-            else atomicMax((long long*)&sec[k[r]], (long long)c);
+        for (int r = 0; r < R; ++r) {
+          const uint32_t i = i0 + r * 64 + lane;
+          ok[r] = i < n;
+          const size_t at = base + (ok[r] ? i : n - 1);
+          if (ONE) {
+            const uint32_t v = gld(p.recs, at);
+            k[r] = idbits ? v >> idbits : v - (uint32_t)key0;
+            raw[r] = v & idmask;
+          } else {
+            const u32x2 v = gld((const u32x2*)p.recs, at);
+            k[r] = v.x - (uint32_t)key0;
+            raw[r] = v.y;
           }
         }
+#pragma unroll
+        for (int r = 0; r < R; ++r) val[r] = raw[r];
+        if (idbits && need_val) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) val[r] = LDM == 1 ? sdict[raw[r] & (slice - 1)] : gld((const uint32_t*)p.pdict, raw[r]);
+        }
+        part_reduce_batch<NS, R>(ptab, K, op, vt, idbits, k, raw, val, ok);
       }
     }
   }
@@ -2730,14 +2831,13 @@ PGPU_MODE_FUNCS(PGPU_MODE_PART, part)
 
 hipError_t pgpu_prepare_part_reduce() {
   hipError_t e = hipSuccess;
-#define PART_ATTR(NS)                                                                                  \
-  if (e == hipSuccess)                                                                                 \
-    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, true>,                                \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_PART_LDS_BYTES);          \
-  if (e == hipSuccess)                                                                                 \
-    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, false>,                               \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_PART_LDS_BYTES);
+#define PART_ATTR_1(NS, ONE, LDM)                                                               \
+  if (e == hipSuccess)                                                                          \
+    e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, ONE, LDM>,                      \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_LDS_LIMIT);
+#define PART_ATTR(NS) PART_ATTR_1(NS, true, 0) PART_ATTR_1(NS, true, 1) PART_ATTR_1(NS, false, 0)
   PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
+#undef PART_ATTR_1
 #undef PART_ATTR
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)part_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2751,12 +2851,14 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
-  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8;
+  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 + (p.ldict ? (size_t)4 << p.slice_shift : 0);
+  const dim3 g(p.nparts);
   switch (p.nsec - 1) {
-#define PART_LAUNCH(NS)                                                                                  \
-  case NS:                                                                                               \
-    if (p.rw == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true>), dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
-    else hipLaunchKernelGGL((part_reduce_kernel<NS, false>), dim3(p.nparts), dim3(1024), lds, st, p, nwg); \
+#define PART_LAUNCH(NS)                                                                                    \
+  case NS:                                                                                                 \
+    if (p.rw == 1 && p.ldict == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true, 1>), g, dim3(1024), lds, st, p, nwg); \
+    else if (p.rw == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true, 0>), g, dim3(1024), lds, st, p, nwg); \
+    else hipLaunchKernelGGL((part_reduce_kernel<NS, false, 0>), g, dim3(1024), lds, st, p, nwg); \
     return hipGetLastError();
     PART_LAUNCH(0) PART_LAUNCH(1) PART_LAUNCH(2) PART_LAUNCH(3) PART_LAUNCH(4)
 #undef PART_LAUNCH

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -22,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pinot_gpu.h"
@@ -140,6 +143,12 @@ struct PinnedMem {
   }
 };
 
+// System.currentTimeMillis (QueryContext end times are on this clock)
+int64_t now_epoch_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
 struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
@@ -147,6 +156,7 @@ struct Workspace {
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
   PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
+  PinnedMem h_cancel;                  // the query's cancel word (DevParams::cancel), polled by its kernels
   bool busy = false;
   ~Workspace() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -233,6 +243,9 @@ struct pgpu_query {
   std::vector<FilterReplay> replay;
   bool exact_filter = false;
   hipEvent_t done = nullptr;  // submitted queries: recorded after the last copy of this query
+  // deadline (ms since the epoch, 0 = none) and why the query was stopped (0 = it was not)
+  int64_t deadline_ms = 0;
+  std::atomic<int> stop{0};  // PGPU_E_CANCELLED / PGPU_E_TIMEOUT
 };
 
 namespace {
@@ -1594,22 +1607,37 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     }
   }
   const int part_rw = pcol >= 0 && !part_idbits ? 2 : 1;
+  // phase 2 reads SUM values from an LDS copy of the shared dictionary when it fits beside the partition's table,
+  // instead of gathering them from L2 (one 128-B line per 4-B lookup)
+  int slice_shift = 0, ldict = 0;
+  uint32_t pdict_n = 0;
+  if (part_idbits) {
+    const HostColumn* h0 = &q->segments[0].segment->cols[q->segments[0].column_map[pcol]];
+    pdict_n = (uint32_t)h0->dict_card;
+    bool need_val = false;
+    for (int s = 1; s < L.num_sections; ++s)
+      need_val |= L.section_op[s] == PGPU_RED_SUM_I64 || L.section_op[s] == PGPU_RED_SUM_F64;
+    while ((1ull << slice_shift) < pdict_n) ++slice_shift;
+    static const bool no_ldict = getenv("PGPU_NO_LDICT") && atoi(getenv("PGPU_NO_LDICT")) != 0;
+    ldict = need_val && !no_ldict && (8ull * L.num_sections << pshift) + (4ull << slice_shift) <= PGPU_LDS_LIMIT;
+  }
   // partitioned group-by whose segments need no candidate queue: phase 1 by part_scan_kernel (self-loading waves,
   // records written through per-partition LDS rings of >= two 128-B lines); two workgroups per CU when the rings
   // fit, else one
   static const bool no_pscan = getenv("PGPU_NO_PSCAN") && atoi(getenv("PGPU_NO_PSCAN")) != 0;
   p.pscan = 0;
-  if (!no_pscan && p.mode == PGPU_MODE_PART && nparts <= PGPU_PSCAN_MAX_PARTS) {
+  const uint64_t ptotal = nparts;
+  if (!no_pscan && p.mode == PGPU_MODE_PART && ptotal <= PGPU_PSCAN_MAX_PARTS) {
     bool ok = true;
     for (const DevSeg& ds : pk.segs) ok &= ds.rprog_len == 0;
     const size_t wave_bytes = 256 * (size_t)p.mask_rows;
-    const size_t fixed_b = 8 * nparts + 4 * wave_bytes;
-    const uint64_t min_rc = 64 / part_rw;
+    const size_t fixed_b = 8 * ((ptotal + 66) & ~1ull) + 4 * 64 * part_rw + 4 * wave_bytes;  // + dummies, cancel word
+    const uint64_t min_rc = 64 / part_rw;  // rings of at least two 128-B lines
     for (int per_cu = 2; ok && per_cu >= 1 && !p.pscan; --per_cu) {
       const size_t budget = PGPU_LDS_LIMIT / per_cu;
       if (budget <= fixed_b) continue;
       uint64_t rc = 1;
-      while (rc < 1024 && fixed_b + 4ull * nparts * part_rw * (rc * 2) <= budget) rc *= 2;
+      while (rc < 1024 && fixed_b + 4ull * ptotal * part_rw * (rc * 2) <= budget) rc *= 2;
       if (rc < min_rc) continue;
       p.pscan = (int32_t)rc;
       p.pscan_wave_bytes = (int32_t)wave_bytes;
@@ -1617,7 +1645,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       if (g >= 8) g &= ~7;
       p.direct = 0;
       grid = std::max(1, g);
-      dyn = align16(fixed_b + 4ull * nparts * part_rw * rc);
+      dyn = align16(fixed_b + 4ull * ptotal * part_rw * rc);
     }
   }
   {
@@ -1658,6 +1686,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS + 16);
+  if (e == hipSuccess) e = ws->h_cancel.ensure(16);
   if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   if (p.mode == PGPU_MODE_PART) {
@@ -1665,11 +1694,14 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     // HBM atomics, so an underestimate costs time, never correctness.  Bounded by half the free HBM.
     p.pshift = pshift;
     p.nparts = (int32_t)nparts;
+    p.slice_shift = slice_shift;
+    p.ldict = ldict;
+    p.pdict_n = pdict_n;
     p.pcol = pcol;
     p.rw = part_rw;
     p.rec_idbits = part_idbits;
     p.pdict = part_pdict;
-    const double per = pk.est_matched / ((double)grid * (double)nparts);
+    const double per = pk.est_matched / ((double)grid * (double)p.nparts);
     uint64_t cap = (uint64_t)(1.25 * per) + 32;
     if (q->flags & PGPU_Q_PART_SPILL) cap = 16;
     // regions of an odd number of 128-B lines: the active (partially written) line of every region then falls on
@@ -1680,7 +1712,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     cap = lines * per_line;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-    const uint64_t regions = nparts * (uint64_t)grid;
+    const uint64_t regions = (uint64_t)p.nparts * (uint64_t)grid;
     const uint64_t have = ws->recs.n;
     const uint64_t budget = std::max<uint64_t>(have, (uint64_t)free_b / 2);
     const uint64_t max_cap = budget / (regions * 4ull * p.rw);
@@ -1730,7 +1762,13 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // copy sits between two queries' kernels
   void* h_arena_dev = nullptr;
   void* h_stats_dev = nullptr;
-  e = hipHostGetDevicePointer(&h_arena_dev, ws->h_arena.p, 0);
+  void* h_cancel_dev = nullptr;
+  // the workspace is free, so no kernel of an earlier query polls its cancel word any more
+  const bool expired = q->deadline_ms > 0 && now_epoch_ms() >= q->deadline_ms;
+  __atomic_store_n((int32_t*)ws->h_cancel.p, expired ? 1 : 0, __ATOMIC_SEQ_CST);
+  e = hipHostGetDevicePointer(&h_cancel_dev, ws->h_cancel.p, 0);
+  p.cancel = (const int32_t*)h_cancel_dev;
+  if (e == hipSuccess) e = hipHostGetDevicePointer(&h_arena_dev, ws->h_arena.p, 0);
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
@@ -1792,6 +1830,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     qq->replay.push_back(std::move(r));
   }
   qq->stats.filter_stats_exact = exact ? 1 : 0;
+  qq->deadline_ms = q->deadline_ms;
+  if (expired) qq->stop = PGPU_E_TIMEOUT;
   *out_query = qq;
   return PGPU_OK;
 }
@@ -1802,11 +1842,37 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   return launch_impl(ctx, q, stream, dev_table, table_bytes, nullptr, out_query);
 }
 
+int pgpu_query_cancel(pgpu_query* qq) {
+  if (!qq) return fail(PGPU_E_INVALID, "null query");
+  int none = 0;
+  qq->stop.compare_exchange_strong(none, PGPU_E_CANCELLED);
+  __atomic_store_n((int32_t*)qq->ws->h_cancel.p, 1, __ATOMIC_SEQ_CST);
+  return PGPU_OK;
+}
+
 int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
   HIP_TRY(hipSetDevice(qq->ctx->device));
-  if (qq->done) HIP_TRY(hipEventSynchronize(qq->done));
-  else HIP_TRY(hipStreamSynchronize(qq->stream));
+  if (qq->deadline_ms > 0 && qq->done) {
+    // BaseCombineOperator.mergeResults polls with the time left: past the deadline the query is told to stop
+    // and drains (its kernels skip their remaining tiles)
+    for (int spins = 0;; ++spins) {
+      const hipError_t qe = hipEventQuery(qq->done);
+      if (qe == hipSuccess) break;
+      if (qe != hipErrorNotReady) return fail(PGPU_E_HIP, "query wait: %s", hipGetErrorString(qe));
+      if (qq->stop.load() == 0 && now_epoch_ms() >= qq->deadline_ms) {
+        int none = 0;
+        qq->stop.compare_exchange_strong(none, PGPU_E_TIMEOUT);
+        __atomic_store_n((int32_t*)qq->ws->h_cancel.p, 1, __ATOMIC_SEQ_CST);
+      }
+      if (spins < 2000) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  } else if (qq->done) {
+    HIP_TRY(hipEventSynchronize(qq->done));
+  } else {
+    HIP_TRY(hipStreamSynchronize(qq->stream));
+  }
   const int64_t* s = (const int64_t*)qq->ws->h_stats.p;
   qq->stats.num_docs_scanned = s[PGPU_STAT_MATCHED];
   qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED];
@@ -1815,6 +1881,11 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
+  if (const int st = qq->stop.load()) {
+    if (out_stats) *out_stats = qq->stats;
+    return fail(st, st == PGPU_E_TIMEOUT ? "query passed its deadline before it finished (EXECUTION_TIMEOUT_ERROR)"
+                                         : "query cancelled");
+  }
   if (qq->exact_filter) {
     // the reference's iterators replayed over the leaves' bitmaps (pgpu_iterstats.cpp)
     const uint32_t* bits = (const uint32_t*)qq->ws->h_leafbits.p;

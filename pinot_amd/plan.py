@@ -24,6 +24,7 @@ the server keeps its CPU plan for it.
 from __future__ import annotations
 
 import ctypes as C
+import time
 import hashlib
 import math
 from fractions import Fraction
@@ -358,8 +359,11 @@ class GpuPlanMaker:
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
                  collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False,
-                 exact_filter_stats: bool = False):
+                 exact_filter_stats: bool = False, timeout_ms: Optional[int] = None):
         self.ctx = ctx
+        # timeout_ms: the query's budget from submit (QueryOptions timeoutMs -> QueryContext.getEndTimeMs); past it
+        # the query is cancelled and collect raises QueryTimeoutError (EXECUTION_TIMEOUT_ERROR)
+        self.timeout_ms = timeout_ms
         # exact_filter_stats: numEntriesScannedInFilter as the reference's iterators count it, also where they
         # leap-frog (PGPU_Q_EXACT_FILTER_STATS: one more pass over every filter leaf, replayed on the host)
         self.exact_filter_stats = exact_filter_stats
@@ -529,7 +533,8 @@ class GpuPlanMaker:
                          flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags | extra_flags |
                          (_lib.PGPU_Q_EXACT_FILTER_STATS if self.exact_filter_stats else 0),
                          reduce_docs=reduce_docs, num_groups_limit=self.num_groups_limit,
-                         array_based_threshold=self.max_init_group_holder_capacity)
+                         array_based_threshold=self.max_init_group_holder_capacity,
+                         deadline_ms=0 if self.timeout_ms is None else int(time.time() * 1000) + int(self.timeout_ms))
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:
@@ -610,6 +615,12 @@ class PendingQuery:
     handle: C.c_void_p
     layout: TableLayout
     globals_: list
+
+    def cancel(self) -> None:
+        """Stop the query (pgpu_query_cancel): its kernels skip their remaining tiles and collect raises
+        QueryCancelledError."""
+        if self.handle is not None and self.handle.value:
+            _lib.check(self.maker.ctx._lib.pgpu_query_cancel(self.handle))
 
     def __del__(self):
         if self.handle is not None and self.handle.value:

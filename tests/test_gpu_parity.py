@@ -438,18 +438,21 @@ def test_bit_sliced_leaves_vs_oracle(gpu_ctx, qi):
             g.release()
 
 
+@pytest.mark.parametrize("card", [4000, 40_000], ids=["dict_in_lds", "dict_gathered"])
 @pytest.mark.parametrize("mtype", [PGPU_INT, PGPU_FLOAT])
 @pytest.mark.parametrize("sql", [
     "SELECT k, SUM(m), MIN(m), MAX(m), AVG(m), COUNT(*) FROM t GROUP BY k",
     "SELECT k, MAX(m), COUNT(*) FROM t WHERE f < 30 GROUP BY k ORDER BY MAX(m) DESC LIMIT 20",
+    "SELECT k, SUM(m), COUNT(*) FROM t WHERE f < 80 GROUP BY k ORDER BY SUM(m) DESC LIMIT 20",
     "SELECT k, COUNT(*) FROM t WHERE f >= 50 GROUP BY k",
 ])
-def test_partitioned_groupby_shared_dictionary(gpu_ctx, sql, mtype):
+def test_partitioned_groupby_shared_dictionary(gpu_ctx, sql, mtype, card):
     """Segments sharing the aggregated column's dictionary: the partitioned group-by writes one-word records
-    (in-partition key, dict id) and phase 2 resolves values / MIN / MAX through the shared dictionary."""
+    (in-partition key, dict id) and phase 2 resolves values / MIN / MAX through the shared dictionary -- copied
+    whole into LDS (4,000 entries) or gathered from L2 (40,000)."""
     from pinot_amd._lib import PGPU_Q_PARTITION
     rng = np.random.default_rng(77 + len(sql))
-    values = np.sort(rng.choice(np.arange(-3000, 50_000), 4000, replace=False))
+    values = np.sort(rng.choice(np.arange(-3000, 50_000), card, replace=False))
     if mtype == PGPU_FLOAT:
         values = values.astype(np.float32) * np.float32(0.5)
     segs = []
