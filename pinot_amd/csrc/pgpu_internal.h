@@ -251,13 +251,25 @@ struct DevParams {
   int32_t slice_shift;
   int32_t ldict;
   uint32_t pdict_n;               // pdict entries
+  uint32_t cancel_gen;            // this launch's generation (see cancel)
+  // PART region sizing (part_scan phase 1): a sampled counting pass (psample = tile stride) fills pcount, then
+  // part_plan_kernel sizes each partition's region in proportion (pcap / poff within a workgroup's block of
+  // pblock records) and splits heavy partitions across several phase-2 workgroups (p2work: {q, w0, w1, split}
+  // per phase-2 workgroup, q < 0 = idle).  pcap == nullptr: uniform regions of rcap records.
+  uint32_t* pcount;
+  uint32_t* pcap;
+  uint32_t* poff;
+  int32_t* p2work;
+  uint64_t pblock;
+  int32_t psample;
+  int32_t p2grid;
   // HASH mode: key words follow the sections in `table` (word 0 at table + nsec * G; two-level keys: the
   // interned word-0 values at + G); segmask = distinct-key bitmaps of the tracked segments ([rows][G / 32]);
   // hflag[0] = a probe sequence ran out of slots (query fails)
   uint32_t* segmask;
   int32_t* hflag;
   uint32_t* leaf_bits;            // PGPU_Q_EXACT_FILTER_STATS (see DevSeg::leaf_bits_off)
-  const int32_t* cancel;          // != 0: stop (pgpu_query_cancel / deadline); pinned host word, polled per tile range
+  const int32_t* cancel;          // == cancel_gen: stop (pgpu_query_cancel / deadline); HBM word, polled per tile range
   int32_t key_words;
   int32_t key_split;
   int32_t segmask_rows;

@@ -185,10 +185,11 @@ FI void loader_flag_store(int* p, int v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
 }
 
-// The query's cancel word (pinned host memory, written by pgpu_query_cancel): one uncached system-scope load.
+// The query's cancel word (HBM, written by pgpu_query_cancel through a side-stream memset): one uncached load.
 FI bool query_cancelled(const DevParams& p) {
   if (!p.cancel) return false;
-  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0;
+  const int v = __hip_atomic_load(p.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return (uint32_t)__builtin_amdgcn_readfirstlane(v) == p.cancel_gen;
 }
 
 // s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the immediate must be a constant).
@@ -1204,9 +1205,13 @@ FI int64_t* table_base(const DevParams& p, const Lds& L) {
   return MODE == PGPU_MODE_LDS ? L.ltab : p.table;
 }
 
-// PART mode: region of (partition q, phase-1 workgroup w): a workgroup's regions are contiguous, so its record
-// streams stay within a few pages (one region per partition would put every store on a different page)
-FI size_t part_region(const DevParams& p, uint32_t q, uint32_t w) { return (size_t)w * p.nparts + q; }
+// PART mode: region of (partition q, phase-1 workgroup w) = records [part_base, + part_cap).  A workgroup's
+// regions are one contiguous block of pblock records, so its record streams stay within a few pages (one region
+// per partition would put every store on a different page); sized per partition by part_plan_kernel, or uniform.
+FI size_t part_base(const DevParams& p, uint32_t q, uint32_t w) {
+  return (size_t)w * p.pblock + (p.poff ? (size_t)p.poff[q] : (size_t)q * (uint32_t)p.rcap);
+}
+FI uint32_t part_cap(const DevParams& p, uint32_t q) { return p.pcap ? p.pcap[q] : (uint32_t)p.rcap; }
 
 // PART mode: append the records {key[, raw]} of the live entries to this workgroup's region of each key's
 // partition.  All N slot reservations (LDS cursor atomics) are issued before the first store.  A full region
@@ -1232,7 +1237,7 @@ FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], co
   for (int r = 0; r < N; ++r) {
     if (!((live >> r) & 1u)) continue;
     if (slot[r] < cap) {
-      const size_t rec = part_region(p, key[r] >> p.pshift, blockIdx.x) * (size_t)cap + slot[r];
+      const size_t rec = part_base(p, key[r] >> p.pshift, blockIdx.x) + slot[r];
       if (p.rw == 1)
         p.recs[rec] = p.rec_idbits ? ((key[r] & ((1u << p.pshift) - 1)) << p.rec_idbits) | raw[r] : key[r];
       else *(u32x2*)(p.recs + 2 * rec) = u32x2{key[r], raw[r]};
@@ -2210,7 +2215,7 @@ __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams
 // one record to its region position `slot`, or into the HBM table when the region is full
 FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, uint32_t r0, uint32_t r1) {
   if (slot < cap) {
-    const size_t at = part_region(p, q, blockIdx.x) * (size_t)cap + slot;
+    const size_t at = part_base(p, q, blockIdx.x) + slot;
     if (p.rw == 1) p.recs[at] = r0;
     else *(u32x2*)(p.recs + 2 * at) = u32x2{r0, r1};
   } else if (p.rw == 2) {
@@ -2227,16 +2232,18 @@ FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, u
 // out eight partitions per step: 8 lanes per line, one 16-B ds_read_b128 / global_store_dwordx4 each, offsets in
 // 32 bits from the workgroup's region block.  The rest -- a line's head or tail piece (after a ring overflow, and
 // at the end) and records past a full region -- take a per-record walk, two partitions per step.
-FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring, uint32_t RC,
-                    uint32_t cap, int wave, bool final) {
+FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring,
+                    const uint32_t* lcap, const uint32_t* loff, uint32_t RC, int wave, bool final) {
   const int lane = lane_id(), np = p.nparts, half = lane >> 5, j = lane & 31, g = lane >> 3, sub = lane & 7;
   const uint32_t rw = (uint32_t)p.rw, lsh = rw == 1 ? 5u : 4u, line = 1u << lsh;  // records per 128-B line
-  uint32_t* wrec = p.recs + (size_t)blockIdx.x * (size_t)np * cap * rw;  // part_region(p, q, blockIdx.x) = this + q
+  uint32_t* wrec = p.recs + (size_t)blockIdx.x * p.pblock * rw;  // this workgroup's block (part_base)
   for (int qb = wave * 64; qb < np; qb += 64 * PGPU_PSCAN_WAVES) {
     const int q = qb + lane;
-    uint32_t H = 0, E = 0;
+    uint32_t H = 0, E = 0, cap = 0, off = 0;
     if (q < np) {
       H = head[q];
+      cap = lcap[q];
+      off = loff[q];
       const uint32_t T = tail[q];
       if (T - H > RC) {  // the ring overflowed this step: it holds [H, H + RC), the rest went straight to HBM
         E = H + RC;
@@ -2257,11 +2264,12 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
     for (int pb = 0; pb < 64; pb += 8) {
       const int src = pb + g;
       const uint32_t fl = (uint32_t)__shfl((int)FL, src, 64), ll = (uint32_t)__shfl((int)LL, src, 64);
+      const uint32_t of = (uint32_t)__shfl((int)off, src, 64);
       const uint32_t qq = (uint32_t)(qb + src);
       for (uint32_t l = fl; l < ll; ++l) {
         const uint32_t s = l << lsh;
         const u32x4 v = *(const u32x4*)(ring + (qq * RC + (s & (RC - 1))) * rw + 4 * sub);
-        *(u32x4*)(wrec + (qq * cap + s) * rw + 4 * sub) = v;
+        *(u32x4*)(wrec + (of + s) * rw + 4 * sub) = v;
       }
     }
     if (!__ballot(rest)) continue;
@@ -2271,11 +2279,12 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
       const int src = 2 * pp + half;
       const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
       const uint32_t lo = (uint32_t)__shfl((int)FL, src, 64) << lsh, hi = (uint32_t)__shfl((int)LL, src, 64) << lsh;
+      const uint32_t cp = (uint32_t)__shfl((int)cap, src, 64), of = (uint32_t)__shfl((int)off, src, 64);
       const uint32_t qq = (uint32_t)(qb + src);
       for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
         const uint32_t s = s0 + j / rw;
         if (s < h || s >= e || (s >= lo && s < hi)) continue;
-        if (s < cap) wrec[(qq * cap + s) * rw + (j & (rw - 1))] = ring[(qq * RC + (s & (RC - 1))) * rw + (j & (rw - 1))];
+        if (s < cp) wrec[(of + s) * rw + (j & (rw - 1))] = ring[(qq * RC + (s & (RC - 1))) * rw + (j & (rw - 1))];
         else spill = true;
       }
     }
@@ -2284,12 +2293,13 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
       for (int pp = 0; pp < 32; ++pp) {
         const int src = 2 * pp + half;
         const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
+        const uint32_t cp = (uint32_t)__shfl((int)cap, src, 64);
         const uint32_t qq = (uint32_t)(qb + src);
         for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
           const uint32_t s = s0 + j / rw;
-          if (s < h || s >= e || s < cap || (j & (rw - 1))) continue;
+          if (s < h || s >= e || s < cp || (j & (rw - 1))) continue;
           const uint32_t* r = ring + (qq * RC + (s & (RC - 1))) * rw;
-          pscan_put(p, qq, s, cap, r[0], rw == 2 ? r[1] : 0u);
+          pscan_put(p, qq, s, cp, r[0], rw == 2 ? r[1] : 0u);
         }
       }
       __builtin_amdgcn_s_waitcnt(0);  // nothing of this rare path stays pending into the store loops above
@@ -2297,6 +2307,9 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
   }
 }
 
+// COUNT: the sizing pass -- every psample-th tile, matched records counted per partition into pcount, nothing
+// written.  Otherwise phase 1 proper.
+template <bool COUNT>
 __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2306,7 +2319,9 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   const int npad = (np + 64 + 2) & ~1;   // + the cancel word; keeps the ring 16-B aligned
   uint32_t* head = (uint32_t*)dyn_smem;
   uint32_t* tail = head + npad;           // [np + 64] slots taken (= records of this workgroup in the partition)
-  uint32_t* ring = tail + npad;           // [np][RC * rw], then one dummy record per lane
+  uint32_t* lcap = tail + npad;           // [npad] region capacity / offset in the block per partition
+  uint32_t* loff = lcap + npad;
+  uint32_t* ring = loff + npad;           // [np][RC * rw], then one dummy record per lane
   Cons cv;
   cv.masks = (uint32_t*)((unsigned char*)(ring + ((size_t)np * RC + 64) * p.rw) + (size_t)wave * p.pscan_wave_bytes);
   cv.queue = nullptr;
@@ -2314,17 +2329,24 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   cv.acc = nullptr;
   cv.qtiles = nullptr;
   for (int i = threadIdx.x; i < 2 * npad; i += PGPU_PSCAN_THREADS) head[i] = 0u;
+  if (!COUNT)
+    for (int i = threadIdx.x; i < np; i += PGPU_PSCAN_THREADS) {
+      lcap[i] = part_cap(p, i);
+      loff[i] = p.poff ? p.poff[i] : (uint32_t)i * (uint32_t)p.rcap;
+    }
   __syncthreads();
   const int nb = gridDim.x, b = blockIdx.x;
   const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
-  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
-  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
-  const uint32_t cap = (uint32_t)p.rcap, pmask = (1u << p.pshift) - 1u;
+  const int S = COUNT ? p.psample : 1;
+  const int ntl = COUNT ? (p.total_tiles + S - 1) / S : p.total_tiles;  // tiles of this pass
+  const int t0 = (int)(((int64_t)ntl * lb) / nb);
+  const int t1 = (int)(((int64_t)ntl * (lb + 1)) / nb);
+  const uint32_t pmask = (1u << p.pshift) - 1u;
   const int idbits = p.rec_idbits;
   int64_t matched = 0, scanned = 0, dense_bytes = 0;
   Prof pf;
 #ifdef PGPU_PROFILE_BUILD
-  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+  pf.on = !COUNT && (p.flags & PGPU_FLAG_PROFILE) != 0;
 #pragma unroll
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
@@ -2333,9 +2355,9 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   int cseg = -1;
   const int nsteps = (t1 - t0 + PGPU_PSCAN_WAVES - 1) / PGPU_PSCAN_WAVES;
   for (int step = 0; step < nsteps; ++step) {
-    const int tile = t0 + step * PGPU_PSCAN_WAVES + wave;
+    const int tile = (t0 + step * PGPU_PSCAN_WAVES + wave) * S;
     int64_t tp = now(pf);
-    if (tile < t1) {
+    if (tile < t1 * S && tile < p.total_tiles) {
       if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
       const Cursor cu = cursor_at(p, tile);
       if (cu.seg != cseg) {
@@ -2376,6 +2398,11 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
 #pragma unroll
           for (int i = 0; i < 32; ++i) key[i] += ids[i] * st;
         }
+        if (COUNT) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i)
+            if (lane_bit(mm, i)) atomicAdd(&tail[key[i] >> p.pshift], 1u);
+        } else {
         if (p.pcol >= 0) {
           const DevColumn c = col_of(ss, p.pcol);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
@@ -2415,8 +2442,8 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             if (p.rw == 1) ring[at] = r0;
             else *(u32x2*)(ring + 2 * at) = u32x2{r0, val[i]};
             if (live && !in) {  // the partition's ring is full: straight to the region (a store, nothing to wait on)
-              if (slot[j] < cap) {
-                const size_t rec = part_region(p, qq[j], blockIdx.x) * (size_t)cap + slot[j];
+              if (slot[j] < lcap[qq[j]]) {
+                const size_t rec = (size_t)blockIdx.x * p.pblock + loff[qq[j]] + slot[j];
                 if (p.rw == 1) p.recs[rec] = r0;
                 else *(u32x2*)(p.recs + 2 * rec) = u32x2{r0, val[i]};
               } else {
@@ -2433,14 +2460,16 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             if ((spm >> i) & 1u) part_spill(p, key[i], p.pcol >= 0 ? val[i] : 0u);
           __builtin_amdgcn_s_waitcnt(0);
         }
+        }
       }
     }
+    if (COUNT) continue;
     PROF_ADD(pf, PGPU_P_C_AGG, tp);  // inserts (0 when the tile had no match)
     tp = now(pf);
     __syncthreads();
     PROF_ADD(pf, PGPU_P_C_FULL, tp);  // barrier waits
     tp = now(pf);
-    pscan_flush(p, head, tail, ring, RC, cap, wave, false);
+    pscan_flush(p, head, tail, ring, lcap, loff, RC, wave, false);
     if (wave == 0 && step % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p) && lane == 0) head[np + 64] = 1u;
     PROF_ADD(pf, PGPU_P_C_FLUSH, tp);
     tp = now(pf);
@@ -2448,7 +2477,13 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
     PROF_ADD(pf, PGPU_P_C_FULL, tp);
     if (head[np + 64]) break;  // cancelled: the workgroup stops together (the word was set before the barrier)
   }
-  pscan_flush(p, head, tail, ring, RC, cap, wave, true);
+  if (COUNT) {
+    __syncthreads();
+    for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
+      if (tail[q]) atomicAdd(&p.pcount[q], tail[q]);
+    return;
+  }
+  pscan_flush(p, head, tail, ring, lcap, loff, RC, wave, true);
   const size_t w = (size_t)blockIdx.x * PGPU_PSCAN_WAVES + wave;
   PROF_ADD(pf, PGPU_P_C_TOTAL, t_all);
 #ifdef PGPU_PROFILE_BUILD
@@ -2466,7 +2501,88 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
     o[PGPU_STAT_DENSE_BYTES] = dense_bytes;
   }
   for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
-    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = tail[q] < cap ? tail[q] : cap;
+    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = tail[q] < lcap[q] ? tail[q] : lcap[q];
+}
+
+// Region sizing and phase-2 work split from the sampled counts (one 1024-thread workgroup):
+//   pcap[q] = the workgroup block's pblock records shared in proportion to count[q] (smoothed so that a
+//             partition the sample missed still gets lines), in whole 128-B lines; poff = their prefix sums;
+//   p2work  = phase-2 workgroups: partition q gets 1 + its share of the p2grid - np spare workgroups in
+//             proportion to its excess over the mean count, each taking a contiguous run of phase-1 regions.
+FI uint32_t block_excl_scan(uint32_t v, uint32_t* scratch) {  // 1024 threads; scratch >= 16 words
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  const uint32_t x = (uint32_t)wave_excl_scan((int)v);
+  if (lane == 63) scratch[wave] = x + v;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += scratch[w];
+  __syncthreads();
+  return base + x;
+}
+
+__global__ __launch_bounds__(1024) void part_plan_kernel(DevParams p, int grid1) {
+  __shared__ uint32_t scratch[32];
+  __shared__ uint64_t tot[2];
+  const int np = p.nparts, t = threadIdx.x;
+  const uint32_t line = 32u / (uint32_t)p.rw;
+  if (t < 2) tot[t] = 0;
+  __syncthreads();
+  // two partitions per thread (np <= PGPU_PSCAN_MAX_PARTS = 2048)
+  uint32_t c[2];
+  for (int k = 0; k < 2; ++k) c[k] = 2 * t + k < np ? p.pcount[2 * t + k] : 0u;
+  atomicAdd((unsigned long long*)&tot[0], (unsigned long long)(c[0] + c[1]));
+  __syncthreads();
+  const uint64_t sum = tot[0];
+  const uint64_t smooth = sum / (8ull * (uint64_t)np) + 1;  // cold partitions keep ~1/8 of the mean share
+  const double wsum = (double)sum + (double)smooth * np;
+  // every partition keeps one line; the rest of the block is shared out (floors: the caps never exceed pblock)
+  const uint64_t rest = p.pblock > (uint64_t)np * line ? p.pblock - (uint64_t)np * line : 0;
+  uint32_t cap[2];
+  for (int k = 0; k < 2; ++k) {
+    const double share = ((double)c[k] + (double)smooth) / wsum;
+    const uint64_t cp = (uint64_t)((double)rest * share) / line * line;
+    cap[k] = 2 * t + k < np ? (uint32_t)(line + cp) : 0u;
+  }
+  const uint32_t off = block_excl_scan(cap[0] + cap[1], scratch);
+  for (int k = 0; k < 2; ++k)
+    if (2 * t + k < np) {
+      p.pcap[2 * t + k] = cap[k];
+      p.poff[2 * t + k] = off + (k ? cap[0] : 0u);
+    }
+  // phase-2 split: a partition of r times the mean count gets round(r) workgroups, scaled into the spare ones
+  const double mean = (double)sum / np;
+  const int spare = max(0, p.p2grid - np);
+  uint32_t ns[2];
+  __shared__ uint32_t extra;
+  if (t == 0) extra = 0;
+  __syncthreads();
+  for (int k = 0; k < 2; ++k) {
+    uint32_t s = 2 * t + k < np ? 1u : 0u;
+    if (s && mean > 0) s = max(1u, (uint32_t)((double)c[k] / mean + 0.5));
+    ns[k] = s;
+    if (s > 1) atomicAdd(&extra, s - 1);
+  }
+  __syncthreads();
+  for (int k = 0; k < 2; ++k) {
+    if (ns[k] > 1 && extra > (uint32_t)spare) ns[k] = 1 + (uint32_t)((uint64_t)(ns[k] - 1) * spare / extra);
+    if (ns[k] > (uint32_t)grid1) ns[k] = (uint32_t)grid1;  // at least one phase-1 region per phase-2 workgroup
+  }
+  const uint32_t w0 = block_excl_scan(ns[0] + ns[1], scratch);
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t first = w0 + (k ? ns[0] : 0u);
+    for (uint32_t j = 0; j < ns[k]; ++j) {
+      int32_t* wk = p.p2work + 4 * (first + j);
+      wk[0] = 2 * t + k;
+      wk[1] = (int32_t)((uint64_t)j * grid1 / ns[k]);
+      wk[2] = (int32_t)((uint64_t)(j + 1) * grid1 / ns[k]);
+      wk[3] = ns[k] > 1;
+    }
+  }
+  // idle tail of the phase-2 grid
+  __shared__ uint32_t nused;
+  if (t == 1023) nused = w0 + ns[0] + ns[1];
+  __syncthreads();
+  for (int i = (int)nused + t; i < p.p2grid; i += 1024) p.p2work[4 * i] = -1;
 }
 #endif  // TU_HAS(3)
 
@@ -2515,7 +2631,18 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
   uint32_t* sdict = (uint32_t*)(ptab + (size_t)(NS + 1) * (1u << p.pshift));  // LDM 1: [1 << slice_shift]
   const uint32_t K = 1u << p.pshift;
-  const uint32_t q = blockIdx.x;
+  // this workgroup's partition and run of phase-1 regions [w0, w1) (part_plan_kernel), or all of partition blockIdx.x
+  uint32_t q = blockIdx.x;
+  int w0 = 0, w1 = nwg;
+  bool split = false;
+  if (p.p2work) {
+    const int32_t* wk = p.p2work + 4 * blockIdx.x;
+    if (wk[0] < 0) return;
+    q = (uint32_t)wk[0];
+    w0 = wk[1];
+    w1 = wk[2];
+    split = wk[3] != 0;
+  }
   const uint64_t key0 = (uint64_t)q * K;
   const uint32_t nk = (uint32_t)min((uint64_t)K, p.G - key0);
   const int lane = lane_id(), wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
@@ -2541,10 +2668,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   for (int s = 0; s < NS; ++s) need_val |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
   {
     constexpr int R = 16;
-    for (int w = wave; w < nwg; w += nwaves) {
-      if (((w - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
+    for (int w = w0 + wave; w < w1; w += nwaves) {
+      if (((w - w0 - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
       const uint32_t n = p.rcount[(size_t)q * nwg + w];
-      const size_t base = part_region(p, q, w) * (size_t)p.rcap;
+      const size_t base = part_base(p, q, w);
       for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
         uint32_t k[R], raw[R], val[R];
         bool ok[R];
@@ -2582,7 +2709,8 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       int64_t v = ptab[(size_t)s * K + k];
       if (idbits && s > 0 && (p.sec_op[s] == PGPU_RED_MIN_I64 || p.sec_op[s] == PGPU_RED_MAX_I64))
         v = raw_to_cell(gld((const uint32_t*)p.pdict, (uint32_t)v), vt, p.sec_op[s]);  // id -> cell key
-      *cell = cell_combine(p.sec_op[s], *cell, v);
+      if (split) cell_atomic(cell, p.sec_op[s], v);  // several workgroups share the partition
+      else *cell = cell_combine(p.sec_op[s], *cell, v);
     }
   }
 }
@@ -2840,19 +2968,32 @@ hipError_t pgpu_prepare_part_reduce() {
 #undef PART_ATTR_1
 #undef PART_ATTR
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)part_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)part_scan_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PGPU_LDS_LIMIT);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)part_scan_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             PGPU_LDS_LIMIT);
   return e;
 }
 
+// Phase 1 by part_scan_kernel; with per-partition regions (p.pcap), first the sampled counting pass and the
+// sizing / phase-2 plan, all on the stream (no host round trip).
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
-  hipLaunchKernelGGL(part_scan_kernel, dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+  if (p.pcap) {
+    hipError_t e = hipMemsetAsync(p.pcount, 0, 4ull * p.nparts, st);
+    if (e != hipSuccess) return e;
+    const int sampled = (p.total_tiles + p.psample - 1) / p.psample;
+    const int cg = max(1, min(grid, (sampled + PGPU_PSCAN_WAVES - 1) / PGPU_PSCAN_WAVES));
+    hipLaunchKernelGGL(part_scan_kernel<true>, dim3(cg), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+    hipLaunchKernelGGL(part_plan_kernel, dim3(1), dim3(1024), 0, st, p, grid);
+  }
+  hipLaunchKernelGGL(part_scan_kernel<false>, dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
   return hipGetLastError();
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
   const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 + (p.ldict ? (size_t)4 << p.slice_shift : 0);
-  const dim3 g(p.nparts);
+  const dim3 g(p.p2work ? p.p2grid : p.nparts);
   switch (p.nsec - 1) {
 #define PART_LAUNCH(NS)                                                                                    \
   case NS:                                                                                                 \

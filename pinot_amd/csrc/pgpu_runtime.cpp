@@ -153,10 +153,12 @@ struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
   DevMem arena, slab, stats, stats_out, table, cmp_counts, cmp_total, cmp_keys, cmp_cells, prof, recs, rcount;
+  DevMem pcount, pcap, poff, p2work;   // PART region sizing / phase-2 plan (part_plan_kernel)
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
   PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
-  PinnedMem h_cancel;                  // the query's cancel word (DevParams::cancel), polled by its kernels
+  DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
+  uint32_t cancel_gen = 0;
   bool busy = false;
   ~Workspace() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -177,9 +179,11 @@ struct pgpu_context {
   // pgpu_query_submit: all submitted queries run back to back on one stream (each kernel fills the GPU, so
   // nothing is lost by serialising them, and their HIP events then time each kernel alone)
   hipStream_t qstream = nullptr;
+  hipStream_t cstream = nullptr;  // pgpu_query_cancel: writes cancel words while the query stream is busy
   ~pgpu_context() {
     pool.clear();
     if (qstream) (void)hipStreamDestroy(qstream);
+    if (cstream) (void)hipStreamDestroy(cstream);
   }
 };
 
@@ -1631,7 +1635,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     bool ok = true;
     for (const DevSeg& ds : pk.segs) ok &= ds.rprog_len == 0;
     const size_t wave_bytes = 256 * (size_t)p.mask_rows;
-    const size_t fixed_b = 8 * ((ptotal + 66) & ~1ull) + 4 * 64 * part_rw + 4 * wave_bytes;  // + dummies, cancel word
+    const size_t fixed_b = 16 * ((ptotal + 66) & ~1ull) + 4 * 64 * part_rw + 4 * wave_bytes;  // + caps, dummies, cancel
     const uint64_t min_rc = 64 / part_rw;  // rings of at least two 128-B lines
     for (int per_cu = 2; ok && per_cu >= 1 && !p.pscan; --per_cu) {
       const size_t budget = PGPU_LDS_LIMIT / per_cu;
@@ -1686,7 +1690,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS + 16);
-  if (e == hipSuccess) e = ws->h_cancel.ensure(16);
+  if (e == hipSuccess) e = ws->d_cancel.ensure(16);
   if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   if (p.mode == PGPU_MODE_PART) {
@@ -1721,6 +1725,26 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.rcap = (int32_t)std::max<uint64_t>(cap, 16);
     e = ws->recs.ensure(regions * (uint64_t)p.rcap * 4ull * p.rw);
     if (e == hipSuccess) e = ws->rcount.ensure(4ull * regions);
+    p.pblock = (uint64_t)p.nparts * (uint64_t)p.rcap;  // records per phase-1 workgroup block
+    p.pcount = p.pcap = p.poff = nullptr;
+    p.p2work = nullptr;
+    p.p2grid = p.nparts;
+    static const bool no_psize = getenv("PGPU_NO_PSIZE") && atoi(getenv("PGPU_NO_PSIZE")) != 0;
+    if (p.pscan && !no_psize && !(q->flags & PGPU_Q_PART_SPILL)) {
+      // regions sized from a sampled count (~8K tiles) and heavy partitions split in phase 2: skewed keys
+      // (Zipf) would otherwise overflow their regions into HBM atomics and leave one phase-2 workgroup with most
+      // of the records
+      p.psample = std::max(1, p.total_tiles / 8192);
+      p.p2grid = 2 * p.nparts;
+      if (e == hipSuccess) e = ws->pcount.ensure(4ull * p.nparts);
+      if (e == hipSuccess) e = ws->pcap.ensure(4ull * p.nparts);
+      if (e == hipSuccess) e = ws->poff.ensure(4ull * p.nparts);
+      if (e == hipSuccess) e = ws->p2work.ensure(16ull * p.p2grid);
+      p.pcount = (uint32_t*)ws->pcount.p;
+      p.pcap = (uint32_t*)ws->pcap.p;
+      p.poff = (uint32_t*)ws->poff.p;
+      p.p2work = (int32_t*)ws->p2work.p;
+    }
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "group-by record buffers: %s", hipGetErrorString(e)));
     p.recs = (uint32_t*)ws->recs.p;
     p.rcount = (uint32_t*)ws->rcount.p;
@@ -1762,12 +1786,13 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // copy sits between two queries' kernels
   void* h_arena_dev = nullptr;
   void* h_stats_dev = nullptr;
-  void* h_cancel_dev = nullptr;
-  // the workspace is free, so no kernel of an earlier query polls its cancel word any more
+  // cancel word in HBM: a query is stopped when the word equals its generation (no reset that could race a
+  // cancel issued from another stream); the kernels poll it with uncached loads
+  if (++ws->cancel_gen == 0) ws->cancel_gen = 1;
+  p.cancel = (const int32_t*)ws->d_cancel.p;
+  p.cancel_gen = ws->cancel_gen;
   const bool expired = q->deadline_ms > 0 && now_epoch_ms() >= q->deadline_ms;
-  __atomic_store_n((int32_t*)ws->h_cancel.p, expired ? 1 : 0, __ATOMIC_SEQ_CST);
-  e = hipHostGetDevicePointer(&h_cancel_dev, ws->h_cancel.p, 0);
-  p.cancel = (const int32_t*)h_cancel_dev;
+  if (expired) e = hipMemsetD32Async((hipDeviceptr_t)ws->d_cancel.p, (int)ws->cancel_gen, 1, st);
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_arena_dev, ws->h_arena.p, 0);
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
@@ -1842,12 +1867,24 @@ int pgpu_query_launch(pgpu_context* ctx, const pgpu_query_desc* q, void* stream,
   return launch_impl(ctx, q, stream, dev_table, table_bytes, nullptr, out_query);
 }
 
+// Write the query's generation into its cancel word from the context's side stream (the query stream is busy).
+static int signal_cancel(pgpu_query* qq) {
+  HIP_TRY(hipSetDevice(qq->ctx->device));
+  hipStream_t cs = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(qq->ctx->mu);
+    if (!qq->ctx->cstream) HIP_TRY(hipStreamCreateWithFlags(&qq->ctx->cstream, hipStreamNonBlocking));
+    cs = qq->ctx->cstream;
+  }
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)qq->params.cancel, (int)qq->params.cancel_gen, 1, cs));
+  return PGPU_OK;
+}
+
 int pgpu_query_cancel(pgpu_query* qq) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
   int none = 0;
-  qq->stop.compare_exchange_strong(none, PGPU_E_CANCELLED);
-  __atomic_store_n((int32_t*)qq->ws->h_cancel.p, 1, __ATOMIC_SEQ_CST);
-  return PGPU_OK;
+  if (!qq->stop.compare_exchange_strong(none, PGPU_E_CANCELLED)) return PGPU_OK;  // already stopped
+  return signal_cancel(qq);
 }
 
 int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
@@ -1862,8 +1899,10 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
       if (qe != hipErrorNotReady) return fail(PGPU_E_HIP, "query wait: %s", hipGetErrorString(qe));
       if (qq->stop.load() == 0 && now_epoch_ms() >= qq->deadline_ms) {
         int none = 0;
-        qq->stop.compare_exchange_strong(none, PGPU_E_TIMEOUT);
-        __atomic_store_n((int32_t*)qq->ws->h_cancel.p, 1, __ATOMIC_SEQ_CST);
+        if (qq->stop.compare_exchange_strong(none, PGPU_E_TIMEOUT)) {
+          const int rc = signal_cancel(qq);
+          if (rc) return rc;
+        }
       }
       if (spins < 2000) std::this_thread::yield();
       else std::this_thread::sleep_for(std::chrono::microseconds(20));

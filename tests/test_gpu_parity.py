@@ -350,7 +350,7 @@ def test_synth_segments_upload_d2d(gpu_ctx):
     """GPU-generated segments (device-to-device upload) answer exactly like the same segments built on the host."""
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.synth import WORKLOADS, build_segment_cpu, build_segments_gpu
-    for wn in ("range_in", "adanalytics", "groupby1m"):
+    for wn in ("range_in", "adanalytics", "groupby1m", "groupby1m_zipf"):
         w = WORKLOADS[wn]
         n = 300_007
         gsegs = build_segments_gpu(gpu_ctx, w, [3, 4], n)
