@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 3
+#define PGPU_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -99,6 +99,22 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
                                 uint64_t num_bytes, int32_t cardinality);
 int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
                                     int32_t cardinality);
+/* Raw (no-dictionary) single-value column of a fixed-width type (INT / LONG / FLOAT / DOUBLE): the file
+ * FixedByteChunkSVForwardIndexWriter writes (`<column>.sv.raw.fwd`, seglocal/io/writer/impl/
+ * FixedByteChunkSVForwardIndexWriter.java:39-104, header BaseChunkSVForwardIndexWriter.java:125-160), versions 1-4,
+ * chunks PASS_THROUGH / SNAPPY / LZ4 / LZ4_LENGTH_PREFIXED (ChunkCompressionType ordinals 0, 1, 3, 4; ZSTANDARD
+ * returns PGPU_E_UNSUPPORTED).  Decoded once into HBM as the values by doc id, replacing FixedByteChunkSVForwardIndexReader /
+ * FixedBytePower2ChunkSVForwardIndexReader (seglocal/segment/index/readers/forward/BaseChunkSVForwardIndexReader.java:56-157).
+ * Such a column has no dictionary (do not call pgpu_segment_add_dictionary); it may be aggregated (SUM / MIN / MAX /
+ * AVG) and filtered through PGPU_F_RAW_SCAN / PGPU_F_RANGE_INDEX leaves, but not grouped on (the reference groups raw
+ * columns with NoDictionary*GroupKeyGenerator, a value-hash path outside this one: PGPU_E_UNSUPPORTED). */
+int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_t data_type, const void* bytes,
+                                       uint64_t num_bytes);
+/* Range index of a column (`<column>.bitmap.range`): only its header is read -- version 2 is the exact bit-sliced
+ * index (BitSlicedRangeIndexCreator.java:38,115-125; BitSlicedRangeIndexReader.java:41-55), version 1 the legacy
+ * RangeIndexReaderImpl with partial matches.  The GPU answers range-index leaves from the forward index (same doc set);
+ * the version decides the leaf's statistics (see PGPU_F_RANGE_INDEX). */
+int pgpu_segment_add_range_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes);
 int pgpu_segment_seal(pgpu_segment* seg);
 /* HBM bytes held by the segment (all columns, including padding and container directories). */
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);
@@ -139,6 +155,23 @@ int pgpu_buffer_release(pgpu_buffer* buf);
 #define PGPU_F_OR_CHILD_END 9
 #define PGPU_F_OR_END 10
 #define PGPU_F_NOT 11
+/* Raw-value leaves (columns uploaded with pgpu_segment_add_raw_forward_index):
+ *   RAW_SCAN   : ScanBasedFilterOperator with a RawValueBased*PredicateEvaluator (its entries count towards
+ *                numEntriesScannedInFilter like a dictionary scan's)
+ *   RANGE_INDEX: RangeIndexBasedFilterOperator (FilterOperatorUtils.java:57-64: RANGE predicates on a column with a
+ *                range index, AND priority 2).  On a dictionary column it carries the dict-id range [lo, hi) like a
+ *                SCAN leaf; on a raw column raw values as below.  An exact (version 2) range index scans no entries;
+ *                its raw-column bounds are used inclusively whatever the predicate's flags, as the reference's
+ *                Int/Long/Float/DoubleRangeEvaluator pass getLowerBound / getUpperBound to the index
+ *                (RangeIndexBasedFilterOperator.java:165-290), and floating values compare by FPOrdering ordinals
+ *                (NaN = -infinity).
+ * Raw values are given in `values`: 8-byte int64 for INT / LONG columns, IEEE double for FLOAT / DOUBLE columns (the
+ * literal parsed as the evaluator parses it: Integer.parseInt, Float.parseFloat, ...).
+ *   PGPU_PRED_RANGE: values[0] lower, values[1] upper bound; lo = 1 when the lower bound is inclusive, hi = 1 when
+ *                    the upper is (an unbounded side is the type's extreme, inclusive)
+ *   PGPU_PRED_SET  : num_ids values (EQ: one); negate for NOT_EQ / NOT_IN */
+#define PGPU_F_RAW_SCAN 12
+#define PGPU_F_RANGE_INDEX 13
 
 #define PGPU_PRED_RANGE 0
 #define PGPU_PRED_SET 1
@@ -152,6 +185,7 @@ typedef struct {
   const int32_t* ids; /* SET / INVERTED: dict ids; SORTED: 2*num_ids ints (start, end inclusive) */
   int32_t num_ids;
   int32_t reserved;
+  const void* values; /* RAW_SCAN / raw RANGE_INDEX: the predicate's values (see PGPU_F_RAW_SCAN) */
 } pgpu_filter_node;
 
 /* aggregation functions (core/query/aggregation/function/<X>AggregationFunction.java) */

@@ -30,6 +30,7 @@ from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_ST
 from pinot_amd.query import UNBOUNDED, FilterContext, Predicate, QueryContext
 from pinot_amd.segment import SegmentData
 
+from .rawfwd import read_raw_forward
 from .segment_writer import NATIVE, read_inverted_bitmap, unpack_fixed_bit
 
 EOF = -(2 ** 31)  # Constants.EOF = Integer.MIN_VALUE
@@ -72,7 +73,18 @@ class DecodedSegment:
             self._ids[col] = a
         return a
 
+    def raw_values(self, col: str) -> np.ndarray:
+        """A raw (no-dictionary) column's values by doc id (FixedByteChunkSVForwardIndexReader)."""
+        a = self._ids.get(("raw", col))
+        if a is None:
+            c = self.seg.column(col)
+            a = read_raw_forward(c.raw_forward, c.data_type, self.num_docs)
+            self._ids[("raw", col)] = a
+        return a
+
     def values(self, col: str):
+        if self.seg.column(col).raw_forward is not None:
+            return self.raw_values(col)
         d = self.dictionary(col)
         ids = self.ids(col)
         if isinstance(d, list):
@@ -177,6 +189,72 @@ def _truth_on_dictionary(d, dt: int, p: Predicate, pad=None) -> np.ndarray:
     return m
 
 
+# ---- raw-value predicates (no dictionary) --------------------------------------------------------------------------
+_IRANGE = {PGPU_INT: (-(1 << 31), (1 << 31) - 1), PGPU_LONG: (-(1 << 63), (1 << 63) - 1)}
+
+
+def _raw_literal(v: str, dt: int):
+    """Integer.parseInt / Long.parseLong / Float.parseFloat / Double.parseDouble of a literal (ValueError where the
+    reference throws NumberFormatException)."""
+    if dt in (PGPU_INT, PGPU_LONG):
+        body = v[1:] if v[:1] in "+-" else v
+        if not (body.isascii() and body.isdigit()):
+            raise ValueError(f"NumberFormatException: {v!r}")
+        x = int(v)
+        if not _IRANGE[dt][0] <= x <= _IRANGE[dt][1]:
+            raise ValueError(f"NumberFormatException: {v!r}")
+        return x
+    t = v.strip()
+    core = t.lstrip("+-")
+    if core in ("NaN", "Infinity"):
+        x = float(t.replace("Infinity", "inf"))
+    else:
+        if not core or any(ch.isalpha() and ch not in "eEfFdD" for ch in core):
+            raise ValueError(f"NumberFormatException: {v!r}")
+        x = float(t.rstrip("fFdD"))
+    return float(np.float32(x)) if dt == PGPU_FLOAT else x
+
+
+def _fp_ordinal_key(a: np.ndarray) -> np.ndarray:
+    """FPOrdering.ordinalOf order (segment-local/utils/FPOrdering.java): NaN and -inf lowest, -0 == 0."""
+    a = np.asarray(a, dtype=np.float64)
+    return np.where(np.isnan(a), -np.inf, a) + 0.0  # + 0.0 turns -0.0 into 0.0
+
+
+def raw_predicate_mask(ds: DecodedSegment, p: Predicate, range_index: bool) -> np.ndarray:
+    """Per doc: the raw-value evaluator's applySV (RangePredicateEvaluatorFactory.java:62-110 + the Int/Long/Float/
+    DoubleRawValueBasedRangePredicateEvaluator classes; Equals / NotEquals / In / NotIn raw evaluators with
+    fastutil sets: float members equal by their bits).  range_index: RangeIndexBasedFilterOperator's evaluation --
+    the evaluator's bounds inclusive whatever the flags (RangeIndexBasedFilterOperator.java:165-290), floats
+    compared by FPOrdering ordinals."""
+    c = ds.seg.column(p.column)
+    dt = c.data_type
+    v = ds.raw_values(p.column)
+    fp = dt in (PGPU_FLOAT, PGPU_DOUBLE)
+    if p.type == "RANGE":
+        lu, uu = p.lower == UNBOUNDED, p.upper == UNBOUNDED
+        ext = _IRANGE[dt] if not fp else (-math.inf, math.inf)
+        lo = ext[0] if lu else _raw_literal(p.lower, dt)
+        hi = ext[1] if uu else _raw_literal(p.upper, dt)
+        li = lu or p.lower_inclusive or range_index
+        hi_i = uu or p.upper_inclusive or range_index
+        x = v.astype(np.float64) if fp else v.astype(np.int64)
+        if fp and range_index:
+            x = _fp_ordinal_key(x)
+            lo, hi = float(_fp_ordinal_key(np.array([lo]))[0]), float(_fp_ordinal_key(np.array([hi]))[0])
+        m = (x >= lo) if li else (x > lo)
+        m &= (x <= hi) if hi_i else (x < hi)
+        return m
+    lits = [_raw_literal(x, dt) for x in p.values]
+    if fp:
+        bits = v.astype(np.float64).view(np.int64)
+        want = np.array(lits, dtype=np.float64).view(np.int64)
+        m = np.isin(bits, want)
+    else:
+        m = np.isin(v.astype(np.int64), np.array(lits, dtype=np.int64))
+    return ~m if p.type in ("NOT_EQ", "NOT_IN") else m
+
+
 def predicate_mask(ds: DecodedSegment, p: Predicate) -> np.ndarray:
     """Boolean per doc: does the doc's value satisfy the predicate (truth per dictionary value, gathered by the
     doc's dict id — value semantics, since the dictionary holds the values)."""
@@ -188,12 +266,13 @@ def predicate_mask(ds: DecodedSegment, p: Predicate) -> np.ndarray:
 # ---- physical operator tree (restated FilterOperatorUtils) ------------------------------------------------------
 @dataclass
 class POp:
-    kind: str                 # EMPTY ALL SCAN BITMAP SORTED AND OR NOT
+    kind: str                 # EMPTY ALL SCAN RAW_SCAN BITMAP SORTED RANGE_INDEX AND OR NOT
     children: List["POp"] = field(default_factory=list)
     mask: Optional[np.ndarray] = None   # leaf doc set
 
     def priority(self) -> int:
-        return {"SORTED": 0, "BITMAP": 1, "AND": 3, "OR": 4, "SCAN": 5}.get(self.kind) if self.kind != "NOT" \
+        return {"SORTED": 0, "BITMAP": 1, "RANGE_INDEX": 2, "AND": 3, "OR": 4, "SCAN": 5,
+                "RAW_SCAN": 5}.get(self.kind) if self.kind != "NOT" \
             else self.children[0].priority()
 
 
@@ -229,8 +308,12 @@ def build_physical(ds: DecodedSegment, f: Optional[FilterContext]) -> POp:
             return POp("ALL")
         return POp("NOT", [ch])
     p = f.predicate
-    m = predicate_mask(ds, p)
     col = ds.seg.column(p.column)
+    if col.raw_forward is not None:
+        # no dictionary: no always-true / -false folding, no sorted / inverted index (FilterOperatorUtils.java:42-81)
+        ri = p.type == "RANGE" and col.range_index is not None
+        return POp("RANGE_INDEX" if ri else "RAW_SCAN", mask=raw_predicate_mask(ds, p, ri))
+    m = predicate_mask(ds, p)
     # alwaysTrue / alwaysFalse are decided on the dictionary (every dict value matches / none does)
     d = ds.dictionary(p.column)
     pad = _padder(col.pad_char, col.entry_width) if col.data_type == PGPU_STRING else None
@@ -241,6 +324,8 @@ def build_physical(ds: DecodedSegment, f: Optional[FilterContext]) -> POp:
         return POp("ALL")
     if col.sorted_index is not None:
         return POp("SORTED", mask=m)
+    if p.type == "RANGE" and col.range_index is not None:  # exact dict-id range of the range index
+        return POp("RANGE_INDEX", mask=m)
     if p.type != "RANGE" and col.inverted is not None:
         # the inverted index is read through its own bytes: checks the Roaring writer too
         ids = ds.ids(p.column)
@@ -441,9 +526,9 @@ class _Not:
 
 def make_iterator(op: POp, n: int, counter: list):
     """FilterBlockDocIdSet.iterator() of the physical operator `op`."""
-    if op.kind == "SCAN":
+    if op.kind in ("SCAN", "RAW_SCAN"):
         return _Scan(op.mask, counter)
-    if op.kind == "BITMAP":
+    if op.kind in ("BITMAP", "RANGE_INDEX"):  # RangeIndexBasedFilterOperator: a BitmapDocIdSet
         return _Docs(np.flatnonzero(op.mask), "bitmap")
     if op.kind == "SORTED":
         return _Docs(np.flatnonzero(op.mask), "sorted")
@@ -491,6 +576,8 @@ def entries_scanned_in_filter(op: POp, n: int) -> Tuple[int, np.ndarray]:
 
 # ---- aggregation -------------------------------------------------------------------------------------------------
 def _as_float_values(ds: DecodedSegment, col: str, docs: np.ndarray) -> np.ndarray:
+    if ds.seg.column(col).raw_forward is not None:
+        return ds.raw_values(col)[docs]
     d = ds.dictionary(col)
     if isinstance(d, list):
         raise ValueError(f"non-numeric column {col}")
@@ -543,12 +630,17 @@ def final(fn: str, v):
     return float(v)
 
 
-def fits_non_scan(query: QueryContext, num_docs: int) -> bool:
+def fits_non_scan(query: QueryContext, num_docs: int, seg: Optional[SegmentData] = None) -> bool:
     """AggregationPlanNode.isFitForNonScanBasedPlan (core/plan/AggregationPlanNode.java:234-262) for the functions
     this path serves: aggregation-only, no FILTER clauses, only COUNT / MIN / MAX (dictionary-encoded columns).
     Empty segments are left to the scan plan (their dictionaries hold no min / max)."""
-    return (not query.group_by and not query.has_filtered_aggregations and num_docs > 0
-            and all(a.function in ("COUNT", "MIN", "MAX") for a in query.aggregations))
+    if (query.group_by or query.has_filtered_aggregations or num_docs <= 0
+            or any(a.function not in ("COUNT", "MIN", "MAX") for a in query.aggregations)):
+        return False
+    # raw columns: MIN / MAX come from the column metadata's min / max values, when it has them (METADATA_BASED_FUNCTIONS)
+    return seg is None or all(seg.column(a.column).raw_forward is None or
+                              (seg.column(a.column).min_value is not None and seg.column(a.column).max_value is not None)
+                              for a in query.aggregations if a.function != "COUNT")
 
 
 @dataclass
@@ -567,13 +659,16 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
     ds = seg if isinstance(seg, DecodedSegment) else DecodedSegment(seg)
     n = ds.num_docs
     op = build_physical(ds, query.filter)
-    if op.kind == "ALL" and fits_non_scan(query, n):
+    if op.kind == "ALL" and fits_non_scan(query, n, ds.seg):
         # NonScanBasedAggregationOperator (core/operator/query/NonScanBasedAggregationOperator.java:85-101,253-256):
         # COUNT from metadata, MIN / MAX from the dictionary's first / last value; stats (total, 0, 0, total)
         agg = []
         for a in query.aggregations:
             if a.function == "COUNT":
                 agg.append(n)
+            elif ds.seg.column(a.column).raw_forward is not None:
+                c = ds.seg.column(a.column)
+                agg.append(float(c.min_value if a.function == "MIN" else c.max_value))
             else:
                 d = ds.dictionary(a.column)
                 agg.append(float(d[0] if a.function == "MIN" else d[-1]))

@@ -255,13 +255,23 @@ def read_inverted_bitmap(data: bytes, cardinality: int, dict_id: int) -> np.ndar
 
 # ---- segment builder ------------------------------------------------------------------------------------------
 def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] = (),
-                  sorted_columns: Optional[Iterable[str]] = None, allow_runs: bool = True) -> SegmentData:
+                  sorted_columns: Optional[Iterable[str]] = None, allow_runs: bool = True,
+                  raw: Iterable[str] = (), raw_codec: int = 0, raw_version: int = 2,
+                  range_index: Iterable[str] = (), range_index_version: int = 2,
+                  raw_min_max: bool = True) -> SegmentData:
     """Build an immutable segment from raw column values.
 
     `columns`: name -> (data_type, values).  A column is stored with a sorted index when its dict ids are
     non-decreasing (the segment creator's isSorted detection) unless `sorted_columns` restricts the set.
-    `inverted`: columns whose inverted index is loaded (IndexLoadingConfig.getInvertedIndexColumns)."""
+    `inverted`: columns whose inverted index is loaded (IndexLoadingConfig.getInvertedIndexColumns).
+    `raw`: no-dictionary columns (noDictionaryColumns), written as FixedByteChunkSVForwardIndexWriter files with
+    `raw_codec` / `raw_version` (oracle/rawfwd.py); `raw_min_max` records their metadata min / max.
+    `range_index`: columns with a range index (rangeIndexColumns) of `range_index_version` (header only, see
+    oracle.rawfwd.range_index_header)."""
+    from .rawfwd import range_index_header, write_raw_forward
     inverted = set(inverted)
+    raw = set(raw)
+    range_index = set(range_index)
     n = None
     seg = None
     for cname, (dt, values) in columns.items():
@@ -270,6 +280,16 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
             seg = SegmentData(name, n)
         if len(values) != n:
             raise ValueError("ragged columns")
+        if cname in raw:
+            vals = np.asarray(values, dtype=NATIVE[dt])
+            col = ColumnIndexes(cname, dt, len(np.unique(vals)) if n else 0,
+                                raw_forward=write_raw_forward(vals, dt, raw_codec, raw_version))
+            if raw_min_max and n:
+                col.min_value, col.max_value = vals.min().item(), vals.max().item()
+            if cname in range_index:
+                col.range_index = range_index_header(range_index_version, int(vals.min()) if n and dt < 2 else 0)
+            seg.columns[cname] = col
+            continue
         uniq, ids = build_dictionary(values, dt)
         card = len(uniq)
         is_sorted = bool(np.all(np.diff(ids) >= 0)) if n else True
@@ -283,6 +303,8 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
             col.forward = pack_fixed_bit(ids, bits_per_value(card))
         if cname in inverted:
             col.inverted = inverted_index_bytes(ids, card, allow_runs)
+        if cname in range_index:
+            col.range_index = range_index_header(range_index_version, 0)
         seg.columns[cname] = col
     return seg
 
@@ -315,6 +337,19 @@ def write_segment_dir(seg: SegmentData, path: str, version: str = "v3", pad_char
             f"segment.padding.character = {pad_text}", f"segment.index.version = {version}"]
     indexes = []  # (column, index name, v1 extension, bytes)
     for c in seg.columns.values():
+        if c.raw_forward is not None:  # no-dictionary column (ColumnMetadataImpl hasDictionary = false)
+            meta += [f"column.{c.name}.cardinality = {c.cardinality}", f"column.{c.name}.totalDocs = {seg.num_docs}",
+                     f"column.{c.name}.dataType = {_TYPE_NAME[c.data_type]}",
+                     f"column.{c.name}.bitsPerElement = {bits_per_value(max(c.cardinality, 1))}",
+                     f"column.{c.name}.lengthOfEachEntry = 0", f"column.{c.name}.isSorted = false",
+                     f"column.{c.name}.hasDictionary = false", f"column.{c.name}.hasInvertedIndex = false",
+                     f"column.{c.name}.isSingleValues = true"]
+            if c.min_value is not None and c.max_value is not None:
+                meta += [f"column.{c.name}.minValue = {c.min_value!r}", f"column.{c.name}.maxValue = {c.max_value!r}"]
+            indexes.append((c.name, "forward_index", ".sv.raw.fwd", bytes(c.raw_forward)))
+            if c.range_index is not None:
+                indexes.append((c.name, "range_index", ".bitmap.range", bytes(c.range_index)))
+            continue
         if c.data_type == PGPU_STRING:
             dbytes, width = string_dictionary_bytes(list(c.dictionary), pad)
         else:
@@ -335,6 +370,8 @@ def write_segment_dir(seg: SegmentData, path: str, version: str = "v3", pad_char
             indexes.append((c.name, "forward_index", ".sv.unsorted.fwd", bytes(c.forward)))
         if c.inverted is not None:
             indexes.append((c.name, "inverted_index", ".bitmap.inv", bytes(c.inverted)))
+        if c.range_index is not None:
+            indexes.append((c.name, "range_index", ".bitmap.range", bytes(c.range_index)))
     with open(os.path.join(root, "metadata.properties"), "w") as f:
         f.write("\n".join(meta) + "\n")
     if version == "v3":

@@ -28,7 +28,8 @@ PGPU_INT, PGPU_LONG, PGPU_FLOAT, PGPU_DOUBLE, PGPU_STRING = range(5)
 PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
 
 (PGPU_F_MATCH_ALL, PGPU_F_EMPTY, PGPU_F_SCAN, PGPU_F_INVERTED, PGPU_F_SORTED, PGPU_F_AND_BEGIN,
- PGPU_F_AND_CHILD_END, PGPU_F_AND_END, PGPU_F_OR_BEGIN, PGPU_F_OR_CHILD_END, PGPU_F_OR_END, PGPU_F_NOT) = range(12)
+ PGPU_F_AND_CHILD_END, PGPU_F_AND_END, PGPU_F_OR_BEGIN, PGPU_F_OR_CHILD_END, PGPU_F_OR_END, PGPU_F_NOT,
+ PGPU_F_RAW_SCAN, PGPU_F_RANGE_INDEX) = range(14)
 PGPU_PRED_RANGE, PGPU_PRED_SET = 0, 1
 PGPU_AGG_COUNT, PGPU_AGG_SUM, PGPU_AGG_MIN, PGPU_AGG_MAX, PGPU_AGG_AVG = range(5)
 PGPU_RED_SUM_I64, PGPU_RED_SUM_F64, PGPU_RED_MIN_I64, PGPU_RED_MAX_I64 = range(4)
@@ -36,7 +37,7 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class PinotGpuError(RuntimeError):
@@ -64,7 +65,7 @@ class QueryCancelledError(PinotGpuError):
 class FilterNode(C.Structure):
     _fields_ = [("op", C.c_int32), ("column", C.c_int32), ("pred", C.c_int32), ("negate", C.c_int32),
                 ("lo", C.c_int32), ("hi", C.c_int32), ("ids", C.POINTER(C.c_int32)), ("num_ids", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("reserved", C.c_int32), ("values", C.c_void_p)]
 
 
 class Agg(C.Structure):
@@ -125,6 +126,8 @@ SIGNATURES = [
     ("pgpu_segment_add_sorted_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32]),
     ("pgpu_segment_add_dictionary", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_uint64, C.c_int32]),
     ("pgpu_segment_add_inverted_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32]),
+    ("pgpu_segment_add_raw_forward_index", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_uint64]),
+    ("pgpu_segment_add_range_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64]),
     ("pgpu_segment_seal", C.c_int, [_P]),
     ("pgpu_segment_device_bytes", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_release", C.c_int, [_P]),

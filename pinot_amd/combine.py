@@ -31,7 +31,7 @@ import numpy as np
 from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
-from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, finish, key_words_out,
+from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, check_group_columns, GroupTable, QueryResult, finish, key_words_out,
                    merge_filtered)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
@@ -240,6 +240,7 @@ class DistributedExecutor:
         if not self._agree(hit is not None):
             hit = None
         if hit is None:
+            check_group_columns(query, segments)
             dicts = []
             for g in query.group_by:
                 local, _ = self.pm.global_dictionary(g, segments)
@@ -382,8 +383,8 @@ class DistributedExecutor:
                 continue
             sec, vt = L.agg_section[ai], L.agg_value_type[ai]
             for s in p.non_scan:
-                d = s.dictionaries[a.column]
-                k = minmax_key(float(d[0] if a.function == "MIN" else d[-1]), vt)
+                lo, hi = s.min_max(a.column)
+                k = minmax_key(lo if a.function == "MIN" else hi, vt)
                 cur = int(view[sec, 0].item())
                 view[sec, 0] = min(cur, k) if a.function == "MIN" else max(cur, k)
         stats["num_docs_scanned"] += cnt

@@ -58,6 +58,11 @@
 #define PGPU_COL_NONE 0
 #define PGPU_COL_FIXED_BIT 1
 #define PGPU_COL_SORTED 2
+// Raw (no-dictionary) column: DevColumn::dict holds the values by doc id (little-endian, decoded from the
+// FixedByteChunkSVForwardIndexWriter chunks at upload), so a raw column's "dict id" of doc d is d itself and every
+// dictionary gather of the aggregation paths reads the value directly.  Predicates on it become per-segment match
+// bitmaps (rawpred_kernel) read by PGPU_I_BITS leaves.
+#define PGPU_COL_RAW 3
 
 // Roaring container types
 #define PGPU_CT_ARRAY 0
@@ -114,6 +119,7 @@ struct DevSeg {
   // negated when f_sneg[j] (0 ranges = the leaf decodes the packed layout)
   int32_t f_nr[2];
   int32_t f_sneg[2];
+  int32_t f_nostat[2];            // fast leaf j does not count towards numEntriesScannedInFilter (range-index leaf)
   uint32_t f_rng[2][PGPU_SLICE_RANGES][2];
   int32_t track;                  // HASH mode: 1 + row of this segment's distinct-key bitmap (0 = not counted)
   // PGPU_Q_EXACT_FILTER_STATS: the leaves of the segment's whole (unsplit) filter program, in prefix order --
@@ -138,6 +144,8 @@ struct DevSeg {
 #define PGPU_I_OR_CHILD 9
 #define PGPU_I_OR_END 10
 #define PGPU_I_NOT 11
+// match bits precomputed per doc (raw-value leaves: rawpred_kernel output at DevInstr::fwd, bit d % 32 of word d / 32)
+#define PGPU_I_BITS 12
 
 struct DevInstr {
   int32_t op;
@@ -159,8 +167,34 @@ struct DevInstr {
   const uint32_t* fwd;
   const int32_t* sorted;
   uint32_t ids[8];    // LIST ids
+  // leaf entries do not count towards numEntriesScannedInFilter: RangeIndexBasedFilterOperator (an exact bit-sliced
+  // range index) answers the leaf from its bitmaps (RangeIndexBasedFilterOperator.java:58-64); on the GPU the same
+  // doc set comes from the forward index
+  int32_t nostat;
+  int32_t pad_[3];
 };
-static_assert(sizeof(DevInstr) == 112, "DevInstr layout");
+static_assert(sizeof(DevInstr) == 128, "DevInstr layout");
+
+// One raw-value filter leaf of one segment (ScanBasedFilterOperator with a RawValueBased*PredicateEvaluator, or
+// RangeIndexBasedFilterOperator over a raw column): rawpred_kernel evaluates it over every doc into a bitmap before
+// the query kernel runs (PGPU_I_BITS reads it).
+struct RawLeaf {
+  const void* values;   // the column's little-endian values (DevColumn::dict of a PGPU_COL_RAW column)
+  uint32_t* out;        // ntiles * 64 words; bit d % 32 of word d / 32, 0 past num_docs
+  int32_t num_docs;
+  int32_t words;
+  int32_t vtype;        // PGPU_INT .. PGPU_DOUBLE
+  int32_t pred;         // PGPU_PRED_RANGE / PGPU_PRED_SET
+  int32_t flags;        // RANGE: bit 0 lower inclusive, bit 1 upper inclusive (unbounded = inclusive type extreme)
+  int32_t negate;       // NOT_EQ / NOT_IN
+  int32_t nvals;        // SET: values at vals
+  int32_t pad_;
+  int64_t lo, hi;       // RANGE bounds: int64 (INT / LONG) or double bits (FLOAT / DOUBLE)
+  const int64_t* vals;  // SET: int64 values ascending (INT / LONG) or order-preserving keys of the doubles ascending
+};
+#define PGPU_RAW_RANGE_LO_INCL 1
+#define PGPU_RAW_RANGE_HI_INCL 2
+#define PGPU_RAW_RANGE_ORDINAL 4  // range-index semantics for FLOAT / DOUBLE: NaN orders as -infinity (FPOrdering)
 
 struct DevAgg {
   int32_t fn;       // PGPU_AGG_*
@@ -284,6 +318,7 @@ static_assert(sizeof(DevParams) <= 4096, "DevParams is a kernel argument");
 
 #define PGPU_FLAG_STATS 1
 #define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)
+#define PGPU_FLAG_NT 4        // direct kernel: tile DMAs with the non-temporal policy (PGPU_DIRECT_NT=1)
 #define PGPU_NPROF 12
 // loader phases
 #define PGPU_P_L_TOTAL 0

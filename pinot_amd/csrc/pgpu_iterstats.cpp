@@ -252,7 +252,9 @@ int parse(const pgpu_filter_node* nd, int n, int i, int* leaf, Node* out) {
     case PGPU_F_SCAN:
     case PGPU_F_INVERTED:
     case PGPU_F_SORTED:
-      if (op == PGPU_F_SCAN || op == PGPU_F_INVERTED || op == PGPU_F_SORTED) out->leaf = (*leaf)++;
+    case PGPU_F_RAW_SCAN:
+    case PGPU_F_RANGE_INDEX:
+      if (op != PGPU_F_MATCH_ALL && op != PGPU_F_EMPTY) out->leaf = (*leaf)++;
       return i + 1;
     case PGPU_F_NOT: {
       out->kids.emplace_back();
@@ -283,7 +285,9 @@ struct Builder {
   std::unique_ptr<Iter> make(const Node& x) {
     switch (x.op) {
       case PGPU_F_SCAN:
+      case PGPU_F_RAW_SCAN:  // SVScanDocIdIterator over raw values counts like the dictionary scan
         return std::unique_ptr<Iter>(new ScanIter(&(*leaves)[x.leaf], counter));
+      case PGPU_F_RANGE_INDEX:  // RangeIndexBasedFilterOperator: a BitmapDocIdSet of the exact index's matches
       case PGPU_F_INVERTED:
         return std::unique_ptr<Iter>(new DocsIter(std::make_shared<BitSet>((*leaves)[x.leaf]), BITMAP));
       case PGPU_F_SORTED:
@@ -383,7 +387,7 @@ int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, 
 namespace {
 
 bool has_scan(const Node& x) {
-  if (x.op == PGPU_F_SCAN) return true;
+  if (x.op == PGPU_F_SCAN || x.op == PGPU_F_RAW_SCAN) return true;
   for (const Node& k : x.kids)
     if (has_scan(k)) return true;
   return false;
@@ -403,8 +407,8 @@ bool gpu_count_matches(const Node& x) {
       int idx = 0, scans = 0;
       bool rest = false, rest_scans = false;
       for (const Node& k : x.kids) {
-        if (k.op == PGPU_F_SORTED || k.op == PGPU_F_INVERTED) ++idx;
-        else if (k.op == PGPU_F_SCAN) ++scans;
+        if (k.op == PGPU_F_SORTED || k.op == PGPU_F_INVERTED || k.op == PGPU_F_RANGE_INDEX) ++idx;
+        else if (k.op == PGPU_F_SCAN || k.op == PGPU_F_RAW_SCAN) ++scans;
         else {
           rest = true;
           rest_scans |= has_scan(k);

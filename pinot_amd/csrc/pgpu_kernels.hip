@@ -390,6 +390,18 @@ FI void decode_ids(int bits, const uint32_t* region, const uint32_t* fwd, int ti
   PGPU_DISPATCH_B(bits, DEC_CALL)
 #undef DEC_CALL
 }
+// The lane's 32 "ids" of an aggregation / group column: dict ids, or for a raw (no-dictionary) column the doc ids
+// themselves -- its value array takes the dictionary's place (DevColumn::dict), so every gather serves both.
+FI void column_ids(int kind, int bits, const uint32_t* region, const uint32_t* fwd, int tile_in_seg,
+                   uint32_t (&ids)[32]) {
+  if (kind == PGPU_COL_RAW) {
+    const uint32_t d0 = (uint32_t)tile_in_seg * WT + 32u * (uint32_t)lane_id();
+#pragma unroll
+    for (int i = 0; i < 32; ++i) ids[i] = d0 + (uint32_t)i;
+    return;
+  }
+  decode_ids(bits, region, fwd, tile_in_seg, ids);
+}
 
 // ---- predicates -----------------------------------------------------------------------------------------------
 #define PRED_RANGE 0
@@ -478,6 +490,11 @@ struct ColRef {
 };
 template <int N>
 FI void gather_ids(const ColRef& c, const int32_t (&d)[N], uint32_t (&id)[N]) {
+  if (c.kind == PGPU_COL_RAW) {  // the value array is indexed by doc id
+#pragma unroll
+    for (int u = 0; u < N; ++u) id[u] = (uint32_t)d[u];
+    return;
+  }
   if (c.kind == PGPU_COL_SORTED) {
 #pragma unroll
     for (int u = 0; u < N; ++u) id[u] = sorted_dict_id(c.sorted, c.card, d[u]);
@@ -957,11 +974,11 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
       const DevInstr* in = p.instrs + ss.prog_begin + cld(&sg->fast_ins[j]);
       ss.f_bits[j] = cld(&in->bits);
       ss.f_off[j] = cld(&in->stage_off);
-      ss.f_kind[j] = cld(&in->pred);
+      ss.f_kind[j] = cld(&in->pred) | (cld(&in->nostat) ? 0x100 : 0);
       ss.f_neg[j] = cld(&in->negate);
       const int32_t lo = cld(&in->lo), hi = cld(&in->hi);
       ss.f_lo[j] = (uint32_t)lo;
-      ss.f_span[j] = ss.f_kind[j] == PRED_MASK ? (uint32_t)hi : (uint32_t)(hi - lo);
+      ss.f_span[j] = (ss.f_kind[j] & 0xFF) == PRED_MASK ? (uint32_t)hi : (uint32_t)(hi - lo);
     }
   }
 }
@@ -1040,6 +1057,17 @@ FI uint32_t leaf_inv(const DevParams& p, const DocCtx& t, const DevInstr& in, ui
   }
   return in.negate ? ~m : m;
 }
+// precomputed match bits (raw-value leaves): the lane's 32 docs are one word of the segment's bitmap
+FI uint32_t leaf_bits(const TileCtx& t, const DevInstr& in) { return gld(in.fwd, (size_t)(t.doc0 >> 5) + lane_id()); }
+FI uint32_t leaf_bits(const DocCtx& t, const DevInstr& in) {
+  uint32_t w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) w[u] = gld(in.fwd, (size_t)(t.doc[u] >> 5));
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) m |= ((w[u] >> (t.doc[u] & 31)) & 1u) << u;
+  return m;
+}
 FI uint32_t leaf_sorted(const DevParams& p, const TileCtx& t, const DevInstr& in) {
   const uint32_t m = sorted_ranges_word(p.pool + in.pool_off, in.n, t.doc0);
   return in.negate ? ~m : m;
@@ -1077,8 +1105,16 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
           m = sgpr(m) == 0xdeadbeefu ? m + 1 : m;  // force completion before the timestamp
           PROF_ADD(pf, PGPU_P_C_DECODE, tde);
         }
-        if (lane_id() == 0) scanned += n;
+        if (lane_id() == 0 && !in.nostat) scanned += n;
         mrow(cv, in.dst) = m;
+        break;
+      }
+      case PGPU_I_BITS: {
+        if (!in.nostat) {
+          const int n = wave_sum_i32(__popc(care));
+          if (lane_id() == 0) scanned += n;
+        }
+        mrow(cv, in.dst) = leaf_bits(t, in) & care;
         break;
       }
       case PGPU_I_INV: mrow(cv, in.dst) = leaf_inv(p, t, in, scratch) & t.valid; break;
@@ -1146,10 +1182,11 @@ FI uint32_t fast_filter(const SegState& ss, const TileCtx& t, uint32_t& lane_sca
 #pragma unroll 1
   for (int j = 0; j < ss.fast; ++j) {
     if (j > 0 && __builtin_amdgcn_ballot_w64(m != 0) == 0) return 0u;
-    lane_scanned += __popc(m);
+    const int kind_ns = j ? ss.f_kind[1] : ss.f_kind[0];  // predicate kind | nostat << 8
+    if (!(kind_ns >> 8)) lane_scanned += __popc(m);
+    const int kind = kind_ns & 0xFF;
     const int bits = j ? ss.f_bits[1] : ss.f_bits[0];
     const int off = j ? ss.f_off[1] : ss.f_off[0];
-    const int kind = j ? ss.f_kind[1] : ss.f_kind[0];
     const uint32_t lo = j ? ss.f_lo[1] : ss.f_lo[0];
     const uint32_t span = j ? ss.f_span[1] : ss.f_span[0];
     const bool neg = (j ? ss.f_neg[1] : ss.f_neg[0]) != 0;
@@ -1329,7 +1366,7 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
     gather_ids(colref(c), doc, id);
 #pragma unroll
     for (int u = 0; u < U; ++u) id[u] = ((m >> u) & 1u) ? id[u] : 0u;
-    if (MODE == PGPU_MODE_AGG && (ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64)) {
+    if (MODE == PGPU_MODE_AGG && (ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64) && c.kind != PGPU_COL_RAW) {
       // sorted dictionary + order-preserving cell key: one value gather per lane, at the extreme live id
       const bool is_min = ag.op == PGPU_RED_MIN_I64;
       uint32_t best = is_min ? 0xFFFFFFFFu : 0u;
@@ -1420,8 +1457,9 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
           for (int a = 0; a < p.nagg; ++a) used |= p.aggs[a].fn != PGPU_AGG_COUNT && p.aggs[a].col == k;
           if (!used) continue;
           const DevColumn c = col_of(ss, k);
-          if (c.kind != PGPU_COL_FIXED_BIT) continue;
-          const uint32_t b = (uint32_t)c.bits;
+          if (c.kind != PGPU_COL_FIXED_BIT && c.kind != PGPU_COL_RAW) continue;
+          const uint32_t b = c.kind == PGPU_COL_RAW ? (c.dict_type == PGPU_INT || c.dict_type == PGPU_FLOAT ? 32u : 64u)
+                                                   : (uint32_t)c.bits;
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const bool live = (m >> u) & 1u;
@@ -1469,7 +1507,7 @@ FI void dense_agg_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const Se
     if (ag.fn == PGPU_AGG_COUNT) continue;
     const bool r0 = ag.col == ss.reg_col0;
     const DevColumn c = col_of(ss, ag.col);
-    if (ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64) {
+    if ((ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64) && c.kind != PGPU_COL_RAW) {
       // dictionaries are sorted ascending and the MIN / MAX cell key is order-preserving, so the extreme value
       // sits at the extreme dict id: reduce the ids in registers, then gather one value per lane
       const bool is_min = ag.op == PGPU_RED_MIN_I64;
@@ -1562,7 +1600,7 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
           for (int i = 0; i < 32; ++i) ids[i] = rb[i];
         } else {
           const DevColumn c = col_of(ss, col);
-          decode_ids(c.bits, staged_region(ss, t.slot, col), c.fwd, t.tile_in_seg, ids);
+          column_ids(c.kind, c.bits, staged_region(ss, t.slot, col), c.fwd, t.tile_in_seg, ids);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) lo[i] = h ? ids[16 + i] : ids[i];
@@ -1790,7 +1828,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
         const int col = j == 0 ? ss.reg_col0 : ss.reg_col1;
         const DevColumn c = col_of(ss, col);
         uint32_t ids[32];
-        decode_ids(c.bits, staged_region(ss, slot, col), c.fwd, t.tile_in_seg, ids);
+        column_ids(c.kind, c.bits, staged_region(ss, slot, col), c.fwd, t.tile_in_seg, ids);
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
           if (j == 0) ra[i] = ids[i];
@@ -1883,13 +1921,20 @@ FI void glds16_asm(uint32_t voff, const void* sbase, uint32_t lds_dst) {
                : "=&s"(keep)
                : "v"(voff), "s"(sbase), "s"(lds_dst));
 }
+// Non-temporal form (PGPU_FLAG_NT): once-read tile bytes need not stay in L2 (MI355X_MICROARCH.md nt-weights).
+FI void glds16_asm_nt(uint32_t voff, const void* sbase, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst));
+}
 FI const void* uniform_ptr(const void* p) {
   const uint64_t v = (uint64_t)p;
   const uint32_t lo = (uint32_t)sgpr((int)(uint32_t)v), hi = (uint32_t)sgpr((int)(uint32_t)(v >> 32));
   return (const void*)(((uint64_t)hi << 32) | lo);
 }
 // The tile's staged (bit-sliced, linear) regions into `slot`: 16 B per lane, 1 KiB per instruction.
-FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* slot, uint32_t voff16) {
+FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* slot, uint32_t voff16, bool nt) {
   const int lane = lane_id();
 #pragma unroll
   for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
@@ -1899,7 +1944,10 @@ FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* 
     const uint32_t dst = sgpr((int)lds_off(slot + sc.off[j]));
     const int ninstr = (b + 3) >> 2;
     for (int k = 0; k < ninstr; ++k) {
-      if (64 * k + lane < 16 * b) glds16_asm(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
+      if (64 * k + lane < 16 * b) {
+        if (nt) glds16_asm_nt(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
+        else glds16_asm(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
+      }
     }
   }
 }
@@ -1944,7 +1992,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
     for (int k = 0; k < own; ++k) {
       while (issued < own && issued < k + D) {
         if (issued > 0 && cursor_advance(p, ci, NW)) load_stage(p, ci.seg, sc);
-        issue_tile_direct(sc, ci.tile_in_seg, slots + (size_t)islot * S, voff16);
+        issue_tile_direct(sc, ci.tile_in_seg, slots + (size_t)islot * S, voff16, (p.flags & PGPU_FLAG_NT) != 0);
         ++issued;
         if (++islot == D) islot = 0;
       }
@@ -2388,7 +2436,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
           const DevColumn c = col_of(ss, p.gcols[g]);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
           uint32_t ids[32];
-          decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, ids);
+          column_ids(c.kind, c.bits, nullptr, c.fwd, t.tile_in_seg, ids);
           const int32_t* remap = cld(ss.remaps, g);
           if (remap) {
 #pragma unroll
@@ -2406,7 +2454,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
         if (p.pcol >= 0) {
           const DevColumn c = col_of(ss, p.pcol);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
-          decode_ids(c.bits, nullptr, c.fwd, t.tile_in_seg, val);
+          column_ids(c.kind, c.bits, nullptr, c.fwd, t.tile_in_seg, val);
           if (!idbits) {
 #pragma unroll
             for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
@@ -2804,6 +2852,7 @@ __global__ __launch_bounds__(256) void leafbits_kernel(DevParams p) {
     if (in.op == PGPU_I_SCAN) m = leaf_scan(p, t, in, t.valid, dummy);
     else if (in.op == PGPU_I_INV) m = leaf_inv(p, t, in, scratch[wave]) & t.valid;
     else if (in.op == PGPU_I_SORTED) m = leaf_sorted(p, t, in) & t.valid;
+    else if (in.op == PGPU_I_BITS) m = leaf_bits(t, in) & t.valid;
     p.leaf_bits[off + (int64_t)k * c.ntiles * 64 + (int64_t)c.tile_in_seg * 64 + lane] = m;
   }
 }
@@ -3039,6 +3088,87 @@ __global__ __launch_bounds__(256) void bitslice_kernel(const uint32_t* fwd, uint
 #define BS_CALL(B) bitslice_b<B>(fwd, out, tile, lane)
   PGPU_DISPATCH_B(bits, BS_CALL)
 #undef BS_CALL
+}
+
+// ---- raw-value filter leaves ---------------------------------------------------------------------------------------
+// Predicate of a leaf over a raw (no-dictionary) column, exactly as the reference's raw-value evaluators apply it
+// per doc: Int/Long/Float/DoubleRawValueBasedRangePredicateEvaluator.applySV (RangePredicateEvaluatorFactory.java:
+// 273-460: inclusive / exclusive bounds, unbounded = the type's extreme, inclusive), the raw EQ / NOT_EQ evaluators
+// (EqualsPredicateEvaluatorFactory / NotEqualsPredicateEvaluatorFactory: primitive ==) and the raw IN / NOT_IN sets
+// (InPredicateEvaluatorFactory / NotInPredicateEvaluatorFactory: fastutil open hash sets, i.e. float / double
+// members compared by their bits -- here by the order-preserving key of the value, a bijection of the bits).
+FI bool raw_set_has(const int64_t* vals, int n, int64_t k) {
+  int a = 0, z = n - 1;
+  while (a <= z) {
+    const int m = (a + z) >> 1;
+    const int64_t v = gld(vals, (size_t)m);
+    if (v == k) return true;
+    if (v < k) a = m + 1; else z = m - 1;
+  }
+  return false;
+}
+FI bool raw_match(const RawLeaf& L, uint64_t bits) {
+  bool r;
+  if (L.vtype == PGPU_INT || L.vtype == PGPU_LONG) {
+    const int64_t x = L.vtype == PGPU_INT ? (int64_t)(int32_t)(uint32_t)bits : (int64_t)bits;
+    if (L.pred == PGPU_PRED_RANGE)
+      r = ((L.flags & PGPU_RAW_RANGE_LO_INCL) ? x >= L.lo : x > L.lo) && ((L.flags & PGPU_RAW_RANGE_HI_INCL) ? x <= L.hi : x < L.hi);
+    else
+      r = raw_set_has(L.vals, L.nvals, x);
+  } else {
+    double x = L.vtype == PGPU_FLOAT ? (double)__uint_as_float((uint32_t)bits) : __longlong_as_double((int64_t)bits);
+    if (L.pred == PGPU_PRED_RANGE) {
+      if ((L.flags & PGPU_RAW_RANGE_ORDINAL) && x != x) x = -__builtin_inf();  // FPOrdering.ordinalOf(NaN) = 0
+      const double lo = __longlong_as_double(L.lo), hi = __longlong_as_double(L.hi);
+      r = ((L.flags & PGPU_RAW_RANGE_LO_INCL) ? lo <= x : lo < x) && ((L.flags & PGPU_RAW_RANGE_HI_INCL) ? hi >= x : hi > x);
+    } else {
+      r = raw_set_has(L.vals, L.nvals, key_of_double(x));
+    }
+  }
+  return r != (L.negate != 0);
+}
+// One wave per 1024 docs of leaf blockIdx.y: 16 coalesced value loads per lane in flight, one ballot per 64 docs,
+// lanes 0..31 write the chunk's 32 match words (docs past num_docs never match).  An HBM streaming kernel: 4 or 8
+// bytes read per doc, 1 bit written.
+template <int W>
+__device__ void rawpred_wave(const RawLeaf& L, int64_t c, int lane) {
+  constexpr int NU = 16;
+  const int64_t d0 = c * 1024;
+  uint64_t v[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const size_t d = (size_t)(d0 + u * 64 + lane);
+    v[u] = W == 4 ? (uint64_t)gld((const uint32_t*)L.values, d) : (uint64_t)gld((const uint64_t*)L.values, d);
+  }
+  uint64_t bal[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const bool live = d0 + u * 64 + lane < L.num_docs;
+    bal[u] = __builtin_amdgcn_ballot_w64(live && raw_match(L, v[u]));
+  }
+  if (lane < 32) {
+    uint64_t b = 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) b = (lane >> 1) == u ? bal[u] : b;
+    L.out[c * 32 + lane] = (uint32_t)(b >> (32 * (lane & 1)));
+  }
+}
+__global__ __launch_bounds__(256) void rawpred_kernel(const RawLeaf* leaves) {
+  const RawLeaf L = cld(leaves + blockIdx.y);
+  const int lane = threadIdx.x & 63;
+  const int64_t nchunks = L.words / 32;
+  const bool w4 = L.vtype == PGPU_INT || L.vtype == PGPU_FLOAT;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunks; c += (int64_t)gridDim.x * 4) {
+    if (w4) rawpred_wave<4>(L, c, lane);
+    else rawpred_wave<8>(L, c, lane);
+  }
+}
+
+hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {
+  if (nleaves <= 0) return hipSuccess;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (max_words / 32 + 3) / 4));
+  hipLaunchKernelGGL(rawpred_kernel, dim3((unsigned)blocks, (unsigned)nleaves), dim3(256), 0, st, dev_leaves);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st) {

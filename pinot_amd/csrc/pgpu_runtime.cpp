@@ -50,6 +50,10 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
                                   int num_leaves, int32_t num_docs);
 bool pgpu_filter_count_is_reference(const pgpu_filter_node* nodes, int num_nodes);
+// pgpu_rawfwd.cpp
+int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t num_docs, std::vector<uint8_t>* out,
+                            std::string* err);
+hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 
 namespace {
 
@@ -156,8 +160,10 @@ struct Workspace {
   DevMem pcount, pcap, poff, p2work;   // PART region sizing / phase-2 plan (part_plan_kernel)
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
+  DevMem rawbits;                      // match bitmaps of the raw-value leaves (rawpred_kernel)
   PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
   DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
+  PinnedMem h_cancel;                  // its source for pgpu_query_cancel's copy-engine write
   uint32_t cancel_gen = 0;
   bool busy = false;
   ~Workspace() {
@@ -209,7 +215,8 @@ struct HostColumn {
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
-  double max_abs = 0;                  // numeric dictionary: largest |value| (integer SUM overflow bound)
+  double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
+  int32_t range_index = 0;             // range index version (2 = exact bit-sliced, 1 = legacy), 0 = none
   uint64_t dict_hash[2] = {0, 0};      // two independent 64-bit hashes of the dictionary bytes (shared-dict checks)
 };
 
@@ -523,7 +530,8 @@ int pgpu_segment_add_forward_index(pgpu_segment* seg, int32_t column, const void
     return fail(PGPU_E_INVALID, "forward index of column %d: %llu bytes < %llu needed", column,
                 (unsigned long long)num_bytes, (unsigned long long)need);
   HostColumn& c = seg->cols[column];
-  if (c.kind == PGPU_COL_SORTED) return fail(PGPU_E_INVALID, "column %d already has a sorted index", column);
+  if (c.kind == PGPU_COL_SORTED || c.kind == PGPU_COL_RAW)
+    return fail(PGPU_E_INVALID, "column %d already has a forward index", column);
   const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
   const uint64_t alloc = std::max<uint64_t>(ntiles * PGPU_TILE / 8 * bits_per_value, need) + 16;
   HIP_TRY(hipSetDevice(seg->ctx->device));
@@ -573,6 +581,7 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
     return fail(PGPU_E_INVALID, "dictionary of column %d: bad type %d / cardinality %d", column, data_type,
                 cardinality);
   HostColumn& c = seg->cols[column];
+  if (c.kind == PGPU_COL_RAW) return fail(PGPU_E_INVALID, "column %d is a raw (no-dictionary) column", column);
   c.dict_type = data_type;
   c.dict_card = cardinality;
   if (data_type == PGPU_STRING) return PGPU_OK;
@@ -626,6 +635,54 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
   c.dict_hash[1] = h2;
   c.hdict = std::move(le);
   c.max_abs = max_abs;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_t data_type, const void* bytes,
+                                       uint64_t num_bytes) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (data_type < PGPU_INT || data_type > PGPU_DOUBLE)
+    return fail(PGPU_E_UNSUPPORTED, "raw forward index of column %d: type %d is not fixed-width numeric", column, data_type);
+  HostColumn& c = seg->cols[column];
+  if (c.kind != PGPU_COL_NONE || c.dict_card)
+    return fail(PGPU_E_INVALID, "column %d already has a forward index or dictionary", column);
+  if (!bytes) return fail(PGPU_E_INVALID, "null raw forward index");
+  const int w = type_width(data_type);
+  std::vector<uint8_t> le;
+  std::string err;
+  rc = pgpu_decode_raw_forward((const uint8_t*)bytes, num_bytes, w, seg->num_docs, &le, &err);
+  if (rc) return fail(rc, "raw forward index of column %d: %s", column, err.c_str());
+  double max_abs = 0;
+  if (data_type == PGPU_INT || data_type == PGPU_LONG)
+    for (int32_t i = 0; i < seg->num_docs; ++i) {
+      int64_t v;
+      if (w == 4) { int32_t x; memcpy(&x, &le[4 * (size_t)i], 4); v = x; }
+      else memcpy(&v, &le[8 * (size_t)i], 8);
+      max_abs = std::max(max_abs, std::fabs((double)v));
+    }
+  // padded to whole PGPU_TILE-doc tiles (+16 B) like a fixed-bit stream: the kernels read whole tiles of "ids"
+  const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
+  const uint64_t alloc = std::max<uint64_t>(1, ntiles) * PGPU_TILE * w + 16;
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.dict, le.data(), le.size(), alloc, PGPU_MEM_HOST));
+  c.kind = PGPU_COL_RAW;
+  c.dict_type = data_type;
+  c.fwd_card = seg->num_docs;
+  c.fwd_bytes = num_bytes;
+  c.dict_bytes = le.size();
+  c.max_abs = max_abs;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_range_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (!bytes || num_bytes < 4) return fail(PGPU_E_INVALID, "range index of column %d: %llu bytes", column,
+                                           (unsigned long long)num_bytes);
+  const int32_t version = (int32_t)be32((const uint8_t*)bytes);
+  if (version != 1 && version != 2) return fail(PGPU_E_INVALID, "range index of column %d: version %d", column, version);
+  seg->cols[column].range_index = version;
   return PGPU_OK;
 }
 
@@ -843,7 +900,82 @@ struct Packer {
   double est_matched = 0;   // estimated matched docs (LDS-table decision)
   std::vector<int32_t> tracked;  // HASH: query segments whose distinct keys are counted (bitmap row order)
   int64_t leaf_words = 0;        // PGPU_Q_EXACT_FILTER_STATS: 32-bit words of all leaf bitmaps
+  // raw-value leaves: until launch, RawLeaf::out holds the bitmap's word offset in Workspace::rawbits and
+  // RawLeaf::vals its set's offset in rawvals; PGPU_I_BITS instructions (bits_instrs) hold the word offset in fwd
+  std::vector<RawLeaf> raws;
+  std::vector<int64_t> rawvals;
+  int64_t raw_words = 0;
+  std::vector<int> bits_instrs;
+  bool legacy_range = false;     // a version-1 range-index leaf: the GPU's filter count is not the reference's
 };
+
+// The bitmap word offset of a raw-value leaf (rawpred_kernel output), shared by identical leaves of one segment
+// (the exact-statistics pass converts every program a second time).
+int64_t raw_leaf(Packer& pk, const pgpu_segment* seg, const HostColumn& hc, const DevColumn& dc,
+                 const pgpu_filter_node& nd, bool range_index, int* rc) {
+  *rc = PGPU_OK;
+  RawLeaf L{};
+  L.values = dc.dict;
+  L.num_docs = seg->num_docs;
+  L.words = (int32_t)(((int64_t)seg->num_docs + PGPU_WT - 1) / PGPU_WT * 64);
+  L.vtype = hc.dict_type;
+  L.pred = nd.pred;
+  L.negate = nd.negate ? 1 : 0;
+  const bool fp = hc.dict_type == PGPU_FLOAT || hc.dict_type == PGPU_DOUBLE;
+  if (!nd.values && !(nd.pred == PGPU_PRED_SET && nd.num_ids == 0)) {
+    *rc = fail(PGPU_E_INVALID, "raw-value leaf on column %d without values", nd.column);
+    return -1;
+  }
+  std::vector<int64_t> set;
+  if (nd.pred == PGPU_PRED_RANGE) {
+    if (range_index) {  // RangeIndexBasedFilterOperator: the evaluator's bounds, inclusive (ordinals for floats)
+      L.flags = PGPU_RAW_RANGE_LO_INCL | PGPU_RAW_RANGE_HI_INCL | (fp ? PGPU_RAW_RANGE_ORDINAL : 0);
+    } else {
+      L.flags = (nd.lo ? PGPU_RAW_RANGE_LO_INCL : 0) | (nd.hi ? PGPU_RAW_RANGE_HI_INCL : 0);
+    }
+    int64_t b[2];
+    memcpy(b, nd.values, 16);
+    if (fp && range_index)
+      for (int k = 0; k < 2; ++k) {
+        double d;
+        memcpy(&d, &b[k], 8);
+        if (d != d) d = -INFINITY;
+        memcpy(&b[k], &d, 8);
+      }
+    L.lo = b[0];
+    L.hi = b[1];
+  } else if (nd.pred == PGPU_PRED_SET) {
+    if (nd.num_ids < 0) {
+      *rc = fail(PGPU_E_INVALID, "raw SET of %d values", nd.num_ids);
+      return -1;
+    }
+    set.resize(nd.num_ids);
+    if (nd.num_ids) memcpy(set.data(), nd.values, 8ull * nd.num_ids);
+    if (fp)  // members compare by the order-preserving key of their bits (a bijection: fastutil set semantics)
+      for (int64_t& k : set) k = k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
+    std::sort(set.begin(), set.end());
+    set.erase(std::unique(set.begin(), set.end()), set.end());
+    L.nvals = (int32_t)set.size();
+  } else {
+    *rc = fail(PGPU_E_INVALID, "raw-value predicate kind %d", nd.pred);
+    return -1;
+  }
+  for (size_t i = 0; i < pk.raws.size(); ++i) {
+    const RawLeaf& o = pk.raws[i];
+    if (o.values != L.values || o.pred != L.pred || o.negate != L.negate || o.flags != L.flags || o.lo != L.lo ||
+        o.hi != L.hi || o.nvals != L.nvals)
+      continue;
+    const int64_t vo = (int64_t)(intptr_t)o.vals;
+    if (L.nvals && !std::equal(set.begin(), set.end(), pk.rawvals.begin() + vo)) continue;
+    return (int64_t)(intptr_t)o.out;
+  }
+  L.vals = (const int64_t*)(intptr_t)pk.rawvals.size();
+  pk.rawvals.insert(pk.rawvals.end(), set.begin(), set.end());
+  L.out = (uint32_t*)(intptr_t)pk.raw_words;
+  pk.raw_words += L.words;
+  pk.raws.push_back(L);
+  return (int64_t)(intptr_t)L.out;
+}
 
 // Convert one prefix-order filter program into slot-resolved device instructions appended to pk.instrs.
 int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_filter_node* nodes, int count,
@@ -948,6 +1080,44 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
           return fail(PGPU_E_INVALID, "predicate kind %d", nd.pred);
         }
         emit(in);
+        close_nots();
+        break;
+      }
+      case PGPU_F_RAW_SCAN:
+      case PGPU_F_RANGE_INDEX: {
+        const DevColumn* c;
+        int rc = col_of(nd.column, &c);
+        if (rc) return rc;
+        const HostColumn& hc = seg->cols[sp.column_map[nd.column]];
+        const bool ri = nd.op == PGPU_F_RANGE_INDEX;
+        if (ri && !hc.range_index) return fail(PGPU_E_INVALID, "RANGE_INDEX leaf on column %d without range index", nd.column);
+        if (ri && nd.pred != PGPU_PRED_RANGE) return fail(PGPU_E_INVALID, "RANGE_INDEX leaf with a non-RANGE predicate");
+        if (ri && hc.range_index == 1) pk.legacy_range = true;
+        const int32_t nostat = ri && hc.range_index == 2 ? 1 : 0;
+        if (c->kind != PGPU_COL_RAW) {
+          if (!ri) return fail(PGPU_E_INVALID, "RAW_SCAN on dictionary-encoded column %d", nd.column);
+          // range index of a dictionary column: its dict-id range evaluated like a scan leaf, counted as the index
+          pgpu_filter_node sn = nd;
+          sn.op = PGPU_F_SCAN;
+          rc = convert_filter(q, sp, &sn, 1, seg, pk);
+          if (rc) return rc;
+          // convert_filter appended one SCAN leaf writing slot 0 with valid-docs care: re-target it
+          DevInstr& li = pk.instrs.back();
+          li.dst = cur;
+          li.care = care;
+          li.nostat = nostat;
+          close_nots();
+          break;
+        }
+        const int64_t woff = raw_leaf(pk, seg, hc, *c, nd, ri, &rc);
+        if (rc) return rc;
+        in.op = PGPU_I_BITS;
+        in.kind = PGPU_COL_RAW;
+        in.negate = 0;  // folded into the bitmap
+        in.nostat = nostat;
+        in.fwd = (const uint32_t*)(intptr_t)woff;
+        const int idx = emit(in);
+        pk.bits_instrs.push_back(base + idx);
         close_nots();
         break;
       }
@@ -1077,6 +1247,15 @@ int analyze(const SegView& v, int i, double* sel, std::vector<int>* scans) {
   switch (x.op) {
     case PGPU_F_MATCH_ALL: *sel = 1.0; return i + 1;
     case PGPU_F_EMPTY: *sel = 0.0; return i + 1;
+    case PGPU_F_RAW_SCAN:
+    case PGPU_F_RANGE_INDEX:
+      if (!valid_col(x.column)) return -1;
+      if (v.dev(x.column)->kind == PGPU_COL_RAW) {  // a precomputed bitmap word per lane: never staged
+        *sel = 0.5;
+        return i + 1;
+      }
+      if (x.op == PGPU_F_RAW_SCAN) return -1;
+      [[fallthrough]];  // range index of a dictionary column: a dict-id range scan on the GPU
     case PGPU_F_SCAN: {
       if (!valid_col(x.column)) return -1;
       const double card = std::max(1, v.dev(x.column)->card);
@@ -1204,11 +1383,15 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   } else {
     // the hash group-by computes 64-bit keys and slots per doc in the candidate path only
     bool dense = p.mode != PGPU_MODE_HASH;
-    for (int qc : aggcols)
-      dense &= v.dev(qc)->kind == PGPU_COL_FIXED_BIT && sector_touch(rho, v.dev(qc)->bits) >= kDenseTouch;
+    for (int qc : aggcols) {
+      const DevColumn* dc = v.dev(qc);
+      const int b = dc->kind == PGPU_COL_RAW ? 8 * type_width(dc->dict_type) : dc->bits;
+      dense &= (dc->kind == PGPU_COL_FIXED_BIT || dc->kind == PGPU_COL_RAW) && sector_touch(rho, b) >= kDenseTouch;
+    }
     agg_mode = dense ? PGPU_AM_DENSE : PGPU_AM_SPARSE;
     if (dense)
-      for (int qc : aggcols) add_stage(qc);
+      for (int qc : aggcols)
+        if (v.dev(qc)->kind == PGPU_COL_FIXED_BIT) add_stage(qc);
   }
   auto fits = [&]() {
     int instrs = 0, bytes = 0;
@@ -1369,6 +1552,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   p.G = L.num_keys;
   p.flags = (q->flags & PGPU_Q_STATS) ? PGPU_FLAG_STATS : 0;
   if (profile_enabled()) p.flags |= PGPU_FLAG_PROFILE;
+  static const bool direct_nt = getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) != 0;
+  if (direct_nt) p.flags |= PGPU_FLAG_NT;
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
   uint64_t stride64 = 1;
@@ -1424,6 +1609,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     for (int g = 0; g < q->num_group_columns; ++g) {
       const DevColumn& c = pk.cols[ds.col_begin + p.gcols[g]];
       if (c.kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "segment %d: group column without forward index", s);
+      if (c.kind == PGPU_COL_RAW)  // NoDictionary*GroupKeyGenerator: a value-hash path the GPU does not run
+        return fail(PGPU_E_UNSUPPORTED, "segment %d: GROUP BY on a raw (no-dictionary) column", s);
       const pgpu_buffer* rb = sp.group_remap ? sp.group_remap[g] : nullptr;
       if (rb && rb->length < c.card) return fail(PGPU_E_INVALID, "segment %d: remap shorter than cardinality", s);
       if (!rb && c.card > q->group_cardinalities[g])
@@ -1453,7 +1640,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       ds.leaf_begin = (int32_t)pk.pool.size();
       for (int i = base; i < (int)pk.instrs.size(); ++i) {
         const int op = pk.instrs[i].op;
-        if (op == PGPU_I_SCAN || op == PGPU_I_INV || op == PGPU_I_SORTED) pk.pool.push_back(i);
+        if (op == PGPU_I_SCAN || op == PGPU_I_INV || op == PGPU_I_SORTED || op == PGPU_I_BITS) pk.pool.push_back(i);
       }
       ds.leaf_len = (int32_t)pk.pool.size() - ds.leaf_begin;
       pk.leaf_words += (int64_t)ds.leaf_len * ds.ntiles * 64;
@@ -1667,12 +1854,17 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     release_ws(ctx, ws);
     return code;
   };
-  // NULL stream: the context's query stream (queries run back to back; each has its own completion event)
-  if (!stream) {
+  // NULL stream: the context's query stream (queries run back to back; each has its own completion event).  The
+  // cancel stream is created here too, never in pgpu_query_cancel (stream creation may wait for the device).
+  {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!ctx->qstream) {
+    if (!stream && !ctx->qstream) {
       const hipError_t ce = hipStreamCreateWithFlags(&ctx->qstream, hipStreamNonBlocking);
       if (ce != hipSuccess) return bail(fail(PGPU_E_HIP, "query stream: %s", hipGetErrorString(ce)));
+    }
+    if (!ctx->cstream) {
+      const hipError_t ce = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking);
+      if (ce != hipSuccess) return bail(fail(PGPU_E_HIP, "cancel stream: %s", hipGetErrorString(ce)));
     }
   }
   hipStream_t st = stream ? (hipStream_t)stream : ctx->qstream;
@@ -1683,14 +1875,29 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_cols = align16(o_ins + pk.instrs.size() * sizeof(DevInstr));
   const size_t o_pool = align16(o_cols + pk.cols.size() * sizeof(DevColumn));
   const size_t o_rem = align16(o_pool + pk.pool.size() * 4);
-  const size_t total = align16(o_rem + pk.remaps.size() * sizeof(void*)) + 16;
+  const size_t o_raw = align16(o_rem + pk.remaps.size() * sizeof(void*));
+  const size_t o_rvals = align16(o_raw + pk.raws.size() * sizeof(RawLeaf));
+  const size_t total = align16(o_rvals + pk.rawvals.size() * 8) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total);
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
   if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
   if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS + 16);
-  if (e == hipSuccess) e = ws->d_cancel.ensure(16);
+  // the cancel copy's pinned source is allocated here, never in pgpu_query_cancel: an allocation there could wait
+  // for the device -- i.e. for the very kernel the cancel is meant to stop
+  if (e == hipSuccess) e = ws->h_cancel.ensure(16);
+  if (e == hipSuccess && !ws->d_cancel.p) {
+    // uncached device memory: the kernels' polls read HBM, so pgpu_query_cancel's copy-engine write (which bypasses
+    // the GPU's L2) is seen at the next poll
+    e = hipExtMallocWithFlags(&ws->d_cancel.p, 16, hipDeviceMallocUncached);
+    if (e == hipSuccess) {
+      ws->d_cancel.n = 16;
+      e = hipMemset(ws->d_cancel.p, 0, 16);
+    } else {
+      ws->d_cancel.p = nullptr;
+    }
+  }
   if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   if (p.mode == PGPU_MODE_PART) {
@@ -1749,6 +1956,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.recs = (uint32_t*)ws->recs.p;
     p.rcount = (uint32_t*)ws->rcount.p;
   }
+  if (pk.raw_words > 0) {
+    e = ws->rawbits.ensure(4ull * pk.raw_words);
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "raw-value leaf bitmaps: %s", hipGetErrorString(e)));
+  }
   if (pk.leaf_words > 0) {
     e = ws->leafbits.ensure(4ull * pk.leaf_words);
     if (e == hipSuccess) e = ws->h_leafbits.ensure(4ull * pk.leaf_words);
@@ -1766,12 +1977,23 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.segmask = p.segmask_rows ? (uint32_t*)ws->segmask.p : nullptr;
   }
   char* h = (char*)ws->h_arena.p;
+  char* d = (char*)ws->arena.p;
+  // raw-value leaves: offsets -> device pointers (bitmaps in the workspace, set values in the arena)
+  for (int idx : pk.bits_instrs)
+    pk.instrs[idx].fwd = (const uint32_t*)ws->rawbits.p + (intptr_t)pk.instrs[idx].fwd;
+  int64_t max_raw_words = 0;
+  for (RawLeaf& r : pk.raws) {
+    r.out = (uint32_t*)ws->rawbits.p + (intptr_t)r.out;
+    r.vals = (const int64_t*)(d + o_rvals) + (intptr_t)r.vals;
+    max_raw_words = std::max<int64_t>(max_raw_words, r.words);
+  }
+  memcpy(h + o_raw, pk.raws.data(), pk.raws.size() * sizeof(RawLeaf));
+  memcpy(h + o_rvals, pk.rawvals.data(), pk.rawvals.size() * 8);
   memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
   memcpy(h + o_ins, pk.instrs.data(), pk.instrs.size() * sizeof(DevInstr));
   memcpy(h + o_cols, pk.cols.data(), pk.cols.size() * sizeof(DevColumn));
   memcpy(h + o_pool, pk.pool.data(), pk.pool.size() * 4);
   memcpy(h + o_rem, pk.remaps.data(), pk.remaps.size() * sizeof(void*));
-  char* d = (char*)ws->arena.p;
   p.segs = (const DevSeg*)(d + o_segs);
   p.instrs = (const DevInstr*)(d + o_ins);
   p.cols = (const DevColumn*)(d + o_cols);
@@ -1797,6 +2019,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
+  // raw-value leaves' match bitmaps (timed with the query: they are part of its filter)
+  if (e == hipSuccess && !pk.raws.empty())
+    e = pgpu_launch_rawpred((const RawLeaf*)(d + o_raw), (int)pk.raws.size(), max_raw_words, st);
   if (e == hipSuccess)
     e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
@@ -1838,7 +2063,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   bool exact = true;
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
-    exact = exact && pgpu_filter_count_is_reference(sp.filter, sp.num_filter_nodes);
+    exact = exact && !pk.legacy_range && pgpu_filter_count_is_reference(sp.filter, sp.num_filter_nodes);
     if (!qq->exact_filter) continue;
     pgpu_query::FilterReplay r;
     r.nodes.assign(sp.filter, sp.filter + sp.num_filter_nodes);
@@ -1876,7 +2101,11 @@ static int signal_cancel(pgpu_query* qq) {
     if (!qq->ctx->cstream) HIP_TRY(hipStreamCreateWithFlags(&qq->ctx->cstream, hipStreamNonBlocking));
     cs = qq->ctx->cstream;
   }
-  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)qq->params.cancel, (int)qq->params.cancel_gen, 1, cs));
+  // A copy-engine (SDMA) write from pinned host memory: it lands while the query kernel holds every CU, where a
+  // memset -- a blit kernel -- would only run after the kernel it is meant to stop.
+  if (!qq->ws->h_cancel.p) return fail(PGPU_E_INVALID, "query has no cancel word");
+  __atomic_store_n((volatile uint32_t*)qq->ws->h_cancel.p, qq->params.cancel_gen, __ATOMIC_SEQ_CST);
+  HIP_TRY(hipMemcpyAsync((void*)qq->params.cancel, qq->ws->h_cancel.p, 4, hipMemcpyHostToDevice, cs));
   return PGPU_OK;
 }
 

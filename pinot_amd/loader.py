@@ -44,7 +44,7 @@ LEGACY_PAD = "%"
 _STORED_TYPE = {"INT": PGPU_INT, "BOOLEAN": PGPU_INT, "LONG": PGPU_LONG, "TIMESTAMP": PGPU_LONG,
                 "FLOAT": PGPU_FLOAT, "DOUBLE": PGPU_DOUBLE, "STRING": PGPU_STRING}
 _V1_EXT = {"dictionary": ".dict", "forward_unsorted": ".sv.unsorted.fwd", "forward_sorted": ".sv.sorted.fwd",
-           "inverted_index": ".bitmap.inv"}
+           "forward_raw": ".sv.raw.fwd", "inverted_index": ".bitmap.inv", "range_index": ".bitmap.range"}
 
 
 class UnsupportedSegmentError(ValueError):
@@ -247,11 +247,22 @@ def load_segment(path: str, columns: Optional[Iterable[str]] = None) -> SegmentD
         dtype_name = _col_meta(props, col, "dataType").upper()
         if dtype_name not in _STORED_TYPE:
             raise UnsupportedSegmentError(f"column {col}: data type {dtype_name} is not on the GPU path")
-        if _col_meta(props, col, "hasDictionary", "true").lower() != "true":
-            raise UnsupportedSegmentError(f"column {col}: raw (no-dictionary) forward index")
         if _col_meta(props, col, "isSingleValues", "true").lower() != "true":
             raise UnsupportedSegmentError(f"column {col}: multi-value column")
         dt = _STORED_TYPE[dtype_name]
+        if _col_meta(props, col, "hasDictionary", "true").lower() != "true":
+            # raw (no-dictionary) column: FixedByteChunkSVForwardIndexReader bytes, decoded in the library
+            if dt == PGPU_STRING:
+                raise UnsupportedSegmentError(f"column {col}: raw STRING (var-byte) forward index")
+            fwd = index_bytes(col, "forward_raw")
+            if fwd is None:
+                raise SegmentFormatError(f"column {col}: raw forward index not found")
+            c = ColumnIndexes(col, dt, card, raw_forward=fwd, range_index=index_bytes(col, "range_index"))
+            mn, mx = props.get(f"column.{col}.minValue"), props.get(f"column.{col}.maxValue")
+            if mn is not None and mx is not None:  # ColumnMetadataImpl min / max (the non-scan MIN / MAX)
+                c.min_value, c.max_value = float(mn), float(mx)
+            seg.columns[col] = c
+            continue
         is_sorted = _col_meta(props, col, "isSorted", "false").lower() == "true"
         bits = int(_col_meta(props, col, "bitsPerElement", num_bits_per_value(card - 1)))
         if not is_sorted and bits != num_bits_per_value(card - 1):
@@ -281,5 +292,6 @@ def load_segment(path: str, columns: Optional[Iterable[str]] = None) -> SegmentD
                 raise SegmentFormatError(f"column {col}: forward index missing or shorter than {need} bytes")
             c.forward = fwd
         c.inverted = index_bytes(col, "inverted_index")
+        c.range_index = index_bytes(col, "range_index")
         seg.columns[col] = c
     return seg

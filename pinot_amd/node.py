@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import QueryDesc, QueryStats, TableLayout
-from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, finish, key_words_out
+from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, check_group_columns, finish, key_words_out
 from .query import QueryContext
 from .segment import GpuContext, GpuSegment
 
@@ -62,6 +62,7 @@ class GpuNode:
         if len(segments_by_device) != len(self.contexts):
             raise ValueError("one segment list per device")
         everything = [s for segs in segments_by_device for s in segs]
+        check_group_columns(query, everything)
         globs = [union_dictionary(g, everything) for g in query.group_by]
         keep, descs = [], []
         for pm, segs in zip(self.planners, segments_by_device):

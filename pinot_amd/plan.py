@@ -38,7 +38,8 @@ from ._lib import (ExprNode, Literal, PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX
                    PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64,
                    PGPU_RED_SUM_I64, PGPU_STRING, Agg, FilterNode, QueryDesc, QueryStats, SegmentPlan, TableLayout,
                    UnsupportedPlanError)
-from .predicate import DictPredicateEvaluator, SortedDictionary, get_predicate_evaluator
+from .predicate import (DictPredicateEvaluator, RawPredicateEvaluator, SortedDictionary, get_predicate_evaluator,
+                        get_raw_predicate_evaluator)
 from .query import UNBOUNDED, FilterContext, QueryContext, split_filtered_aggregations
 from .segment import GpuContext, GpuSegment
 
@@ -51,10 +52,11 @@ DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY = 10_000
 # ---- physical filter operators (host-side tree) ---------------------------------------------------------------
 @dataclass
 class FilterOp:
-    kind: str                                 # EMPTY, ALL, SCAN, INV, SORTED, AND, OR, NOT
+    kind: str                                 # EMPTY, ALL, SCAN, INV, SORTED, RANGE_INDEX, RAW_SCAN, AND, OR, NOT
     children: List["FilterOp"] = field(default_factory=list)
     column: Optional[str] = None
     evaluator: Optional[DictPredicateEvaluator] = None
+    raw: Optional[RawPredicateEvaluator] = None   # RAW_SCAN / RANGE_INDEX over a raw (no-dictionary) column
     doc_ranges: Optional[List[Tuple[int, int]]] = None
     negate: bool = False
 
@@ -64,13 +66,15 @@ class FilterOp:
             return 0
         if self.kind == "INV":
             return 1
+        if self.kind == "RANGE_INDEX":
+            return 2
         if self.kind == "AND":
             return 3
         if self.kind == "OR":
             return 4
         if self.kind == "NOT":
             return self.children[0].priority()
-        return 5  # SCAN
+        return 5  # SCAN / RAW_SCAN
 
 
 EMPTY = FilterOp("EMPTY")
@@ -128,6 +132,12 @@ class SegmentFilterPlanner:
 
     def _leaf(self, p) -> FilterOp:
         col = self.seg.column(p.column)
+        if col.is_raw:
+            # FilterOperatorUtils.getLeafFilterOperator (:42-81) without a dictionary: no always-true / -false
+            # folding, no sorted or inverted index; RANGE over a range index, else a raw-value scan
+            rv = get_raw_predicate_evaluator(p, col.data_type)
+            kind = "RANGE_INDEX" if p.type == "RANGE" and col.range_index is not None else "RAW_SCAN"
+            return FilterOp(kind, column=p.column, raw=rv)
         ev = get_predicate_evaluator(p, self.dictionary(p.column))
         if ev.always_false:
             return EMPTY
@@ -136,6 +146,8 @@ class SegmentFilterPlanner:
         if col.is_sorted:
             return FilterOp("SORTED", column=p.column, evaluator=ev,
                             doc_ranges=self._sorted_ranges(self.seg.sorted_pairs(p.column), ev))
+        if p.type == "RANGE" and col.range_index is not None:
+            return FilterOp("RANGE_INDEX", column=p.column, evaluator=ev)
         if p.type != "RANGE" and col.inverted is not None:
             return FilterOp("INV", column=p.column, evaluator=ev)
         return FilterOp("SCAN", column=p.column, evaluator=ev)
@@ -157,29 +169,58 @@ class SegmentFilterPlanner:
 
 # numpy images of the C structs (include/pinot_gpu.h; sizes checked against ctypes below), so a whole query's
 # per-segment programs are packed into a few buffers instead of thousands of ctypes objects
-NODE_DTYPE = np.dtype({"names": ["op", "column", "pred", "negate", "lo", "hi", "ids", "num_ids", "reserved"],
-                       "formats": ["<i4"] * 6 + ["<u8", "<i4", "<i4"],
-                       "offsets": [0, 4, 8, 12, 16, 20, 24, 32, 36], "itemsize": 40})
+NODE_DTYPE = np.dtype({"names": ["op", "column", "pred", "negate", "lo", "hi", "ids", "num_ids", "reserved",
+                                 "values"],
+                       "formats": ["<i4"] * 6 + ["<u8", "<i4", "<i4", "<u8"],
+                       "offsets": [0, 4, 8, 12, 16, 20, 24, 32, 36, 40], "itemsize": 48})
 PLAN_DTYPE = np.dtype({"names": ["segment", "column_map", "filter", "num_filter_nodes", "reserved", "group_remap"],
                        "formats": ["<u8", "<u8", "<u8", "<i4", "<i4", "<u8"],
                        "offsets": [0, 8, 16, 24, 28, 32], "itemsize": 40})
 assert NODE_DTYPE.itemsize == C.sizeof(FilterNode) and PLAN_DTYPE.itemsize == C.sizeof(SegmentPlan)
 
 
-def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list) -> None:
+def raw_node_values(rv: RawPredicateEvaluator) -> Tuple[int, int, int, List[int]]:
+    """(pred, lo flag, hi flag, 8-byte values as int64 bit patterns) of a raw-value leaf (include/pinot_gpu.h
+    PGPU_F_RAW_SCAN): int64 for INT / LONG columns, IEEE doubles for FLOAT / DOUBLE."""
+    def word(v) -> int:
+        if rv.is_floating:
+            return int(np.array([v], dtype=np.float64).view(np.int64)[0])
+        return int(v)
+    if rv.kind == "RANGE":
+        return (_lib.PGPU_PRED_RANGE, int(rv.lower_inclusive), int(rv.upper_inclusive),
+                [word(rv.lower), word(rv.upper)])
+    return _lib.PGPU_PRED_SET, 0, 0, [word(v) for v in rv.values]
+
+
+def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list, vals: list) -> None:
     """Append the prefix-order program of pgpu_filter_node as tuples (op, column, pred, negate, lo, hi, ids
-    offset, num_ids) to `nodes`; id lists go to the shared pool `ids` (offsets in int32 units)."""
+    offset, num_ids, values offset) to `nodes`; id lists go to the shared pool `ids` (offsets in int32 units),
+    raw-value leaves' values to `vals` (int64 bit patterns, offsets in 8-byte units)."""
     F = _lib
 
-    def pool(vals: Sequence[int]) -> int:
+    def pool(v: Sequence[int]) -> int:
         off = len(ids)
-        ids.extend(vals)
+        ids.extend(v)
+        return off
+
+    def vpool(v: Sequence[int]) -> int:
+        off = len(vals)
+        vals.extend(v)
         return off
 
     def rec(o: FilterOp):
         k = o.kind
         if k == "EMPTY" or k == "ALL":
             nodes.append((F.PGPU_F_EMPTY if k == "EMPTY" else F.PGPU_F_MATCH_ALL, 0, 0, 0, 0, 0, 0, 0))
+        elif (k == "RAW_SCAN" or k == "RANGE_INDEX") and o.raw is not None:
+            rv = o.raw
+            pred, lo, hi, words = raw_node_values(rv)
+            nodes.append((F.PGPU_F_RAW_SCAN if k == "RAW_SCAN" else F.PGPU_F_RANGE_INDEX, col_index[o.column], pred,
+                          1 if rv.is_exclusive else 0, lo, hi, 0, len(words) if pred == F.PGPU_PRED_SET else 0,
+                          vpool(words)))
+        elif k == "RANGE_INDEX":  # dictionary column: the dict-id range of the range index's exact answer
+            ev = o.evaluator
+            nodes.append((F.PGPU_F_RANGE_INDEX, col_index[o.column], F.PGPU_PRED_RANGE, 0, ev.start, ev.end, 0, 0))
         elif k == "SCAN":
             ev = o.evaluator
             neg = 1 if ev.is_exclusive else 0
@@ -217,6 +258,16 @@ def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list
             raise ValueError(k)
 
     rec(op)
+
+
+def check_group_columns(query: QueryContext, segments: Sequence[GpuSegment]) -> None:
+    """GROUP BY on a raw (no-dictionary) column is the reference's NoDictionary*GroupKeyGenerator (a value-hash
+    path): not run on the GPU."""
+    for g in query.group_by:
+        for s in segments:
+            if s.column(g).is_raw:
+                raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                           f"GROUP BY on raw (no-dictionary) column {g!r} of segment {s.name}")
 
 
 # ---- results ---------------------------------------------------------------------------------------------------
@@ -448,6 +499,8 @@ class GpuPlanMaker:
             p = fc.predicate
             if seg0.column(p.column).data_type == PGPU_STRING:
                 return False
+            if any(s.column(p.column).is_raw or s.column(p.column).range_index is not None for s in segments):
+                return False  # raw-value leaves / range-index leaves: planned per segment here
             kind = {"EQ": _lib.PGPU_P_EQ, "NOT_EQ": _lib.PGPU_P_NOT_EQ, "IN": _lib.PGPU_P_IN,
                     "NOT_IN": _lib.PGPU_P_NOT_IN, "RANGE": _lib.PGPU_P_RANGE}[p.type]
             if p.type == "RANGE":
@@ -485,9 +538,11 @@ class GpuPlanMaker:
         columns = query.columns
         col_index = {c: i for i, c in enumerate(columns)}
         nseg = len(segments)
+        check_group_columns(query, segments)
         globals_ = [self.global_dictionary(g, segments) for g in query.group_by]
         nodes: list = []
         ids: list = []
+        vals: list = []
         starts = []
         cmaps = []
         flt = query.filter if plan_filters else None
@@ -498,17 +553,19 @@ class GpuPlanMaker:
             if flt is not None:
                 op = SegmentFilterPlanner(seg).build(flt)
                 if op.kind != "ALL":
-                    emit_program(op, col_index, nodes, ids)
+                    emit_program(op, col_index, nodes, ids, vals)
         starts.append(len(nodes))
         cmap = np.array(cmaps, dtype=np.int32).reshape(nseg, max(1, len(columns)))
         pool = np.array(ids if ids else [0], dtype=np.int32)
+        vpool = np.array(vals if vals else [0], dtype=np.int64)
         narr = np.zeros(max(1, len(nodes)), dtype=NODE_DTYPE)
         if nodes:
-            t = np.array(nodes, dtype=np.int64)
+            t = np.array([nd if len(nd) == 9 else nd + (-1,) for nd in nodes], dtype=np.int64)
             for j, name in enumerate(("op", "column", "pred", "negate", "lo", "hi")):
                 narr[name] = t[:, j]
             narr["ids"] = pool.ctypes.data + 4 * t[:, 6]
             narr["num_ids"] = t[:, 7]
+            narr["values"] = np.where(t[:, 8] >= 0, vpool.ctypes.data + 8 * np.maximum(t[:, 8], 0), 0).astype(np.uint64)
         ng = len(query.group_by)
         remap = np.zeros((nseg, max(1, ng)), dtype=np.uint64)
         for g, (_, rms) in enumerate(globals_):
@@ -525,7 +582,7 @@ class GpuPlanMaker:
             *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
         gcols = (C.c_int32 * max(1, ng))(*[col_index[g] for g in query.group_by])
         gcards = (C.c_int32 * max(1, ng))(*[len(g[0]) for g in globals_])
-        keep = [cmap, pool, narr, remap, plans, aggs, gcols, gcards]
+        keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards]
         desc = QueryDesc(num_columns=len(columns), num_segments=nseg,
                          segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
                          num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
@@ -603,7 +660,9 @@ class GpuPlanMaker:
         if q.group_by or q.has_filtered_aggregations or any(a.function not in ("COUNT", "MIN", "MAX")
                                                             for a in q.aggregations):
             return [False] * len(segments)
-        return [s.num_docs > 0 and SegmentFilterPlanner(s).build(q.filter).kind == "ALL" for s in segments]
+        return [s.num_docs > 0 and SegmentFilterPlanner(s).build(q.filter).kind == "ALL" and
+                all(s.min_max(a.column) is not None for a in q.aggregations if a.function != "COUNT")
+                for s in segments]
 
 
 @dataclass
@@ -679,8 +738,8 @@ def merge_non_scan(query: QueryContext, scanned: Optional[QueryResult], segments
             if a.function == "COUNT":
                 v += s.num_docs
             else:
-                d = s.dictionaries[a.column]
-                v = min(v, float(d[0])) if a.function == "MIN" else max(v, float(d[-1]))
+                lo, hi = s.min_max(a.column)
+                v = min(v, lo) if a.function == "MIN" else max(v, hi)
         vals.append(v)
     st = res.stats
     for s in segments:

@@ -165,3 +165,88 @@ def get_predicate_evaluator(p: Predicate, dictionary: SortedDictionary) -> DictP
         return DictPredicateEvaluator(p, card, "RANGE", start=start, end=end, always_false=n <= 0,
                                       always_true=n == card)
     raise ValueError(f"unsupported predicate type {p.type}")
+
+
+# ---- raw (no-dictionary) columns --------------------------------------------------------------------------------
+_INT_RANGE = {PGPU_INT: (-(1 << 31), (1 << 31) - 1), PGPU_LONG: (-(1 << 63), (1 << 63) - 1)}
+
+
+def _java_parse_integral(value: str, data_type: int) -> int:
+    """Integer.parseInt / Long.parseLong: optional sign, decimal digits only, in range (NumberFormatException
+    otherwise, which fails the query in the reference)."""
+    s = value
+    body = s[1:] if s[:1] in "+-" else s
+    if not body or not body.isascii() or not body.isdigit():
+        raise ValueError(f"NumberFormatException: For input string: \"{value}\"")
+    v = int(s)
+    lo, hi = _INT_RANGE[data_type]
+    if not lo <= v <= hi:
+        raise ValueError(f"NumberFormatException: For input string: \"{value}\"")
+    return v
+
+
+def _java_parse_floating(value: str, data_type: int) -> float:
+    """Float.parseFloat / Double.parseDouble (surrounding whitespace trimmed; NaN / Infinity spelled as Java does)."""
+    s = value.strip()
+    t = s[1:] if s[:1] in "+-" else s
+    if t in ("NaN", "Infinity"):
+        v = float(s.replace("Infinity", "inf"))
+    elif any(ch.isalpha() and ch not in "eEdDfF" for ch in t) or not t:
+        raise ValueError(f"NumberFormatException: For input string: \"{value}\"")
+    else:
+        v = float(t.rstrip("dDfF")) * (-1.0 if s[:1] == "-" else 1.0)
+    return float(np.float32(v)) if data_type == PGPU_FLOAT else v
+
+
+def parse_raw_literal(value: str, data_type: int):
+    """The literal as the raw-value evaluators parse it for the column's stored type."""
+    if data_type in (PGPU_INT, PGPU_LONG):
+        return _java_parse_integral(value, data_type)
+    if data_type in (PGPU_FLOAT, PGPU_DOUBLE):
+        return _java_parse_floating(value, data_type)
+    raise ValueError(f"raw-value predicates on stored type {data_type} are not on this path")
+
+
+@dataclass
+class RawPredicateEvaluator:
+    """PredicateEvaluatorProvider's raw-value branch (core/operator/filter/predicate/PredicateEvaluatorProvider.java
+    :38-89) for INT / LONG / FLOAT / DOUBLE columns:
+      * RangePredicateEvaluatorFactory.newRawValueBasedEvaluator (:62-110): an unbounded side is the type's extreme,
+        inclusive (Integer.MIN_VALUE / Long.MAX_VALUE / Float.NEGATIVE_INFINITY ...);
+      * EqualsPredicateEvaluatorFactory / NotEqualsPredicateEvaluatorFactory raw evaluators: one parsed value;
+      * InPredicateEvaluatorFactory / NotInPredicateEvaluatorFactory raw evaluators: a set of parsed values.
+    A raw evaluator is never always-true / always-false (there is no dictionary to decide it on)."""
+
+    predicate: Predicate
+    data_type: int
+    kind: str                       # "RANGE" or "SET"
+    lower: Union[int, float] = 0    # RANGE bounds (with inclusive flags)
+    upper: Union[int, float] = 0
+    lower_inclusive: bool = True
+    upper_inclusive: bool = True
+    values: Sequence = ()           # SET members (EQ: one)
+
+    @property
+    def is_exclusive(self) -> bool:
+        return self.predicate.is_exclusive
+
+    @property
+    def is_floating(self) -> bool:
+        return self.data_type in (PGPU_FLOAT, PGPU_DOUBLE)
+
+
+def get_raw_predicate_evaluator(p: Predicate, data_type: int) -> RawPredicateEvaluator:
+    if p.type == "RANGE":
+        lu, uu = p.lower == UNBOUNDED, p.upper == UNBOUNDED
+        if data_type in (PGPU_INT, PGPU_LONG):
+            lo_ext, hi_ext = _INT_RANGE[data_type]
+        else:
+            lo_ext, hi_ext = float("-inf"), float("inf")
+        lo = lo_ext if lu else parse_raw_literal(p.lower, data_type)
+        hi = hi_ext if uu else parse_raw_literal(p.upper, data_type)
+        return RawPredicateEvaluator(p, data_type, "RANGE", lower=lo, upper=hi,
+                                     lower_inclusive=lu or p.lower_inclusive, upper_inclusive=uu or p.upper_inclusive)
+    if p.type in ("EQ", "NOT_EQ", "IN", "NOT_IN"):
+        vals = tuple(parse_raw_literal(v, data_type) for v in p.values)
+        return RawPredicateEvaluator(p, data_type, "SET", values=vals)
+    raise ValueError(f"unsupported predicate type {p.type}")

@@ -7,6 +7,8 @@
 * forward index   ``<col>.sv.unsorted.fwd``  fixed-bit, MSB-first (FixedBitSVForwardIndexReaderV2.java:62-96)
 * sorted index    ``<col>.sv.sorted.fwd``    (start, end) per dict id (SortedIndexReaderImpl.java:37-121)
 * inverted index  ``<col>.bitmap.inv``       offsets + Roaring bitmaps (BitmapInvertedIndexReader.java:45-61)
+* raw forward     ``<col>.sv.raw.fwd``       no-dictionary values in chunks (BaseChunkSVForwardIndexReader.java:56-101)
+* range index     ``<col>.bitmap.range``     only its version is used (BitSlicedRangeIndexReader.java:41-55)
 
 (file names: segspi/V1Constants.java:25-105).  ``GpuSegment`` copies them to HBM once
 (``pgpu_segment_add_*``), the analogue of an ``IndexingOverride`` wrapping ``newForwardIndexReader`` /
@@ -53,6 +55,20 @@ class ColumnIndexes:
     forward_device_bytes: int = 0
     pad_char: str = "\0"                    # STRING dictionaries: segment.padding.character (legacy '%')
     entry_width: int = 0                     # STRING dictionaries: lengthOfEachEntry (bytes per padded value)
+    raw_forward: Optional[bytes] = None      # no-dictionary column: the FixedByteChunkSVForwardIndexWriter file
+    range_index: Optional[bytes] = None      # `<col>.bitmap.range` (its header version decides the leaf's stats)
+    min_value: Optional[float] = None        # metadata min / max (raw columns: the non-scan MIN / MAX answer,
+    max_value: Optional[float] = None        # NonScanBasedAggregationOperator via DataSourceMetadata)
+
+    @property
+    def is_raw(self) -> bool:
+        return self.raw_forward is not None
+
+    @property
+    def range_index_version(self) -> int:
+        if self.range_index is None:
+            return 0
+        return int.from_bytes(self.range_index[:4], "big")
 
     @property
     def bits_per_value(self) -> int:
@@ -62,7 +78,9 @@ class ColumnIndexes:
     def is_sorted(self) -> bool:
         return self.sorted_index is not None
 
-    def dictionary_values(self) -> Union[np.ndarray, List[str]]:
+    def dictionary_values(self) -> Union[np.ndarray, List[str], None]:
+        if self.is_raw:
+            return None
         if self.data_type == PGPU_STRING:
             return list(self.dictionary)
         return np.frombuffer(self.dictionary, dtype=_BE_DTYPE[self.data_type]).astype(_NATIVE[self.data_type])
@@ -197,6 +215,12 @@ class GpuSegment:
         lib = self.ctx._lib
         seg = self.handle
         card = col.cardinality
+        if col.is_raw:
+            r = col.raw_forward
+            _lib.check(lib.pgpu_segment_add_raw_forward_index(seg, slot, col.data_type, r, len(r)))
+            if col.range_index is not None:
+                _lib.check(lib.pgpu_segment_add_range_index(seg, slot, col.range_index, len(col.range_index)))
+            return
         if col.data_type == PGPU_STRING:
             _lib.check(lib.pgpu_segment_add_dictionary(seg, slot, PGPU_STRING, None, 0, card))
         else:
@@ -216,6 +240,8 @@ class GpuSegment:
         if col.inverted is not None:
             inv = col.inverted
             _lib.check(lib.pgpu_segment_add_inverted_index(seg, slot, inv, len(inv), card))
+        if col.range_index is not None:
+            _lib.check(lib.pgpu_segment_add_range_index(seg, slot, col.range_index, len(col.range_index)))
 
     def column(self, name: str) -> ColumnIndexes:
         return self.data.column(name)
@@ -231,6 +257,17 @@ class GpuSegment:
                                  entry_width=col.entry_width)
             cache[name] = d
         return d
+
+    def min_max(self, name: str):
+        """(min, max) of a column as the non-scan plan reads them: the sorted dictionary's ends, or a raw column's
+        metadata min / max (None when the metadata has none: the segment is then scanned)."""
+        col = self.column(name)
+        if col.is_raw:
+            if col.min_value is None or col.max_value is None:
+                return None
+            return float(col.min_value), float(col.max_value)
+        d = self.dictionaries[name]
+        return float(d[0]), float(d[-1])
 
     def sorted_pairs(self, name: str) -> np.ndarray:
         cache = self.__dict__.setdefault("_sorted_pairs", {})

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_struct_sizes():
     lib = _lib.load()
     assert lib.pgpu_abi_version() == _lib.ABI_VERSION
-    assert C.sizeof(_lib.FilterNode) == 40
+    assert C.sizeof(_lib.FilterNode) == 48
     assert C.sizeof(_lib.Agg) == 8
     assert C.sizeof(_lib.QueryStats) == 64
 

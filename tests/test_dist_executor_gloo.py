@@ -74,6 +74,9 @@ class HostSegment:
     def sorted_pairs(self, name):
         return self._gs.sorted_pairs(self, name)
 
+    def min_max(self, name):
+        return self._gs.min_max(self, name)
+
 
 def _plan_maker():
     from pinot_amd.plan import GpuPlanMaker

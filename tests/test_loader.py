@@ -165,7 +165,8 @@ def test_unsupported_columns(tmp_path):
     meta = os.path.join(root, "metadata.properties")
     text = open(meta).read()
     open(meta, "w").write(text.replace("column.class.hasDictionary = true", "column.class.hasDictionary = false"))
-    with pytest.raises(UnsupportedSegmentError, match="raw"):
+    # a raw column is served now (tests/test_raw_columns.py); one whose .sv.raw.fwd file is missing is malformed
+    with pytest.raises(SegmentFormatError, match="raw forward index"):
         load_segment(str(tmp_path / "s"))
     assert set(load_segment(str(tmp_path / "s"), columns=["sorted"]).columns) == {"sorted"}
     open(meta, "w").write(text.replace("column.class.dataType = INT", "column.class.dataType = BYTES"))
