@@ -346,6 +346,38 @@ int pgpu_query_cancel(pgpu_query* query);
 int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
                        int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups);
 
+/* ---- ORDER BY ... LIMIT trim on the GPU ------------------------------------------------------------------------
+ * GroupByOrderByCombineOperator keeps an IndexedTable whose finish() hands the broker only the top
+ * trimSize = max(5 * limit, 5000) records by the first ORDER BY expression (GroupByUtils.getTableCapacity,
+ * core/util/GroupByUtils.java:24-41; TableResizer.getTopRecords, core/data/table/TableResizer.java; IndexedTable.finish,
+ * core/data/table/IndexedTable.java:135-156).  Here the non-empty groups of a (reduced) table are ranked on the GPU
+ * by one order key -- an aggregation's final value (extractFinalResult as a double: SUM, MIN, MAX, AVG = sum / count;
+ * COUNT as an integer) or a group column's value (its global dictionary id: global dictionaries are sorted) -- and
+ * the best k are compacted: every group whose key is at least as good as the k-th best's, so ties at the boundary are
+ * all kept and the caller's full ORDER BY ... LIMIT over the returned rows equals the one over the whole table.
+ * Radix select over 64-bit order keys (8 passes of 8 bits), no host round trip between passes. */
+#define PGPU_TOPK_AGG 0
+#define PGPU_TOPK_GROUP 1
+typedef struct {
+  int32_t source;                     /* PGPU_TOPK_AGG / PGPU_TOPK_GROUP */
+  int32_t agg_fn;                     /* AGG: PGPU_AGG_* of the aggregation */
+  int32_t agg_index;                  /* AGG: its index in the query (layout agg_section / agg_sum_parts / type) */
+  int32_t group_index;                /* GROUP: its position among the group columns */
+  int32_t descending;
+  int32_t num_group_columns;          /* GROUP: the query's group columns ... */
+  const int32_t* group_cardinalities; /* ... and global cardinalities (mixed-radix decode of the key) */
+  uint64_t k;                         /* keep the best k groups (ties with the k-th kept too); 0 = keep all */
+  uint64_t key_base;                  /* dense tables: global key of cell 0 (a reduce-scatter slice), else 0 */
+} pgpu_topk;
+
+/* pgpu_table_compact restricted to the best groups by `order` (out_num_groups = the rows returned). */
+int pgpu_table_topk(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
+                    const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
+                    uint64_t* out_num_groups);
+/* pgpu_query_collect returning only the best groups by `order` (NULL = all, as pgpu_query_collect). */
+int pgpu_query_collect_topk(pgpu_query* query, const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells,
+                            uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats);
+
 /* Single-GPU asynchronous form (the combine operator of one server: BaseCombineOperator.getNextBlock submits the
  * segments' work and blocks in mergeResults, core/operator/combine/BaseCombineOperator.java:79-146):
  *   pgpu_query_submit  packs the plan, enqueues the query on a context-owned stream with its own partial table

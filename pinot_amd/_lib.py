@@ -99,6 +99,15 @@ class QueryStats(C.Structure):
                 ("filter_stats_exact", C.c_int64)]
 
 
+PGPU_TOPK_AGG, PGPU_TOPK_GROUP = 0, 1
+
+
+class TopK(C.Structure):
+    _fields_ = [("source", C.c_int32), ("agg_fn", C.c_int32), ("agg_index", C.c_int32), ("group_index", C.c_int32),
+                ("descending", C.c_int32), ("num_group_columns", C.c_int32),
+                ("group_cardinalities", C.POINTER(C.c_int32)), ("k", C.c_uint64), ("key_base", C.c_uint64)]
+
+
 PGPU_X_PRED, PGPU_X_AND, PGPU_X_OR, PGPU_X_NOT = range(4)
 PGPU_P_EQ, PGPU_P_NOT_EQ, PGPU_P_IN, PGPU_P_NOT_IN, PGPU_P_RANGE = range(5)
 
@@ -141,6 +150,10 @@ SIGNATURES = [
     ("pgpu_query_cancel", C.c_int, [_P]),
     ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pgpu_table_topk", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(TopK), C.POINTER(C.c_int64),
+                                  C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pgpu_query_collect_topk", C.c_int, [_P, C.POINTER(TopK), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                          C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_query_submit", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(_P)]),
     ("pgpu_query_collect", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
                                      C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),

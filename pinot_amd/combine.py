@@ -31,8 +31,8 @@ import numpy as np
 from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
-from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, check_group_columns, GroupTable, QueryResult, finish, key_words_out,
-                   merge_filtered)
+from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
+                   key_words_out, merge_filtered, topk_spec)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
@@ -323,16 +323,22 @@ class DistributedExecutor:
                 "sparse_sector_bytes": st.sparse_sector_bytes, "dense_bytes": st.dense_bytes,
                 "kernel_ms": st.kernel_ms, "filter_stats_exact": st.filter_stats_exact}
 
-    def _compact(self, L: TableLayout, table):
+    def _compact(self, L: TableLayout, table, order=None):
+        """Non-empty rows of a device table (pgpu_table_compact), or only the best ones by `order` selected on the
+        GPU (pgpu_table_topk)."""
         cap = int(L.num_keys)
         kw = key_words_out(L)
         keys = np.empty(max(cap, 1) * kw, dtype=np.int64)
         cells = np.empty((max(cap, 1), L.num_sections), dtype=np.int64)
         ng = C.c_uint64()
-        _lib.check(self.pm.ctx._lib.pgpu_table_compact(
-            self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()), None,
-            keys.ctypes.data_as(C.POINTER(C.c_int64)), cells.ctypes.data_as(C.POINTER(C.c_int64)), cap,
-            C.byref(ng)))
+        kp, cp = keys.ctypes.data_as(C.POINTER(C.c_int64)), cells.ctypes.data_as(C.POINTER(C.c_int64))
+        if order is not None:
+            _lib.check(self.pm.ctx._lib.pgpu_table_topk(self.pm.ctx.handle, C.byref(L), C.c_void_p(table.data_ptr()),
+                                                        None, C.byref(order), kp, cp, cap, C.byref(ng)))
+        else:
+            _lib.check(self.pm.ctx._lib.pgpu_table_compact(self.pm.ctx.handle, C.byref(L),
+                                                           C.c_void_p(table.data_ptr()), None, kp, cp, cap,
+                                                           C.byref(ng)))
         n = ng.value
         return (keys[: n * kw].reshape(n, kw) if kw > 1 else keys[:n]), cells[:n]
 
@@ -509,7 +515,9 @@ class DistributedExecutor:
         CL = TableLayout()
         C.memmove(C.byref(CL), C.byref(L), C.sizeof(TableLayout))
         CL.num_keys = int(chunk.shape[1])
-        keys, cells = self._compact(CL, chunk.reshape(-1).contiguous())
+        # this rank's top max(5 * limit, 5000) of its key slice, selected on the GPU (ORDER BY), else on the host
+        order = topk_spec(query, [len(g) for g in p.globals_], max(5 * query.limit, self.TOPK_MIN), key_base=key0)
+        keys, cells = self._compact(CL, chunk.reshape(-1).contiguous(), order)
         keys, cells = self._trim(query, L, keys + key0, cells, p.globals_)
         return self._gather_rows(keys, cells, L)
 

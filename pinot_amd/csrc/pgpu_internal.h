@@ -18,6 +18,7 @@
 // sparse aggregation).  The loader's DMA queue never waits behind a consumer's gathers (separate waves, separate
 // vmcnt), which is what keeps enough bytes in flight per CU.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define PGPU_TILE 4096          // forward-index padding granularity in docs
@@ -307,7 +308,7 @@ struct DevParams {
   int32_t key_words;
   int32_t key_split;
   int32_t segmask_rows;
-  int32_t pad3;
+  int32_t cancel_poll;            // self-loading waves: tiles between cancel polls (PGPU_CANCEL_POLL, env override)
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
@@ -352,4 +353,130 @@ inline int pgpu_stage_region_bytes(int bits, bool sliced = false) {
 }
 inline int pgpu_stage_instrs(int bits, bool sliced = false) {
   return (bits % 8 == 0 && !sliced) ? bits / 4 + 1 : (bits + 3) / 4;
+}
+
+// ---- GPU ORDER BY ... LIMIT trim (pgpu_table_topk) ----------------------------------------------------------------
+// Order key of one table row, shared by the device selection (topk_* kernels) and the host path of small tables:
+// an unsigned 64-bit key, larger = better, whose order (and ties) equal the host's final-value ORDER BY order
+// (plan.py GroupColumns.order_and_limit): doubles of the final values (-0.0 folded into 0.0), integer counts,
+// group ids.  Every function compiles for both sides (this header is only included by hipcc-built files).
+#define PGPU_TK_COUNT 0
+#define PGPU_TK_SUM_I64 1
+#define PGPU_TK_SUM_SPLIT 2   // three 21-bit-part sections, exact as a 128-bit integer
+#define PGPU_TK_SUM_F64 3
+#define PGPU_TK_MINMAX_INT 4  // order-preserving cell = the integer value
+#define PGPU_TK_MINMAX_FP 5   // order-preserving cell = key of the double
+#define PGPU_TK_AVG_I64 6
+#define PGPU_TK_AVG_SPLIT 7
+#define PGPU_TK_AVG_F64 8
+#define PGPU_TK_GROUP 9
+struct TopkDev {
+  int32_t mode;
+  int32_t sec;       // first value section
+  int32_t desc;
+  int32_t word;      // GROUP, hash tables: key word (0 / 1) holding the column
+  uint64_t stride;   // GROUP: id = (word / stride) % card
+  uint64_t card;
+  uint64_t G;
+  int32_t nsec;
+  int32_t kw;        // 0 dense (cell index = key), 1 one hash key word, 2 two-level hash key
+  uint64_t key_base; // dense: key of cell 0
+};
+struct TopkState {  // radix-select state: the best-k threshold's high bits found so far
+  uint64_t prefix, mask, kleft;
+};
+
+__host__ __device__ inline uint64_t pgpu_tk_double(double d) {
+  d = d + 0.0;  // -0.0 -> 0.0: equal doubles, equal keys
+  int64_t b;
+  __builtin_memcpy(&b, &d, 8);
+  const int64_t k = b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
+  return (uint64_t)k ^ 0x8000000000000000ull;
+}
+// (hi:lo) two's-complement 128-bit integer -> nearest double (ties to even), via a 64-bit window with a sticky bit.
+__host__ __device__ inline double pgpu_i128_to_double(int64_t hi, uint64_t lo) {
+  const bool neg = hi < 0;
+  uint64_t h = (uint64_t)hi, l = lo;
+  if (neg) {  // negate
+    l = ~l + 1;
+    h = ~h + (l == 0 ? 1 : 0);
+  }
+  if (h == 0) return neg ? -(double)l : (double)l;
+  const int lz = __builtin_clzll(h);    // h != 0
+  const int shift = 64 - lz;            // bits of l below the 64-bit window (1..64)
+  uint64_t m;
+  if (shift == 64) {
+    m = h | (l != 0 ? 1u : 0u);
+  } else {
+    m = (h << lz) | (l >> shift);
+    if (l & ((1ull << shift) - 1)) m |= 1;  // sticky: > 11 guard bits remain below the 53-bit mantissa
+  }
+  double d = (double)m;
+  for (int i = 0; i < shift; ++i) d *= 2.0;  // exact scaling by 2^shift
+  return neg ? -d : d;
+}
+__host__ __device__ inline double pgpu_tk_split_sum(const int64_t* t, uint64_t G, int sec, uint64_t row) {
+  // c0 + c1 * 2^21 + c2 * 2^42 with 128-bit arithmetic (each part sum is a signed int64)
+  const int64_t c[3] = {t[(uint64_t)sec * G + row], t[(uint64_t)(sec + 1) * G + row], t[(uint64_t)(sec + 2) * G + row]};
+  int64_t hi = 0;
+  uint64_t lo = 0;
+  for (int p = 0; p < 3; ++p) {
+    const int sh = 21 * p;
+    const uint64_t vlo = sh ? ((uint64_t)c[p] << sh) : (uint64_t)c[p];
+    const int64_t vhi = sh ? (c[p] >> (64 - sh)) : (c[p] < 0 ? -1 : 0);
+    const uint64_t nlo = lo + vlo;
+    hi += vhi + (nlo < lo ? 1 : 0);
+    lo = nlo;
+  }
+  return pgpu_i128_to_double(hi, lo);
+}
+__host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDev& s, uint64_t row) {
+  const uint64_t G = s.G;
+  const int64_t cnt = t[row];
+  uint64_t u = 0;
+  switch (s.mode) {
+    case PGPU_TK_COUNT: u = (uint64_t)cnt ^ 0x8000000000000000ull; break;
+    case PGPU_TK_SUM_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row]); break;
+    case PGPU_TK_SUM_SPLIT: u = pgpu_tk_double(pgpu_tk_split_sum(t, G, s.sec, row)); break;
+    case PGPU_TK_SUM_F64: {
+      double d;
+      __builtin_memcpy(&d, &t[(uint64_t)s.sec * G + row], 8);
+      u = pgpu_tk_double(d);
+      break;
+    }
+    case PGPU_TK_MINMAX_INT: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row]); break;
+    case PGPU_TK_MINMAX_FP: {
+      const int64_t k = t[(uint64_t)s.sec * G + row];
+      const int64_t b = k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
+      double d;
+      __builtin_memcpy(&d, &b, 8);
+      u = pgpu_tk_double(d);
+      break;
+    }
+    case PGPU_TK_AVG_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row] / (double)cnt); break;
+    case PGPU_TK_AVG_SPLIT: u = pgpu_tk_double(pgpu_tk_split_sum(t, G, s.sec, row) / (double)cnt); break;
+    case PGPU_TK_AVG_F64: {
+      double d;
+      __builtin_memcpy(&d, &t[(uint64_t)s.sec * G + row], 8);
+      u = pgpu_tk_double(d / (double)cnt);
+      break;
+    }
+    default: {  // PGPU_TK_GROUP
+      uint64_t w;
+      if (s.kw == 0) {
+        w = s.key_base + row;
+      } else {
+        const int64_t* w0 = t + (uint64_t)s.nsec * G;
+        if (s.kw == 1) {
+          w = (uint64_t)w0[row];
+        } else {
+          const uint64_t c = (uint64_t)w0[row];
+          w = s.word == 0 ? (uint64_t)w0[G + (c >> 32)] : (c & 0xFFFFFFFFull);
+        }
+      }
+      u = (w / s.stride) % s.card;
+      break;
+    }
+  }
+  return s.desc ? u : ~u;  // best = largest key: the largest values (DESC) or the smallest (ASC)
 }

@@ -1987,6 +1987,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
     StageCache sc;
     load_stage(p, ci.seg, sc);
     int issued = 0, islot = 0, pslot = 0;
+    int poll = p.cancel_poll;
     uint32_t voff16;
     asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(voff16) : "v"(opaque_lane()));  // lane * 16, kept live
     for (int k = 0; k < own; ++k) {
@@ -1996,7 +1997,10 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
         ++issued;
         if (++islot == D) islot = 0;
       }
-      if (k % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p)) break;  // in-flight DMAs drain below
+      if (--poll == 0) {
+        poll = p.cancel_poll;
+        if (query_cancelled(p)) break;  // in-flight DMAs drain below
+      }
       const int next_instrs = (issued - k - 1) * p.min_instrs;  // lower bound of the DMAs issued after tile k
       if (k > 0) cursor_advance(p, cur, NW);
       if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES || cur.seg != cseg)) {
@@ -2880,12 +2884,19 @@ __global__ __launch_bounds__(256) void export_kernel(const int64_t* __restrict__
 #define CMP_BLOCK 256
 #define CMP_PER_BLOCK 4096
 
-__global__ void compact_count_kernel(const int64_t* table, uint64_t G, int32_t* block_counts) {
+// A row is kept when its count is > 0 and, under a top-k selection (okey != nullptr), its order key reaches the
+// selected threshold (TopkState::prefix after the last radix pass).
+__device__ inline bool cmp_keep(const int64_t* table, uint64_t G, uint64_t k, const uint64_t* okey,
+                                const TopkState* ts) {
+  return k < G && table[k] > 0 && (!okey || okey[k] >= ts->prefix);
+}
+__global__ void compact_count_kernel(const int64_t* table, uint64_t G, int32_t* block_counts, const uint64_t* okey,
+                                     const TopkState* ts) {
   const uint64_t base = (uint64_t)blockIdx.x * CMP_PER_BLOCK;
   int c = 0;
   for (int i = threadIdx.x; i < CMP_PER_BLOCK; i += CMP_BLOCK) {
     const uint64_t k = base + i;
-    if (k < G && table[k] > 0) ++c;
+    if (cmp_keep(table, G, k, okey, ts)) ++c;
   }
   c = wave_sum_i32(c);
   __shared__ int ws[CMP_BLOCK / 64];
@@ -2929,7 +2940,8 @@ __device__ inline void write_key(const int64_t* table, uint64_t G, int32_t nsec,
 }
 
 __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw,
-                                     const int32_t* block_offsets, int64_t* out_keys, int64_t* out_cells) {
+                                     const int32_t* block_offsets, int64_t* out_keys, int64_t* out_cells,
+                                     const uint64_t* okey, const TopkState* ts) {
   const uint64_t base = (uint64_t)blockIdx.x * CMP_PER_BLOCK;
   __shared__ int wbase[CMP_BLOCK / 64 + 1];
   __shared__ int running;
@@ -2938,7 +2950,7 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int i0 = 0; i0 < CMP_PER_BLOCK; i0 += CMP_BLOCK) {
     const uint64_t k = base + i0 + threadIdx.x;
-    const bool f = k < G && table[k] > 0;
+    const bool f = cmp_keep(table, G, k, okey, ts);
     const uint64_t bal = __ballot(f);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
     if (lane == 0) wbase[wave] = __popcll(bal);
@@ -3261,14 +3273,72 @@ hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_o
 
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, int32_t* block_counts,
                                int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only,
-                               hipStream_t st) {
+                               hipStream_t st, const uint64_t* okey, const TopkState* ts) {
   const int nb = (int)((G + CMP_PER_BLOCK - 1) / CMP_PER_BLOCK);
   if (count_only) {
-    hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, block_counts);
+    hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, block_counts, okey, ts);
     hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(64), 0, st, block_counts, nb, total);
   } else {
     hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(CMP_BLOCK), 0, st, table, G, nsec, kw, block_counts,
-                       out_keys, out_cells);
+                       out_keys, out_cells, okey, ts);
+  }
+  return hipGetLastError();
+}
+
+// ---- top-k selection (pgpu_table_topk): order keys, then 8 radix passes of 8 bits from the top ----------------
+__global__ __launch_bounds__(256) void topk_key_kernel(const int64_t* table, TopkDev s, uint64_t* okey) {
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < s.G; k += (uint64_t)gridDim.x * 256)
+    okey[k] = table[k] > 0 ? pgpu_topk_key(table, s, k) : 0ull;
+}
+__global__ void topk_init_kernel(TopkState* ts, uint32_t* hist, uint64_t k) {
+  if (threadIdx.x == 0) {
+    ts->prefix = 0;
+    ts->mask = 0;
+    ts->kleft = k;
+  }
+  hist[threadIdx.x] = 0;
+}
+// Histogram of digit (key >> shift) & 255 over the non-empty rows whose higher digits equal the prefix so far.
+__global__ __launch_bounds__(256) void topk_hist_kernel(const int64_t* table, const uint64_t* okey, uint64_t G,
+                                                        const TopkState* ts, int shift, uint32_t* hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t prefix = ts->prefix, mask = ts->mask;
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < G; k += (uint64_t)gridDim.x * 256) {
+    const uint64_t u = okey[k];
+    if (table[k] > 0 && (u & mask) == prefix) atomicAdd(&h[(u >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+// The digit holding the kleft-th best key: walk the bins from 255 down (one thread; 256 bins).
+__global__ void topk_pick_kernel(TopkState* ts, uint32_t* hist, int shift) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = hist[threadIdx.x];
+  hist[threadIdx.x] = 0;  // ready for the next pass
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint64_t kleft = ts->kleft, cum = 0;
+  int d = 255;
+  for (; d > 0; --d) {
+    if (cum + h[d] >= kleft) break;
+    cum += h[d];
+  }
+  // fewer than kleft rows under the prefix: d = 0 keeps every one of them (the threshold's low bits stay 0)
+  ts->kleft = kleft > cum ? kleft - cum : 1;
+  ts->prefix |= (uint64_t)d << shift;
+  ts->mask |= 255ull << shift;
+}
+
+hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, uint64_t* okey, TopkState* ts,
+                            uint32_t* hist, hipStream_t st) {
+  const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(2048, (s.G + 255) / 256));
+  hipLaunchKernelGGL(topk_key_kernel, dim3(blocks), dim3(256), 0, st, table, s, okey);
+  hipLaunchKernelGGL(topk_init_kernel, dim3(1), dim3(256), 0, st, ts, hist, k);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    hipLaunchKernelGGL(topk_hist_kernel, dim3(blocks), dim3(256), 0, st, table, okey, s.G, ts, shift, hist);
+    hipLaunchKernelGGL(topk_pick_kernel, dim3(1), dim3(256), 0, st, ts, hist, shift);
   }
   return hipGetLastError();
 }

@@ -42,7 +42,10 @@ hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void
                                 bool init_table, hipStream_t st);
 hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, int32_t* block_counts,
-                               int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st);
+                               int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st,
+                               const uint64_t* okey = nullptr, const TopkState* ts = nullptr);
+hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, uint64_t* okey, TopkState* ts,
+                            uint32_t* hist, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
@@ -161,6 +164,7 @@ struct Workspace {
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
   DevMem rawbits;                      // match bitmaps of the raw-value leaves (rawpred_kernel)
+  DevMem tk_keys, tk_state;            // pgpu_table_topk: per-row order keys, radix-select state + histogram
   PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
   DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
   PinnedMem h_cancel;                  // its source for pgpu_query_cancel's copy-engine write
@@ -1552,6 +1556,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   p.G = L.num_keys;
   p.flags = (q->flags & PGPU_Q_STATS) ? PGPU_FLAG_STATS : 0;
   if (profile_enabled()) p.flags |= PGPU_FLAG_PROFILE;
+  static const int cancel_poll = getenv("PGPU_CANCEL_POLL") ? std::max(1, atoi(getenv("PGPU_CANCEL_POLL"))) : PGPU_CANCEL_POLL;
+  p.cancel_poll = cancel_poll;
   static const bool direct_nt = getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) != 0;
   if (direct_nt) p.flags |= PGPU_FLAG_NT;
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
@@ -2224,9 +2230,59 @@ int pgpu_query_release(pgpu_query* qq) {
 
 namespace {
 
+// The order key of a pgpu_topk over a table layout (include/pinot_gpu.h; keys in pgpu_internal.h).
+int topk_spec(const pgpu_table_layout* L, const pgpu_topk* o, TopkDev* out) {
+  TopkDev t{};
+  t.G = L->num_keys;
+  t.nsec = L->num_sections;
+  t.kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;
+  t.desc = o->descending ? 1 : 0;
+  t.key_base = o->key_base;
+  if (o->source == PGPU_TOPK_AGG) {
+    const int a = o->agg_index;
+    if (a < 0 || a >= 16) return fail(PGPU_E_INVALID, "top-k aggregation index %d", a);
+    const int sec = L->agg_section[a];
+    t.sec = sec;
+    const bool split = L->agg_sum_parts[a] == 3;
+    const int op = L->section_op[sec];
+    const int vt = L->agg_value_type[a];
+    switch (o->agg_fn) {
+      case PGPU_AGG_COUNT: t.mode = PGPU_TK_COUNT; break;
+      case PGPU_AGG_SUM:
+        t.mode = op == PGPU_RED_SUM_F64 ? PGPU_TK_SUM_F64 : (split ? PGPU_TK_SUM_SPLIT : PGPU_TK_SUM_I64);
+        break;
+      case PGPU_AGG_AVG:
+        t.mode = op == PGPU_RED_SUM_F64 ? PGPU_TK_AVG_F64 : (split ? PGPU_TK_AVG_SPLIT : PGPU_TK_AVG_I64);
+        break;
+      case PGPU_AGG_MIN:
+      case PGPU_AGG_MAX:
+        t.mode = (vt == PGPU_INT || vt == PGPU_LONG) ? PGPU_TK_MINMAX_INT : PGPU_TK_MINMAX_FP;
+        break;
+      default: return fail(PGPU_E_INVALID, "top-k aggregation fn %d", o->agg_fn);
+    }
+    if (o->agg_fn != PGPU_AGG_COUNT && sec <= 0) return fail(PGPU_E_INVALID, "top-k aggregation %d has no section", a);
+  } else if (o->source == PGPU_TOPK_GROUP) {
+    const int g = o->group_index, n = o->num_group_columns;
+    if (g < 0 || g >= n || !o->group_cardinalities) return fail(PGPU_E_INVALID, "top-k group column %d", g);
+    const int split = t.kw == 2 ? L->key_split : n;
+    t.word = g < split ? 0 : 1;
+    uint64_t st = 1;
+    for (int j = t.word == 0 ? 0 : split; j < g; ++j) st *= (uint64_t)std::max(1, o->group_cardinalities[j]);
+    t.stride = st;
+    t.card = (uint64_t)std::max(1, o->group_cardinalities[g]);
+    t.mode = PGPU_TK_GROUP;
+  } else {
+    return fail(PGPU_E_INVALID, "top-k source %d", o->source);
+  }
+  *out = t;
+  return PGPU_OK;
+}
+
+// Compact the non-empty rows of a device table into host buffers; with `order` (k > 0) only the best k by its key
+// (ties with the k-th kept), selected on the device by radix select.
 int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, const void* dev_table,
                  hipStream_t st, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
-                 uint64_t* out_num_groups) {
+                 uint64_t* out_num_groups, const pgpu_topk* order = nullptr) {
   const uint64_t G = L->num_keys;
   const int nsec = L->num_sections;
   const int kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;  // 0: the cell index is the key
@@ -2235,8 +2291,22 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
   HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16));
   HIP_TRY(ws->cmp_total.ensure(16));
   HIP_TRY(ws->h_total.ensure(16));
+  const uint64_t* okey = nullptr;
+  const TopkState* tstate = nullptr;
+  if (order && order->k > 0) {
+    TopkDev spec;
+    const int rc = topk_spec(L, order, &spec);
+    if (rc) return rc;
+    HIP_TRY(ws->tk_keys.ensure(8 * G + 16));
+    HIP_TRY(ws->tk_state.ensure(sizeof(TopkState) + 4 * 256 + 16));
+    TopkState* ts = (TopkState*)ws->tk_state.p;
+    uint32_t* hist = (uint32_t*)((char*)ws->tk_state.p + sizeof(TopkState));
+    HIP_TRY(pgpu_launch_topk((const int64_t*)dev_table, spec, order->k, (uint64_t*)ws->tk_keys.p, ts, hist, st));
+    okey = (const uint64_t*)ws->tk_keys.p;
+    tstate = ts;
+  }
   HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p,
-                              (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st));
+                              (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st, okey, tstate));
   HIP_TRY(hipMemcpyAsync(ws->h_total.p, ws->cmp_total.p, 8, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const uint64_t n = (uint64_t)*(const int64_t*)ws->h_total.p;
@@ -2248,7 +2318,7 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
   HIP_TRY(ws->cmp_keys.ensure(8 * n * okw));
   HIP_TRY(ws->cmp_cells.ensure(8 * n * nsec));
   HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p, nullptr,
-                              (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st));
+                              (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st, okey, tstate));
   HIP_TRY(hipMemcpyAsync(out_keys, ws->cmp_keys.p, 8 * n * okw, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(out_cells, ws->cmp_cells.p, 8 * n * nsec, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -2269,6 +2339,20 @@ int pgpu_table_compact(pgpu_context* ctx, const pgpu_table_layout* layout, const
   if (!ws) return rc;
   rc = compact_into(ctx, ws, layout, dev_table, stream ? (hipStream_t)stream : ws->stream, out_keys, out_cells,
                     capacity, out_num_groups);
+  release_ws(ctx, ws);
+  return rc;
+}
+
+int pgpu_table_topk(pgpu_context* ctx, const pgpu_table_layout* layout, const void* dev_table, void* stream,
+                    const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
+                    uint64_t* out_num_groups) {
+  if (!ctx || !layout || !dev_table || !out_num_groups) return fail(PGPU_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = 0;
+  Workspace* ws = acquire_ws(ctx, &rc);
+  if (!ws) return rc;
+  rc = compact_into(ctx, ws, layout, dev_table, stream ? (hipStream_t)stream : ws->stream, out_keys, out_cells,
+                    capacity, out_num_groups, order);
   release_ws(ctx, ws);
   return rc;
 }
@@ -2646,10 +2730,20 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
 
 int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
                        uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
+  return pgpu_query_collect_topk(qq, nullptr, out_keys, out_cells, capacity, out_num_groups, out_stats);
+}
+
+int pgpu_query_collect_topk(pgpu_query* qq, const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells,
+                            uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats) {
   if (!qq || !qq->tws || !out_num_groups) return fail(PGPU_E_INVALID, "query was not submitted");
   int rc = pgpu_query_wait(qq, out_stats);
   const pgpu_table_layout& L = qq->layout;
-  if (rc == PGPU_OK && qq->small) {
+  if (rc == PGPU_OK && order && order->k > 0) {
+    // the ORDER BY ... LIMIT trim runs on the device copy of the table (small tables too: the host copy is only
+    // a shortcut for plain compaction)
+    rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->ws->stream, out_keys, out_cells, capacity,
+                      out_num_groups, order);
+  } else if (rc == PGPU_OK && qq->small) {
     const int64_t* t = (const int64_t*)qq->tws->h_table.p;
     const uint64_t G = L.num_keys;
     const int nsec = L.num_sections;

@@ -378,6 +378,33 @@ def order_and_limit(query: QueryContext, rows: List[tuple]) -> List[tuple]:
     return rows[: query.limit]
 
 
+def table_capacity(limit: int) -> int:
+    """GroupByUtils.getTableCapacity (core/util/GroupByUtils.java:24-41): the IndexedTable's trim size."""
+    return max(5 * limit, 5000)
+
+
+def topk_spec(query: QueryContext, cards: Sequence[int], k: int, key_base: int = 0) -> Optional[_lib.TopK]:
+    """pgpu_topk for the query's first ORDER BY expression (include/pinot_gpu.h): the groups the server's
+    IndexedTable.finish would hand the broker, ties at the k-th kept.  None when there is nothing to trim by."""
+    if not query.group_by or not query.order_by or k <= 0:
+        return None
+    ob = query.order_by[0]
+    names = list(query.group_by) + [a.result_name for a in query.aggregations]
+    i = names.index(ob.expression)
+    ng = len(query.group_by)
+    t = _lib.TopK()
+    t.k, t.key_base, t.descending = int(k), int(key_base), 0 if ob.ascending else 1
+    if i < ng:
+        carr = (C.c_int32 * ng)(*[int(c) for c in cards])  # global cardinality per group column
+        t.source, t.group_index, t.num_group_columns = _lib.PGPU_TOPK_GROUP, i, ng
+        t.group_cardinalities = C.cast(carr, C.POINTER(C.c_int32))
+        t._keep = carr  # the cardinalities live as long as the spec
+    else:
+        t.source, t.agg_index = _lib.PGPU_TOPK_AGG, i - ng
+        t.agg_fn = AGG_FN[query.aggregations[i - ng].function]
+    return t
+
+
 def to_select_order(query: QueryContext, row: tuple) -> tuple:
     names = list(query.group_by) + [a.result_name for a in query.aggregations]
     out = []
@@ -410,8 +437,11 @@ class GpuPlanMaker:
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
                  collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False,
-                 exact_filter_stats: bool = False, timeout_ms: Optional[int] = None):
+                 exact_filter_stats: bool = False, timeout_ms: Optional[int] = None, gpu_topk: bool = True):
         self.ctx = ctx
+        # gpu_topk: a GROUP BY ... ORDER BY ... LIMIT query brings back only the groups the server's IndexedTable
+        # keeps (table_capacity(limit), ties kept), selected on the GPU (pgpu_query_collect_topk)
+        self.gpu_topk = gpu_topk
         # timeout_ms: the query's budget from submit (QueryOptions timeoutMs -> QueryContext.getEndTimeMs); past it
         # the query is cancelled and collect raises QueryTimeoutError (EXECUTION_TIMEOUT_ERROR)
         self.timeout_ms = timeout_ms
@@ -626,12 +656,15 @@ class GpuPlanMaker:
         n = C.c_uint64()
         st = QueryStats()
         h, pending.handle = pending.handle, None
-        _lib.check(self.ctx._lib.pgpu_query_collect(h, keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                                    cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
-                                                    C.byref(st)))
+        query = pending.query
+        order = (topk_spec(query, [len(g[0]) for g in pending.globals_], table_capacity(query.limit))
+                 if self.gpu_topk else None)
+        _lib.check(self.ctx._lib.pgpu_query_collect_topk(h, C.byref(order) if order is not None else None,
+                                                         keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                         cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
+                                                         C.byref(st)))
         table = GroupTable.sorted(keys[: n.value * kw].reshape(-1, kw) if kw > 1 else keys[: n.value],
                                   cells[: n.value], L)
-        query = pending.query
         stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
                                num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),

@@ -200,7 +200,7 @@ def _numpy_executor(pm):
         def _wait_local(self, handle):
             return handle
 
-        def _compact(self, L, table):
+        def _compact(self, L, table, order=None):  # every row: the host trim (_trim) then does the top-k
             rows = L.num_sections + (1 if L.key_kind == PGPU_KEYS_HASH else 0)
             t = table.cpu().numpy()[: rows * int(L.num_keys)].reshape(rows, int(L.num_keys))
             live = np.flatnonzero(t[0] > 0)
