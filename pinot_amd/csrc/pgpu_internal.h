@@ -36,8 +36,9 @@
 #define PGPU_MAX_GCOLS 16
 #define PGPU_MAX_STAGE 6        // staged (LDS-streamed) columns per segment
 #define PGPU_RING_MAX 64        // ring slots (flag arrays are sized for this)
-#define PGPU_CQ_CAP 1280        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile):
-                                // flush threshold + half a tile (a denser tile is queued in two halves)
+#define PGPU_CQ_CAP 1024        // candidate-queue entries (uint16: consumer-tile index << 11 | doc in tile):
+                                // a tile that does not fit behind the queued entries is flushed, then queued
+                                // and flushed in two halves of <= 1024
 #define PGPU_CQ_FLUSH 256       // candidate-queue flush threshold
 #define PGPU_CQ_TILES 32        // a queue spans at most 32 of the consumer's tiles (5-bit tile index)
 #define PGPU_AGG_LIST 1024      // dense-agg key / value list entries (int32 each, DENSE variant)
@@ -319,7 +320,7 @@ static_assert(sizeof(DevParams) <= 4096, "DevParams is a kernel argument");
 
 #define PGPU_FLAG_STATS 1
 #define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)
-#define PGPU_FLAG_NT 4        // direct kernel: tile DMAs with the non-temporal policy (PGPU_DIRECT_NT=1)
+#define PGPU_FLAG_NT 4        // direct kernel: tile DMAs with the non-temporal policy (default; PGPU_DIRECT_NT=0 off)
 #define PGPU_NPROF 12
 // loader phases
 #define PGPU_P_L_TOTAL 0

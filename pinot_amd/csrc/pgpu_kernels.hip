@@ -1911,6 +1911,10 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
 // ================================================================================================================
 #define PGPU_DIRECT_THREADS 256
 #define PGPU_DIRECT_WAVES (PGPU_DIRECT_THREADS / 64)
+#ifndef PGPU_DIRECT_MIN_WAVES
+#define PGPU_DIRECT_MIN_WAVES 5  // waves per SIMD the register budget must allow (<= 96 VGPRs; the other modes
+                                 // keep 4: their accumulators / table paths would spill to scratch)
+#endif
 
 // saddr form: wave-uniform base in an SGPR pair + this lane's byte offset (a VGPR that lives for the whole kernel),
 // so no VGPR is written right before the DMA -- a freshly written address VGPR draws a conservative vmcnt(0) from
@@ -1947,6 +1951,45 @@ FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* 
       if (64 * k + lane < 16 * b) {
         if (nt) glds16_asm_nt(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
         else glds16_asm(voff16, uniform_ptr(base + 1024 * k), dst + 1024 * k);
+      }
+    }
+  }
+}
+
+// A self-loading wave's filtered tile: count it (COUNT-only segment), or queue its candidate docs for the residual
+// filter and the sparse aggregation (a tile that does not fit behind the queued entries is flushed in two halves).
+template <int MODE, int NW>
+FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
+                          int tile_in_seg, uint32_t mm, int& qn, int& qt, uint32_t& lane_matched, int64_t& matched,
+                          int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
+  const int lane = lane_id();
+  if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
+    lane_matched += __popc(mm);
+  } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
+    const int cnt = __popc(mm);
+    const int ex = wave_excl_scan(cnt);
+    const int nm = __builtin_amdgcn_readlane(ex + cnt, 63);
+    if (qn + nm <= PGPU_CQ_CAP) {
+      if (lane == 0) cv.qtiles[qt] = tile_in_seg;
+      const uint32_t tag = (uint32_t)qt << 11;
+      ++qt;
+      int q = qn + ex;
+      for (uint32_t left = mm; left; left &= left - 1)
+        cv.queue[q++] = (uint16_t)(tag | (uint32_t)(32 * lane + __builtin_ctz(left)));
+      qn += nm;
+    } else {
+      if (qn) {
+        flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+        qn = qt = 0;
+      }
+      if (lane == 0) cv.qtiles[0] = tile_in_seg;
+      for (int half = 0; half < 2; ++half) {
+        const uint32_t mh = (lane >> 5) == half ? mm : 0u;
+        const int nh = wave_sum_i32(__popc(mh));
+        if (nh == 0) continue;
+        int q = wave_excl_scan(__popc(mh));
+        for (uint32_t left = mh; left; left &= left - 1) cv.queue[q++] = (uint16_t)(32 * lane + __builtin_ctz(left));
+        flush_queue<MODE, NW>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
       }
     }
   }
@@ -2041,36 +2084,8 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
       // the slot's planes have been read (lgkmcnt): it is rewritten by the issue of tile k + D, after this point
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);
-      if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
-        lane_matched += __popc(mm);
-      } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
-        const int cnt = __popc(mm);
-        const int ex = wave_excl_scan(cnt);
-        const int nm = __builtin_amdgcn_readlane(ex + cnt, 63);
-        if (qn + nm <= PGPU_CQ_CAP) {
-          if (lane == 0) cv.qtiles[qt] = cur.tile_in_seg;
-          const uint32_t tag = (uint32_t)qt << 11;
-          ++qt;
-          int q = qn + ex;
-          for (uint32_t left = mm; left; left &= left - 1)
-            cv.queue[q++] = (uint16_t)(tag | (uint32_t)(32 * lane + __builtin_ctz(left)));
-          qn += nm;
-        } else {
-          if (qn) {
-            flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
-            qn = qt = 0;
-          }
-          if (lane == 0) cv.qtiles[0] = cur.tile_in_seg;
-          for (int half = 0; half < 2; ++half) {
-            const uint32_t mh = (lane >> 5) == half ? mm : 0u;
-            const int nh = wave_sum_i32(__popc(mh));
-            if (nh == 0) continue;
-            int q = wave_excl_scan(__popc(mh));
-            for (uint32_t left = mh; left; left &= left - 1) cv.queue[q++] = (uint16_t)(32 * lane + __builtin_ctz(left));
-            flush_queue<MODE, NW>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
-          }
-        }
-      }
+      direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, mm, qn, qt, lane_matched, matched, scanned,
+                                  sector_bytes, dense_bytes, pf);
       PROF_ADD(pf, PGPU_P_C_AGG, ta);
     }
     if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
@@ -2108,7 +2123,10 @@ FI Lds carve_direct(unsigned char* base, const DevParams& p) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_direct(DevParams p) {
+FI void direct_epilogue(const DevParams& p, const Lds& L, const Stats& st, int wave, int lane, Prof& pf);
+
+template <int MODE>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS, (MODE == PGPU_MODE_GLOBAL || MODE == PGPU_MODE_HASH) ? PGPU_DIRECT_MIN_WAVES : 4) void query_kernel_direct(DevParams p) {
   constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2132,6 +2150,13 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_direct(DevPa
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
   const Stats st = direct_consumer<MODE>(p, L, wave, t0, t1 - t0, pf);
+  direct_epilogue<MODE>(p, L, st, wave, lane, pf);
+}
+
+// Per-wave statistics and partials of a self-loading kernel, then the workgroup's table flush (LDS / PART modes).
+template <int MODE>
+FI void direct_epilogue(const DevParams& p, const Lds& L, const Stats& st, int wave, int lane, Prof& pf) {
+  constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
   const size_t w = (size_t)blockIdx.x * NWAVES + wave;
 #ifdef PGPU_PROFILE_BUILD
   if (pf.on && lane == 0) {
@@ -2171,6 +2196,190 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_direct(DevPa
       p.rcount[(size_t)q * gridDim.x + blockIdx.x] = n < (uint32_t)p.rcap ? n : (uint32_t)p.rcap;
     }
   }
+}
+
+// ================================================================================================================
+// REGISTER-DIRECT variant (p.direct == 2): every segment's only staged column is one bit-sliced fast leaf of at most
+// PGPU_RDIRECT_PLANES bits.  Its planes go straight into VGPRs -- plane k of lane l is one coalesced 4-B load per
+// lane, 256 B per wave-instruction -- with RD tiles in flight per wave (a register ring, unrolled), no LDS staging
+// at all: tools/stream_bench.hip reads such a stream at 5.6-6.0 TB/s where the LDS-DMA self-loading kernel
+// streamed 3.8 TB/s (its in-flight bytes are bounded by the LDS slots).  Candidate handling as in direct_consumer.
+// ================================================================================================================
+#define PGPU_RDIRECT_PLANES 16
+#define PGPU_RDIRECT_DEPTH 2
+struct RdIssue {  // the issue cursor's segment: its sliced column
+  const uint32_t* sliced;
+  int bits;
+};
+FI void rd_load_issue(const DevParams& p, int seg, RdIssue& is) {
+  const DevSeg* sg = p.segs + seg;
+  const DevColumn* cols = p.cols + cld(&sg->col_begin);
+  const int qc = cld(&sg->stage_col[0]);
+  is.sliced = (const uint32_t*)cld(&cols[qc].sliced);
+  is.bits = cld(&cols[qc].bits);
+}
+FI void rd_load_tile(const RdIssue& is, int tile_in_seg, uint32_t (&x)[PGPU_RDIRECT_PLANES]) {
+  const uint32_t* src = is.sliced + (size_t)tile_in_seg * is.bits * 64 + lane_id();
+#pragma unroll
+  for (int k = 0; k < PGPU_RDIRECT_PLANES; ++k)
+    x[k] = k < is.bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;  // planes past the width: 0 (inert below)
+}
+// The fast leaf on register planes: OR of dict-id ranges [lo, hi) (x < c as a borrow chain; planes past the
+// column's width are 0 and leave the chain unchanged, and c = 2^bits sets the borrow there), then negated.
+FI uint32_t rd_lt(const uint32_t (&x)[PGPU_RDIRECT_PLANES], uint32_t c) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_RDIRECT_PLANES; ++k)
+    br = __builtin_amdgcn_bitop3_b32((uint32_t)-(int32_t)((c >> k) & 1u), x[k], br, 0xB2);
+  return (c >> PGPU_RDIRECT_PLANES) ? ~0u : br;
+}
+FI uint32_t rd_filter(const SegState& ss, const uint32_t (&x)[PGPU_RDIRECT_PLANES], uint32_t valid,
+                      uint32_t& lane_scanned) {
+  if (!(ss.f_kind[0] >> 8)) lane_scanned += __popc(valid);
+  uint32_t m = rd_lt(x, ss.f_r0hi[0]) & ~rd_lt(x, ss.f_r0lo[0]);
+  for (int r = 1; r < ss.f_nr[0]; ++r) {
+    const uint32_t lo = cld(&ss.sg->f_rng[0][r][0]), hi = cld(&ss.sg->f_rng[0][r][1]);
+    m |= rd_lt(x, hi) & ~rd_lt(x, lo);
+  }
+  return valid & (ss.f_sneg[0] ? ~m : m);
+}
+
+template <int MODE>
+FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH;
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  uint32_t lane_scanned = 0, lane_matched = 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int qn = 0, qt = 0;
+  SegState ss;
+  int cseg = -1;
+  if (cidx < ntiles) {
+    const int own = (ntiles - cidx + NW - 1) / NW;  // this wave's tiles: cidx, cidx + NW, ...
+    Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
+    RdIssue is;
+    rd_load_issue(p, ci.seg, is);
+    uint32_t x[RD][PGPU_RDIRECT_PLANES];
+#pragma unroll
+    for (int s = 0; s < RD; ++s) {
+      if (s < own) {
+        if (s > 0 && cursor_advance(p, ci, NW)) rd_load_issue(p, ci.seg, is);
+        rd_load_tile(is, ci.tile_in_seg, x[s]);
+      }
+    }
+    int poll = p.cancel_poll;
+    bool stop = false;
+    for (int k0 = 0; k0 < own && !stop; k0 += RD) {
+#pragma unroll
+      for (int s = 0; s < RD; ++s) {
+        const int k = k0 + s;
+        if (k >= own || stop) break;
+        if (--poll == 0) {
+          poll = p.cancel_poll;
+          if (query_cancelled(p)) {
+            stop = true;
+            break;
+          }
+        }
+        if (k > 0) cursor_advance(p, cur, NW);
+        if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES || cur.seg != cseg)) {
+          const int64_t tq = now(pf);
+          flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+          PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+          qn = qt = 0;
+        }
+        if (cur.seg != cseg) {
+          cseg = cur.seg;
+          load_seg(p, cseg, ss);
+        }
+        const int64_t tf = now(pf);
+#ifdef PGPU_PROFILE_BUILD
+        if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+#endif
+        const int doc0 = cur.tile_in_seg * WT;
+        uint32_t valid;
+        {
+          const int ndocs = min(WT, ss.num_docs - doc0);
+          const int rem = ndocs - 32 * lane;
+          valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * ss.f_bits[0] + 7) / 8;
+        }
+        const uint32_t mm = rd_filter(ss, x[s], valid, lane_scanned);
+        // refill this register slot with the tile RD ahead (its loads overlap this tile's candidate handling)
+        if (k + RD < own) {
+          if (cursor_advance(p, ci, NW)) rd_load_issue(p, ci.seg, is);
+          rd_load_tile(is, ci.tile_in_seg, x[s]);
+        }
+        PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+        const int64_t ta = now(pf);
+        direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, mm, qn, qt, lane_matched, matched, scanned,
+                                    sector_bytes, dense_bytes, pf);
+        PROF_ADD(pf, PGPU_P_C_AGG, ta);
+      }
+    }
+    if (qn && !stop) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+  }
+  {
+    const int64_t ls = wave_sum_i64((int64_t)lane_scanned), lm = wave_sum_i64((int64_t)lane_matched);
+    if (lane == 0) {
+      scanned += ls;
+      matched += lm;
+    }
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  if (MODE == PGPU_MODE_AGG) {
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  }
+  Stats st;
+  st.matched = matched;
+  st.scanned = scanned;
+  st.sector_bytes = sector_bytes;
+  st.dense_bytes = dense_bytes;
+  return st;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevParams p) {
+  constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  if (MODE == PGPU_MODE_LDS) {
+    const int n = p.nsec * (int)p.G;
+    for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+  }
+  if (MODE == PGPU_MODE_PART)
+    for (int i = threadIdx.x; i < p.nparts; i += NT) ((uint32_t*)L.ltab)[i] = 0u;
+  __syncthreads();
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const Stats st = rdirect_consumer<MODE>(p, L, wave, t0, t1 - t0, pf);
+  direct_epilogue<MODE>(p, L, st, wave, lane, pf);
 }
 
 // ---- the query kernel ----------------------------------------------------------------------------------------------
@@ -2983,7 +3192,10 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);       \
+    if (p.direct == 2)                                                                                          \
+      hipLaunchKernelGGL((query_kernel_rdirect<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);     \
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_prepare_##NAME(size_t lds_bytes) {                                                            \
@@ -2994,6 +3206,9 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
                               (int)lds_bytes);                                                                  \
     if (e == hipSuccess)                                                                                        \
       e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                              (int)lds_bytes);                                                                  \
+    if (e == hipSuccess)                                                                                        \
+      e = hipFuncSetAttribute((const void*)query_kernel_rdirect<M>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                               (int)lds_bytes);                                                                  \
     return e;                                                                                                   \
   }

@@ -1558,7 +1558,9 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   if (profile_enabled()) p.flags |= PGPU_FLAG_PROFILE;
   static const int cancel_poll = getenv("PGPU_CANCEL_POLL") ? std::max(1, atoi(getenv("PGPU_CANCEL_POLL"))) : PGPU_CANCEL_POLL;
   p.cancel_poll = cancel_poll;
-  static const bool direct_nt = getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) != 0;
+  // once-read tile streams take the non-temporal policy (measured on config 5: 0.407 -> 0.399 ms); PGPU_DIRECT_NT=0
+  // restores the default policy
+  static const bool direct_nt = !(getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) == 0);
   if (direct_nt) p.flags |= PGPU_FLAG_NT;
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
@@ -1769,7 +1771,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     static const int env_slots = getenv("PGPU_DIRECT_SLOTS") ? atoi(getenv("PGPU_DIRECT_SLOTS")) : 0;
     static const int env_wgs = getenv("PGPU_DIRECT_WGS") ? atoi(getenv("PGPU_DIRECT_WGS")) : 0;  // per CU
     if (env_slots >= 2) D = std::min(env_slots, 1 + 63 / max_instrs);
-    const int wgs = env_wgs >= 1 ? env_wgs : 5;  // as many 4-wave workgroups as LDS and VGPRs allow (<= 20 waves)
+    // as many 4-wave workgroups as LDS and VGPRs allow: 5 (20 waves) where the kernel fits 96 VGPRs
+    // (PGPU_DIRECT_MIN_WAVES), else 4 -- a fifth workgroup that cannot be resident only adds a tail
+    const int wgs = env_wgs >= 1 ? env_wgs : ((p.mode == PGPU_MODE_GLOBAL || p.mode == PGPU_MODE_HASH) ? 5 : 4);
     auto ddyn_of = [&](int d) { return (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + (size_t)4 * d * S; };
     while (D > 2 && wgs * ddyn_of(D) > PGPU_LDS_LIMIT) --D;
     const size_t ddyn = ddyn_of(D);
@@ -1782,6 +1786,25 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       p.min_instrs = std::max(1, min_instrs);
       grid = std::max(1, g);
       dyn = ddyn;
+    }
+    // register-direct (query_kernel_rdirect): one bit-sliced fast leaf of <= 16 bits per segment is the only staged
+    // column -- its planes stream into VGPRs, no LDS slots (tools/stream_bench.hip: 5.6-6.0 TB/s)
+    static const bool no_rdirect = getenv("PGPU_NO_RDIRECT") && atoi(getenv("PGPU_NO_RDIRECT")) != 0;
+    bool rd = ok && !no_rdirect;
+    for (const DevSeg& ds : pk.segs)
+      if (ds.ntiles) {
+        const DevColumn& c = pk.cols[ds.col_begin + ds.stage_col[0]];
+        rd &= ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1 && c.bits >= 1 && c.bits <= 16;
+      }
+    const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;
+    if (rd && rdyn <= PGPU_LDS_LIMIT) {
+      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : 4, PGPU_LDS_LIMIT / rdyn);  // 120 VGPRs
+      int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
+      if (g >= 8) g &= ~7;
+      p.direct = 2;
+      p.dslots = 0;
+      grid = std::max(1, g);
+      dyn = rdyn;
     }
   }
   // one-word PART records (in-partition key, dict id) when every segment holds the same dictionary for the
@@ -2293,7 +2316,7 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
   HIP_TRY(ws->h_total.ensure(16));
   const uint64_t* okey = nullptr;
   const TopkState* tstate = nullptr;
-  if (order && order->k > 0) {
+  if (order && order->k > 0 && G > order->k) {  // a table of at most k cells has nothing to trim
     TopkDev spec;
     const int rc = topk_spec(L, order, &spec);
     if (rc) return rc;
@@ -2738,7 +2761,7 @@ int pgpu_query_collect_topk(pgpu_query* qq, const pgpu_topk* order, int64_t* out
   if (!qq || !qq->tws || !out_num_groups) return fail(PGPU_E_INVALID, "query was not submitted");
   int rc = pgpu_query_wait(qq, out_stats);
   const pgpu_table_layout& L = qq->layout;
-  if (rc == PGPU_OK && order && order->k > 0) {
+  if (rc == PGPU_OK && order && order->k > 0 && L.num_keys > order->k) {
     // the ORDER BY ... LIMIT trim runs on the device copy of the table (small tables too: the host copy is only
     // a shortcut for plain compaction)
     rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->ws->stream, out_keys, out_cells, capacity,

@@ -73,3 +73,29 @@ def rows_close(r1, r2, rel=1e-9):
             elif not close(a, b, rel):
                 return False
     return True
+
+
+def trims(query, ngroups: int) -> bool:
+    """Whether a GROUP BY ... ORDER BY ... LIMIT result holds only the server's trimmed groups (IndexedTable.finish
+    keeps max(5 * limit, 5000) of them, GroupByUtils.getTableCapacity): the GPU path returns those."""
+    return bool(query.group_by and query.order_by) and ngroups > max(5 * query.limit, 5000)
+
+
+def check_groups(res, ref, rel=1e-9):
+    """GPU group rows against the oracle's.  All groups when the query keeps them all; under the ORDER BY ... LIMIT
+    trim, the GPU's groups are a subset of the oracle's with equal values, at least the trim size, and the final
+    rows carry the oracle's ORDER BY values in order."""
+    q = res.query
+    n = len(q.group_by)
+    g = {r[:n]: r for r in res.group_rows}
+    o = {r[:n]: r for r in ref.group_rows}
+    if trims(q, len(o)):
+        assert set(g) <= set(o) and len(g) >= max(5 * q.limit, 5000), (len(g), len(o))
+        names = [s if isinstance(s, str) else s.result_name for s in q.select]
+        i = names.index(q.order_by[0].expression)
+        a, b = [r[i] for r in res.rows], [r[i] for r in ref.rows]
+        assert len(a) == len(b) and all(close(x, y, rel) for x, y in zip(a, b)), (a[:5], b[:5])
+    else:
+        assert set(g) == set(o), (len(g), len(o))
+    for k in g:
+        assert rows_close([g[k]], [o[k]], rel), (k, g[k], o[k])

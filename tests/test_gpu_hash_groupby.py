@@ -15,7 +15,7 @@ from pinot_amd._lib import PGPU_DOUBLE, PGPU_INT, PGPU_KEYS_DENSE, PGPU_KEYS_HAS
 from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
-from tests.helpers import rows_close
+from tests.helpers import check_groups, rows_close
 
 pytestmark = pytest.mark.gpu
 
@@ -34,9 +34,7 @@ def _run(gpu_ctx, sql, segs, **kw):
 
 
 def _same(res, ref):
-    assert sorted(r[: len(res.query.group_by)] for r in res.group_rows) == \
-        sorted(r[: len(res.query.group_by)] for r in ref.group_rows)
-    assert rows_close(sorted(res.group_rows), sorted(ref.group_rows), 1e-9)
+    check_groups(res, ref, 1e-9)
     if res.query.order_by:  # without ORDER BY the LIMIT keeps arbitrary groups (in the reference too)
         assert rows_close([list(r) for r in res.rows], [list(r) for r in ref.rows], 1e-9)
     assert res.stats.num_docs_scanned == ref.num_docs_scanned

@@ -13,7 +13,7 @@ from pinot_amd._lib import PGPU_DOUBLE, PGPU_INT, PGPU_KEYS_HASH, PGPU_LONG, PGP
 from pinot_amd.plan import ExecutionStats, GpuPlanMaker, GroupTable, finish, key_words_out
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
-from tests.helpers import close, rows_close
+from tests.helpers import check_groups, close, rows_close
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -44,7 +44,7 @@ def _check(res, ref):
     assert res.stats.num_docs_scanned == ref.num_docs_scanned
     assert res.stats.num_total_docs == ref.num_total_docs
     if res.query.group_by:
-        assert rows_close(sorted(res.group_rows), sorted(ref.group_rows), 1e-9)
+        check_groups(res, ref, 1e-9)
         assert rows_close([list(r) for r in res.rows], [list(r) for r in ref.rows], 1e-9)
     else:
         assert all(close(a, b, 1e-9) for a, b in zip(res.aggregation_result, ref.aggregation_result))

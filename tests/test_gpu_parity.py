@@ -15,7 +15,8 @@ from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_ST
 from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
-from tests.helpers import (baseball_segment, close, fast_count_segment, load_kat, rows_close, sv_segment)
+from tests.helpers import (baseball_segment, check_groups, close, fast_count_segment, load_kat, rows_close,
+                           sv_segment)
 
 pytestmark = pytest.mark.gpu
 KAT = load_kat()
@@ -41,11 +42,7 @@ def _assert_same(res, ref, rel=1e-9):
         for a, b in zip(res.aggregation_result, ref.aggregation_result):
             assert close(a, b, rel), (res.aggregation_result, ref.aggregation_result)
     else:
-        g = {r[: len(res.query.group_by)]: r for r in res.group_rows}
-        o = {r[: len(res.query.group_by)]: r for r in ref.group_rows}
-        assert set(g) == set(o)
-        for k in g:
-            assert rows_close([g[k]], [o[k]], rel), (k, g[k], o[k])
+        check_groups(res, ref, rel)
     assert res.stats.num_docs_scanned == ref.num_docs_scanned
     assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
     assert res.stats.num_total_docs == ref.num_total_docs

@@ -13,7 +13,7 @@ from pinot_amd._lib import PGPU_INT, PGPU_LONG, PGPU_Q_SUM_SPLIT
 from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
-from tests.helpers import close, rows_close
+from tests.helpers import check_groups, close, rows_close
 
 pytestmark = pytest.mark.gpu
 
@@ -36,8 +36,7 @@ def _check(gpu_ctx, sql, segs, flags=0):
         res = GpuPlanMaker(gpu_ctx, query_flags=flags).execute(q, gs)
         ref = engine.execute(q, segs)
         if q.group_by:
-            assert sorted(r[0] for r in res.group_rows) == sorted(r[0] for r in ref.group_rows)
-            assert rows_close(sorted(res.group_rows), sorted(ref.group_rows), 1e-9)
+            check_groups(res, ref, 1e-9)
         else:
             for a, b in zip(res.aggregation_result, ref.aggregation_result):
                 assert close(a, b, 1e-9), (res.aggregation_result, ref.aggregation_result)

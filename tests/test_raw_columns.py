@@ -13,7 +13,7 @@ from oracle import engine, rawfwd
 from oracle.segment_writer import build_segment
 from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, UnsupportedPlanError
 from pinot_amd.query import parse_sql
-from tests.helpers import close, rows_close
+from tests.helpers import check_groups, close, rows_close
 
 CODECS = [(rawfwd.PASS_THROUGH, 2), (rawfwd.SNAPPY, 2), (rawfwd.LZ4, 3), (rawfwd.LZ4_LENGTH_PREFIXED, 4)]
 
@@ -124,11 +124,7 @@ def _gpu_vs_oracle(gpu_ctx, segs, sql, exact=True, **opts):
             g.release()
     ref = engine.execute(q, segs, iterator_stats=True)
     if q.group_by:
-        g = {r[: len(q.group_by)]: r for r in res.group_rows}
-        o = {r[: len(q.group_by)]: r for r in ref.group_rows}
-        assert set(g) == set(o)
-        for k in g:
-            assert rows_close([g[k]], [o[k]]), (k, g[k], o[k])
+        check_groups(res, ref)
     else:
         for a, b in zip(res.aggregation_result, ref.aggregation_result):
             assert close(a, b), (res.aggregation_result, ref.aggregation_result)
