@@ -151,6 +151,15 @@ WORKLOADS: Dict[str, Workload] = {
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
         {"num_groups_limit": 2_000_000}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+    # PMC calibration (not a bench line): config 5's filter stream alone, a known byte count for FETCH_SIZE
+    "adanalytics_count": Workload(
+        "adanalytics_count", "adAnalytics",
+        [SynthColumn("daysSinceEpoch", 1024, _days),
+         SynthColumn("accountId", 1 << 20, _accounts),
+         SynthColumn("clicks", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 11)),
+         SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
+        "SELECT COUNT(*) FROM adAnalytics WHERE daysSinceEpoch BETWEEN 17849 AND 17856",
+        {}, 5, "config 5's filter stream alone (FETCH_SIZE calibration of the register-direct stream)"),
     "adanalytics_inv": Workload(
         "adanalytics_inv", "adAnalytics",
         [SynthColumn("daysSinceEpoch", 1024, _days),
