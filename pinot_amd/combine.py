@@ -32,7 +32,7 @@ from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
 from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
-                   key_words_out, merge_filtered, topk_spec)
+                   key_words_out, merge_filtered, table_capacity, topk_spec)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
@@ -440,10 +440,16 @@ class DistributedExecutor:
         finally:
             self._tables.setdefault(int(table.numel()), []).append(table)
 
+    def _trim_cap(self, query) -> int:
+        """GroupByUtils.getTableCapacity(limit, min.server.group.trim.size) of the plan maker (TOPK_MIN without
+        one); a non-positive minimum disables the trim (GroupByOrderByCombineOperator.java:80-95)."""
+        m = getattr(self.pm, "min_server_group_trim_size", self.TOPK_MIN)
+        return table_capacity(query.limit, m)
+
     def _trim(self, query, L, keys, cells, globals_):
         """This rank's candidate rows: its top max(5 * limit, TOPK_MIN) by the ORDER BY expressions (the rows'
         values are final here), or that many smallest keys without ORDER BY."""
-        cap = max(5 * query.limit, self.TOPK_MIN)  # GroupByUtils.getTableCapacity
+        cap = self._trim_cap(query)
         if len(keys) <= cap:
             return keys, cells
         t = GroupTable.sorted(keys, cells, L)
@@ -516,7 +522,8 @@ class DistributedExecutor:
         C.memmove(C.byref(CL), C.byref(L), C.sizeof(TableLayout))
         CL.num_keys = int(chunk.shape[1])
         # this rank's top max(5 * limit, 5000) of its key slice, selected on the GPU (ORDER BY), else on the host
-        order = topk_spec(query, [len(g) for g in p.globals_], max(5 * query.limit, self.TOPK_MIN), key_base=key0)
+        cap = self._trim_cap(query)
+        order = topk_spec(query, [len(g) for g in p.globals_], cap, key_base=key0) if cap < (1 << 62) else None
         keys, cells = self._compact(CL, chunk.reshape(-1).contiguous(), order)
         keys, cells = self._trim(query, L, keys + key0, cells, p.globals_)
         return self._gather_rows(keys, cells, L)

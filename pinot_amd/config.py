@@ -1,0 +1,149 @@
+"""Server configuration of the GPU path: the ``pinot.server.query.executor.*`` keys the reference's plan maker reads,
+plus the ``pinot.server.query.executor.gpu.*`` keys of this path.
+
+Reference keys honoured (their defaults are the reference's):
+
+* ``pinot.server.query.executor.timeout`` — query budget in ms when the query sets none
+  (CommonConstants.java:302, DEFAULT_QUERY_EXECUTOR_TIMEOUT_MS 15,000 at :366);
+* ``…num.groups.limit`` (100,000), ``…max.init.group.holder.capacity`` (10,000),
+  ``…min.server.group.trim.size`` (5,000; <= 0 disables the server trim)
+  (core/plan/maker/InstancePlanMakerImplV2.java:66-87).
+
+GPU keys:
+
+* ``…gpu.enabled`` (true): false keeps every query on the CPU plan maker;
+* ``…gpu.devices`` ("all"): the devices this server drives — ``all``, a list ``0,2,5`` or a mask ``0x25``;
+* ``…gpu.min.segment.docs`` (0): segments with fewer docs are not made HBM-resident (GpuIndexingOverride keeps
+  the reference's readers), so a query touching one stays on the CPU;
+* ``…gpu.min.query.docs`` (0): queries over fewer docs in total stay on the CPU (their launch would cost more
+  than the scan);
+* ``…gpu.exact.filter.stats`` (false): numEntriesScannedInFilter as the reference's iterators count it where
+  they leap-frog (one more pass, PGPU_Q_EXACT_FILTER_STATS);
+* ``…gpu.topk`` (true): select the ORDER BY trim on the GPU (pgpu_query_collect_topk).
+
+INTEGRATION.md §3.3 shows the Java side reading the same keys from the server's PinotConfiguration.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Mapping, Optional, Sequence, Tuple
+
+EXECUTOR_PREFIX = "pinot.server.query.executor."
+GPU_PREFIX = EXECUTOR_PREFIX + "gpu."
+DEFAULT_QUERY_EXECUTOR_TIMEOUT_MS = 15_000
+
+
+def _bool(v: str) -> bool:
+    s = str(v).strip().lower()
+    if s in ("true", "1", "yes", "on"):
+        return True
+    if s in ("false", "0", "no", "off"):
+        return False
+    raise ValueError(f"not a boolean: {v!r}")
+
+
+def parse_devices(spec: str, num_visible: int) -> List[int]:
+    """``all`` | ``0,2,5`` | ``0x25`` → sorted device ordinals below ``num_visible``."""
+    s = str(spec).strip().lower()
+    if s in ("", "all", "*"):
+        return list(range(num_visible))
+    if s.startswith("0x"):
+        mask = int(s, 16)
+        ids = [i for i in range(mask.bit_length()) if (mask >> i) & 1]
+    else:
+        ids = sorted({int(x) for x in s.split(",") if x.strip()})
+    bad = [i for i in ids if i < 0 or i >= num_visible]
+    if bad:
+        raise ValueError(f"{GPU_PREFIX}devices names device(s) {bad}, only {num_visible} visible")
+    if not ids:
+        raise ValueError(f"{GPU_PREFIX}devices selects no device")
+    return ids
+
+
+@dataclass
+class GpuExecutorConfig:
+    timeout_ms: int = DEFAULT_QUERY_EXECUTOR_TIMEOUT_MS
+    num_groups_limit: int = 100_000
+    max_init_group_holder_capacity: int = 10_000
+    min_server_group_trim_size: int = 5000
+    enabled: bool = True
+    devices: str = "all"
+    min_segment_docs: int = 0
+    min_query_docs: int = 0
+    exact_filter_stats: bool = False
+    topk: bool = True
+
+    @classmethod
+    def from_properties(cls, props: Mapping[str, str]) -> "GpuExecutorConfig":
+        """Read the keys from a flat server configuration (PinotConfiguration / properties file)."""
+        c = cls()
+
+        def get(key: str, conv, attr: str):
+            if key in props:
+                try:
+                    setattr(c, attr, conv(props[key]))
+                except ValueError as e:
+                    raise ValueError(f"bad value for {key}: {props[key]!r} ({e})") from None
+
+        get(EXECUTOR_PREFIX + "timeout", int, "timeout_ms")
+        get(EXECUTOR_PREFIX + "num.groups.limit", int, "num_groups_limit")
+        get(EXECUTOR_PREFIX + "max.init.group.holder.capacity", int, "max_init_group_holder_capacity")
+        get(EXECUTOR_PREFIX + "min.server.group.trim.size", int, "min_server_group_trim_size")
+        get(GPU_PREFIX + "enabled", _bool, "enabled")
+        get(GPU_PREFIX + "devices", str, "devices")
+        get(GPU_PREFIX + "min.segment.docs", int, "min_segment_docs")
+        get(GPU_PREFIX + "min.query.docs", int, "min_query_docs")
+        get(GPU_PREFIX + "exact.filter.stats", _bool, "exact_filter_stats")
+        get(GPU_PREFIX + "topk", _bool, "topk")
+        unknown = [k for k in props if k.startswith(GPU_PREFIX) and k[len(GPU_PREFIX):] not in _GPU_KEYS]
+        if unknown:
+            raise ValueError(f"unknown GPU executor key(s): {unknown}")
+        if c.num_groups_limit <= 0:
+            raise ValueError(f"{EXECUTOR_PREFIX}num.groups.limit must be positive")
+        return c
+
+    @classmethod
+    def from_file(cls, path: str) -> "GpuExecutorConfig":
+        """A Java-style properties file (``key=value`` / ``key: value``, ``#`` / ``!`` comments)."""
+        props = {}
+        with open(path, encoding="utf-8") as f:
+            for line in f:
+                s = line.strip()
+                if not s or s[0] in "#!":
+                    continue
+                sep = min((i for i in (s.find("="), s.find(":")) if i >= 0), default=-1)
+                if sep < 0:
+                    continue
+                props[s[:sep].strip()] = s[sep + 1:].strip()
+        return cls.from_properties(props)
+
+    def device_ids(self, num_visible: int) -> List[int]:
+        return parse_devices(self.devices, num_visible)
+
+    def resident(self, num_docs: int) -> bool:
+        """Whether a segment of ``num_docs`` is uploaded to HBM (GpuIndexingOverride's decision)."""
+        return self.enabled and num_docs >= self.min_segment_docs
+
+    def offload(self, segment_docs: Sequence[int]) -> Tuple[bool, str]:
+        """Whether a query over segments of these sizes runs on the GPU, and why not when it does not."""
+        if not self.enabled:
+            return False, f"{GPU_PREFIX}enabled=false"
+        small = [i for i, n in enumerate(segment_docs) if not self.resident(n)]
+        if small:
+            return False, f"{len(small)} segment(s) below {GPU_PREFIX}min.segment.docs={self.min_segment_docs}"
+        total = sum(segment_docs)
+        if total < self.min_query_docs:
+            return False, f"{total} docs below {GPU_PREFIX}min.query.docs={self.min_query_docs}"
+        return True, ""
+
+    def plan_maker(self, ctx, timeout_ms: Optional[int] = None):
+        """A GpuPlanMaker with these settings (``timeout_ms``: the query's own budget, else the executor's)."""
+        from .plan import GpuPlanMaker
+        return GpuPlanMaker(ctx, num_groups_limit=self.num_groups_limit,
+                            max_init_group_holder_capacity=self.max_init_group_holder_capacity,
+                            exact_filter_stats=self.exact_filter_stats,
+                            timeout_ms=self.timeout_ms if timeout_ms is None else timeout_ms,
+                            gpu_topk=self.topk, min_server_group_trim_size=self.min_server_group_trim_size)
+
+
+_GPU_KEYS = ("enabled", "devices", "min.segment.docs", "min.query.docs", "exact.filter.stats", "topk")

@@ -378,9 +378,13 @@ def order_and_limit(query: QueryContext, rows: List[tuple]) -> List[tuple]:
     return rows[: query.limit]
 
 
-def table_capacity(limit: int) -> int:
-    """GroupByUtils.getTableCapacity (core/util/GroupByUtils.java:24-41): the IndexedTable's trim size."""
-    return max(5 * limit, 5000)
+DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE = 5000  # GroupByUtils.DEFAULT_MIN_NUM_GROUPS
+
+
+def table_capacity(limit: int, min_trim: int = DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE) -> int:
+    """GroupByUtils.getTableCapacity(limit, minNumGroups) (core/util/GroupByUtils.java:24-41): the IndexedTable's
+    trim size; GroupByOrderByCombineOperator.java:80-95 disables the trim for a non-positive minimum."""
+    return max(5 * limit, min_trim) if min_trim > 0 else (1 << 62)
 
 
 def topk_spec(query: QueryContext, cards: Sequence[int], k: int, key_base: int = 0) -> Optional[_lib.TopK]:
@@ -437,8 +441,12 @@ class GpuPlanMaker:
     def __init__(self, ctx: GpuContext, num_groups_limit: int = DEFAULT_NUM_GROUPS_LIMIT,
                  max_init_group_holder_capacity: int = DEFAULT_MAX_INIT_GROUP_HOLDER_CAPACITY,
                  collect_stats: bool = False, query_flags: int = 0, host_planning: bool = False,
-                 exact_filter_stats: bool = False, timeout_ms: Optional[int] = None, gpu_topk: bool = True):
+                 exact_filter_stats: bool = False, timeout_ms: Optional[int] = None, gpu_topk: bool = True,
+                 min_server_group_trim_size: int = DEFAULT_MIN_SERVER_GROUP_TRIM_SIZE):
         self.ctx = ctx
+        # pinot.server.query.executor.min.server.group.trim.size (InstancePlanMakerImplV2.java:80-84): the minimum
+        # of the server's ORDER BY trim; <= 0 disables it (every group comes back)
+        self.min_server_group_trim_size = min_server_group_trim_size
         # gpu_topk: a GROUP BY ... ORDER BY ... LIMIT query brings back only the groups the server's IndexedTable
         # keeps (table_capacity(limit), ties kept), selected on the GPU (pgpu_query_collect_topk)
         self.gpu_topk = gpu_topk
@@ -657,8 +665,9 @@ class GpuPlanMaker:
         st = QueryStats()
         h, pending.handle = pending.handle, None
         query = pending.query
-        order = (topk_spec(query, [len(g[0]) for g in pending.globals_], table_capacity(query.limit))
-                 if self.gpu_topk else None)
+        order = (topk_spec(query, [len(g[0]) for g in pending.globals_],
+                           table_capacity(query.limit, self.min_server_group_trim_size))
+                 if self.gpu_topk and self.min_server_group_trim_size > 0 else None)
         _lib.check(self.ctx._lib.pgpu_query_collect_topk(h, C.byref(order) if order is not None else None,
                                                          keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                                          cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
