@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 4
+#define PGPU_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -115,6 +115,26 @@ int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_
  * RangeIndexReaderImpl with partial matches.  The GPU answers range-index leaves from the forward index (same doc set);
  * the version decides the leaf's statistics (see PGPU_F_RANGE_INDEX). */
 int pgpu_segment_add_range_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes);
+/* Multi-value dictionary-encoded column: the file FixedBitMVForwardIndexWriter writes (`<column>.mv.fwd`,
+ * seglocal/io/writer/impl/FixedBitMVForwardIndexWriter.java:73-159): big-endian chunk offsets, a row-start bitmap
+ * over the value index, the values' dict ids fixed-bit (`bits_per_value`), `num_values` = the column metadata's
+ * totalNumberOfEntries.  Replaces FixedBitMVForwardIndexReader.getDictIdMV (seglocal/segment/index/readers/forward/
+ * FixedBitMVForwardIndexReader.java:58-140): the row offsets are found once at upload, the ids stay packed in HBM.
+ * Add the dictionary first (pgpu_segment_add_dictionary; numeric types) and optionally an inverted index.  A SCAN
+ * leaf on such a column has applyMV semantics (BaseDictionaryBasedPredicateEvaluator.java:133-149): a row matches
+ * when any of its values is in the leaf's dict-id set / range, and `negate` keeps the rows none of whose values is
+ * (the exclusive NEQ / NOT IN forms); it counts each row's length towards numEntriesScannedInFilter
+ * (MVScanDocIdIterator.java:56-100).  The column cannot be grouped on or aggregated directly (PGPU_E_UNSUPPORTED):
+ * the *MV aggregation functions read its row columns (below). */
+int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                      int32_t bits_per_value, int32_t cardinality, int64_t num_values);
+/* Per-row reductions of a multi-value column, installed as raw columns in other slots of the same segment (-1 skips
+ * one): len_column = values per row (INT), sum_column = the row's sum (LONG for INT / LONG, DOUBLE for FLOAT /
+ * DOUBLE values), min_column / max_column = the row's smallest / largest value (the column's type).  COUNTMV /
+ * SUMMV / MINMV / MAXMV / AVGMV (CountMV..AvgMVAggregationFunction: every value of every matched row) are then
+ * SUM(len) / SUM(sum) / MIN(min) / MAX(max) / SUM(sum) / SUM(len) over the matched rows. */
+int pgpu_segment_add_mv_row_columns(pgpu_segment* seg, int32_t column, int32_t len_column, int32_t sum_column,
+                                    int32_t min_column, int32_t max_column);
 int pgpu_segment_seal(pgpu_segment* seg);
 /* HBM bytes held by the segment (all columns, including padding and container directories). */
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);

@@ -12,6 +12,10 @@ References (abbreviations as in SURVEY.md):
   SVScanDocIdIterator.next/advance/applyAnd ............... core/operator/dociditerators/SVScanDocIdIterator.java:57-94
   AndDocIdIterator / OrDocIdIterator / NotDocIdIterator ... core/operator/dociditerators/*.java
   Sum/Count/Min/Max/AvgAggregationFunction ................ core/query/aggregation/function/*.java
+  multi-value: MVScanDocIdIterator (entries += row length) . core/operator/dociditerators/MVScanDocIdIterator.java:56-100
+               BaseDictionaryBasedPredicateEvaluator.applyMV core/operator/filter/predicate/
+                 (any value for inclusive, every value for exclusive)   BaseDictionaryBasedPredicateEvaluator.java:133-149
+               Count/Sum/Min/Max/AvgMVAggregationFunction . core/query/aggregation/function/*MVAggregationFunction.java
   DictionaryBasedGroupKeyGenerator (holders, limit) ........ core/query/aggregation/groupby/DictionaryBasedGroupKeyGenerator.java:100-1016
   AggregationOperator / AggregationGroupByOrderByOperator stats core/operator/query/AggregationOperator.java:58-87
   combine + broker reduce (merge, ORDER BY, LIMIT) ........ core/operator/combine/*.java, core/data/table/IndexedTable.java:103-156
@@ -31,7 +35,9 @@ from pinot_amd.query import UNBOUNDED, FilterContext, Predicate, QueryContext
 from pinot_amd.segment import SegmentData
 
 from .rawfwd import read_raw_forward
-from .segment_writer import NATIVE, read_inverted_bitmap, unpack_fixed_bit
+from .segment_writer import NATIVE, read_inverted_bitmap, read_mv_forward, unpack_fixed_bit
+
+MV_FUNCTIONS = {"COUNTMV": "COUNT", "SUMMV": "SUM", "MINMV": "MIN", "MAXMV": "MAX", "AVGMV": "AVG"}
 
 EOF = -(2 ** 31)  # Constants.EOF = Integer.MIN_VALUE
 
@@ -71,6 +77,15 @@ class DecodedSegment:
                 a = unpack_fixed_bit(c.forward, bits, self.num_docs)
             assert len(a) == self.num_docs
             self._ids[col] = a
+        return a
+
+    def mv(self, col: str):
+        """(offsets[num_docs + 1], dict ids of every value) of a multi-value column."""
+        a = self._ids.get(("mv", col))
+        if a is None:
+            c = self.seg.column(col)
+            a = read_mv_forward(c.mv_forward, self.num_docs, c.num_values, c.bits_per_value)
+            self._ids[("mv", col)] = a
         return a
 
     def raw_values(self, col: str) -> np.ndarray:
@@ -260,7 +275,15 @@ def predicate_mask(ds: DecodedSegment, p: Predicate) -> np.ndarray:
     doc's dict id — value semantics, since the dictionary holds the values)."""
     c = ds.seg.column(p.column)
     pad = _padder(c.pad_char, c.entry_width) if c.data_type == PGPU_STRING else None
-    return _truth_on_dictionary(ds.dictionary(p.column), c.data_type, p, pad)[ds.ids(p.column)]
+    truth = _truth_on_dictionary(ds.dictionary(p.column), c.data_type, p, pad)
+    if c.mv_forward is not None:
+        # applyMV: an inclusive predicate matches a row holding any matching value, an exclusive one a row whose
+        # every value passes (no excluded value) -- rows are never empty
+        off, ids = ds.mv(p.column)
+        t = truth[ids].astype(np.int8)
+        red = np.minimum.reduceat(t, off[:-1]) if p.is_exclusive else np.maximum.reduceat(t, off[:-1])
+        return red.astype(bool)
+    return truth[ds.ids(p.column)]
 
 
 # ---- physical operator tree (restated FilterOperatorUtils) ------------------------------------------------------
@@ -269,6 +292,7 @@ class POp:
     kind: str                 # EMPTY ALL SCAN RAW_SCAN BITMAP SORTED RANGE_INDEX AND OR NOT
     children: List["POp"] = field(default_factory=list)
     mask: Optional[np.ndarray] = None   # leaf doc set
+    weights: Optional[np.ndarray] = None  # multi-value scan: entries read per doc (row lengths)
 
     def priority(self) -> int:
         return {"SORTED": 0, "BITMAP": 1, "RANGE_INDEX": 2, "AND": 3, "OR": 4, "SCAN": 5,
@@ -328,15 +352,21 @@ def build_physical(ds: DecodedSegment, f: Optional[FilterContext]) -> POp:
         return POp("RANGE_INDEX", mask=m)
     if p.type != "RANGE" and col.inverted is not None:
         # the inverted index is read through its own bytes: checks the Roaring writer too
-        ids = ds.ids(p.column)
         inv_mask = np.zeros(ds.num_docs, dtype=bool)
-        matching = np.unique(ids[m]) if not p.is_exclusive else np.unique(ids[~m])
+        if col.mv_forward is not None:  # getMatchingDictIds / getNonMatchingDictIds of the dictionary
+            tr = _truth_on_dictionary(d, col.data_type, p, pad)
+            matching = np.flatnonzero(~tr if p.is_exclusive else tr)
+        else:
+            ids = ds.ids(p.column)
+            matching = np.unique(ids[m]) if not p.is_exclusive else np.unique(ids[~m])
         for i in matching:
             inv_mask[read_inverted_bitmap(col.inverted, col.cardinality, int(i))] = True
         if p.is_exclusive:
             inv_mask = ~inv_mask
         assert np.array_equal(inv_mask, m), "inverted index disagrees with forward index"
         return POp("BITMAP", mask=m)
+    if col.mv_forward is not None:
+        return POp("SCAN", mask=m, weights=np.diff(ds.mv(p.column)[0]))
     return POp("SCAN", mask=m)
 
 
@@ -364,12 +394,18 @@ def eval_mask(op: POp, n: int) -> np.ndarray:
 class _Scan:
     kind = "scan"
 
-    def __init__(self, mask: np.ndarray, counter: list):
+    def __init__(self, mask: np.ndarray, counter: list, weights: Optional[np.ndarray] = None):
         self.n = len(mask)
         self.hits = np.flatnonzero(mask)
         self.mask = mask
         self.nxt = 0
         self.counter = counter
+        self.weights = weights  # MVScanDocIdIterator: a doc read costs its row length
+        self.cum = None if weights is None else np.concatenate([[0], np.cumsum(weights)])
+
+    def _read(self, a: int, b: int) -> None:
+        """docs [a, b) read."""
+        self.counter[0] += (b - a) if self.cum is None else int(self.cum[b] - self.cum[a])
 
     def next(self):
         if self.nxt >= self.n:
@@ -377,10 +413,10 @@ class _Scan:
         i = bisect.bisect_left(self.hits, self.nxt)
         if i < len(self.hits):
             d = int(self.hits[i])
-            self.counter[0] += d - self.nxt + 1
+            self._read(self.nxt, d + 1)
             self.nxt = d + 1
             return d
-        self.counter[0] += self.n - self.nxt
+        self._read(self.nxt, self.n)
         self.nxt = self.n
         return EOF
 
@@ -389,7 +425,7 @@ class _Scan:
         return self.next()
 
     def apply_and(self, docs: np.ndarray) -> np.ndarray:
-        self.counter[0] += len(docs)
+        self.counter[0] += len(docs) if self.weights is None else int(self.weights[docs].sum())
         return docs[self.mask[docs]]
 
 
@@ -527,7 +563,7 @@ class _Not:
 def make_iterator(op: POp, n: int, counter: list):
     """FilterBlockDocIdSet.iterator() of the physical operator `op`."""
     if op.kind in ("SCAN", "RAW_SCAN"):
-        return _Scan(op.mask, counter)
+        return _Scan(op.mask, counter, op.weights)
     if op.kind in ("BITMAP", "RANGE_INDEX"):  # RangeIndexBasedFilterOperator: a BitmapDocIdSet
         return _Docs(np.flatnonzero(op.mask), "bitmap")
     if op.kind == "SORTED":
@@ -575,8 +611,20 @@ def entries_scanned_in_filter(op: POp, n: int) -> Tuple[int, np.ndarray]:
 
 
 # ---- aggregation -------------------------------------------------------------------------------------------------
-def _as_float_values(ds: DecodedSegment, col: str, docs: np.ndarray) -> np.ndarray:
-    if ds.seg.column(col).raw_forward is not None:
+def _as_float_values(ds: DecodedSegment, col: str, docs: np.ndarray, fn: str = "") -> np.ndarray:
+    c = ds.seg.column(col)
+    if (c.mv_forward is not None) != (fn in MV_FUNCTIONS):
+        raise ValueError(f"{fn} on {'a multi' if c.mv_forward is not None else 'a single'}-value column {col}")
+    if c.mv_forward is not None:
+        # the docs' values in doc order, each row's in its stored order (getDictIdMV then the dictionary)
+        off, ids = ds.mv(col)
+        if len(docs) == 0:
+            sel = np.zeros(0, dtype=np.int64)
+        else:
+            lens = off[docs + 1] - off[docs]
+            sel = np.repeat(off[docs] - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(lens.sum())
+        return ds.dictionary(col)[ids[sel]]
+    if c.raw_forward is not None:
         return ds.raw_values(col)[docs]
     d = ds.dictionary(col)
     if isinstance(d, list):
@@ -596,7 +644,10 @@ def _sum_reference(vals: np.ndarray) -> float:
 
 
 def aggregate(fn: str, vals: Optional[np.ndarray], count: int):
-    """Intermediate result of one aggregation over the matching docs of one segment."""
+    """Intermediate result of one aggregation over the matching docs of one segment (the *MV functions over the
+    docs' values: COUNTMV counts values, AVGMV divides by the value count)."""
+    if fn in MV_FUNCTIONS:
+        return aggregate(MV_FUNCTIONS[fn], vals, len(vals))
     if fn == "COUNT":
         return count
     if fn == "SUM":
@@ -612,6 +663,7 @@ def aggregate(fn: str, vals: Optional[np.ndarray], count: int):
 
 def merge(fn: str, a, b):
     """AggregationFunction.merge."""
+    fn = MV_FUNCTIONS.get(fn, fn)
     if fn in ("COUNT", "SUM"):
         return a + b
     if fn == "MIN":
@@ -623,6 +675,7 @@ def merge(fn: str, a, b):
 
 def final(fn: str, v):
     """AggregationFunction.extractFinalResult."""
+    fn = MV_FUNCTIONS.get(fn, fn)
     if fn == "AVG":
         return -math.inf if v[1] == 0 else v[0] / v[1]
     if fn == "COUNT":
@@ -635,7 +688,7 @@ def fits_non_scan(query: QueryContext, num_docs: int, seg: Optional[SegmentData]
     this path serves: aggregation-only, no FILTER clauses, only COUNT / MIN / MAX (dictionary-encoded columns).
     Empty segments are left to the scan plan (their dictionaries hold no min / max)."""
     if (query.group_by or query.has_filtered_aggregations or num_docs <= 0
-            or any(a.function not in ("COUNT", "MIN", "MAX") for a in query.aggregations)):
+            or any(a.function not in ("COUNT", "MIN", "MAX", "MINMV", "MAXMV") for a in query.aggregations)):
         return False
     # raw columns: MIN / MAX come from the column metadata's min / max values, when it has them (METADATA_BASED_FUNCTIONS)
     return seg is None or all(seg.column(a.column).raw_forward is None or
@@ -671,7 +724,7 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
                 agg.append(float(c.min_value if a.function == "MIN" else c.max_value))
             else:
                 d = ds.dictionary(a.column)
-                agg.append(float(d[0] if a.function == "MIN" else d[-1]))
+                agg.append(float(d[0] if a.function in ("MIN", "MINMV") else d[-1]))
         return SegmentResult(aggregation=agg, num_docs_scanned=n, num_total_docs=n)
     mask = eval_mask(op, n)
     docs = np.flatnonzero(mask)
@@ -681,9 +734,12 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
         assert np.array_equal(it_docs, docs), "iterator model disagrees with the mask algebra"
     res.num_entries_scanned_post_filter = len(docs) * len(query.projected_columns)
     if not query.group_by:
-        res.aggregation = [aggregate(a.function, None if a.column is None else _as_float_values(ds, a.column, docs),
-                                     len(docs)) for a in query.aggregations]
+        res.aggregation = [aggregate(a.function, None if a.column is None else
+                                     _as_float_values(ds, a.column, docs, a.function), len(docs))
+                           for a in query.aggregations]
         return res
+    if any(ds.seg.column(g).mv_forward is not None for g in query.group_by):
+        raise NotImplementedError("GROUP BY a multi-value column")
     # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long)
     cards = [ds.seg.column(g).cardinality for g in query.group_by]
     prod = 1
@@ -712,7 +768,7 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
             v = d[int(uniq[part_g[0], j])]
             vals.append(v.item() if hasattr(v, "item") else v)
         groups[tuple(vals)] = [aggregate(a.function, None if a.column is None else
-                                         _as_float_values(ds, a.column, part_docs), len(part_docs))
+                                         _as_float_values(ds, a.column, part_docs, a.function), len(part_docs))
                                for a in query.aggregations]
     res.groups = groups
     return res

@@ -14,6 +14,11 @@
                     2 + 4*runs bytes are smaller than the array / bitmap form)
 * inverted index    BitmapInvertedIndexWriter: (card+1) big-endian int32 absolute offsets, then the bitmaps
                     (seglocal/segment/creator/impl/inv/BitmapInvertedIndexWriter.java:35-124)
+* MV forward index  FixedBitMVForwardIndexWriter: big-endian int32 chunk offsets (value index of each chunk's first
+                    row; ceil(2048 / (numValues / numDocs)) rows per chunk), a row-start bitmap over the value
+                    index (PinotDataBitSet.setBit, MSB-first), then the values' dict ids fixed-bit
+                    (seglocal/io/writer/impl/FixedBitMVForwardIndexWriter.java:73-159,
+                     seglocal/segment/index/readers/forward/FixedBitMVForwardIndexReader.java:58-140)
 """
 from __future__ import annotations
 
@@ -81,6 +86,50 @@ def read_int(data: bytes, index: int, bits: int) -> int:
         cur = (cur << 8) | data[byte]
         left -= 8
     return (cur << left) | (data[byte + 1] >> (8 - left))
+
+
+# ---- multi-value forward index ---------------------------------------------------------------------------------
+def mv_docs_per_chunk(num_docs: int, num_values: int) -> int:
+    """FixedBitMVForwardIndexWriter.java:77-78: ceil(2048 / (float)(totalNumValues / numDocs)), integer division
+    inside (the reader repeats it, FixedBitMVForwardIndexReader.java:61)."""
+    avg = num_values // num_docs
+    return int(np.ceil(np.float32(2048) / np.float32(avg)))
+
+
+def write_mv_forward(rows: Sequence[np.ndarray], bits: int) -> bytes:
+    """FixedBitMVForwardIndexWriter file of per-row dict-id arrays (every row holds at least one value, as the
+    segment creator's null-default placeholder guarantees)."""
+    num_docs = len(rows)
+    lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=num_docs)
+    if num_docs == 0 or np.any(lens == 0):
+        raise ValueError("multi-value rows must hold at least one value")
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    num_values = int(lens.sum())
+    per = mv_docs_per_chunk(num_docs, num_values)
+    chunks = starts[::per].astype(">i4").tobytes()
+    bitmap = np.zeros((num_values + 7) // 8 * 8, dtype=np.uint8)
+    bitmap[starts] = 1
+    ids = np.concatenate([np.asarray(r, dtype=np.int64) for r in rows])
+    return chunks + np.packbits(bitmap).tobytes() + pack_fixed_bit(ids, bits)
+
+
+def read_mv_forward(data: bytes, num_docs: int, num_values: int, bits: int):
+    """(offsets[num_docs + 1], dict ids[num_values]) of a FixedBitMVForwardIndexWriter file, found through the
+    row-start bitmap as FixedBitMVForwardIndexReader.getDictIdMV finds a row (its chunk offsets only speed that up;
+    they are checked here)."""
+    per = mv_docs_per_chunk(num_docs, num_values)
+    nchunks = (num_docs + per - 1) // per
+    hdr = 4 * nchunks
+    nb = (num_values + 7) // 8
+    bm = np.unpackbits(np.frombuffer(data, dtype=np.uint8, count=nb, offset=hdr))[:num_values]
+    starts = np.flatnonzero(bm)
+    if len(starts) != num_docs or (num_docs and starts[0] != 0):
+        raise ValueError("row-start bitmap does not hold one start per row")
+    chunks = np.frombuffer(data, dtype=">i4", count=nchunks)
+    if not np.array_equal(chunks.astype(np.int64), starts[::per]):
+        raise ValueError("chunk offsets disagree with the row-start bitmap")
+    ids = unpack_fixed_bit(data[hdr + nb:], bits, num_values)
+    return np.concatenate([starts, [num_values]]).astype(np.int64), ids
 
 
 # ---- dictionaries ----------------------------------------------------------------------------------------------
@@ -258,7 +307,7 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
                   sorted_columns: Optional[Iterable[str]] = None, allow_runs: bool = True,
                   raw: Iterable[str] = (), raw_codec: int = 0, raw_version: int = 2,
                   range_index: Iterable[str] = (), range_index_version: int = 2,
-                  raw_min_max: bool = True) -> SegmentData:
+                  raw_min_max: bool = True, mv: Iterable[str] = ()) -> SegmentData:
     """Build an immutable segment from raw column values.
 
     `columns`: name -> (data_type, values).  A column is stored with a sorted index when its dict ids are
@@ -267,11 +316,14 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
     `raw`: no-dictionary columns (noDictionaryColumns), written as FixedByteChunkSVForwardIndexWriter files with
     `raw_codec` / `raw_version` (oracle/rawfwd.py); `raw_min_max` records their metadata min / max.
     `range_index`: columns with a range index (rangeIndexColumns) of `range_index_version` (header only, see
-    oracle.rawfwd.range_index_header)."""
+    oracle.rawfwd.range_index_header).
+    `mv`: multi-value columns; their values are a sequence of per-row value arrays (FixedBitMVForwardIndexWriter;
+    an inverted index lists every doc holding the id)."""
     from .rawfwd import range_index_header, write_raw_forward
     inverted = set(inverted)
     raw = set(raw)
     range_index = set(range_index)
+    mv = set(mv)
     n = None
     seg = None
     for cname, (dt, values) in columns.items():
@@ -280,6 +332,31 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Iterable[str] 
             seg = SegmentData(name, n)
         if len(values) != n:
             raise ValueError("ragged columns")
+        if cname in mv:
+            rows = [np.asarray(r, dtype=NATIVE[dt]) if dt != PGPU_STRING else list(r) for r in values]
+            flat = np.concatenate(rows) if dt != PGPU_STRING else [v for r in rows for v in r]
+            uniq, ids = build_dictionary(flat, dt)
+            card = len(uniq)
+            lens = np.fromiter((len(r) for r in rows), dtype=np.int64, count=n)
+            starts = np.concatenate([[0], np.cumsum(lens)])
+            id_rows = [ids[starts[i]:starts[i + 1]] for i in range(n)]
+            col = ColumnIndexes(cname, dt, card, dictionary=(list(uniq) if dt == PGPU_STRING
+                                                              else dictionary_bytes(uniq, dt)),
+                                mv_forward=write_mv_forward(id_rows, bits_per_value(card)),
+                                num_values=int(lens.sum()), max_values=int(lens.max()) if n else 0)
+            if cname in inverted:
+                docs = np.repeat(np.arange(n, dtype=np.int64), lens)
+                pairs = np.unique(np.stack([ids.astype(np.int64), docs], axis=1), axis=0)
+                order = np.argsort(pairs[:, 0], kind="stable")
+                bounds = np.searchsorted(pairs[order, 0], np.arange(card + 1))
+                blobs = [roaring_serialize(pairs[order[bounds[i]:bounds[i + 1]], 1], allow_runs)
+                         for i in range(card)]
+                offs = [4 * (card + 1)]
+                for b in blobs:
+                    offs.append(offs[-1] + len(b))
+                col.inverted = np.asarray(offs, dtype=">i4").tobytes() + b"".join(blobs)
+            seg.columns[cname] = col
+            continue
         if cname in raw:
             vals = np.asarray(values, dtype=NATIVE[dt])
             col = ColumnIndexes(cname, dt, len(np.unique(vals)) if n else 0,
@@ -354,6 +431,21 @@ def write_segment_dir(seg: SegmentData, path: str, version: str = "v3", pad_char
             dbytes, width = string_dictionary_bytes(list(c.dictionary), pad)
         else:
             dbytes, width = bytes(c.dictionary), 0
+        if c.mv_forward is not None:  # multi-value column (isSingleValues = false)
+            meta += [f"column.{c.name}.cardinality = {c.cardinality}", f"column.{c.name}.totalDocs = {seg.num_docs}",
+                     f"column.{c.name}.dataType = {_TYPE_NAME[c.data_type]}",
+                     f"column.{c.name}.bitsPerElement = {bits_per_value(c.cardinality)}",
+                     f"column.{c.name}.lengthOfEachEntry = {width}", f"column.{c.name}.isSorted = false",
+                     f"column.{c.name}.hasDictionary = true",
+                     f"column.{c.name}.hasInvertedIndex = {'true' if c.inverted is not None else 'false'}",
+                     f"column.{c.name}.isSingleValues = false",
+                     f"column.{c.name}.maxNumberOfMultiValues = {c.max_values}",
+                     f"column.{c.name}.totalNumberOfEntries = {c.num_values}"]
+            indexes.append((c.name, "dictionary", ".dict", dbytes))
+            indexes.append((c.name, "forward_index", ".mv.fwd", bytes(c.mv_forward)))
+            if c.inverted is not None:
+                indexes.append((c.name, "inverted_index", ".bitmap.inv", bytes(c.inverted)))
+            continue
         sorted_col = c.sorted_index is not None
         meta += [f"column.{c.name}.cardinality = {c.cardinality}", f"column.{c.name}.totalDocs = {seg.num_docs}",
                  f"column.{c.name}.dataType = {_TYPE_NAME[c.data_type]}",

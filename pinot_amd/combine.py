@@ -32,7 +32,8 @@ from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
 from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
-                   key_words_out, merge_filtered, table_capacity, topk_spec)
+                   has_mv_aggregations, key_words_out, merge_filtered, mv_lower, mv_raise, table_capacity,
+                   topk_spec)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
@@ -533,6 +534,12 @@ class DistributedExecutor:
             res = self.pm.execute(query, segments)
             self.last_stats = res.stats
             return res
+        if has_mv_aggregations(query):
+            # *MV aggregations over the multi-value columns' row columns (pinot_amd/mv.py), raised on rank 0
+            check_group_columns(query, segments)
+            low, mv_parts = mv_lower(query)
+            res = self.execute(low, segments)
+            return None if res is None else mv_raise(query, mv_parts, res)
         if query.has_filtered_aggregations:
             # one reduced pass per FILTER clause plus the main pass (FilteredAggregationOperator), merged on rank 0
             parts = split_filtered_aggregations(query)

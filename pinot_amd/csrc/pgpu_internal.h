@@ -65,6 +65,9 @@
 // dictionary gather of the aggregation paths reads the value directly.  Predicates on it become per-segment match
 // bitmaps (rawpred_kernel) read by PGPU_I_BITS leaves.
 #define PGPU_COL_RAW 3
+// Multi-value dictionary column: DevColumn::fwd holds the values' dict ids fixed-bit (value index order); its row
+// offsets live beside it.  SCAN leaves on it become per-segment match bitmaps (mvpred_kernel) read as PGPU_I_BITS.
+#define PGPU_COL_MV 4
 
 // Roaring container types
 #define PGPU_CT_ARRAY 0
@@ -194,6 +197,20 @@ struct RawLeaf {
   int64_t lo, hi;       // RANGE bounds: int64 (INT / LONG) or double bits (FLOAT / DOUBLE)
   const int64_t* vals;  // SET: int64 values ascending (INT / LONG) or order-preserving keys of the doubles ascending
 };
+// A SCAN leaf on a multi-value column (applyMV): bit d set when any value of row d is in [lo, hi) (RANGE) or in the
+// id set (SET), complemented within [0, num_docs) when negate.
+struct MvLeaf {
+  const uint32_t* fwd;  // the values' dict ids, fixed-bit MSB-first (the file's raw-data section), padded
+  const int32_t* off;   // num_docs + 1 row offsets into the value index
+  const uint32_t* set;  // SET: membership bits over dict ids (bit id % 32 of word id / 32); null for RANGE
+  uint32_t* out;        // ntiles * 64 words; bit d % 32 of word d / 32, 0 past num_docs
+  int32_t num_docs;
+  int32_t words;
+  int32_t bits;
+  int32_t lo, hi;       // RANGE: lo <= id < hi
+  int32_t negate;
+};
+
 #define PGPU_RAW_RANGE_LO_INCL 1
 #define PGPU_RAW_RANGE_HI_INCL 2
 #define PGPU_RAW_RANGE_ORDINAL 4  // range-index semantics for FLOAT / DOUBLE: NaN orders as -infinity (FPOrdering)
@@ -310,6 +327,7 @@ struct DevParams {
   int32_t key_split;
   int32_t segmask_rows;
   int32_t cancel_poll;            // self-loading waves: tiles between cancel polls (PGPU_CANCEL_POLL, env override)
+  int32_t rd_planes;              // register-direct: planes per tile held in VGPRs (>= every leaf's width; 8/10/12/16)
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

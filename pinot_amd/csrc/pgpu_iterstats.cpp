@@ -69,20 +69,24 @@ struct Iter {
 };
 
 // SVScanDocIdIterator: every doc from the resume position up to (and including) the next match is read.
+// MVScanDocIdIterator (MVScanDocIdIterator.java:56-100) is the same walk reading each row's length in entries:
+// `off` (row offsets) turns a doc range into its entry count.
 struct ScanIter : Iter {
   const BitSet* bits;
   int32_t nxt = 0;
   int64_t* counter;
-  ScanIter(const BitSet* b, int64_t* c) : bits(b), counter(c) { kind = SCAN; }
+  const int32_t* off;
+  ScanIter(const BitSet* b, int64_t* c, const int32_t* o = nullptr) : bits(b), counter(c), off(o) { kind = SCAN; }
+  int64_t entries(int32_t a, int32_t b) const { return off ? (int64_t)off[b] - off[a] : (int64_t)b - a; }
   int32_t next() override {
     if (nxt >= bits->n) return kEOF;
     const int32_t d = bits->next(nxt);
     if (d != kEOF) {
-      *counter += (int64_t)d - nxt + 1;
+      *counter += entries(nxt, d + 1);
       nxt = d + 1;
       return d;
     }
-    *counter += (int64_t)bits->n - nxt;
+    *counter += entries(nxt, bits->n);
     nxt = bits->n;
     return kEOF;
   }
@@ -92,7 +96,15 @@ struct ScanIter : Iter {
   }
   // applyAnd: reads one entry per candidate doc
   void apply_and(BitSet& docs) const {
-    *counter += docs.count();
+    if (!off) {
+      *counter += docs.count();
+    } else {
+      for (size_t i = 0; i < docs.w.size(); ++i)
+        for (uint64_t m = docs.w[i]; m; m &= m - 1) {
+          const int32_t d = (int32_t)(i * 64 + __builtin_ctzll(m));
+          *counter += (int64_t)off[d + 1] - off[d];
+        }
+    }
     for (size_t i = 0; i < docs.w.size(); ++i) docs.w[i] &= bits->w[i];
   }
 };
@@ -281,12 +293,13 @@ struct Builder {
   const std::vector<BitSet>* leaves;
   int32_t n;
   int64_t* counter;
+  const int32_t* const* leaf_off;  // per leaf: multi-value row offsets or null (may be null altogether)
 
   std::unique_ptr<Iter> make(const Node& x) {
     switch (x.op) {
       case PGPU_F_SCAN:
       case PGPU_F_RAW_SCAN:  // SVScanDocIdIterator over raw values counts like the dictionary scan
-        return std::unique_ptr<Iter>(new ScanIter(&(*leaves)[x.leaf], counter));
+        return std::unique_ptr<Iter>(new ScanIter(&(*leaves)[x.leaf], counter, leaf_off ? leaf_off[x.leaf] : nullptr));
       case PGPU_F_RANGE_INDEX:  // RangeIndexBasedFilterOperator: a BitmapDocIdSet of the exact index's matches
       case PGPU_F_INVERTED:
         return std::unique_ptr<Iter>(new DocsIter(std::make_shared<BitSet>((*leaves)[x.leaf]), BITMAP));
@@ -368,7 +381,7 @@ struct Builder {
 // leaf_words[k] = match bits of leaf k (prefix order), doc d at bit d % 32 of word d / 32.  Returns -1 on a
 // malformed program.
 int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
-                                  int num_leaves, int32_t num_docs) {
+                                  int num_leaves, int32_t num_docs, const int32_t* const* leaf_offsets) {
   if (num_nodes <= 0) return 0;
   Node root;
   int leaf = 0;
@@ -377,7 +390,7 @@ int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, 
   leaves.reserve(num_leaves);
   for (int k = 0; k < num_leaves; ++k) leaves.push_back(BitSet::from_words32(leaf_words[k], num_docs));
   int64_t counter = 0;
-  Builder b{&leaves, num_docs, &counter};
+  Builder b{&leaves, num_docs, &counter, leaf_offsets};
   std::unique_ptr<Iter> it = b.make(root);
   while (it->next() != kEOF) {
   }
@@ -439,7 +452,7 @@ extern "C" int pgpu_filter_entries_scanned(const pgpu_filter_node* nodes, int32_
                                            int64_t* out) {
   if (!out || num_docs < 0 || num_leaves < 0 || (num_nodes > 0 && !nodes) || (num_leaves > 0 && !leaf_bits))
     return PGPU_E_INVALID;
-  const int64_t c = reference_entries_scanned(nodes, num_nodes, leaf_bits, num_leaves, num_docs);
+  const int64_t c = reference_entries_scanned(nodes, num_nodes, leaf_bits, num_leaves, num_docs, nullptr);
   if (c < 0) return PGPU_E_INVALID;
   *out = c;
   return PGPU_OK;

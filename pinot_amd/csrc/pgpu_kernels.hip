@@ -2200,12 +2200,11 @@ FI void direct_epilogue(const DevParams& p, const Lds& L, const Stats& st, int w
 
 // ================================================================================================================
 // REGISTER-DIRECT variant (p.direct == 2): every segment's only staged column is one bit-sliced fast leaf of at most
-// PGPU_RDIRECT_PLANES bits.  Its planes go straight into VGPRs -- plane k of lane l is one coalesced 4-B load per
+// PL = p.rd_planes bits (8, 10, 12 or 16: the borrow chains cost one v_bitop3 per plane, so PL tracks the width).  Its planes go straight into VGPRs -- plane k of lane l is one coalesced 4-B load per
 // lane, 256 B per wave-instruction -- with RD tiles in flight per wave (a register ring, unrolled), no LDS staging
 // at all: tools/stream_bench.hip reads such a stream at 5.6-6.0 TB/s where the LDS-DMA self-loading kernel
 // streamed 3.8 TB/s (its in-flight bytes are bounded by the LDS slots).  Candidate handling as in direct_consumer.
 // ================================================================================================================
-#define PGPU_RDIRECT_PLANES 16
 #define PGPU_RDIRECT_DEPTH 2
 struct RdIssue {  // the issue cursor's segment: its sliced column
   const uint32_t* sliced;
@@ -2218,22 +2217,25 @@ FI void rd_load_issue(const DevParams& p, int seg, RdIssue& is) {
   is.sliced = (const uint32_t*)cld(&cols[qc].sliced);
   is.bits = cld(&cols[qc].bits);
 }
-FI void rd_load_tile(const RdIssue& is, int tile_in_seg, uint32_t (&x)[PGPU_RDIRECT_PLANES]) {
+template <int PL>
+FI void rd_load_tile(const RdIssue& is, int tile_in_seg, uint32_t (&x)[PL]) {
   const uint32_t* src = is.sliced + (size_t)tile_in_seg * is.bits * 64 + lane_id();
 #pragma unroll
-  for (int k = 0; k < PGPU_RDIRECT_PLANES; ++k)
+  for (int k = 0; k < PL; ++k)
     x[k] = k < is.bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;  // planes past the width: 0 (inert below)
 }
 // The fast leaf on register planes: OR of dict-id ranges [lo, hi) (x < c as a borrow chain; planes past the
 // column's width are 0 and leave the chain unchanged, and c = 2^bits sets the borrow there), then negated.
-FI uint32_t rd_lt(const uint32_t (&x)[PGPU_RDIRECT_PLANES], uint32_t c) {
+template <int PL>
+FI uint32_t rd_lt(const uint32_t (&x)[PL], uint32_t c) {
   uint32_t br = 0;
 #pragma unroll
-  for (int k = 0; k < PGPU_RDIRECT_PLANES; ++k)
+  for (int k = 0; k < PL; ++k)
     br = __builtin_amdgcn_bitop3_b32((uint32_t)-(int32_t)((c >> k) & 1u), x[k], br, 0xB2);
-  return (c >> PGPU_RDIRECT_PLANES) ? ~0u : br;
+  return (c >> PL) ? ~0u : br;
 }
-FI uint32_t rd_filter(const SegState& ss, const uint32_t (&x)[PGPU_RDIRECT_PLANES], uint32_t valid,
+template <int PL>
+FI uint32_t rd_filter(const SegState& ss, const uint32_t (&x)[PL], uint32_t valid,
                       uint32_t& lane_scanned) {
   if (!(ss.f_kind[0] >> 8)) lane_scanned += __popc(valid);
   uint32_t m = rd_lt(x, ss.f_r0hi[0]) & ~rd_lt(x, ss.f_r0lo[0]);
@@ -2244,7 +2246,7 @@ FI uint32_t rd_filter(const SegState& ss, const uint32_t (&x)[PGPU_RDIRECT_PLANE
   return valid & (ss.f_sneg[0] ? ~m : m);
 }
 
-template <int MODE>
+template <int MODE, int PL>
 FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
   constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH;
   const int64_t t_start = now(pf);
@@ -2274,7 +2276,7 @@ FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
     Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
     RdIssue is;
     rd_load_issue(p, ci.seg, is);
-    uint32_t x[RD][PGPU_RDIRECT_PLANES];
+    uint32_t x[RD][PL];
 #pragma unroll
     for (int s = 0; s < RD; ++s) {
       if (s < own) {
@@ -2355,7 +2357,7 @@ FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
   return st;
 }
 
-template <int MODE>
+template <int MODE, int PL>
 __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevParams p) {
   constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
@@ -2378,7 +2380,7 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevP
 #pragma unroll
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
-  const Stats st = rdirect_consumer<MODE>(p, L, wave, t0, t1 - t0, pf);
+  const Stats st = rdirect_consumer<MODE, PL>(p, L, wave, t0, t1 - t0, pf);
   direct_epilogue<MODE>(p, L, st, wave, lane, pf);
 }
 
@@ -3184,6 +3186,11 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 }  // namespace
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
+template <int M, int PL>
+static hipError_t rd_attr(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void*)query_kernel_rdirect<M, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
 // Per aggregation mode (one translation unit each): launch the ring or direct query kernel, set its LDS attribute.
 #define PGPU_MODE_FUNCS(M, NAME)                                                                                  \
   hipError_t pgpu_launch_query_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {          \
@@ -3192,9 +3199,16 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    if (p.direct == 2)                                                                                          \
-      hipLaunchKernelGGL((query_kernel_rdirect<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);    \
-    else                                                                                                        \
+    if (p.direct == 2) {                                                                                        \
+      if (p.rd_planes <= 8)                                                                                     \
+        hipLaunchKernelGGL((query_kernel_rdirect<M, 8>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+      else if (p.rd_planes <= 10)                                                                               \
+        hipLaunchKernelGGL((query_kernel_rdirect<M, 10>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+      else if (p.rd_planes <= 12)                                                                               \
+        hipLaunchKernelGGL((query_kernel_rdirect<M, 12>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+      else                                                                                                      \
+        hipLaunchKernelGGL((query_kernel_rdirect<M, 16>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+    } else                                                                                                      \
       hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);     \
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
@@ -3207,9 +3221,10 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
     if (e == hipSuccess)                                                                                        \
       e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                               (int)lds_bytes);                                                                  \
-    if (e == hipSuccess)                                                                                        \
-      e = hipFuncSetAttribute((const void*)query_kernel_rdirect<M>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                              (int)lds_bytes);                                                                  \
+    if (e == hipSuccess) e = rd_attr<M, 8>(lds_bytes);                                                          \
+    if (e == hipSuccess) e = rd_attr<M, 10>(lds_bytes);                                                         \
+    if (e == hipSuccess) e = rd_attr<M, 12>(lds_bytes);                                                         \
+    if (e == hipSuccess) e = rd_attr<M, 16>(lds_bytes);                                                         \
     return e;                                                                                                   \
   }
 #define PGPU_MODE_DECLS(NAME)                                                                   \
@@ -3389,6 +3404,43 @@ __global__ __launch_bounds__(256) void rawpred_kernel(const RawLeaf* leaves) {
     if (w4) rawpred_wave<4>(L, c, lane);
     else rawpred_wave<8>(L, c, lane);
   }
+}
+
+// ---- multi-value SCAN leaves: one lane per row, 64 rows per ballot ------------------------------------------------
+// PinotDataBitSet.readInt of value v (MSB-first): the 64-bit big-endian window of the two 32-bit words holding it.
+FI uint32_t mv_read(const uint32_t* fwd, int64_t bit, int bits) {
+  const int64_t w = bit >> 5;
+  const uint64_t hi = __builtin_bswap32(__builtin_nontemporal_load(fwd + w));
+  const uint64_t lo = __builtin_bswap32(__builtin_nontemporal_load(fwd + w + 1));
+  const uint64_t win = (hi << 32) | lo;
+  return (uint32_t)((win >> (64 - (int)(bit & 31) - bits)) & ((1ull << bits) - 1));
+}
+
+__global__ __launch_bounds__(256) void mvpred_kernel(const MvLeaf* leaves) {
+  const MvLeaf L = cld(leaves + blockIdx.y);
+  const int lane = threadIdx.x & 63;
+  const int64_t nblk = L.words / 2;  // 64 rows per block
+  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < nblk; b += (int64_t)gridDim.x * 4) {
+    const int64_t d = b * 64 + lane;
+    bool hit = false;
+    if (d < L.num_docs) {
+      const int32_t s = L.off[d], e = L.off[d + 1];
+      for (int32_t v = s; v < e && !hit; ++v) {  // applyMV: the first matching value decides
+        const uint32_t id = mv_read(L.fwd, (int64_t)v * L.bits, L.bits);
+        hit = L.set ? ((L.set[id >> 5] >> (id & 31)) & 1u) != 0 : ((int32_t)id >= L.lo && (int32_t)id < L.hi);
+      }
+      hit = hit != (L.negate != 0);
+    }
+    const uint64_t m = __ballot(hit);
+    if (lane < 2) L.out[2 * b + lane] = (uint32_t)(lane ? (m >> 32) : m);
+  }
+}
+
+hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {
+  if (nleaves <= 0) return hipSuccess;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(4096, (max_words / 2 + 3) / 4));
+  hipLaunchKernelGGL(mvpred_kernel, dim3((unsigned)blocks, (unsigned)nleaves), dim3(256), 0, st, dev_leaves);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {

@@ -51,12 +51,13 @@ hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 // pgpu_iterstats.cpp
 int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
-                                  int num_leaves, int32_t num_docs);
+                                  int num_leaves, int32_t num_docs, const int32_t* const* leaf_offsets = nullptr);
 bool pgpu_filter_count_is_reference(const pgpu_filter_node* nodes, int num_nodes);
 // pgpu_rawfwd.cpp
 int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t num_docs, std::vector<uint8_t>* out,
                             std::string* err);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
+hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 
 namespace {
 
@@ -222,6 +223,11 @@ struct HostColumn {
   double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
   int32_t range_index = 0;             // range index version (2 = exact bit-sliced, 1 = legacy), 0 = none
   uint64_t dict_hash[2] = {0, 0};      // two independent 64-bit hashes of the dictionary bytes (shared-dict checks)
+  // multi-value column (PGPU_COL_MV): fwd = the values' ids fixed-bit, mv_off = row offsets (num_docs + 1)
+  DevMem mv_off;
+  std::vector<int32_t> mv_offsets;     // host copy (row lengths: exact filter statistics, row columns)
+  std::vector<uint8_t> mv_raw;         // host copy of the packed ids until seal (row columns)
+  int64_t mv_values = 0;
 };
 
 }  // namespace
@@ -254,7 +260,9 @@ struct pgpu_query {
     std::vector<std::vector<int32_t>> ids;
     int32_t num_docs = 0, num_leaves = 0, ntiles = 0;
     int64_t bits_off = 0;
+    std::vector<const int32_t*> leaf_off;  // per leaf: row offsets of a multi-value SCAN leaf, else null
   };
+  int64_t mv_entries = 0;  // entries of multi-value SCAN leaves that are a segment's whole filter (kernel: nostat)
   std::vector<FilterReplay> replay;
   bool exact_filter = false;
   hipEvent_t done = nullptr;  // submitted queries: recorded after the last copy of this query
@@ -690,6 +698,137 @@ int pgpu_segment_add_range_index(pgpu_segment* seg, int32_t column, const void* 
   return PGPU_OK;
 }
 
+int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
+                                      int32_t bits_per_value, int32_t cardinality, int64_t num_values) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  const int32_t n = seg->num_docs;
+  if (bits_per_value < 1 || bits_per_value > 31 || cardinality < 1 || !bytes || n < 1 || num_values < n ||
+      num_values > INT32_MAX)
+    return fail(PGPU_E_INVALID, "MV forward index of column %d: bits %d, cardinality %d, %lld values, %d docs", column,
+                bits_per_value, cardinality, (long long)num_values, n);
+  HostColumn& c = seg->cols[column];
+  if (c.kind != PGPU_COL_NONE) return fail(PGPU_E_INVALID, "column %d already has a forward index", column);
+  if (c.dict_type == PGPU_STRING) return fail(PGPU_E_UNSUPPORTED, "multi-value STRING column %d", column);
+  // FixedBitMVForwardIndexWriter.java:77-87: ceil(2048 / (float)(numValues / numDocs)) rows per chunk
+  const float avg = (float)(num_values / n);
+  const int64_t per = (int64_t)std::ceil(2048.0f / avg);
+  const int64_t nchunks = (n + per - 1) / per;
+  const uint64_t hdr = 4ull * nchunks, bm = ((uint64_t)num_values + 7) / 8;
+  const uint64_t raw = ((uint64_t)num_values * bits_per_value + 7) / 8;
+  if (num_bytes < hdr + bm + raw)
+    return fail(PGPU_E_INVALID, "MV forward index of column %d: %llu bytes < %llu", column, (unsigned long long)num_bytes,
+                (unsigned long long)(hdr + bm + raw));
+  const uint8_t* b = (const uint8_t*)bytes;
+  std::vector<int32_t> off;
+  off.reserve((size_t)n + 1);
+  for (int64_t v = 0; v < num_values; ++v)  // row starts: PinotDataBitSet bits, MSB first
+    if ((b[hdr + (v >> 3)] >> (7 - (v & 7))) & 1) off.push_back((int32_t)v);
+  if ((int64_t)off.size() != n || off[0] != 0)
+    return fail(PGPU_E_INVALID, "MV forward index of column %d: %zu row starts for %d docs", column, off.size(), n);
+  for (int64_t k = 0; k < nchunks; ++k)  // the chunk offsets must agree (a corrupt file fails here, not in a kernel)
+    if ((int64_t)(int32_t)be32(b + 4 * k) != off[k * per])
+      return fail(PGPU_E_INVALID, "MV forward index of column %d: chunk %lld offset disagrees with the bitmap", column,
+                  (long long)k);
+  off.push_back((int32_t)num_values);
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.fwd, b + hdr + bm, raw, raw + 16, PGPU_MEM_HOST));
+  HIP_TRY(upload(c.mv_off, off.data(), off.size() * 4, off.size() * 4, PGPU_MEM_HOST));
+  c.mv_raw.assign(b + hdr + bm, b + hdr + bm + raw);
+  c.mv_raw.resize(raw + 8, 0);
+  c.mv_offsets.swap(off);
+  c.mv_values = num_values;
+  c.kind = PGPU_COL_MV;
+  c.bits = bits_per_value;
+  c.fwd_card = cardinality;
+  c.fwd_bytes = num_bytes;
+  return PGPU_OK;
+}
+
+namespace {
+// Install host little-endian values as a raw column in `slot` (padded like a decoded raw forward index).
+int install_raw(pgpu_segment* seg, int32_t slot, int32_t data_type, std::vector<uint8_t>& le, double max_abs) {
+  int rc = check_column(seg, slot);
+  if (rc) return rc;
+  HostColumn& c = seg->cols[slot];
+  if (c.kind != PGPU_COL_NONE || c.dict_card) return fail(PGPU_E_INVALID, "row column slot %d is not empty", slot);
+  const int w = type_width(data_type);
+  const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
+  const uint64_t alloc = std::max<uint64_t>(1, ntiles) * PGPU_TILE * w + 16;
+  HIP_TRY(upload(c.dict, le.data(), le.size(), alloc, PGPU_MEM_HOST));
+  c.kind = PGPU_COL_RAW;
+  c.dict_type = data_type;
+  c.fwd_card = seg->num_docs;
+  c.dict_bytes = le.size();
+  c.max_abs = max_abs;
+  return PGPU_OK;
+}
+}  // namespace
+
+int pgpu_segment_add_mv_row_columns(pgpu_segment* seg, int32_t column, int32_t len_column, int32_t sum_column,
+                                    int32_t min_column, int32_t max_column) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  const HostColumn& c = seg->cols[column];
+  if (c.kind != PGPU_COL_MV || c.mv_raw.empty())
+    return fail(PGPU_E_INVALID, "column %d: no multi-value forward index (or the segment is sealed)", column);
+  if (c.hdict.empty() || c.dict_card != c.fwd_card)
+    return fail(PGPU_E_INVALID, "column %d: row columns need the numeric dictionary first", column);
+  const int32_t n = seg->num_docs, t = c.dict_type;
+  const bool fp = t == PGPU_FLOAT || t == PGPU_DOUBLE;
+  const int w = type_width(t);
+  auto value = [&](uint32_t id, int64_t* iv, double* dv) {
+    if (t == PGPU_INT) { int32_t x; memcpy(&x, &c.hdict[4 * (size_t)id], 4); *iv = x; *dv = x; }
+    else if (t == PGPU_LONG) { int64_t x; memcpy(&x, &c.hdict[8 * (size_t)id], 8); *iv = x; *dv = (double)x; }
+    else if (t == PGPU_FLOAT) { float x; memcpy(&x, &c.hdict[4 * (size_t)id], 4); *iv = 0; *dv = x; }
+    else { double x; memcpy(&x, &c.hdict[8 * (size_t)id], 8); *iv = 0; *dv = x; }
+  };
+  std::vector<uint8_t> lens(4 * (size_t)n), sums(8 * (size_t)n), mins(w * (size_t)n), maxs(w * (size_t)n);
+  double max_len = 0, max_sum = 0, max_val = c.max_abs;
+  const uint8_t* raw = c.mv_raw.data();
+  const int bits = c.bits;
+  for (int32_t d = 0; d < n; ++d) {
+    const int32_t s0 = c.mv_offsets[d], e0 = c.mv_offsets[d + 1];
+    const int32_t len = e0 - s0;
+    memcpy(&lens[4 * (size_t)d], &len, 4);
+    max_len = std::max(max_len, (double)len);
+    int64_t isum = 0;
+    double dsum = 0;
+    uint32_t lo_id = UINT32_MAX, hi_id = 0;
+    for (int32_t v = s0; v < e0; ++v) {
+      const uint64_t bit = (uint64_t)v * bits;
+      const uint8_t* q = raw + (bit >> 3);
+      uint64_t win = 0;
+      for (int k = 0; k < 8; ++k) win = (win << 8) | q[k];
+      const uint32_t id = (uint32_t)((win >> (64 - (int)(bit & 7) - bits)) & ((1ull << bits) - 1));
+      if (id >= (uint32_t)c.dict_card) return fail(PGPU_E_INVALID, "column %d: dict id %u out of range", column, id);
+      int64_t iv;
+      double dv;
+      value(id, &iv, &dv);
+      isum += iv;   // |row sum| <= maxNumberOfMultiValues * max |value| < 2^63 for 31-bit ids of LONGs below 2^32
+      dsum += dv;   // SumMVAggregationFunction: the row's values added in order, as doubles
+      lo_id = std::min(lo_id, id);
+      hi_id = std::max(hi_id, id);
+    }
+    if (fp) {
+      memcpy(&sums[8 * (size_t)d], &dsum, 8);
+      max_sum = std::max(max_sum, std::fabs(dsum));
+    } else {
+      memcpy(&sums[8 * (size_t)d], &isum, 8);
+      max_sum = std::max(max_sum, std::fabs((double)isum));
+    }
+    // the dictionary is sorted: the row's smallest / largest value is the value of its smallest / largest id
+    memcpy(&mins[w * (size_t)d], &c.hdict[w * (size_t)lo_id], w);
+    memcpy(&maxs[w * (size_t)d], &c.hdict[w * (size_t)hi_id], w);
+  }
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  if (len_column >= 0 && (rc = install_raw(seg, len_column, PGPU_INT, lens, max_len))) return rc;
+  if (sum_column >= 0 && (rc = install_raw(seg, sum_column, fp ? PGPU_DOUBLE : PGPU_LONG, sums, max_sum))) return rc;
+  if (min_column >= 0 && (rc = install_raw(seg, min_column, t, mins, max_val))) return rc;
+  if (max_column >= 0 && (rc = install_raw(seg, max_column, t, maxs, max_val))) return rc;
+  return PGPU_OK;
+}
+
 int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
                                     int32_t cardinality) {
   int rc = check_column(seg, column);
@@ -773,6 +912,7 @@ int pgpu_segment_seal(pgpu_segment* seg) {
       return fail(PGPU_E_INVALID, "column %zu: dictionary cardinality %d != index cardinality %d", i, c.dict_card,
                   c.fwd_card);
     seg->dev[i] = d;
+    std::vector<uint8_t>().swap(c.mv_raw);
   }
   HIP_TRY(hipDeviceSynchronize());
   seg->sealed = true;
@@ -783,7 +923,7 @@ int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes) {
   if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
   uint64_t t = 0;
   for (const HostColumn& c : seg->cols)
-    t += c.fwd.n + c.sliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n;
+    t += c.fwd.n + c.sliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n + c.mv_off.n;
   *out_bytes = t;
   return PGPU_OK;
 }
@@ -911,7 +1051,55 @@ struct Packer {
   int64_t raw_words = 0;
   std::vector<int> bits_instrs;
   bool legacy_range = false;     // a version-1 range-index leaf: the GPU's filter count is not the reference's
+  // multi-value SCAN leaves: until launch, MvLeaf::out holds the bitmap's word offset in Workspace::rawbits and
+  // MvLeaf::set its membership words' offset in mvsets
+  std::vector<MvLeaf> mvs;
+  std::vector<uint32_t> mvsets;
 };
+
+// The bitmap word offset of a multi-value SCAN leaf (mvpred_kernel output), shared by identical leaves.
+int64_t mv_leaf(Packer& pk, const pgpu_segment* seg, const HostColumn& hc, const pgpu_filter_node& nd, int* rc) {
+  *rc = PGPU_OK;
+  MvLeaf L{};
+  L.fwd = (const uint32_t*)hc.fwd.p;
+  L.off = (const int32_t*)hc.mv_off.p;
+  L.num_docs = seg->num_docs;
+  L.words = (int32_t)(((int64_t)seg->num_docs + PGPU_WT - 1) / PGPU_WT * 64);
+  L.bits = hc.bits;
+  L.negate = nd.negate ? 1 : 0;
+  const int32_t card = hc.fwd_card;
+  std::vector<uint32_t> set;
+  if (nd.pred == PGPU_PRED_RANGE) {
+    L.lo = std::max(0, nd.lo);
+    L.hi = std::max(L.lo, std::min(nd.hi, card));
+  } else if (nd.pred == PGPU_PRED_SET) {
+    set.assign(((size_t)card + 31) / 32 + 1, 0u);
+    for (int k = 0; k < nd.num_ids; ++k) {
+      const int32_t id = nd.ids[k];
+      if (id < 0 || id >= card) {
+        *rc = fail(PGPU_E_INVALID, "SET id %d out of range", id);
+        return -1;
+      }
+      set[id >> 5] |= 1u << (id & 31);
+    }
+  } else {
+    *rc = fail(PGPU_E_INVALID, "predicate kind %d", nd.pred);
+    return -1;
+  }
+  for (const MvLeaf& o : pk.mvs) {
+    if (o.off != L.off || o.negate != L.negate || o.lo != L.lo || o.hi != L.hi || (o.set == nullptr) != set.empty())
+      continue;
+    if (!set.empty() && !std::equal(set.begin(), set.end(), pk.mvsets.begin() + (intptr_t)o.set - 1)) continue;
+    return (int64_t)(intptr_t)o.out;
+  }
+  // set offsets are stored + 1 so that null means "RANGE"
+  L.set = set.empty() ? nullptr : (const uint32_t*)(intptr_t)(pk.mvsets.size() + 1);
+  pk.mvsets.insert(pk.mvsets.end(), set.begin(), set.end());
+  L.out = (uint32_t*)(intptr_t)pk.raw_words;
+  pk.raw_words += L.words;
+  pk.mvs.push_back(L);
+  return (int64_t)(intptr_t)L.out;
+}
 
 // The bitmap word offset of a raw-value leaf (rawpred_kernel output), shared by identical leaves of one segment
 // (the exact-statistics pass converts every program a second time).
@@ -1042,6 +1230,21 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
         int rc = col_of(nd.column, &c);
         if (rc) return rc;
         if (c->kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "SCAN on column %d without forward index", nd.column);
+        if (c->kind == PGPU_COL_RAW) return fail(PGPU_E_INVALID, "SCAN on raw column %d (use RAW_SCAN)", nd.column);
+        if (c->kind == PGPU_COL_MV) {
+          // MVScanDocIdIterator: the applyMV bitmap, its entries (row lengths) counted on the host (nostat)
+          const int64_t woff = mv_leaf(pk, seg, seg->cols[sp.column_map[nd.column]], nd, &rc);
+          if (rc) return rc;
+          in.op = PGPU_I_BITS;
+          in.kind = PGPU_COL_MV;
+          in.negate = 0;  // folded into the bitmap
+          in.nostat = 1;
+          in.fwd = (const uint32_t*)(intptr_t)woff;
+          const int idx = emit(in);
+          pk.bits_instrs.push_back(base + idx);
+          close_nots();
+          break;
+        }
         in.op = PGPU_I_SCAN;
         in.pred = nd.pred;
         in.bits = c->bits;
@@ -1262,6 +1465,10 @@ int analyze(const SegView& v, int i, double* sel, std::vector<int>* scans) {
       [[fallthrough]];  // range index of a dictionary column: a dict-id range scan on the GPU
     case PGPU_F_SCAN: {
       if (!valid_col(x.column)) return -1;
+      if (v.dev(x.column)->kind == PGPU_COL_MV) {  // mvpred_kernel's bitmap word per lane: never staged
+        *sel = 0.5;
+        return i + 1;
+      }
       const double card = std::max(1, v.dev(x.column)->card);
       double s = x.pred == PGPU_PRED_RANGE ? std::max(0, x.hi - x.lo) / card : std::max(0, x.num_ids) / card;
       s = std::min(1.0, s);
@@ -1619,6 +1826,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       if (c.kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "segment %d: group column without forward index", s);
       if (c.kind == PGPU_COL_RAW)  // NoDictionary*GroupKeyGenerator: a value-hash path the GPU does not run
         return fail(PGPU_E_UNSUPPORTED, "segment %d: GROUP BY on a raw (no-dictionary) column", s);
+      if (c.kind == PGPU_COL_MV)  // one group key per value of the row (DictionaryBasedGroupKeyGenerator MV path)
+        return fail(PGPU_E_UNSUPPORTED, "segment %d: GROUP BY on a multi-value column", s);
       const pgpu_buffer* rb = sp.group_remap ? sp.group_remap[g] : nullptr;
       if (rb && rb->length < c.card) return fail(PGPU_E_INVALID, "segment %d: remap shorter than cardinality", s);
       if (!rb && c.card > q->group_cardinalities[g])
@@ -1629,6 +1838,8 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       if (q->aggs[a].fn == PGPU_AGG_COUNT) continue;
       const DevColumn& c = pk.cols[ds.col_begin + q->aggs[a].column];
       if (c.kind == PGPU_COL_NONE || !c.dict) return fail(PGPU_E_INVALID, "segment %d: agg column not readable", s);
+      if (c.kind == PGPU_COL_MV)
+        return fail(PGPU_E_UNSUPPORTED, "segment %d: aggregation over a multi-value column (use its row columns)", s);
       if (c.dict_type != L.agg_value_type[a]) return fail(PGPU_E_INVALID, "segment %d: agg column type differs", s);
     }
     int rc = plan_segment(q, sp, seg, p, pk, ds);
@@ -1791,17 +2002,22 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     // column -- its planes stream into VGPRs, no LDS slots (tools/stream_bench.hip: 5.6-6.0 TB/s)
     static const bool no_rdirect = getenv("PGPU_NO_RDIRECT") && atoi(getenv("PGPU_NO_RDIRECT")) != 0;
     bool rd = ok && !no_rdirect;
+    int rd_bits = 1;
     for (const DevSeg& ds : pk.segs)
       if (ds.ntiles) {
         const DevColumn& c = pk.cols[ds.col_begin + ds.stage_col[0]];
         rd &= ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1 && c.bits >= 1 && c.bits <= 16;
+        rd_bits = std::max(rd_bits, (int)c.bits);
       }
     const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;
     if (rd && rdyn <= PGPU_LDS_LIMIT) {
-      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : 4, PGPU_LDS_LIMIT / rdyn);  // 120 VGPRs
+      // 104-126 VGPRs (4 waves per SIMD) except the aggregation-only mode (136-152: 3)
+      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : (p.mode == PGPU_MODE_AGG ? 3 : 4),
+                                               PGPU_LDS_LIMIT / rdyn);
       int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
       if (g >= 8) g &= ~7;
       p.direct = 2;
+      p.rd_planes = rd_bits <= 8 ? 8 : rd_bits <= 10 ? 10 : rd_bits <= 12 ? 12 : 16;
       p.dslots = 0;
       grid = std::max(1, g);
       dyn = rdyn;
@@ -1906,7 +2122,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_rem = align16(o_pool + pk.pool.size() * 4);
   const size_t o_raw = align16(o_rem + pk.remaps.size() * sizeof(void*));
   const size_t o_rvals = align16(o_raw + pk.raws.size() * sizeof(RawLeaf));
-  const size_t total = align16(o_rvals + pk.rawvals.size() * 8) + 16;
+  const size_t o_mv = align16(o_rvals + pk.rawvals.size() * 8);
+  const size_t o_mvset = align16(o_mv + pk.mvs.size() * sizeof(MvLeaf));
+  const size_t total = align16(o_mvset + pk.mvsets.size() * 4) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total);
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
@@ -2016,6 +2234,14 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     r.vals = (const int64_t*)(d + o_rvals) + (intptr_t)r.vals;
     max_raw_words = std::max<int64_t>(max_raw_words, r.words);
   }
+  int64_t max_mv_words = 0;
+  for (MvLeaf& m : pk.mvs) {
+    m.out = (uint32_t*)ws->rawbits.p + (intptr_t)m.out;
+    m.set = m.set ? (const uint32_t*)(d + o_mvset) + ((intptr_t)m.set - 1) : nullptr;
+    max_mv_words = std::max<int64_t>(max_mv_words, m.words);
+  }
+  memcpy(h + o_mv, pk.mvs.data(), pk.mvs.size() * sizeof(MvLeaf));
+  memcpy(h + o_mvset, pk.mvsets.data(), pk.mvsets.size() * 4);
   memcpy(h + o_raw, pk.raws.data(), pk.raws.size() * sizeof(RawLeaf));
   memcpy(h + o_rvals, pk.rawvals.data(), pk.rawvals.size() * 8);
   memcpy(h + o_segs, pk.segs.data(), pk.segs.size() * sizeof(DevSeg));
@@ -2051,6 +2277,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // raw-value leaves' match bitmaps (timed with the query: they are part of its filter)
   if (e == hipSuccess && !pk.raws.empty())
     e = pgpu_launch_rawpred((const RawLeaf*)(d + o_raw), (int)pk.raws.size(), max_raw_words, st);
+  if (e == hipSuccess && !pk.mvs.empty())
+    e = pgpu_launch_mvpred((const MvLeaf*)(d + o_mv), (int)pk.mvs.size(), max_mv_words, st);
   if (e == hipSuccess)
     e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
@@ -2093,6 +2321,26 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
     exact = exact && !pk.legacy_range && pgpu_filter_count_is_reference(sp.filter, sp.num_filter_nodes);
+    // multi-value SCAN leaves read row lengths, not one entry per doc: a lone one reads every row (all values);
+    // elsewhere only the replay knows which rows the reference's iterators read
+    std::vector<const int32_t*> leaf_off;
+    int nmv = 0;
+    for (int i = 0; i < sp.num_filter_nodes; ++i) {
+      const pgpu_filter_node& nd = sp.filter[i];
+      const bool leaf = nd.op == PGPU_F_SCAN || nd.op == PGPU_F_INVERTED || nd.op == PGPU_F_SORTED ||
+                        nd.op == PGPU_F_RAW_SCAN || nd.op == PGPU_F_RANGE_INDEX;
+      if (!leaf) continue;
+      const HostColumn* hc = nullptr;
+      if (nd.op == PGPU_F_SCAN && nd.column >= 0 && nd.column < q->num_columns) {
+        const int32_t slot = sp.column_map[nd.column];
+        if (slot >= 0 && slot < (int32_t)sp.segment->cols.size()) hc = &sp.segment->cols[slot];
+      }
+      const bool mv = hc && hc->kind == PGPU_COL_MV;
+      leaf_off.push_back(mv ? hc->mv_offsets.data() : nullptr);
+      nmv += mv;
+    }
+    if (nmv && sp.num_filter_nodes == 1) qq->mv_entries += sp.segment->cols[sp.column_map[sp.filter[0].column]].mv_values;
+    else if (nmv) exact = false;
     if (!qq->exact_filter) continue;
     pgpu_query::FilterReplay r;
     r.nodes.assign(sp.filter, sp.filter + sp.num_filter_nodes);
@@ -2106,6 +2354,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     r.num_leaves = pk.segs[s].leaf_len;
     r.ntiles = pk.segs[s].ntiles;
     r.bits_off = pk.segs[s].leaf_bits_off;
+    r.leaf_off = std::move(leaf_off);
     qq->replay.push_back(std::move(r));
   }
   qq->stats.filter_stats_exact = exact ? 1 : 0;
@@ -2172,7 +2421,7 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   }
   const int64_t* s = (const int64_t*)qq->ws->h_stats.p;
   qq->stats.num_docs_scanned = s[PGPU_STAT_MATCHED];
-  qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED];
+  qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED] + qq->mv_entries;
   qq->stats.sparse_sector_bytes = s[PGPU_STAT_SECTOR_BYTES];
   qq->stats.dense_bytes = s[PGPU_STAT_DENSE_BYTES];
   float ms = 0.f;
@@ -2191,7 +2440,7 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
       std::vector<const uint32_t*> leaf(r.num_leaves);
       for (int k = 0; k < r.num_leaves; ++k) leaf[k] = bits + r.bits_off + (int64_t)k * r.ntiles * 64;
       const int64_t c = reference_entries_scanned(r.nodes.data(), (int)r.nodes.size(), leaf.data(), r.num_leaves,
-                                                  r.num_docs);
+                                                  r.num_docs, r.leaf_off.empty() ? nullptr : r.leaf_off.data());
       if (c < 0) return fail(PGPU_E_INVALID, "filter program cannot be replayed for statistics");
       total += c;
     }

@@ -15,9 +15,12 @@ Restates the parts of the server's load path this query path needs (SURVEY.md §
   is absent, ColumnMetadataImpl.java:282-287), read back up to the first padding byte
   (seglocal/io/util/FixedByteValueReaderWriter.java:57-90).
 
+* multi-value columns (``isSingleValues = false``): ``<col>.mv.fwd`` (FixedBitMVForwardIndexReader.java:58-75) with
+  ``totalNumberOfEntries`` / ``maxNumberOfMultiValues`` from the metadata.
+
 The loader only slices bytes; the GPU upload (``GpuSegment``) is the IndexingOverrides seam
-(segspi/index/IndexingOverrides.java:82-92).  Shapes outside this path -- raw (no-dictionary) or multi-value
-columns, BYTES / JSON types -- raise ``UnsupportedSegmentError`` so the server keeps its CPU readers for them.
+(segspi/index/IndexingOverrides.java:82-92).  Shapes outside this path -- raw STRING / BYTES / JSON columns, raw
+multi-value columns -- raise ``UnsupportedSegmentError`` so the server keeps its CPU readers for them.
 """
 from __future__ import annotations
 
@@ -44,7 +47,8 @@ LEGACY_PAD = "%"
 _STORED_TYPE = {"INT": PGPU_INT, "BOOLEAN": PGPU_INT, "LONG": PGPU_LONG, "TIMESTAMP": PGPU_LONG,
                 "FLOAT": PGPU_FLOAT, "DOUBLE": PGPU_DOUBLE, "STRING": PGPU_STRING}
 _V1_EXT = {"dictionary": ".dict", "forward_unsorted": ".sv.unsorted.fwd", "forward_sorted": ".sv.sorted.fwd",
-           "forward_raw": ".sv.raw.fwd", "inverted_index": ".bitmap.inv", "range_index": ".bitmap.range"}
+           "forward_raw": ".sv.raw.fwd", "forward_mv": ".mv.fwd", "inverted_index": ".bitmap.inv",
+           "range_index": ".bitmap.range"}
 
 
 class UnsupportedSegmentError(ValueError):
@@ -247,9 +251,12 @@ def load_segment(path: str, columns: Optional[Iterable[str]] = None) -> SegmentD
         dtype_name = _col_meta(props, col, "dataType").upper()
         if dtype_name not in _STORED_TYPE:
             raise UnsupportedSegmentError(f"column {col}: data type {dtype_name} is not on the GPU path")
-        if _col_meta(props, col, "isSingleValues", "true").lower() != "true":
-            raise UnsupportedSegmentError(f"column {col}: multi-value column")
+        mv = _col_meta(props, col, "isSingleValues", "true").lower() != "true"
         dt = _STORED_TYPE[dtype_name]
+        if mv and _col_meta(props, col, "hasDictionary", "true").lower() != "true":
+            raise UnsupportedSegmentError(f"column {col}: raw multi-value column")
+        if mv and dt == PGPU_STRING:
+            raise UnsupportedSegmentError(f"column {col}: multi-value STRING column")
         if _col_meta(props, col, "hasDictionary", "true").lower() != "true":
             # raw (no-dictionary) column: FixedByteChunkSVForwardIndexReader bytes, decoded in the library
             if dt == PGPU_STRING:
@@ -280,7 +287,16 @@ def load_segment(path: str, columns: Optional[Iterable[str]] = None) -> SegmentD
                     {PGPU_INT: ">i4", PGPU_LONG: ">i8", PGPU_FLOAT: ">f4", PGPU_DOUBLE: ">f8"}[dt]).itemsize:
                 raise SegmentFormatError(f"column {col}: dictionary size {len(dict_bytes)} for cardinality {card}")
             c.dictionary = dict_bytes
-        if is_sorted:
+        if mv:
+            fwd = index_bytes(col, "forward_mv")
+            nv = int(_col_meta(props, col, "totalNumberOfEntries"))
+            if fwd is None:
+                raise SegmentFormatError(f"column {col}: multi-value forward index not found")
+            if num_docs <= 0 or nv < num_docs:
+                raise SegmentFormatError(f"column {col}: {nv} entries for {num_docs} docs")
+            c.mv_forward, c.num_values = fwd, nv
+            c.max_values = int(_col_meta(props, col, "maxNumberOfMultiValues", "0"))
+        elif is_sorted:
             fwd = index_bytes(col, "forward_sorted")
             if fwd is None or len(fwd) < 8 * card:
                 raise SegmentFormatError(f"column {col}: sorted index missing or short")

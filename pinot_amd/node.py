@@ -15,7 +15,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import QueryDesc, QueryStats, TableLayout
-from .plan import ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, check_group_columns, finish, key_words_out
+from .plan import (ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, check_group_columns, finish,
+                   has_mv_aggregations, key_words_out, mv_lower, mv_raise)
 from .query import QueryContext
 from .segment import GpuContext, GpuSegment
 
@@ -63,6 +64,9 @@ class GpuNode:
             raise ValueError("one segment list per device")
         everything = [s for segs in segments_by_device for s in segs]
         check_group_columns(query, everything)
+        if has_mv_aggregations(query):  # *MV aggregations over row columns (pinot_amd/mv.py)
+            low, parts = mv_lower(query)
+            return mv_raise(query, parts, self.execute(low, segments_by_device))
         globs = [union_dictionary(g, everything) for g in query.group_by]
         keep, descs = [], []
         for pm, segs in zip(self.planners, segments_by_device):

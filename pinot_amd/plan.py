@@ -40,7 +40,7 @@ from ._lib import (ExprNode, Literal, PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX
                    UnsupportedPlanError)
 from .predicate import (DictPredicateEvaluator, RawPredicateEvaluator, SortedDictionary, get_predicate_evaluator,
                         get_raw_predicate_evaluator)
-from .query import UNBOUNDED, FilterContext, QueryContext, split_filtered_aggregations
+from .query import MV_AGGS, UNBOUNDED, FilterContext, QueryContext, split_filtered_aggregations
 from .segment import GpuContext, GpuSegment
 
 AGG_FN = {"COUNT": PGPU_AGG_COUNT, "SUM": PGPU_AGG_SUM, "MIN": PGPU_AGG_MIN, "MAX": PGPU_AGG_MAX,
@@ -143,6 +143,10 @@ class SegmentFilterPlanner:
             return EMPTY
         if ev.always_true:
             return ALL
+        if col.is_mv:
+            # multi-value: BitmapBasedFilterOperator with an inverted index (non-RANGE), else MVScanDocIdIterator
+            return FilterOp("INV" if p.type != "RANGE" and col.inverted is not None else "SCAN", column=p.column,
+                            evaluator=ev)
         if col.is_sorted:
             return FilterOp("SORTED", column=p.column, evaluator=ev,
                             doc_ranges=self._sorted_ranges(self.seg.sorted_pairs(p.column), ev))
@@ -268,6 +272,16 @@ def check_group_columns(query: QueryContext, segments: Sequence[GpuSegment]) -> 
             if s.column(g).is_raw:
                 raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
                                            f"GROUP BY on raw (no-dictionary) column {g!r} of segment {s.name}")
+            if s.column(g).is_mv:  # one group key per value of the row: not on the GPU path
+                raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                           f"GROUP BY on multi-value column {g!r} of segment {s.name}")
+    for a in query.aggregations:
+        if a.column is None or not segments:
+            continue
+        mv = segments[0].column(a.column).is_mv
+        if mv != (a.function in MV_AGGS):
+            raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED, f"{a.function} on {'a multi' if mv else 'a single'}"
+                                                                f"-value column {a.column!r}")
 
 
 # ---- results ---------------------------------------------------------------------------------------------------
@@ -639,7 +653,14 @@ class GpuPlanMaker:
 
     def submit(self, query: QueryContext, segments: Sequence[GpuSegment]) -> "PendingQuery":
         """Plan the query and enqueue it on the GPU without waiting (pgpu_query_submit).  Several queries may be
-        in flight: the host plans the next one while the GPU runs this one."""
+        in flight: the host plans the next one while the GPU runs this one.  *MV aggregations run lowered onto
+        the multi-value columns' row columns (pinot_amd/mv.py) and are raised back in collect()."""
+        if has_mv_aggregations(query):
+            check_group_columns(query, segments)
+            low, parts = mv_lower(query)
+            pq = self.submit(low, segments)
+            pq.mv = (query, parts)
+            return pq
         if query.has_filtered_aggregations:
             raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
                                             "filtered aggregations run one pass per FILTER clause: use execute()")
@@ -656,6 +677,10 @@ class GpuPlanMaker:
 
     def collect(self, pending: "PendingQuery") -> QueryResult:
         """Wait for a submitted query and finish it (pgpu_query_collect + ORDER BY / LIMIT on the host)."""
+        if pending.mv is not None:
+            query, parts = pending.mv
+            pending.mv = None
+            return mv_raise(query, parts, self.collect(pending))
         L = pending.layout
         cap = int(min(L.num_keys, 1 << 26))
         kw = key_words_out(L)
@@ -699,7 +724,7 @@ class GpuPlanMaker:
         :171-195): a filter that folds to match-all plus only COUNT / MIN / MAX is answered from segment metadata
         and the dictionary, with no scan (NonScanBasedAggregationOperator)."""
         q = query
-        if q.group_by or q.has_filtered_aggregations or any(a.function not in ("COUNT", "MIN", "MAX")
+        if q.group_by or q.has_filtered_aggregations or any(a.function not in ("COUNT", "MIN", "MAX", "MINMV", "MAXMV")
                                                             for a in q.aggregations):
             return [False] * len(segments)
         return [s.num_docs > 0 and SegmentFilterPlanner(s).build(q.filter).kind == "ALL" and
@@ -716,6 +741,7 @@ class PendingQuery:
     handle: C.c_void_p
     layout: TableLayout
     globals_: list
+    mv: Optional[tuple] = None  # (original query, lowered aggregation indexes) when *MV aggregations were lowered
 
     def cancel(self) -> None:
         """Stop the query (pgpu_query_cancel): its kernels skip their remaining tiles and collect raises
@@ -774,14 +800,14 @@ def merge_non_scan(query: QueryContext, scanned: Optional[QueryResult], segments
     res = QueryResult(query=query, stats=ExecutionStats() if scanned is None else scanned.stats)
     vals = []
     for ai, a in enumerate(query.aggregations):
-        v = {"COUNT": 0, "MIN": math.inf, "MAX": -math.inf}[a.function] if scanned is None else \
-            scanned.aggregation_result[ai]
+        v = {"COUNT": 0, "MIN": math.inf, "MAX": -math.inf, "MINMV": math.inf, "MAXMV": -math.inf}[a.function] \
+            if scanned is None else scanned.aggregation_result[ai]
         for s in segments:
             if a.function == "COUNT":
                 v += s.num_docs
-            else:
+            else:  # MIN / MAX and MINMV / MAXMV: the dictionary's ends (DICTIONARY_BASED_FUNCTIONS)
                 lo, hi = s.min_max(a.column)
-                v = min(v, lo) if a.function == "MIN" else max(v, hi)
+                v = min(v, lo) if a.function in ("MIN", "MINMV") else max(v, hi)
         vals.append(v)
     st = res.stats
     for s in segments:
@@ -914,3 +940,17 @@ class GroupColumns:
         for i in range(len(cnt)):
             out[tuple(g[i] for g in gv)] = [c[i] for c in cols]
         return out
+
+
+def has_mv_aggregations(query: QueryContext) -> bool:
+    return any(a.function in MV_AGGS for a in query.aggregations)
+
+
+def mv_lower(query: QueryContext):
+    from .mv import lower
+    return lower(query)
+
+
+def mv_raise(query: QueryContext, parts, low_res):
+    from .mv import raise_result
+    return raise_result(query, parts, low_res)

@@ -46,7 +46,7 @@ class FilterContext:
 
 @dataclass(frozen=True)
 class AggregationSpec:
-    function: str        # COUNT, SUM, MIN, MAX, AVG
+    function: str        # COUNT, SUM, MIN, MAX, AVG; COUNTMV, SUMMV, MINMV, MAXMV, AVGMV (multi-value columns)
     column: Optional[str]  # None for COUNT(*)
     filter_key: Optional[str] = None  # FILTER(WHERE ...) clause text; its FilterContext is QueryContext.agg_filters
 
@@ -118,7 +118,8 @@ class QueryContext:
 # ---- SQL front end -------------------------------------------------------------------------------------------
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|"
                     r"(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
-_AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG"}
+_AGGS = {"COUNT", "SUM", "MIN", "MAX", "AVG", "COUNTMV", "SUMMV", "MINMV", "MAXMV", "AVGMV"}
+MV_AGGS = {"COUNTMV": "COUNT", "SUMMV": "SUM", "MINMV": "MIN", "MAXMV": "MAX", "AVGMV": "AVG"}
 
 
 class SqlError(ValueError):

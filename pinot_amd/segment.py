@@ -9,6 +9,8 @@
 * inverted index  ``<col>.bitmap.inv``       offsets + Roaring bitmaps (BitmapInvertedIndexReader.java:45-61)
 * raw forward     ``<col>.sv.raw.fwd``       no-dictionary values in chunks (BaseChunkSVForwardIndexReader.java:56-101)
 * range index     ``<col>.bitmap.range``     only its version is used (BitSlicedRangeIndexReader.java:41-55)
+* MV forward      ``<col>.mv.fwd``           chunk offsets, row-start bitmap, fixed-bit ids
+                                             (FixedBitMVForwardIndexReader.java:58-140)
 
 (file names: segspi/V1Constants.java:25-105).  ``GpuSegment`` copies them to HBM once
 (``pgpu_segment_add_*``), the analogue of an ``IndexingOverride`` wrapping ``newForwardIndexReader`` /
@@ -59,6 +61,13 @@ class ColumnIndexes:
     range_index: Optional[bytes] = None      # `<col>.bitmap.range` (its header version decides the leaf's stats)
     min_value: Optional[float] = None        # metadata min / max (raw columns: the non-scan MIN / MAX answer,
     max_value: Optional[float] = None        # NonScanBasedAggregationOperator via DataSourceMetadata)
+    mv_forward: Optional[bytes] = None       # multi-value column: the FixedBitMVForwardIndexWriter file `<col>.mv.fwd`
+    num_values: int = 0                      # multi-value: totalNumberOfEntries
+    max_values: int = 0                      # multi-value: maxNumberOfMultiValues
+
+    @property
+    def is_mv(self) -> bool:
+        return self.mv_forward is not None
 
     @property
     def is_raw(self) -> bool:
@@ -161,6 +170,13 @@ class DeviceBuffer:
 
 _UIDS = itertools.count(1)
 
+MV_ROW_COLUMNS = ("len", "sum", "min", "max")
+
+
+def mv_row_column(column: str, kind: str) -> str:
+    """Slot name of a multi-value column's per-row reduction (GpuSegment._add_row_columns)."""
+    return f"{column}$mv{kind}"
+
 
 class GpuSegment:
     """An immutable segment resident in HBM plus the host-side dictionaries used for predicate evaluation.
@@ -178,11 +194,15 @@ class GpuSegment:
         names = list(columns) if columns is not None else list(data.columns)
         self.slots: Dict[str, int] = {}
         self.dictionaries: Dict[str, Union[np.ndarray, List[str]]] = {}
+        # multi-value columns' per-row reductions (mv_row_columns): raw columns of their own slots
+        self.derived: Dict[str, ColumnIndexes] = {}
+        nmv = 0 if _incremental else sum(1 for n in names if data.column(n).is_mv)
         lib = ctx._lib
         h = C.c_void_p()
-        _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, len(names), C.byref(h)))
+        _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, len(names) + len(MV_ROW_COLUMNS) * nmv,
+                                           C.byref(h)))
         self.handle = h
-        self._capacity = len(names)
+        self._capacity = len(names) + len(MV_ROW_COLUMNS) * nmv
         if _incremental:
             return
         try:
@@ -200,13 +220,35 @@ class GpuSegment:
         return cls(ctx, data, columns=[f"_{i}" for i in range(num_columns)], _incremental=True)
 
     def add_column(self, col: ColumnIndexes) -> None:
-        if len(self.slots) >= self._capacity:
+        need = 1 + (len(MV_ROW_COLUMNS) if col.is_mv else 0)
+        if len(self.slots) + need > self._capacity:
             raise ValueError("segment column capacity exceeded")
         slot = len(self.slots)
         self._upload_column(slot, col)
         self.slots[col.name] = slot
         self.dictionaries[col.name] = col.dictionary_values()
         self.data.columns[col.name] = col
+        if col.is_mv:
+            self._add_row_columns(slot, col)
+
+    def _add_row_columns(self, slot: int, col: ColumnIndexes) -> None:
+        """COUNTMV / SUMMV / MINMV / MAXMV / AVGMV read per-row reductions of the column (pgpu_segment_add_mv_row_columns):
+        raw columns named ``<column>$mv<kind>``."""
+        d = col.dictionary_values()
+        fp = col.data_type in (PGPU_FLOAT, PGPU_DOUBLE)
+        kinds = {"len": PGPU_INT, "sum": PGPU_DOUBLE if fp else PGPU_LONG, "min": col.data_type, "max": col.data_type}
+        slots = {}
+        for k in MV_ROW_COLUMNS:
+            slots[k] = len(self.slots)
+            name = mv_row_column(col.name, k)
+            self.slots[name] = slots[k]
+            self.dictionaries[name] = None
+            # min / max metadata: the dictionary's ends (the non-scan MINMV / MAXMV answer)
+            self.derived[name] = ColumnIndexes(name, kinds[k], 0, raw_forward=b"",
+                                               min_value=float(d[0]) if len(d) else None,
+                                               max_value=float(d[-1]) if len(d) else None)
+        _lib.check(self.ctx._lib.pgpu_segment_add_mv_row_columns(self.handle, slot, slots["len"], slots["sum"],
+                                                                 slots["min"], slots["max"]))
 
     def seal(self) -> None:
         _lib.check(self.ctx._lib.pgpu_segment_seal(self.handle))
@@ -222,11 +264,17 @@ class GpuSegment:
                 _lib.check(lib.pgpu_segment_add_range_index(seg, slot, col.range_index, len(col.range_index)))
             return
         if col.data_type == PGPU_STRING:
+            if col.is_mv:
+                raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED, f"multi-value STRING column {col.name}")
             _lib.check(lib.pgpu_segment_add_dictionary(seg, slot, PGPU_STRING, None, 0, card))
         else:
             d = col.dictionary
             _lib.check(lib.pgpu_segment_add_dictionary(seg, slot, col.data_type, d, len(d), card))
-        if col.sorted_index is not None:
+        if col.is_mv:
+            f = col.mv_forward
+            _lib.check(lib.pgpu_segment_add_mv_forward_index(seg, slot, f, len(f), col.bits_per_value, card,
+                                                             col.num_values))
+        elif col.sorted_index is not None:
             s = col.sorted_index
             _lib.check(lib.pgpu_segment_add_sorted_index(seg, slot, s, len(s), card))
         elif col.forward_device is not None:
@@ -244,7 +292,8 @@ class GpuSegment:
             _lib.check(lib.pgpu_segment_add_range_index(seg, slot, col.range_index, len(col.range_index)))
 
     def column(self, name: str) -> ColumnIndexes:
-        return self.data.column(name)
+        c = self.derived.get(name)
+        return c if c is not None else self.data.column(name)
 
     def sorted_dictionary(self, name: str):
         """Host dictionary used by the predicate evaluators (built once per segment column)."""
