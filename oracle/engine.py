@@ -1,8 +1,10 @@
 """Per-segment query execution and combine, restated on the CPU (test infrastructure; see oracle/__init__.py).
 
-Independent of pinot_amd's planner: predicates are evaluated on decoded VALUES with SQL comparison semantics
-(not on dict ids), the physical filter tree is rebuilt here from FilterOperatorUtils' rules, and the iterator
-model below reproduces numEntriesScannedInFilter.
+Independent of pinot_amd's planner and SQL front end: queries are parsed by oracle/sql.py (engine.execute takes
+SQL text; pinot_amd QueryContexts are read through the same attribute names), predicates are evaluated on decoded
+VALUES with SQL comparison semantics (not on dict ids), the physical filter tree is rebuilt here from
+FilterOperatorUtils' rules, and the iterator model below reproduces numEntriesScannedInFilter.  The segments are
+the reference-format bytes in pinot_amd.segment.SegmentData containers, of which only the byte fields are read.
 
 References (abbreviations as in SURVEY.md):
   FilterPlanNode.constructPhysicalOperator ................ core/plan/FilterPlanNode.java:192-313
@@ -31,8 +33,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING
-from pinot_amd.query import UNBOUNDED, FilterContext, Predicate, QueryContext
 from pinot_amd.segment import SegmentData
+
+from .sql import UNBOUNDED, Pred as Predicate, parse as parse_sql, split_filtered
+
+FilterContext = QueryContext = object  # duck-typed: oracle.sql structures or pinot_amd.query ones
 
 from .rawfwd import read_raw_forward
 from .segment_writer import NATIVE, read_inverted_bitmap, read_mv_forward, unpack_fixed_bit
@@ -84,7 +89,7 @@ class DecodedSegment:
         a = self._ids.get(("mv", col))
         if a is None:
             c = self.seg.column(col)
-            a = read_mv_forward(c.mv_forward, self.num_docs, c.num_values, c.bits_per_value)
+            a = read_mv_forward(c.mv_forward, self.num_docs, c.num_values, _bits(c.cardinality))
             self._ids[("mv", col)] = a
         return a
 
@@ -108,6 +113,11 @@ class DecodedSegment:
 
 
 # ---- predicates on values (SQL semantics) -----------------------------------------------------------------------
+def _bits(cardinality: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue(cardinality - 1)."""
+    return 1 if cardinality - 1 <= 1 else int(cardinality - 1).bit_length()
+
+
 def _lit(v: str, dt: int):
     if dt == PGPU_STRING:
         return v
@@ -786,9 +796,12 @@ class OracleResult:
     num_total_docs: int = 0
 
 
-def execute(query: QueryContext, segments: Sequence[SegmentData], num_groups_limit: int = 100_000,
+def execute(query, segments: Sequence[SegmentData], num_groups_limit: int = 100_000,
             max_init_group_holder_capacity: int = 10_000, iterator_stats: bool = False) -> OracleResult:
-    """All segments of one server + the broker reduce (no group trimming)."""
+    """All segments of one server + the broker reduce (no group trimming).  `query`: SQL text (parsed by
+    oracle/sql.py) or a parsed query."""
+    if isinstance(query, str):
+        query = parse_sql(query)
     if query.has_filtered_aggregations:
         return _execute_filtered(query, segments, num_groups_limit, max_init_group_holder_capacity, iterator_stats)
     fns = [a.function for a in query.aggregations]
@@ -829,15 +842,24 @@ def execute(query: QueryContext, segments: Sequence[SegmentData], num_groups_lim
     return out
 
 
+def _split_filtered(query):
+    from .sql import Agg, Query
+    if isinstance(query, Query):
+        return split_filtered(query)
+    # a pinot_amd QueryContext: its passes restated with the oracle's own structures
+    q = Query(query.table, list(query.select), [Agg(a.function, a.column, a.filter_key) for a in query.aggregations],
+              query.filter, list(query.group_by), list(query.order_by), query.limit, dict(query.agg_filters))
+    return split_filtered(q)
+
+
 def _execute_filtered(query: QueryContext, segments, num_groups_limit, max_init, iterator_stats) -> OracleResult:
     """FilteredAggregationOperator (core/operator/query/FilteredAggregationOperator.java:62-95) over the passes of
     AggregationPlanNode.buildFilterOperatorInternal (:102-145): one per FILTER clause (main AND clause), then the
     main filter; per-segment sums equal the sums over all segments, so the passes run server-wide."""
-    from pinot_amd.query import split_filtered_aggregations
     out = OracleResult()
     n = len(query.aggregations)
     fin, inter = [None] * n, [None] * n
-    for sq, idx in split_filtered_aggregations(query):
+    for sq, idx in _split_filtered(query):
         r = execute(sq, segments, num_groups_limit, max_init, iterator_stats)
         for j, i in enumerate(idx):
             fin[i] = r.aggregation_result[j]
