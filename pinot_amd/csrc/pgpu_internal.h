@@ -211,6 +211,20 @@ struct MvLeaf {
   int32_t negate;
 };
 
+// An inverted-index leaf expanded into a doc bitmap before the query kernel (invexp_kernel): one workgroup per
+// (leaf, 65,536-doc container key) ORs the key's container of every id, complemented within [0, num_docs) when negate.
+struct InvLeafX {
+  const uint32_t* dir;     // DevColumn::inv_dir
+  const DevContainer* ct;  // DevColumn::inv_ct
+  const uint8_t* data;     // DevColumn::inv_data
+  const int32_t* ids;      // the leaf's dict ids
+  uint32_t* out;           // ntiles * 64 words; bit d % 32 of word d / 32, 0 past num_docs
+  int32_t nids;
+  int32_t negate;
+  int32_t num_docs;
+  int32_t words;
+};
+
 #define PGPU_RAW_RANGE_LO_INCL 1
 #define PGPU_RAW_RANGE_HI_INCL 2
 #define PGPU_RAW_RANGE_ORDINAL 4  // range-index semantics for FLOAT / DOUBLE: NaN orders as -infinity (FPOrdering)

@@ -3443,6 +3443,68 @@ hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max
   return hipGetLastError();
 }
 
+// ---- inverted-index leaves expanded to doc bitmaps ---------------------------------------------------------------
+// BitmapBasedFilterOperator's OR of the ids' bitmaps (BitmapBasedFilterOperator.java:66-101), one container key per
+// workgroup: the 64K-doc word range is assembled in LDS (bitmap containers copied, array values and runs set with
+// LDS atomics), then written out in whole lines.  The query kernel reads the result as a BITS leaf: one word per
+// lane and tile instead of a per-tile container search and array scan on the consumer's critical path.
+__global__ __launch_bounds__(256) void invexp_kernel(const InvLeafX* leaves) {
+  __shared__ uint32_t w[2048];
+  const InvLeafX L = cld(leaves + blockIdx.y);
+  const uint32_t key = blockIdx.x;
+  const int64_t word0 = (int64_t)key * 2048;
+  if (word0 >= L.words) return;
+  const int t = threadIdx.x;
+  for (int i = t; i < 2048; i += 256) w[i] = 0u;
+  __syncthreads();
+  const InvIndex ix{L.dir, L.ct, L.data};
+  for (int k = 0; k < L.nids; ++k) {
+    const int32_t ci = find_container(ix, (uint32_t)cld(L.ids + k), key);
+    if (ci < 0) continue;
+    const uint32_t type = cld(&L.ct[ci].type), card = cld(&L.ct[ci].card), offset = cld(&L.ct[ci].offset);
+    if (type == PGPU_CT_BITMAP) {
+      const uint32_t* b = (const uint32_t*)(L.data + offset);
+      for (int i = t; i < 2048; i += 256) w[i] |= gld(b, i);
+    } else if (type == PGPU_CT_RUN) {
+      const uint16_t* r = (const uint16_t*)(L.data + offset);
+      for (uint32_t j = t; j < card; j += 256) {
+        const uint32_t s0 = gld(r, 2 * j), e0 = s0 + gld(r, 2 * j + 1);  // inclusive
+        const uint32_t a = s0 >> 5, z = e0 >> 5;
+        for (uint32_t x = a; x <= z; ++x) {
+          const uint32_t lo = x == a ? (s0 & 31) : 0u, hi = x == z ? (e0 & 31) : 31u;
+          atomicOr(&w[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+        }
+      }
+    } else {
+      const uint16_t* v = (const uint16_t*)(L.data + offset);
+      for (uint32_t j = t; j < card; j += 256) {
+        const uint32_t x = gld(v, j);
+        atomicOr(&w[x >> 5], 1u << (x & 31));
+      }
+    }
+    __syncthreads();
+  }
+  const int64_t nw = min((int64_t)2048, (int64_t)L.words - word0);
+  for (int i = t; i < nw; i += 256) {
+    uint32_t x = w[i];
+    if (L.negate) {
+      const int64_t d0 = (word0 + i) * 32;
+      const int64_t left = (int64_t)L.num_docs - d0;
+      const uint32_t valid = left >= 32 ? 0xFFFFFFFFu : (left <= 0 ? 0u : ((1u << left) - 1u));
+      x = ~x & valid;
+    }
+    L.out[word0 + i] = x;
+  }
+}
+
+hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {
+  if (nleaves <= 0) return hipSuccess;
+  const int64_t keys = (max_words + 2047) / 2048;
+  hipLaunchKernelGGL(invexp_kernel, dim3((unsigned)std::max<int64_t>(1, keys), (unsigned)nleaves), dim3(256), 0, st,
+                     dev_leaves);
+  return hipGetLastError();
+}
+
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {
   if (nleaves <= 0) return hipSuccess;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (max_words / 32 + 3) / 4));

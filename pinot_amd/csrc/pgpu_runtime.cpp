@@ -58,6 +58,7 @@ int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t
                             std::string* err);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
+hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 
 namespace {
 
@@ -1055,7 +1056,38 @@ struct Packer {
   // MvLeaf::set its membership words' offset in mvsets
   std::vector<MvLeaf> mvs;
   std::vector<uint32_t> mvsets;
+  // inverted-index leaves expanded before the query kernel (invexp_kernel): InvLeafX::out = word offset in rawbits,
+  // InvLeafX::ids = offset in invids until launch
+  std::vector<InvLeafX> invx;
+  std::vector<int32_t> invids;
 };
+
+// Inverted leaves are expanded into doc bitmaps while their words stay within this budget (per query); the rest
+// are evaluated per tile (bitmap_word).  PGPU_NO_INVEXP=1 turns the expansion off.
+constexpr int64_t kInvExpMaxWords = (int64_t)1 << 29;  // 2 GiB of bitmaps
+
+int64_t inv_leaf(Packer& pk, const pgpu_segment* seg, const DevColumn& dc, const pgpu_filter_node& nd) {
+  InvLeafX L{};
+  L.dir = dc.inv_dir;
+  L.ct = dc.inv_ct;
+  L.data = dc.inv_data;
+  L.nids = nd.num_ids;
+  L.negate = nd.negate ? 1 : 0;
+  L.num_docs = seg->num_docs;
+  L.words = (int32_t)(((int64_t)seg->num_docs + PGPU_WT - 1) / PGPU_WT * 64);
+  for (const InvLeafX& o : pk.invx) {
+    if (o.dir != L.dir || o.nids != L.nids || o.negate != L.negate) continue;
+    if (!std::equal(nd.ids, nd.ids + nd.num_ids, pk.invids.begin() + (intptr_t)o.ids)) continue;
+    return (int64_t)(intptr_t)o.out;
+  }
+  if (pk.raw_words + L.words > kInvExpMaxWords) return -1;
+  L.ids = (const int32_t*)(intptr_t)pk.invids.size();
+  pk.invids.insert(pk.invids.end(), nd.ids, nd.ids + nd.num_ids);
+  L.out = (uint32_t*)(intptr_t)pk.raw_words;
+  pk.raw_words += L.words;
+  pk.invx.push_back(L);
+  return (int64_t)(intptr_t)L.out;
+}
 
 // The bitmap word offset of a multi-value SCAN leaf (mvpred_kernel output), shared by identical leaves.
 int64_t mv_leaf(Packer& pk, const pgpu_segment* seg, const HostColumn& hc, const pgpu_filter_node& nd, int* rc) {
@@ -1333,6 +1365,23 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
         int rc = col_of(nd.column, &c);
         if (rc) return rc;
         if (!c->inv_dir) return fail(PGPU_E_INVALID, "INVERTED on column %d without inverted index", nd.column);
+        for (int k = 0; k < nd.num_ids; ++k)
+          if (nd.ids[k] < 0 || nd.ids[k] >= c->card) return fail(PGPU_E_INVALID, "bitmap id %d out of range", nd.ids[k]);
+        static const bool no_invexp = getenv("PGPU_NO_INVEXP") && atoi(getenv("PGPU_NO_INVEXP")) != 0;
+        if (!no_invexp && nd.num_ids > 0) {
+          const int64_t woff = inv_leaf(pk, seg, *c, nd);
+          if (woff >= 0) {  // the expanded bitmap as a BITS leaf (a bitmap leaf reads no entries)
+            in.op = PGPU_I_BITS;
+            in.kind = PGPU_COL_FIXED_BIT;
+            in.negate = 0;
+            in.nostat = 1;
+            in.fwd = (const uint32_t*)(intptr_t)woff;
+            const int idx = emit(in);
+            pk.bits_instrs.push_back(base + idx);
+            close_nots();
+            break;
+          }
+        }
         in.op = PGPU_I_INV;
         in.pool_off = (int32_t)pk.pool.size();
         in.n = nd.num_ids;
@@ -2124,7 +2173,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_rvals = align16(o_raw + pk.raws.size() * sizeof(RawLeaf));
   const size_t o_mv = align16(o_rvals + pk.rawvals.size() * 8);
   const size_t o_mvset = align16(o_mv + pk.mvs.size() * sizeof(MvLeaf));
-  const size_t total = align16(o_mvset + pk.mvsets.size() * 4) + 16;
+  const size_t o_inv = align16(o_mvset + pk.mvsets.size() * 4);
+  const size_t o_invids = align16(o_inv + pk.invx.size() * sizeof(InvLeafX));
+  const size_t total = align16(o_invids + pk.invids.size() * 4) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total);
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
@@ -2241,6 +2292,14 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     max_mv_words = std::max<int64_t>(max_mv_words, m.words);
   }
   memcpy(h + o_mv, pk.mvs.data(), pk.mvs.size() * sizeof(MvLeaf));
+  int64_t max_inv_words = 0;
+  for (InvLeafX& x : pk.invx) {
+    x.out = (uint32_t*)ws->rawbits.p + (intptr_t)x.out;
+    x.ids = (const int32_t*)(d + o_invids) + (intptr_t)x.ids;
+    max_inv_words = std::max<int64_t>(max_inv_words, x.words);
+  }
+  memcpy(h + o_inv, pk.invx.data(), pk.invx.size() * sizeof(InvLeafX));
+  memcpy(h + o_invids, pk.invids.data(), pk.invids.size() * 4);
   memcpy(h + o_mvset, pk.mvsets.data(), pk.mvsets.size() * 4);
   memcpy(h + o_raw, pk.raws.data(), pk.raws.size() * sizeof(RawLeaf));
   memcpy(h + o_rvals, pk.rawvals.data(), pk.rawvals.size() * 8);
@@ -2279,6 +2338,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = pgpu_launch_rawpred((const RawLeaf*)(d + o_raw), (int)pk.raws.size(), max_raw_words, st);
   if (e == hipSuccess && !pk.mvs.empty())
     e = pgpu_launch_mvpred((const MvLeaf*)(d + o_mv), (int)pk.mvs.size(), max_mv_words, st);
+  if (e == hipSuccess && !pk.invx.empty())
+    e = pgpu_launch_invexp((const InvLeafX*)(d + o_inv), (int)pk.invx.size(), max_inv_words, st);
   if (e == hipSuccess)
     e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
