@@ -100,6 +100,7 @@ struct DevColumn {
 #define PGPU_AM_DENSE 1   // group / agg column ids decoded from the staged LDS slot
 #define PGPU_AM_SPARSE 2  // matched docs queued; ids gathered per doc
 
+#define PGPU_PREBITS 4
 struct DevSeg {
   int32_t num_docs;
   int32_t tile_begin;             // first global tile of this segment
@@ -134,6 +135,11 @@ struct DevSeg {
   int32_t leaf_begin;
   int32_t pad_;
   int64_t leaf_bits_off;
+  // BITS leaves of the dense program (their instructions' n = slot): the query kernel loads their words for a
+  // tile together before interpreting the program, one round trip instead of one per leaf
+  int32_t nbits;
+  int32_t pad2_;
+  const uint32_t* bits_w[PGPU_PREBITS];
 };
 
 // Filter instruction with statically resolved mask slots.

@@ -1079,10 +1079,35 @@ FI uint32_t leaf_sorted(const DevParams& p, const DocCtx& t, const DevInstr& in)
   return in.negate ? ~m : m;
 }
 
+// The dense program's precomputed-bitmap (BITS) leaves for one tile, loaded together up front (DevSeg::bits_w).
+struct PreBits {
+  uint32_t w[PGPU_PREBITS];
+  FI uint32_t get(int k) const {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < PGPU_PREBITS; ++j) v = k == j ? w[j] : v;
+    return v;
+  }
+};
+FI void prebits_load(const TileCtx& t, int begin, int ss_prog_begin, PreBits& pb) {
+  const DevSeg* sg = t.ss->sg;
+  const int nb = begin == ss_prog_begin ? cld(&sg->nbits) : 0;
+  const size_t wi = (size_t)(t.doc0 >> 5) + lane_id();
+#pragma unroll
+  for (int j = 0; j < PGPU_PREBITS; ++j) pb.w[j] = j < nb ? gld((const uint32_t*)cld(&sg->bits_w[j]), wi) : 0u;
+}
+FI void prebits_load(const DocCtx&, int, int, PreBits&) {}
+FI uint32_t bits_leaf(const TileCtx& t, const DevInstr& in, const PreBits& pb) {
+  return in.n >= 0 ? pb.get(in.n) : leaf_bits(t, in);
+}
+FI uint32_t bits_leaf(const DocCtx& t, const DevInstr& in, const PreBits&) { return leaf_bits(t, in); }
+
 template <class Ctx>
 FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, const Ctx& t, int64_t& scanned,
                         int64_t& dense_bytes, Prof& pf) {
   uint32_t* scratch = cv.masks + (p.mask_rows - 1) * 64;
+  PreBits pb;
+  prebits_load(t, begin, t.ss->prog_begin, pb);
   int pc = 0;
   while (pc < len) {
     const int64_t tfe = now(pf);
@@ -1114,7 +1139,7 @@ FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, 
           const int n = wave_sum_i32(__popc(care));
           if (lane_id() == 0) scanned += n;
         }
-        mrow(cv, in.dst) = leaf_bits(t, in) & care;
+        mrow(cv, in.dst) = bits_leaf(t, in, pb) & care;
         break;
       }
       case PGPU_I_INV: mrow(cv, in.dst) = leaf_inv(p, t, in, scratch) & t.valid; break;

@@ -1692,6 +1692,17 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   int rc = convert_filter(q, sp, dn.data(), (int)dn.size(), seg, pk);
   if (rc) return rc;
   ds.prog_len = (int32_t)pk.instrs.size() - ds.prog_begin;
+  ds.nbits = 0;
+  for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+    DevInstr& in = pk.instrs[i];
+    if (in.op != PGPU_I_BITS) continue;
+    if (ds.nbits < PGPU_PREBITS) {
+      in.n = ds.nbits;
+      ds.bits_w[ds.nbits++] = in.fwd;  // a word offset into the workspace bitmaps until launch
+    } else {
+      in.n = -1;
+    }
+  }
   ds.rprog_begin = (int32_t)pk.instrs.size();
   rc = convert_filter(q, sp, rn.data(), (int)rn.size(), seg, pk);
   if (rc) return rc;
@@ -2279,6 +2290,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // raw-value leaves: offsets -> device pointers (bitmaps in the workspace, set values in the arena)
   for (int idx : pk.bits_instrs)
     pk.instrs[idx].fwd = (const uint32_t*)ws->rawbits.p + (intptr_t)pk.instrs[idx].fwd;
+  for (DevSeg& sg : pk.segs)
+    for (int k = 0; k < sg.nbits; ++k) sg.bits_w[k] = (const uint32_t*)ws->rawbits.p + (intptr_t)sg.bits_w[k];
   int64_t max_raw_words = 0;
   for (RawLeaf& r : pk.raws) {
     r.out = (uint32_t*)ws->rawbits.p + (intptr_t)r.out;
