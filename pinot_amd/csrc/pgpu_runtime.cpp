@@ -1578,6 +1578,10 @@ double sector_touch(double rho, int bits) {
 
 // A column is streamed (dense) when at least half of its sectors would be read anyway.
 constexpr double kDenseTouch = 0.5;
+// Aggregation columns are staged densely only when nearly every 32-B sector holds a matched doc: below that the
+// self-loading kernels' candidate gathers win (config 2, 9.4 % of docs, 16-bit metric, 79 % of sectors touched:
+// dense 2.37 ms, candidates 1.40 ms; 50 % of docs: dense 3.0 ms, candidates 3.8 ms).  PGPU_DENSE_TOUCH overrides.
+constexpr double kDenseAggTouch = 0.95;
 constexpr int kMaxSlotBytes = 27 * 1024;  // keeps >= 3 ring slots next to the consumer areas
 
 int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_segment* seg,
@@ -1643,10 +1647,11 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   } else {
     // the hash group-by computes 64-bit keys and slots per doc in the candidate path only
     bool dense = p.mode != PGPU_MODE_HASH;
+    static const double touch = getenv("PGPU_DENSE_TOUCH") ? atof(getenv("PGPU_DENSE_TOUCH")) : kDenseAggTouch;
     for (int qc : aggcols) {
       const DevColumn* dc = v.dev(qc);
       const int b = dc->kind == PGPU_COL_RAW ? 8 * type_width(dc->dict_type) : dc->bits;
-      dense &= (dc->kind == PGPU_COL_FIXED_BIT || dc->kind == PGPU_COL_RAW) && sector_touch(rho, b) >= kDenseTouch;
+      dense &= (dc->kind == PGPU_COL_FIXED_BIT || dc->kind == PGPU_COL_RAW) && sector_touch(rho, b) >= touch;
     }
     agg_mode = dense ? PGPU_AM_DENSE : PGPU_AM_SPARSE;
     if (dense)
