@@ -2105,7 +2105,12 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
             if (lane == 0) dense_bytes += ((int64_t)ndocs * b + 7) / 8;
           }
       }
-      const uint32_t mm = fast_filter(ss, t, lane_scanned);
+      // fast sliced leaves in registers; a segment with nothing staged (bitmap / sorted / BITS leaves only) runs
+      // its program through the interpreter -- no slot is read
+      const uint32_t mm = ss.fast ? fast_filter(ss, t, lane_scanned)
+                                  : (ss.prog_len > 0 ? run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned,
+                                                                   dense_bytes, pf)
+                                                     : t.valid);
       // the slot's planes have been read (lgkmcnt): it is rewritten by the issue of tile k + D, after this point
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);

@@ -2028,11 +2028,17 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // aggregates densely; each wave streams its own tiles through two private LDS slots (query_kernel_direct)
   static const bool no_direct = getenv("PGPU_NO_DIRECT") && atoi(getenv("PGPU_NO_DIRECT")) != 0;
   p.direct = 0;
-  if (!no_direct && !p.dense && p.mode != PGPU_MODE_PART && pk.tile_bytes > 0) {
+  // a segment whose dense program reads no staged column (bitmap / sorted / precomputed-bitmap leaves only) also runs
+  // on self-loading waves, interpreting its program without slots: the ring's few consumer waves cannot hide the
+  // candidate gathers' latency
+  bool index_only = true;
+  for (const DevSeg& ds : pk.segs) index_only &= ds.ntiles == 0 || (ds.nstage == 0 && ds.fast == 0);
+  if (!no_direct && !p.dense && p.mode != PGPU_MODE_PART && (pk.tile_bytes > 0 || index_only)) {
     bool ok = true;
     for (const DevSeg& ds : pk.segs)
-      ok &= ds.ntiles == 0 || (ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1 &&
-                               (ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE));
+      ok &= ds.ntiles == 0 || ((ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&
+                               ((ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1) ||
+                                (ds.nstage == 0 && ds.fast == 0)));
     // up to five 4-wave workgroups per CU (more waves hide the per-tile latency better than deeper prefetch, which
     // measured flat); each wave keeps D - 1 tiles in flight, aiming at ~12 KiB (HBM latency
     // x per-CU bandwidth), within the 6-bit vmcnt and the LDS
@@ -2070,8 +2076,12 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     int rd_bits = 1;
     for (const DevSeg& ds : pk.segs)
       if (ds.ntiles) {
+        if (!(ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1)) {  // stage_col[0] is set only when staged
+          rd = false;
+          continue;
+        }
         const DevColumn& c = pk.cols[ds.col_begin + ds.stage_col[0]];
-        rd &= ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1 && c.bits >= 1 && c.bits <= 16;
+        rd &= c.bits >= 1 && c.bits <= 16;
         rd_bits = std::max(rd_bits, (int)c.bits);
       }
     const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;

@@ -3,7 +3,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
-for WL in groupby1m range_in bitmap5; do
+for WL in ${WLS:-groupby1m range_in bitmap5}; do
   OUT=$R/gpurun_out/r2wl/$WL; mkdir -p "$OUT"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
     python3 $R/bench.py --no-cpu-baseline --no-check --no-secondary --workload $WL --steps 10 --warmup 2 \
