@@ -468,3 +468,36 @@ def test_partitioned_groupby_shared_dictionary(gpu_ctx, sql, mtype, card):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force", [None, "array", "bitmap", "run"])
+def test_inverted_container_kinds_vs_oracle(gpu_ctx, force):
+    """Every Roaring container kind through the inverted-leaf expansion (invexp_kernel): array values, bitmap words
+    and runs OR-ed per 64K-doc key, complemented for NOT IN / NEQ, on a ragged doc count (last key partial)."""
+    from oracle.segment_writer import build_segment, inverted_index_bytes
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    rng = np.random.default_rng(7)
+    n = 3 * 65536 + 12345
+    runs = np.repeat(rng.integers(0, 12, n // 500 + 1), 500)[:n]  # long runs of equal values
+    cols = {"r": (PGPU_INT, runs), "u": (PGPU_INT, rng.integers(0, 40, n)), "h": (PGPU_INT, rng.integers(0, 2, n) * 2 + 1),
+            "m": (PGPU_INT, rng.integers(0, 1000, n))}
+    seg = build_segment("kinds", cols, inverted=["r", "u", "h"], sorted_columns=[])
+    if force is not None:
+        # the portable format implies the kind from the cardinality: arrays hold <= 4096 values, bitmaps more
+        for c in {"array": ("u",), "bitmap": ("h",), "run": ("r", "u", "h")}[force]:
+            col = seg.column(c)
+            ids = engine.DecodedSegment(seg).ids(c)
+            col.inverted = inverted_index_bytes(ids, col.cardinality, True, force)
+    g = GpuSegment(gpu_ctx, seg)
+    try:
+        for f in ("r IN (3, 7)", "r NOT IN (1, 2, 11)", "u = 5", "u <> 5 AND r IN (0, 4, 9)",
+                  "(u IN (1, 2, 3) OR r = 6) AND NOT (u = 2)", "h IN (1, 4) AND u <> 7", "h <> 3 OR r = 5"):
+            q = parse_sql(f"SELECT COUNT(*), SUM(m) FROM t WHERE {f}")
+            res = GpuPlanMaker(gpu_ctx).execute(q, [g])
+            ref = engine.execute(q, [seg])
+            assert list(res.aggregation_result) == list(ref.aggregation_result), (force, f)
+            assert res.stats.num_docs_scanned == ref.num_docs_scanned
+    finally:
+        g.release()
