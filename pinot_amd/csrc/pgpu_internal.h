@@ -101,6 +101,7 @@ struct DevColumn {
 #define PGPU_AM_SPARSE 2  // matched docs queued; ids gathered per doc
 
 #define PGPU_PREBITS 4
+#define PGPU_FOR_MAX_BITS 16  // frame-of-reference dictionaries: widest per-block offset
 struct DevSeg {
   int32_t num_docs;
   int32_t tile_begin;             // first global tile of this segment
@@ -322,8 +323,11 @@ struct DevParams {
   // PART with one-word records: ldict = phase 2 reads SUM values from pdict copied into LDS beside its table
   // (1 << slice_shift >= pdict_n entries)
   int32_t slice_shift;
-  int32_t ldict;
+  int32_t ldict;                  // 1: pdict copied whole; 2: its frame-of-reference image pfor (PGPU_FOR_*)
   uint32_t pdict_n;               // pdict entries
+  const uint32_t* pfor;           // ldict 2: int32 base per 32-id block, then for_bits-bit offsets packed LSB-first
+  int32_t for_bits;
+  int32_t for_nblk;
   uint32_t cancel_gen;            // this launch's generation (see cancel)
   // PART region sizing (part_scan phase 1): a sampled counting pass (psample = tile stride) fills pcount, then
   // part_plan_kernel sizes each partition's region in proportion (pcap / poff within a workgroup's block of

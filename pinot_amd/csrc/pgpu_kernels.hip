@@ -2951,6 +2951,9 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   if (LDM == 1)
     for (uint32_t i = threadIdx.x; i < slice; i += blockDim.x)
       sdict[i] = i < p.pdict_n ? gld((const uint32_t*)p.pdict, i) : 0u;
+  const int fbits = p.for_bits, fnblk = p.for_nblk;
+  if (LDM == 2)  // the frame-of-reference image: int32 block bases, then the packed offsets
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(fnblk * (1 + fbits) + 1); i += blockDim.x) sdict[i] = gld(p.pfor, i);
   __syncthreads();
   // one-word records: (in-partition key << idbits | dict id) over the shared dictionary; MIN / MAX sections reduce
   // the dict ids (sorted dictionary) and are turned into cell keys when folded into the HBM table
@@ -2987,7 +2990,19 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
         for (int r = 0; r < R; ++r) val[r] = raw[r];
         if (idbits && need_val) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) val[r] = LDM == 1 ? sdict[raw[r] & (slice - 1)] : gld((const uint32_t*)p.pdict, raw[r]);
+          for (int r = 0; r < R; ++r) {
+            if (LDM == 1) {
+              val[r] = sdict[raw[r] & (slice - 1)];
+            } else if (LDM == 2) {
+              // value = block base + the id's fbits-bit offset (may straddle two words)
+              const uint32_t id = ok[r] ? raw[r] : 0u, blk = id >> 5, bit = (id & 31u) * (uint32_t)fbits;
+              const uint32_t* wds = sdict + fnblk + (size_t)blk * fbits + (bit >> 5);
+              const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
+              val[r] = sdict[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
+            } else {
+              val[r] = gld((const uint32_t*)p.pdict, raw[r]);
+            }
+          }
         }
         part_reduce_batch<NS, R>(ptab, K, op, vt, idbits, k, raw, val, ok);
       }
@@ -3284,7 +3299,7 @@ hipError_t pgpu_prepare_part_reduce() {
   if (e == hipSuccess)                                                                          \
     e = hipFuncSetAttribute((const void*)part_reduce_kernel<NS, ONE, LDM>,                      \
                             hipFuncAttributeMaxDynamicSharedMemorySize, PGPU_LDS_LIMIT);
-#define PART_ATTR(NS) PART_ATTR_1(NS, true, 0) PART_ATTR_1(NS, true, 1) PART_ATTR_1(NS, false, 0)
+#define PART_ATTR(NS) PART_ATTR_1(NS, true, 0) PART_ATTR_1(NS, true, 1) PART_ATTR_1(NS, true, 2) PART_ATTR_1(NS, false, 0)
   PART_ATTR(0) PART_ATTR(1) PART_ATTR(2) PART_ATTR(3) PART_ATTR(4)
 #undef PART_ATTR_1
 #undef PART_ATTR
@@ -3313,12 +3328,15 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
-  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 + (p.ldict ? (size_t)4 << p.slice_shift : 0);
+  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 +
+                     (p.ldict == 1 ? (size_t)4 << p.slice_shift
+                                   : (p.ldict == 2 ? (size_t)4 * ((size_t)p.for_nblk * (1 + p.for_bits) + 1) : 0));
   const dim3 g(p.p2work ? p.p2grid : p.nparts);
   switch (p.nsec - 1) {
 #define PART_LAUNCH(NS)                                                                                    \
   case NS:                                                                                                 \
     if (p.rw == 1 && p.ldict == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true, 1>), g, dim3(1024), lds, st, p, nwg); \
+    else if (p.rw == 1 && p.ldict == 2) hipLaunchKernelGGL((part_reduce_kernel<NS, true, 2>), g, dim3(1024), lds, st, p, nwg); \
     else if (p.rw == 1) hipLaunchKernelGGL((part_reduce_kernel<NS, true, 0>), g, dim3(1024), lds, st, p, nwg); \
     else hipLaunchKernelGGL((part_reduce_kernel<NS, false, 0>), g, dim3(1024), lds, st, p, nwg); \
     return hipGetLastError();

@@ -224,6 +224,10 @@ struct HostColumn {
   double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
   int32_t range_index = 0;             // range index version (2 = exact bit-sliced, 1 = legacy), 0 = none
   uint64_t dict_hash[2] = {0, 0};      // two independent 64-bit hashes of the dictionary bytes (shared-dict checks)
+  // INT dictionary in frame-of-reference form (phase 2 of the partitioned group-by keeps it in LDS): per block of
+  // 32 ids its first value, then every id's offset from it in for_bits bits (0 = not encoded)
+  DevMem for_dev;
+  int32_t for_bits = 0, for_nblk = 0;
   // multi-value column (PGPU_COL_MV): fwd = the values' ids fixed-bit, mv_off = row offsets (num_docs + 1)
   DevMem mv_off;
   std::vector<int32_t> mv_offsets;     // host copy (row lengths: exact filter statistics, row columns)
@@ -638,6 +642,35 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
+  if (data_type == PGPU_INT && cardinality >= 2048) {
+    // frame of reference: sorted values differ little within a block of 32 ids
+    const int32_t nblk = (cardinality + 31) / 32;
+    int bits = 0;
+    for (int32_t k = 0; k < nblk; ++k) {
+      const int32_t first = (int32_t)be32(b + 4 * (32 * k));
+      const int32_t last = (int32_t)be32(b + 4 * std::min(cardinality - 1, 32 * k + 31));
+      const uint64_t span = (uint64_t)((int64_t)last - first);
+      int w = 0;
+      while (w < 33 && (span >> w)) ++w;
+      bits = std::max(bits, w);
+    }
+    if (bits >= 1 && bits <= PGPU_FOR_MAX_BITS) {
+      std::vector<uint32_t> img((size_t)nblk * (1 + bits) + 1, 0u);
+      for (int32_t k = 0; k < nblk; ++k) img[k] = be32(b + 4 * (32 * k));
+      uint32_t* words = img.data() + nblk;
+      for (int32_t id = 0; id < cardinality; ++id) {
+        const int32_t blk = id >> 5;
+        const uint32_t off = (uint32_t)((int64_t)(int32_t)be32(b + 4 * id) - (int64_t)(int32_t)img[blk]);
+        const uint32_t bit = (uint32_t)(id & 31) * bits;
+        const size_t w = (size_t)blk * bits + (bit >> 5);
+        words[w] |= off << (bit & 31);
+        if ((bit & 31) + bits > 32) words[w + 1] |= off >> (32 - (bit & 31));
+      }
+      HIP_TRY(upload(c.for_dev, img.data(), img.size() * 4, img.size() * 4, PGPU_MEM_HOST));
+      c.for_bits = bits;
+      c.for_nblk = nblk;
+    }
+  }
   uint64_t h1 = 1469598103934665603ull, h2 = 0x9E3779B97F4A7C15ull;  // FNV-1a, and a multiply-xorshift mix
   for (uint8_t x : le) {
     h1 = (h1 ^ x) * 1099511628211ull;
@@ -1994,7 +2027,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   }
   int pshift = 0;
   while ((8ull * L.num_sections << (pshift + 1)) <= PGPU_PART_LDS_BYTES) ++pshift;
-  const uint64_t nparts = (L.num_keys + (1ull << pshift) - 1) >> pshift;
+  uint64_t nparts = (L.num_keys + (1ull << pshift) - 1) >> pshift;
   part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31) &&
             L.num_sections <= PGPU_PART_MAX_SECTIONS;
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
@@ -2122,6 +2155,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // instead of gathering them from L2 (one 128-B line per 4-B lookup)
   int slice_shift = 0, ldict = 0;
   uint32_t pdict_n = 0;
+  int for_old_pshift = -1;
+  uint64_t for_old_nparts = 0;
+  const HostColumn* for_h = nullptr;
   if (part_idbits) {
     const HostColumn* h0 = &q->segments[0].segment->cols[q->segments[0].column_map[pcol]];
     pdict_n = (uint32_t)h0->dict_card;
@@ -2131,6 +2167,23 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     while ((1ull << slice_shift) < pdict_n) ++slice_shift;
     static const bool no_ldict = getenv("PGPU_NO_LDICT") && atoi(getenv("PGPU_NO_LDICT")) != 0;
     ldict = need_val && !no_ldict && (8ull * L.num_sections << pshift) + (4ull << slice_shift) <= PGPU_LDS_LIMIT;
+    // too large to copy whole: its frame-of-reference image, beside a table of fewer keys per partition
+    static const bool no_for = getenv("PGPU_NO_FOR") && atoi(getenv("PGPU_NO_FOR")) != 0;
+    if (need_val && !ldict && !no_for && h0->for_bits > 0 && h0->dict_type == PGPU_INT) {
+      const uint64_t fb = 4ull * ((uint64_t)h0->for_nblk * (1 + h0->for_bits) + 1);
+      int ps = pshift;
+      while (ps > 9 && (8ull * L.num_sections << ps) + fb > PGPU_LDS_LIMIT) --ps;
+      const uint64_t np2 = (L.num_keys + (1ull << ps) - 1) >> ps;
+      if ((8ull * L.num_sections << ps) + fb <= PGPU_LDS_LIMIT && np2 <= PGPU_PSCAN_MAX_PARTS &&
+          np2 <= PGPU_PART_MAX_PARTS && ps + part_idbits <= 32) {
+        for_old_pshift = pshift;
+        for_old_nparts = nparts;
+        pshift = ps;
+        nparts = np2;
+        ldict = 2;
+        for_h = h0;
+      }
+    }
   }
   // partitioned group-by whose segments need no candidate queue: phase 1 by part_scan_kernel (self-loading waves,
   // records written through per-partition LDS rings of >= two 128-B lines); two workgroups per CU when the rings
@@ -2158,6 +2211,12 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       grid = std::max(1, g);
       dyn = align16(fixed_b + 4ull * ptotal * part_rw * rc);
     }
+  }
+  if (ldict == 2 && !p.pscan) {  // the ring's partition counters were sized for the original geometry
+    pshift = for_old_pshift;
+    nparts = for_old_nparts;
+    ldict = 0;
+    for_h = nullptr;
   }
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -2232,6 +2291,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.slice_shift = slice_shift;
     p.ldict = ldict;
     p.pdict_n = pdict_n;
+    p.pfor = for_h ? (const uint32_t*)for_h->for_dev.p : nullptr;
+    p.for_bits = for_h ? for_h->for_bits : 0;
+    p.for_nblk = for_h ? for_h->for_nblk : 0;
     p.pcol = pcol;
     p.rw = part_rw;
     p.rec_idbits = part_idbits;

@@ -501,3 +501,25 @@ def test_inverted_container_kinds_vs_oracle(gpu_ctx, force):
             assert res.stats.num_docs_scanned == ref.num_docs_scanned
     finally:
         g.release()
+
+
+@pytest.mark.gpu
+def test_partitioned_groupby_shared_dictionary_vs_oracle(gpu_ctx):
+    """Config 4's shape on small segments: 1M-key GROUP BY through the partitioned path, one-word records over the
+    shared 64K-value metric dictionary, whose phase-2 lookups read its frame-of-reference image in LDS."""
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import WORKLOADS, build_segment_cpu
+    w = WORKLOADS["groupby1m"]
+    segs = [build_segment_cpu(w, s, 1 << 19, pack_fixed_bit) for s in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        for sql in (w.sql, "SELECT k, SUM(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) ASC LIMIT 20",
+                    "SELECT k, AVG(m), MIN(m) FROM synth WHERE m > 500000 GROUP BY k ORDER BY AVG(m) DESC LIMIT 50"):
+            q = parse_sql(sql)
+            res = GpuPlanMaker(gpu_ctx, num_groups_limit=2_000_000).execute(q, gs)
+            ref = engine.execute(q, segs, num_groups_limit=2_000_000)
+            assert res.rows == ref.rows, sql
+            assert res.stats.num_docs_scanned == ref.num_docs_scanned
+    finally:
+        for g in gs:
+            g.release()
