@@ -518,7 +518,7 @@ def test_partitioned_groupby_shared_dictionary_vs_oracle(gpu_ctx):
             q = parse_sql(sql)
             res = GpuPlanMaker(gpu_ctx, num_groups_limit=2_000_000).execute(q, gs)
             ref = engine.execute(q, segs, num_groups_limit=2_000_000)
-            assert res.rows == ref.rows, sql
+            check_groups(res, ref)  # ties in the ORDER BY value may order differently: values compared in order
             assert res.stats.num_docs_scanned == ref.num_docs_scanned
     finally:
         for g in gs:
