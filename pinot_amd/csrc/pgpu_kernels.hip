@@ -2942,6 +2942,99 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   int32_t op[NS > 0 ? NS : 1];
 #pragma unroll
   for (int s = 0; s < NS; ++s) op[s] = p.sec_op[1 + s];
+  if constexpr (LDM == 2) {
+    int32_t vt = PGPU_INT;
+    for (int a = 0; a < p.nagg; ++a)
+      if (p.aggs[a].fn != PGPU_AGG_COUNT) vt = p.aggs[a].vtype;
+    // compact table beside the frame-of-reference dictionary: count u32, SUM sections int64, MIN / MAX sections
+    // u32 dict ids (one-word records reduce ids), so 4096 keys and a 64K-value image fit the LDS together
+    unsigned char* base = (unsigned char*)ptab;
+    uint32_t* cnt = (uint32_t*)base;
+    uint32_t soff[NS > 0 ? NS : 1];
+    uint32_t at = 4u * K;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      soff[s] = at;
+      at += (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) ? 8u * K : 4u * K;
+    }
+    uint32_t* fimg = (uint32_t*)(base + at);
+    const int fbits = p.for_bits, fnblk = p.for_nblk;
+    for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) {
+      cnt[i] = 0u;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) ((int64_t*)(base + soff[s]))[i] = 0;
+        else ((uint32_t*)(base + soff[s]))[i] = op[s] == PGPU_RED_MIN_I64 ? 0xFFFFFFFFu : 0u;
+      }
+    }
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(fnblk * (1 + fbits) + 1); i += blockDim.x) fimg[i] = gld(p.pfor, i);
+    __syncthreads();
+    const int idbits = p.rec_idbits;
+    const uint32_t idmask = (1u << idbits) - 1u;
+    constexpr int R = 16;
+    for (int w = w0 + wave; w < w1; w += nwaves) {
+      if (((w - w0 - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
+      const uint32_t n = p.rcount[(size_t)q * nwg + w];
+      const size_t rb = part_base(p, q, w);
+      for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
+        uint32_t k[R], id[R];
+        bool ok[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint32_t i = i0 + r * 64 + lane;
+          ok[r] = i < n;
+          const uint32_t v = gld(p.recs, rb + (ok[r] ? i : n - 1));
+          k[r] = v >> idbits;
+          id[r] = v & idmask;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (ok[r]) atomicAdd(&cnt[k[r]], 1u);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
+            unsigned long long* sec = (unsigned long long*)(base + soff[s]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (!ok[r]) continue;
+              // value = block base + the id's fbits-bit offset (it may straddle two words)
+              const uint32_t blk = id[r] >> 5, bit = (id[r] & 31u) * (uint32_t)fbits;
+              const uint32_t* wds = fimg + fnblk + (size_t)blk * fbits + (bit >> 5);
+              const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
+              const uint32_t val = fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
+              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)val);
+            }
+          } else {
+            uint32_t* sec = (uint32_t*)(base + soff[s]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (!ok[r]) continue;
+              if (op[s] == PGPU_RED_MIN_I64) atomicMin(&sec[k[r]], id[r]);
+              else atomicMax(&sec[k[r]], id[r]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t kk = threadIdx.x; kk < nk; kk += blockDim.x) {
+      if (cnt[kk] == 0u) continue;
+      for (int s = 0; s <= NS; ++s) {
+        int64_t v;
+        if (s == 0) {
+          v = (int64_t)cnt[kk];
+        } else if (op[s - 1] == PGPU_RED_SUM_I64 || op[s - 1] == PGPU_RED_SUM_F64) {
+          v = ((const int64_t*)(base + soff[s - 1]))[kk];
+        } else {  // id -> cell key of its value
+          v = raw_to_cell(gld((const uint32_t*)p.pdict, ((const uint32_t*)(base + soff[s - 1]))[kk]), vt, p.sec_op[s]);
+        }
+        int64_t* cell = &p.table[(size_t)s * p.G + key0 + kk];
+        if (split) cell_atomic(cell, p.sec_op[s], v);
+        else *cell = cell_combine(p.sec_op[s], *cell, v);
+      }
+    }
+    return;
+  }
   int32_t vt = PGPU_INT;
   for (int a = 0; a < p.nagg; ++a)
     if (p.aggs[a].fn != PGPU_AGG_COUNT) vt = p.aggs[a].vtype;
@@ -3328,9 +3421,13 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
-  const size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 +
-                     (p.ldict == 1 ? (size_t)4 << p.slice_shift
-                                   : (p.ldict == 2 ? (size_t)4 * ((size_t)p.for_nblk * (1 + p.for_bits) + 1) : 0));
+  size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 + (p.ldict == 1 ? (size_t)4 << p.slice_shift : 0);
+  if (p.ldict == 2) {  // compact table (count and MIN / MAX ids in 4 B, SUM in 8 B) + the dictionary image
+    lds = (size_t)4 << p.pshift;
+    for (int s = 1; s < p.nsec; ++s)
+      lds += (p.sec_op[s] == PGPU_RED_SUM_I64 || p.sec_op[s] == PGPU_RED_SUM_F64 ? (size_t)8 : (size_t)4) << p.pshift;
+    lds += (size_t)4 * ((size_t)p.for_nblk * (1 + p.for_bits) + 1);
+  }
   const dim3 g(p.p2work ? p.p2grid : p.nparts);
   switch (p.nsec - 1) {
 #define PART_LAUNCH(NS)                                                                                    \

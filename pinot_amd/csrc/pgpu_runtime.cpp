@@ -2171,10 +2171,18 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     static const bool no_for = getenv("PGPU_NO_FOR") && atoi(getenv("PGPU_NO_FOR")) != 0;
     if (need_val && !ldict && !no_for && h0->for_bits > 0 && h0->dict_type == PGPU_INT) {
       const uint64_t fb = 4ull * ((uint64_t)h0->for_nblk * (1 + h0->for_bits) + 1);
+      // fewer keys per partition means more phase-1 partitions and shallower LDS rings per partition, which
+      // skewed keys pay for (config 4 Zipf(1.1): 24 -> 39 ms at 2048 keys); only the unchanged geometry is used
+      // unless PGPU_FOR_SHRINK=1
+      // the compact phase-2 table: count and MIN / MAX ids in 4 B, SUM sections in 8 B per key
+      uint64_t per_key = 4;
+      for (int s = 1; s < L.num_sections; ++s)
+        per_key += L.section_op[s] == PGPU_RED_SUM_I64 || L.section_op[s] == PGPU_RED_SUM_F64 ? 8 : 4;
+      static const bool shrink = getenv("PGPU_FOR_SHRINK") && atoi(getenv("PGPU_FOR_SHRINK")) != 0;
       int ps = pshift;
-      while (ps > 9 && (8ull * L.num_sections << ps) + fb > PGPU_LDS_LIMIT) --ps;
+      while (shrink && ps > 9 && (per_key << ps) + fb > PGPU_LDS_LIMIT) --ps;
       const uint64_t np2 = (L.num_keys + (1ull << ps) - 1) >> ps;
-      if ((8ull * L.num_sections << ps) + fb <= PGPU_LDS_LIMIT && np2 <= PGPU_PSCAN_MAX_PARTS &&
+      if ((per_key << ps) + fb <= PGPU_LDS_LIMIT && np2 <= PGPU_PSCAN_MAX_PARTS &&
           np2 <= PGPU_PART_MAX_PARTS && ps + part_idbits <= 32) {
         for_old_pshift = pshift;
         for_old_nparts = nparts;
