@@ -61,25 +61,27 @@ def available_cores() -> int:
 
 def measure(ex, q, segs, steps, warmup, inflight, world, barrier):
     """Time `steps` whole queries (plan, launch, reduce, finish) with up to `inflight` in flight at N = 1;
-    returns (ms_per_step over the max of ranks, average HIP-event kernel ms, last result)."""
+    returns (ms_per_step over the max of ranks, average HIP-event kernel ms, last result).  The warmup runs the
+    same pipeline for max(warmup, inflight) queries, so every workspace the timed region uses has been sized."""
     import torch
     import torch.distributed as dist
-    for _ in range(warmup):
-        ex.execute(q, segs)
+
+    def run(n):
+        pending, kernel_ms, result, submitted = [], [], None, 0
+        for _ in range(n):
+            while submitted < n and len(pending) < max(1, inflight):
+                pending.append(ex.submit(q, segs))
+                submitted += 1
+            result = ex.collect(pending.pop(0))
+            kernel_ms.append(ex.last_stats.kernel_ms)
+        return result, kernel_ms
+
+    run(max(warmup, inflight if world == 1 else 1))
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    kernel_ms = []
     t_start = time.perf_counter()
-    result = None
-    pending = []
-    submitted = 0
-    for _ in range(steps):
-        while submitted < steps and len(pending) < max(1, inflight):
-            pending.append(ex.submit(q, segs))
-            submitted += 1
-        result = ex.collect(pending.pop(0))
-        kernel_ms.append(ex.last_stats.kernel_ms)
+    result, kernel_ms = run(steps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -131,7 +133,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
     log(f"{name}: generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
     opts = dict(w.options)
     q = parse_sql(w.sql)
-    pm = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000))
+    pm = GpuPlanMaker(ctx, **plan_options(opts))
     ex = DistributedExecutor(pm)
     try:
         algo_bytes, st, breakdown = algorithmic_bytes(ex, pm, q, segs)
@@ -283,9 +285,18 @@ def inverted_bytes_read(q, segs):
 PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789")}
 
 
+def plan_options(opts):
+    """GpuPlanMaker settings of a workload: numGroupsLimit and the server's ORDER BY trim (config 4 runs with
+    minServerGroupTrimSize = -1, SURVEY.md 8(d): every group comes back, so the result is exact)."""
+    return {"num_groups_limit": opts.get("num_groups_limit", 100_000),
+            "min_server_group_trim_size": opts.get("min_server_group_trim_size", 5000)}
+
+
 def parity_check(ctx, w, q, opts):
     """GPU vs oracle on 2 small segments of the workload: the bench query and a looser variant of it
-    (called from the CPU leg only)."""
+    (called from the CPU leg only).  With the server trim off the GPU returns every group, compared as a set
+    with the oracle's; with it on, the final ORDER BY / LIMIT rows must be equal and every returned group must
+    be one of the oracle's groups with the same values (the trim keeps a subset of the table)."""
     from oracle import engine
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.plan import GpuPlanMaker
@@ -300,13 +311,20 @@ def parity_check(ctx, w, q, opts):
     if w.name in PARITY_VARIANTS:
         a, b = PARITY_VARIANTS[w.name]
         queries.append(parse_sql(w.sql.replace(a, b)))
-    out = {"docs": 2 * n, "matched": [], "ok": True}
+    po = plan_options(opts)
+    out = {"docs": 2 * n, "matched": [], "groups": [], "ok": True,
+           "compared": "all groups" if po["min_server_group_trim_size"] <= 0 else "ORDER BY/LIMIT rows + group subset"}
     try:
         for qq in queries:
-            res = GpuPlanMaker(ctx, num_groups_limit=opts.get("num_groups_limit", 100_000)).execute(qq, gs)
-            ref = engine.execute(qq, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
+            res = GpuPlanMaker(ctx, **po).execute(qq, gs)
+            ref = engine.execute(qq, segs, num_groups_limit=po["num_groups_limit"])
             if qq.group_by:
-                ok = sorted(res.group_rows) == sorted(ref.group_rows)
+                got, exp = res.group_rows, ref.group_rows
+                if po["min_server_group_trim_size"] <= 0:
+                    ok = sorted(got) == sorted(exp)
+                else:
+                    ok = set(got) <= set(exp) and list(res.rows) == list(ref.rows)
+                out["groups"].append(len(got))
             else:
                 ok = list(res.aggregation_result) == list(ref.aggregation_result)
             ok = ok and res.stats.num_docs_scanned == ref.num_docs_scanned

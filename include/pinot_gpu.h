@@ -457,6 +457,16 @@ int pgpu_query_launch_expr(pgpu_context* ctx, const pgpu_query_desc* q, const pg
                            int32_t num_nodes, void* stream, void* dev_table, uint64_t table_bytes,
                            pgpu_query** out_query);
 
+/* pgpu_query_submit (expr == NULL: the descriptor's per-segment programs) or pgpu_query_submit_expr, with the
+ * server's ORDER BY ... LIMIT trim known up front (`order`, as for pgpu_query_collect_topk; NULL = every group):
+ * tables above 8 MiB are ranked and compacted on the GPU right behind the query's kernels, on its own stream, so
+ * pgpu_query_collect(_topk) only copies the kept rows out -- a collect never waits behind the next query's kernel
+ * (GroupByOrderByCombineOperator.mergeResults + IndexedTable.finish, core/operator/combine/
+ * GroupByOrderByCombineOperator.java:127-248; trimSize = GroupByUtils.getTableCapacity).  Pass the same order to
+ * pgpu_query_collect_topk (any other order selects again from the intact table). */
+int pgpu_query_submit_ordered(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                              int32_t num_nodes, const pgpu_topk* order, pgpu_query** out_query);
+
 /* ---- node-level combine: one process, several GPUs, RCCL inside the library ------------------------------------
  * For a server that drives all GPUs of a node from one process (a JVM): contexts for the given HIP ordinals and
  * one RCCL communicator clique over them (RCCL is loaded on first use).  Segments are uploaded through each

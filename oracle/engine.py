@@ -48,6 +48,9 @@ EOF = -(2 ** 31)  # Constants.EOF = Integer.MIN_VALUE
 
 
 # ---- decoded segment ------------------------------------------------------------------------------------------
+_BIG_DICTS: Dict[int, tuple] = {}  # id(bytes) -> (the bytes, decoded values): the last decoded >= 16M-entry dictionary
+
+
 class DecodedSegment:
     """Dict ids / values of a SegmentData decoded from its reference-format bytes."""
 
@@ -65,8 +68,15 @@ class DecodedSegment:
             if c.data_type == PGPU_STRING:
                 d = list(c.dictionary)
             else:
-                be = {PGPU_INT: ">i4", PGPU_LONG: ">i8", PGPU_FLOAT: ">f4", PGPU_DOUBLE: ">f8"}[c.data_type]
-                d = np.frombuffer(c.dictionary, dtype=be).astype(NATIVE[c.data_type])
+                hit = _BIG_DICTS.get(id(c.dictionary))
+                if hit is not None and hit[0] is c.dictionary:
+                    d = hit[1]
+                else:
+                    be = {PGPU_INT: ">i4", PGPU_LONG: ">i8", PGPU_FLOAT: ">f4", PGPU_DOUBLE: ">f8"}[c.data_type]
+                    d = np.frombuffer(c.dictionary, dtype=be).astype(NATIVE[c.data_type])
+                    if len(d) >= (1 << 24):  # decoded once for every segment / query sharing the same bytes
+                        _BIG_DICTS.clear()
+                        _BIG_DICTS[id(c.dictionary)] = (c.dictionary, d)
             self._dict[col] = d
         return d
 
@@ -172,19 +182,41 @@ def _truth_on_dictionary(d, dt: int, p: Predicate, pad=None) -> np.ndarray:
         return np.fromiter((ok(v) for v in vals), dtype=bool, count=len(vals))
     v = np.asarray(d)
     if dt in (PGPU_INT, PGPU_LONG):
-        v = v.astype(np.int64)
+        # An integer dictionary is strictly ascending (BaseImmutableDictionary; SegmentDictionaryCreator sorts and
+        # dedups), so each comparison with an integer threshold holds on one prefix or suffix of it: found by
+        # binary search (insertionIndexOf), the same truth per value as comparing every entry, without a pass
+        # over dictionaries of up to 2^30 values.
+        n = len(v)
+        tmin, tmax = (-(1 << 31), (1 << 31) - 1) if v.dtype.itemsize == 4 else (-(1 << 63), (1 << 63) - 1)
+
+        def count_lt(x: int) -> int:  # entries < x, for any Python int
+            if x <= tmin:
+                return 0
+            if x > tmax:
+                return n
+            return int(np.searchsorted(v, np.array(x, dtype=v.dtype), side="left"))  # no whole-array cast
+
+        def prefix(k: int) -> np.ndarray:
+            m = np.zeros(n, dtype=bool)
+            m[:k] = True
+            return m
 
         def eq(lit):
             f = Fraction(lit)
-            return (v == int(f)) if f.denominator == 1 else np.zeros(len(v), bool)
+            m = np.zeros(n, dtype=bool)
+            if f.denominator == 1:
+                i = count_lt(int(f))
+                if i < n and int(v[i]) == int(f):
+                    m[i] = True
+            return m
 
         def ge(lit, inclusive):  # v >= lit  /  v > lit
             f = Fraction(lit)
-            return v >= math.ceil(f) if inclusive else v > math.floor(f)
+            return ~prefix(count_lt(math.ceil(f) if inclusive else math.floor(f) + 1))
 
         def le(lit, inclusive):  # v <= lit  /  v < lit
             f = Fraction(lit)
-            return v <= math.floor(f) if inclusive else v < math.ceil(f)
+            return prefix(count_lt(math.floor(f) + 1 if inclusive else math.ceil(f)))
     else:
         v = v.astype(np.float64)
         cast = (lambda x: float(np.float32(float(x)))) if dt == PGPU_FLOAT else float

@@ -160,6 +160,8 @@ SIGNATURES = [
     ("pgpu_query_collect", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
                                      C.POINTER(C.c_uint64), C.POINTER(QueryStats)]),
     ("pgpu_query_submit_expr", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(ExprNode), C.c_int32, C.POINTER(_P)]),
+    ("pgpu_query_submit_ordered", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(ExprNode), C.c_int32,
+                                            C.POINTER(TopK), C.POINTER(_P)]),
     ("pgpu_query_launch_expr", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(ExprNode), C.c_int32, _P, _P,
                                          C.c_uint64, C.POINTER(_P)]),
     ("pgpu_query_execute", C.c_int, [_P, C.POINTER(QueryDesc), C.POINTER(C.c_int64), C.POINTER(C.c_int64),

@@ -127,6 +127,28 @@ struct DevMem {
     return e;
   }
   hipError_t ensure(size_t bytes) { return n >= bytes ? hipSuccess : alloc(std::max(bytes, n * 3 / 2)); }
+  // Query-path growth: stream-ordered, from the context's memory pool.  hipFree waits for the whole device --
+  // every other query in flight -- so a workspace that grows inside pgpu_query_submit must never call it: the old
+  // block goes back to the pool behind the work already queued on `s` and the new one is carved out in stream
+  // order (the pool keeps its memory reserved, so steady-state growth costs nothing).
+  hipError_t ensure(size_t bytes, hipMemPool_t pool, hipStream_t s) {
+    if (n >= bytes) return hipSuccess;
+    if (!pool) return ensure(bytes);
+    size_t nb = std::max(bytes, n * 3 / 2);
+    if (nb == 0) nb = 16;
+    if (p) {
+      const hipError_t e = hipFreeAsync(p, s);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      n = 0;
+    }
+    void* q = nullptr;
+    const hipError_t e = hipMallocFromPoolAsync(&q, nb, pool, s);
+    if (e != hipSuccess) return e;
+    p = q;
+    n = nb;
+    return hipSuccess;
+  }
 };
 
 struct PinnedMem {
@@ -192,10 +214,18 @@ struct pgpu_context {
   // nothing is lost by serialising them, and their HIP events then time each kernel alone)
   hipStream_t qstream = nullptr;
   hipStream_t cstream = nullptr;  // pgpu_query_cancel: writes cancel words while the query stream is busy
+  // workspace buffers grow from this pool in stream order (DevMem::ensure(bytes, pool, stream)); it never returns
+  // memory to the device on its own (release threshold = max), so no query-path allocation reaches the driver
+  // twice.  nullptr when the device has no memory pools: growth then falls back to hipMalloc / hipFree.
+  hipMemPool_t mpool = nullptr;
   ~pgpu_context() {
     pool.clear();
     if (qstream) (void)hipStreamDestroy(qstream);
     if (cstream) (void)hipStreamDestroy(cstream);
+    if (mpool) {
+      (void)hipDeviceSynchronize();
+      (void)hipMemPoolDestroy(mpool);
+    }
   }
 };
 
@@ -256,6 +286,8 @@ struct pgpu_query {
   Workspace* tws = nullptr;
   pgpu_table_layout layout{};
   bool small = false;
+  bool eager = false;  // compacted on the device at submit (enqueue_compact): collect only copies the rows out
+  bool eager_ordered = false;  // ... restricted to the best groups by the order given at submit
   // HASH mode: tracked segments (query segment index) whose distinct keys are checked against the limit
   std::vector<int32_t> tracked;
   int64_t groups_limit = 0;
@@ -513,6 +545,23 @@ int pgpu_init(int device_ordinal, pgpu_context** out_ctx) {
   auto* ctx = new pgpu_context();
   ctx->device = device_ordinal;
   ctx->num_cus = prop.multiProcessorCount;
+  int pools = 0;
+  if (hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device_ordinal) == hipSuccess && pools) {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device_ordinal;
+    if (hipMemPoolCreate(&ctx->mpool, &props) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      if (hipMemPoolSetAttribute(ctx->mpool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) {
+        (void)hipMemPoolDestroy(ctx->mpool);
+        ctx->mpool = nullptr;
+      }
+    } else {
+      ctx->mpool = nullptr;
+    }
+  }
   *out_ctx = ctx;
   return PGPU_OK;
 }
@@ -1979,8 +2028,16 @@ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 extern "C" {
 
 // host_table (device-visible pointer into pinned host memory, or null): the finished table is also exported there
+namespace {
+int enqueue_compact(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, const void* dev_table,
+                    hipStream_t st, const pgpu_topk* order);
+}  // namespace
+
+// eager: compact the table (only the best groups by eager_order, when given) on the query's stream right behind
+// its kernels, into the workspace; pgpu_query_collect then only copies the rows out (pgpu_query_submit_ordered)
 static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream, void* dev_table,
-                       uint64_t table_bytes, int64_t* host_table, pgpu_query** out_query) {
+                       uint64_t table_bytes, int64_t* host_table, pgpu_query** out_query, bool eager = false,
+                       const pgpu_topk* eager_order = nullptr) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
@@ -2270,10 +2327,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_invids = align16(o_inv + pk.invx.size() * sizeof(InvLeafX));
   const size_t total = align16(o_invids + pk.invids.size() * 4) + 16;
   hipError_t e = ws->h_arena.ensure(total);
-  if (e == hipSuccess) e = ws->arena.ensure(total);
-  if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16);
-  if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16);
-  if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS);
+  if (e == hipSuccess) e = ws->arena.ensure(total, ctx->mpool, st);
+  if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16, ctx->mpool, st);
+  if (e == hipSuccess) e = ws->stats.ensure(8ull * nwaves * PGPU_NSTATS + 16, ctx->mpool, st);
+  if (e == hipSuccess) e = ws->stats_out.ensure(8 * PGPU_NSTATS, ctx->mpool, st);
   if (e == hipSuccess) e = ws->h_stats.ensure(8 * PGPU_NSTATS + 16);
   // the cancel copy's pinned source is allocated here, never in pgpu_query_cancel: an allocation there could wait
   // for the device -- i.e. for the very kernel the cancel is meant to stop
@@ -2289,7 +2346,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       ws->d_cancel.p = nullptr;
     }
   }
-  if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF);
+  if (e == hipSuccess && (p.flags & PGPU_FLAG_PROFILE)) e = ws->prof.ensure(8ull * nwaves * PGPU_NPROF, ctx->mpool, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "workspace allocation: %s", hipGetErrorString(e)));
   if (p.mode == PGPU_MODE_PART) {
     // region capacity: 1.25x the expected records per (partition, workgroup) + slack; full regions spill to
@@ -2324,8 +2381,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     if (cap > max_cap) cap = max_cap / per_line * per_line;
     if (cap > (uint64_t)INT32_MAX) cap = (uint64_t)INT32_MAX / per_line * per_line;
     p.rcap = (int32_t)std::max<uint64_t>(cap, 16);
-    e = ws->recs.ensure(regions * (uint64_t)p.rcap * 4ull * p.rw);
-    if (e == hipSuccess) e = ws->rcount.ensure(4ull * regions);
+    e = ws->recs.ensure(regions * (uint64_t)p.rcap * 4ull * p.rw, ctx->mpool, st);
+    if (e == hipSuccess) e = ws->rcount.ensure(4ull * regions, ctx->mpool, st);
     p.pblock = (uint64_t)p.nparts * (uint64_t)p.rcap;  // records per phase-1 workgroup block
     p.pcount = p.pcap = p.poff = nullptr;
     p.p2work = nullptr;
@@ -2337,10 +2394,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       // of the records
       p.psample = std::max(1, p.total_tiles / 8192);
       p.p2grid = 2 * p.nparts;
-      if (e == hipSuccess) e = ws->pcount.ensure(4ull * p.nparts);
-      if (e == hipSuccess) e = ws->pcap.ensure(4ull * p.nparts);
-      if (e == hipSuccess) e = ws->poff.ensure(4ull * p.nparts);
-      if (e == hipSuccess) e = ws->p2work.ensure(16ull * p.p2grid);
+      if (e == hipSuccess) e = ws->pcount.ensure(4ull * p.nparts, ctx->mpool, st);
+      if (e == hipSuccess) e = ws->pcap.ensure(4ull * p.nparts, ctx->mpool, st);
+      if (e == hipSuccess) e = ws->poff.ensure(4ull * p.nparts, ctx->mpool, st);
+      if (e == hipSuccess) e = ws->p2work.ensure(16ull * p.p2grid, ctx->mpool, st);
       p.pcount = (uint32_t*)ws->pcount.p;
       p.pcap = (uint32_t*)ws->pcap.p;
       p.poff = (uint32_t*)ws->poff.p;
@@ -2351,19 +2408,19 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.rcount = (uint32_t*)ws->rcount.p;
   }
   if (pk.raw_words > 0) {
-    e = ws->rawbits.ensure(4ull * pk.raw_words);
+    e = ws->rawbits.ensure(4ull * pk.raw_words, ctx->mpool, st);
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "raw-value leaf bitmaps: %s", hipGetErrorString(e)));
   }
   if (pk.leaf_words > 0) {
-    e = ws->leafbits.ensure(4ull * pk.leaf_words);
+    e = ws->leafbits.ensure(4ull * pk.leaf_words, ctx->mpool, st);
     if (e == hipSuccess) e = ws->h_leafbits.ensure(4ull * pk.leaf_words);
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "filter-statistics bitmaps: %s", hipGetErrorString(e)));
     p.leaf_bits = (uint32_t*)ws->leafbits.p;
   }
   if (p.mode == PGPU_MODE_HASH) {
     p.segmask_rows = (int32_t)pk.tracked.size();
-    e = ws->hflag.ensure(16);
-    if (e == hipSuccess && p.segmask_rows) e = ws->segmask.ensure((size_t)p.segmask_rows * (L.num_keys / 8) + 16);
+    e = ws->hflag.ensure(16, ctx->mpool, st);
+    if (e == hipSuccess && p.segmask_rows) e = ws->segmask.ensure((size_t)p.segmask_rows * (L.num_keys / 8) + 16, ctx->mpool, st);
     if (e == hipSuccess && p.segmask_rows) e = ws->h_segcnt.ensure(8 * (size_t)p.segmask_rows);
     if (e == hipSuccess) e = hipMemsetAsync(ws->hflag.p, 0, 16, st);
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "hash group-by buffers: %s", hipGetErrorString(e)));
@@ -2458,6 +2515,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = pgpu_launch_leafbits(p, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ws->h_leafbits.p, ws->leafbits.p, 4ull * pk.leaf_words, hipMemcpyDeviceToHost, st);
   }
+  if (e == hipSuccess && eager) {
+    const int crc = enqueue_compact(ctx, ws, &L, dev_table, st, eager_order);
+    if (crc) return bail(crc);
+  }
   // completion of this query alone (later queries may already be queued behind it on the same stream)
   if (e == hipSuccess) e = hipEventRecord(ws->done, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
@@ -2466,6 +2527,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   qq->ctx = ctx;
   qq->ws = ws;
   qq->done = ws->done;
+  qq->eager = eager;
   qq->stream = st;
   qq->params = p;
   qq->grid = grid;
@@ -2719,8 +2781,8 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
   const int kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;  // 0: the cell index is the key
   const int okw = kw > 1 ? kw : 1;
   const uint64_t nb = (G + 4095) / 4096;
-  HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16));
-  HIP_TRY(ws->cmp_total.ensure(16));
+  HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16, ctx->mpool, st));
+  HIP_TRY(ws->cmp_total.ensure(16, ctx->mpool, st));
   HIP_TRY(ws->h_total.ensure(16));
   const uint64_t* okey = nullptr;
   const TopkState* tstate = nullptr;
@@ -2728,8 +2790,8 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
     TopkDev spec;
     const int rc = topk_spec(L, order, &spec);
     if (rc) return rc;
-    HIP_TRY(ws->tk_keys.ensure(8 * G + 16));
-    HIP_TRY(ws->tk_state.ensure(sizeof(TopkState) + 4 * 256 + 16));
+    HIP_TRY(ws->tk_keys.ensure(8 * G + 16, ctx->mpool, st));
+    HIP_TRY(ws->tk_state.ensure(sizeof(TopkState) + 4 * 256 + 16, ctx->mpool, st));
     TopkState* ts = (TopkState*)ws->tk_state.p;
     uint32_t* hist = (uint32_t*)((char*)ws->tk_state.p + sizeof(TopkState));
     HIP_TRY(pgpu_launch_topk((const int64_t*)dev_table, spec, order->k, (uint64_t*)ws->tk_keys.p, ts, hist, st));
@@ -2746,14 +2808,50 @@ int compact_into(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, c
     return fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
                 (unsigned long long)capacity);
   if (n == 0) return PGPU_OK;
-  HIP_TRY(ws->cmp_keys.ensure(8 * n * okw));
-  HIP_TRY(ws->cmp_cells.ensure(8 * n * nsec));
+  HIP_TRY(ws->cmp_keys.ensure(8 * n * okw, ctx->mpool, st));
+  HIP_TRY(ws->cmp_cells.ensure(8 * n * nsec, ctx->mpool, st));
   HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p, nullptr,
                               (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st, okey, tstate));
   HIP_TRY(hipMemcpyAsync(out_keys, ws->cmp_keys.p, 8 * n * okw, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(out_cells, ws->cmp_cells.p, 8 * n * nsec, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   (void)ctx;
+  return PGPU_OK;
+}
+
+// The device half of compact_into, enqueued without any host synchronisation (pgpu_query_submit): capacity for
+// every key, the row count copied into pinned memory.  pgpu_query_collect reads it and copies the rows out.
+int enqueue_compact(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, const void* dev_table,
+                    hipStream_t st, const pgpu_topk* order) {
+  const uint64_t G = L->num_keys;
+  const int nsec = L->num_sections;
+  const int kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;
+  const int okw = kw > 1 ? kw : 1;
+  const uint64_t nb = (G + 4095) / 4096;
+  HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16, ctx->mpool, st));
+  HIP_TRY(ws->cmp_total.ensure(16, ctx->mpool, st));
+  HIP_TRY(ws->h_total.ensure(16));
+  HIP_TRY(ws->cmp_keys.ensure(8 * G * okw + 16, ctx->mpool, st));
+  HIP_TRY(ws->cmp_cells.ensure(8 * G * nsec + 16, ctx->mpool, st));
+  const uint64_t* okey = nullptr;
+  const TopkState* tstate = nullptr;
+  if (order && order->k > 0 && G > order->k) {
+    TopkDev spec;
+    const int rc = topk_spec(L, order, &spec);
+    if (rc) return rc;
+    HIP_TRY(ws->tk_keys.ensure(8 * G + 16, ctx->mpool, st));
+    HIP_TRY(ws->tk_state.ensure(sizeof(TopkState) + 4 * 256 + 16, ctx->mpool, st));
+    TopkState* ts = (TopkState*)ws->tk_state.p;
+    uint32_t* hist = (uint32_t*)((char*)ws->tk_state.p + sizeof(TopkState));
+    HIP_TRY(pgpu_launch_topk((const int64_t*)dev_table, spec, order->k, (uint64_t*)ws->tk_keys.p, ts, hist, st));
+    okey = (const uint64_t*)ws->tk_keys.p;
+    tstate = ts;
+  }
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p,
+                              (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st, okey, tstate));
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p, nullptr,
+                              (int64_t*)ws->cmp_keys.p, (int64_t*)ws->cmp_cells.p, false, st, okey, tstate));
+  HIP_TRY(hipMemcpyAsync(ws->h_total.p, ws->cmp_total.p, 8, hipMemcpyDeviceToHost, st));
   return PGPU_OK;
 }
 
@@ -3115,7 +3213,7 @@ int plan_expr(const pgpu_query_desc* q, const pgpu_expr_node* expr, int32_t num_
 
 extern "C" {
 
-int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** out_query) {
+static int submit_impl(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_topk* order, pgpu_query** out_query) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
@@ -3129,7 +3227,7 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   Workspace* tws = acquire_ws(ctx, &err);  // owns the partial table until pgpu_query_collect
   if (!tws) return err;
   const uint64_t bytes = pgpu_table_bytes(&L);
-  hipError_t e = tws->table.ensure(bytes);
+  hipError_t e = tws->table.ensure(bytes, ctx->mpool, ctx->qstream);
   if (e != hipSuccess) {
     release_ws(ctx, tws);
     return fail(PGPU_E_HIP, "table allocation: %s", hipGetErrorString(e));
@@ -3147,7 +3245,12 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
     }
   }
   pgpu_query* qq = nullptr;
-  rc = launch_impl(ctx, q, ctx->qstream, tws->table.p, tws->table.n, (int64_t*)h_table_dev, &qq);
+  // big tables are compacted right behind the kernels on the query stream: the compaction of query i must not
+  // wait in collect() behind query i+1's kernel, which holds every CU (the table stays intact, so a collect with
+  // another order still selects from it)
+  const bool ordered = order && order->k > 0 && L.num_keys > order->k;
+  rc = launch_impl(ctx, q, ctx->qstream, tws->table.p, tws->table.n, (int64_t*)h_table_dev, &qq, !small,
+                   ordered ? order : nullptr);
   if (rc) {
     release_ws(ctx, tws);
     return rc;
@@ -3155,8 +3258,23 @@ int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** 
   qq->tws = tws;
   qq->layout = L;
   qq->small = small;
+  qq->eager_ordered = ordered;
   *out_query = qq;
   return PGPU_OK;
+}
+
+int pgpu_query_submit(pgpu_context* ctx, const pgpu_query_desc* q, pgpu_query** out_query) {
+  return submit_impl(ctx, q, nullptr, out_query);
+}
+
+int pgpu_query_submit_ordered(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_expr_node* expr,
+                              int32_t num_nodes, const pgpu_topk* order, pgpu_query** out_query) {
+  if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
+  if (!expr) return submit_impl(ctx, q, order, out_query);
+  PlannedDesc pd;
+  const int rc = plan_expr(q, expr, num_nodes, pd);
+  if (rc) return rc;
+  return submit_impl(ctx, &pd.q, order, out_query);  // the descriptor is copied by the submit
 }
 
 int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
@@ -3169,7 +3287,24 @@ int pgpu_query_collect_topk(pgpu_query* qq, const pgpu_topk* order, int64_t* out
   if (!qq || !qq->tws || !out_num_groups) return fail(PGPU_E_INVALID, "query was not submitted");
   int rc = pgpu_query_wait(qq, out_stats);
   const pgpu_table_layout& L = qq->layout;
-  if (rc == PGPU_OK && order && order->k > 0 && L.num_keys > order->k) {
+  const bool trim = order && order->k > 0 && L.num_keys > order->k;
+  if (rc == PGPU_OK && qq->eager && trim == qq->eager_ordered) {
+    // compacted on the device behind the kernels (enqueue_compact): only the rows cross PCIe, on the copy engine
+    const uint64_t n = (uint64_t)*(const int64_t*)qq->ws->h_total.p;
+    *out_num_groups = n;
+    if (n > capacity) {
+      rc = fail(PGPU_E_INVALID, "%llu non-empty groups exceed capacity %llu", (unsigned long long)n,
+                (unsigned long long)capacity);
+    } else if (n > 0) {
+      const int okw = L.key_kind == PGPU_KEYS_HASH && L.key_words == 2 ? 2 : 1;
+      hipStream_t cs = qq->ws->stream;
+      hipError_t e = hipMemcpyAsync(out_keys, qq->ws->cmp_keys.p, 8 * n * okw, hipMemcpyDeviceToHost, cs);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(out_cells, qq->ws->cmp_cells.p, 8 * n * L.num_sections, hipMemcpyDeviceToHost, cs);
+      if (e == hipSuccess) e = hipStreamSynchronize(cs);
+      if (e != hipSuccess) rc = fail(PGPU_E_HIP, "result copy: %s", hipGetErrorString(e));
+    }
+  } else if (rc == PGPU_OK && trim) {
     // the ORDER BY ... LIMIT trim runs on the device copy of the table (small tables too: the host copy is only
     // a shortcut for plain compaction)
     rc = compact_into(qq->ctx, qq->ws, &L, qq->tws->table.p, qq->ws->stream, out_keys, out_cells, capacity,

@@ -668,12 +668,22 @@ class GpuPlanMaker:
         desc, keep, globals_ = self.build_desc(query, segments, plan_filters=expr is None)
         L = self.layout(desc)
         h = C.c_void_p()
-        if expr is None:
-            _lib.check(self.ctx._lib.pgpu_query_submit(self.ctx.handle, C.byref(desc), C.byref(h)))
-        else:
-            _lib.check(self.ctx._lib.pgpu_query_submit_expr(self.ctx.handle, C.byref(desc), expr[0], expr[1],
-                                                            C.byref(h)))
-        return PendingQuery(self, query, len(segments), h, L, globals_)
+        # the server trim is known now: big tables are ranked and compacted behind the kernels (collect only copies)
+        order = self.trim_order(query, globals_)
+        _lib.check(self.ctx._lib.pgpu_query_submit_ordered(
+            self.ctx.handle, C.byref(desc), expr[0] if expr is not None else None, expr[1] if expr is not None else 0,
+            C.byref(order) if order is not None else None, C.byref(h)))
+        pq = PendingQuery(self, query, len(segments), h, L, globals_)
+        pq.order = order
+        return pq
+
+    def trim_order(self, query: QueryContext, globals_) -> Optional[_lib.TopK]:
+        """The IndexedTable trim of GROUP BY ... ORDER BY ... LIMIT (table_capacity(limit), ties kept) as a
+        pgpu_topk, or None when every group comes back (no ORDER BY, trim disabled, or gpu_topk off)."""
+        if not (self.gpu_topk and self.min_server_group_trim_size > 0):
+            return None
+        return topk_spec(query, [len(g[0]) for g in globals_],
+                         table_capacity(query.limit, self.min_server_group_trim_size))
 
     def collect(self, pending: "PendingQuery") -> QueryResult:
         """Wait for a submitted query and finish it (pgpu_query_collect + ORDER BY / LIMIT on the host)."""
@@ -690,9 +700,7 @@ class GpuPlanMaker:
         st = QueryStats()
         h, pending.handle = pending.handle, None
         query = pending.query
-        order = (topk_spec(query, [len(g[0]) for g in pending.globals_],
-                           table_capacity(query.limit, self.min_server_group_trim_size))
-                 if self.gpu_topk and self.min_server_group_trim_size > 0 else None)
+        order = pending.order
         _lib.check(self.ctx._lib.pgpu_query_collect_topk(h, C.byref(order) if order is not None else None,
                                                          keys.ctypes.data_as(C.POINTER(C.c_int64)),
                                                          cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
@@ -742,6 +750,7 @@ class PendingQuery:
     layout: TableLayout
     globals_: list
     mv: Optional[tuple] = None  # (original query, lowered aggregation indexes) when *MV aggregations were lowered
+    order: Optional[object] = None  # the pgpu_topk given at submit (collect passes the same one)
 
     def cancel(self) -> None:
         """Stop the query (pgpu_query_cancel): its kernels skip their remaining tiles and collect raises
@@ -846,51 +855,90 @@ def merge_filtered(query: QueryContext, parts, results: Sequence[QueryResult]) -
 
 class GroupColumns:
     """A compacted group table decoded column-wise (numpy): group values per group column and final values per
-    aggregation, so that ORDER BY / LIMIT over a million groups costs a sort, not a Python loop per group."""
+    aggregation, so that ORDER BY / LIMIT over a million groups costs a sort, not a Python loop per group.
+    Columns are decoded lazily: the ORDER BY keys over every group, everything else only for the rows asked for
+    (``rows(idx)``) -- the broker reduce of a trim-free million-group table touches the rest of it once."""
 
     def __init__(self, query: QueryContext, table: GroupTable, global_dicts: Sequence):
         self.query = query
+        self.table = table
+        self.global_dicts = global_dicts
         L = table.layout
         keys = np.asarray(table.keys, dtype=np.int64)
-        words = [keys[:, 0].copy(), keys[:, 1].copy()] if keys.ndim == 2 else [keys.copy()]
-        split = L.key_split if keys.ndim == 2 else len(global_dicts)
-        self.values = []
-        for gi, g in enumerate(global_dicts):
-            card = len(g)
-            k = words[0 if gi < split else 1]
-            gid = k % card
-            k //= card
-            arr = np.asarray(g, dtype=object) if isinstance(g, list) else np.asarray(g)
-            self.values.append(arr[gid])
-        cnt = table.cells[:, 0] if len(table.keys) else np.zeros(0, dtype=np.int64)
-        self.count = cnt
-        self.finals, self.sums = [], []
-        for ai, a in enumerate(query.aggregations):
-            sec = L.agg_section[ai]
-            op = L.section_op[sec]
-            vt = L.agg_value_type[ai]
-            cell = table.cells[:, sec] if sec > 0 else None
-            fn = a.function
-            s = None
-            if fn == "COUNT":
-                f = cnt.astype(np.int64)
-            elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] == 3:
-                # split integer sum: join the parts exactly (Python ints), round once to double
-                s = np.array([float(join_parts(r, sec, 3)) for r in table.cells], dtype=np.float64)
-                f = s if fn == "SUM" else s / cnt
-            elif fn in ("SUM", "AVG"):
-                s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)
-                f = s if fn == "SUM" else s / cnt  # compacted groups have count > 0
-            else:  # MIN / MAX: order-preserving keys (pgpu_decode_minmax_key)
-                if vt in (PGPU_INT, PGPU_LONG):
-                    f = cell.astype(np.float64)
-                else:
-                    f = np.where(cell >= 0, cell, cell ^ np.int64(0x7FFFFFFFFFFFFFFF)).view(np.float64)
-            self.finals.append(f)
-            self.sums.append(s)
+        self._words = [keys[:, 0], keys[:, 1]] if keys.ndim == 2 else [keys]
+        self._split = L.key_split if keys.ndim == 2 else len(global_dicts)
+        self.count = table.cells[:, 0] if len(table.keys) else np.zeros(0, dtype=np.int64)
+        self._gid_cache: Dict[int, np.ndarray] = {}
+        self._final_cache: Dict[int, tuple] = {}
 
     def __len__(self):
         return len(self.count)
+
+    # -- group columns --
+    def _gids(self, gi: int, idx: Optional[np.ndarray]) -> np.ndarray:
+        """Global dictionary ids of group column gi (mixed-radix digit of its key word)."""
+        word = 0 if gi < self._split else 1
+        first = 0 if word == 0 else self._split
+        last = self._split if word == 0 else len(self.global_dicts)
+        k = self._words[word] if idx is None else self._words[word][idx]
+        if last - first == 1:
+            return k  # the word is this column's id
+        stride = 1
+        for j in range(first, gi):
+            stride *= len(self.global_dicts[j])
+        return (k // stride) % len(self.global_dicts[gi])
+
+    def value(self, gi: int, idx: Optional[np.ndarray] = None) -> np.ndarray:
+        g = self.global_dicts[gi]
+        arr = np.asarray(g, dtype=object) if isinstance(g, list) else np.asarray(g)
+        return arr[self._gids(gi, idx)]
+
+    @property
+    def values(self) -> List[np.ndarray]:
+        return [self.value(gi) for gi in range(len(self.global_dicts))]
+
+    # -- aggregations --
+    def final(self, ai: int, idx: Optional[np.ndarray] = None):
+        """(final values, sums or None) of aggregation ai over every row, or over rows idx."""
+        if idx is None and ai in self._final_cache:
+            return self._final_cache[ai]
+        L = self.table.layout
+        a = self.query.aggregations[ai]
+        sec = L.agg_section[ai]
+        op = L.section_op[sec]
+        vt = L.agg_value_type[ai]
+        cells = self.table.cells if idx is None else self.table.cells[idx]
+        cnt = cells[:, 0]
+        cell = cells[:, sec] if sec > 0 else None
+        fn = a.function
+        s = None
+        if fn == "COUNT":
+            f = cnt.astype(np.int64)
+        elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] == 3:
+            # split integer sum: join the parts exactly (Python ints), round once to double
+            s = np.array([float(join_parts(r, sec, 3)) for r in cells], dtype=np.float64)
+            f = s if fn == "SUM" else s / cnt
+        elif fn in ("SUM", "AVG"):
+            s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)
+            f = s if fn == "SUM" else s / cnt  # compacted groups have count > 0
+        else:  # MIN / MAX: order-preserving keys (pgpu_decode_minmax_key)
+            if vt in (PGPU_INT, PGPU_LONG):
+                f = cell.astype(np.float64)
+            else:
+                f = np.where(cell >= 0, cell, cell ^ np.int64(0x7FFFFFFFFFFFFFFF)).view(np.float64)
+        if idx is None:
+            self._final_cache[ai] = (f, s)
+        return f, s
+
+    @property
+    def finals(self) -> List[np.ndarray]:
+        return [self.final(ai)[0] for ai in range(len(self.query.aggregations))]
+
+    def _column(self, name: str, idx: Optional[np.ndarray] = None) -> np.ndarray:
+        ng = len(self.query.group_by)
+        names = list(self.query.group_by) + [a.result_name for a in self.query.aggregations]
+        i = names.index(name)
+        return self.value(i, idx) if i < ng else self.final(i - ng, idx)[0]
 
     def order_and_limit(self, limit: Optional[int] = None) -> np.ndarray:
         """Row indexes after ORDER BY / LIMIT: stable sort by each ORDER BY expression (GroupByDataTableReducer,
@@ -901,28 +949,30 @@ class GroupColumns:
         lim = q.limit if limit is None else limit
         if not q.order_by:
             return np.arange(min(n, lim))
-        names = list(q.group_by) + [a.result_name for a in q.aggregations]
-        columns = self.values + self.finals
-        keys = []
-        for ob in q.order_by:
-            c = columns[names.index(ob.expression)]
+
+        def key_of(ob, idx=None):
+            c = self._column(ob.expression, idx)
             if c.dtype.kind in "iuf":
                 kk = c.astype(np.float64) if c.dtype.kind == "f" else c.astype(np.int64)
             else:
                 kk = np.unique(c, return_inverse=True)[1].astype(np.int64)
-            keys.append(kk if ob.ascending else -kk)
+            return kk if ob.ascending else -kk
+
+        first = key_of(q.order_by[0])
         if n > 4 * lim > 0:
             # only rows whose primary key is at least as good as the limit-th one can be in the result
-            kth = np.partition(keys[0], lim - 1)[lim - 1]
-            cand = np.flatnonzero(keys[0] <= kth)
-            return cand[np.lexsort([k[cand] for k in keys[::-1]])][: lim]
+            kth = np.partition(first, lim - 1)[lim - 1]
+            cand = np.flatnonzero(first <= kth)
+            keys = [first[cand]] + [key_of(ob, cand) for ob in q.order_by[1:]]
+            return cand[np.lexsort(keys[::-1])][: lim]
+        keys = [first] + [key_of(ob) for ob in q.order_by[1:]]
         return np.lexsort(keys[::-1])[: lim]
 
     def rows(self, idx: Optional[np.ndarray] = None) -> List[tuple]:
-        sel = (lambda a: a) if idx is None else (lambda a: a[idx])
-        parts = [sel(v).tolist() for v in self.values]
-        for a, f in zip(self.query.aggregations, self.finals):
-            parts.append([int(x) for x in sel(f).tolist()] if a.function == "COUNT" else sel(f).tolist())
+        parts = [self.value(gi, idx).tolist() for gi in range(len(self.global_dicts))]
+        for ai, a in enumerate(self.query.aggregations):
+            f = self.final(ai, idx)[0]
+            parts.append([int(x) for x in f.tolist()] if a.function == "COUNT" else f.tolist())
         return [tuple(r) for r in zip(*parts)] if parts else []
 
     def intermediate(self) -> dict:
@@ -930,7 +980,8 @@ class GroupColumns:
         gv = [v.tolist() for v in self.values]
         cnt = self.count.tolist()
         cols = []
-        for a, f, s in zip(self.query.aggregations, self.finals, self.sums):
+        for ai, a in enumerate(self.query.aggregations):
+            f, s = self.final(ai)
             if a.function == "AVG":
                 cols.append([(x, c) for x, c in zip(s.tolist(), cnt)])
             elif a.function == "COUNT":

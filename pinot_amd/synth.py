@@ -131,7 +131,7 @@ WORKLOADS: Dict[str, Workload] = {
         [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
-        {"num_groups_limit": 2_000_000}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
     "bitmap5": Workload(
         "bitmap5", "bitmap5",
         [SynthColumn("a", 4, lambda: np.arange(4, dtype=np.int32) * 10, index="inv"),
@@ -150,7 +150,7 @@ WORKLOADS: Dict[str, Workload] = {
         [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3, dist="zipf", zipf_s=1.1),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
-        {"num_groups_limit": 2_000_000}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
     # PMC calibration (not a bench line): config 5's filter stream alone, a known byte count for FETCH_SIZE
     "adanalytics_count": Workload(
         "adanalytics_count", "adAnalytics",
