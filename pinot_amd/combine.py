@@ -191,6 +191,13 @@ STAT_FIELDS = ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries
                "num_total_docs", "num_segments_processed", "sparse_sector_bytes", "dense_bytes")
 
 
+def _uids_of(key) -> tuple:
+    """The segment uids inside a cache key: the key itself (_docs) or its last element (_globals, _split)."""
+    if not key:
+        return ()
+    return key if isinstance(key[0], int) else key[-1]
+
+
 class DistributedExecutor:
     """Executes a query over this rank's GPU segments and merges every rank's partial table (rank 0 finishes).
 
@@ -217,6 +224,16 @@ class DistributedExecutor:
         self._split: Dict[tuple, tuple] = {}
         self._tables: Dict[int, list] = {}
         self.last_stats = None
+        ctx = getattr(plan_maker, "ctx", None)
+        if hasattr(ctx, "add_listener"):
+            ctx.add_listener(self)
+
+    def segment_released(self, uid: int) -> None:
+        """Forget the agreements naming a released segment (every rank then agrees on a miss: the hit / miss
+        decisions stay collective, _agree)."""
+        for cache in (self._globals, self._docs, self._split):
+            for k in [k for k in cache if uid in _uids_of(k)]:
+                del cache[k]
 
     # ---- collective helpers ------------------------------------------------------------------------------------
     def _allreduce_i64(self, vals: Sequence[int], op: str = "sum") -> List[int]:

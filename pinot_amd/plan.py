@@ -478,6 +478,17 @@ class GpuPlanMaker:
         self.max_init_group_holder_capacity = max_init_group_holder_capacity
         self.collect_stats = collect_stats
         self._global_dicts: Dict[tuple, tuple] = {}
+        if hasattr(ctx, "add_listener"):
+            ctx.add_listener(self)  # segment_released: forget global dictionaries naming a released segment
+
+    def segment_released(self, uid: int) -> None:
+        for k in [k for k in self._global_dicts if uid in k[1]]:
+            self._evict_global(k)
+
+    def _evict_global(self, key: tuple) -> None:
+        entry = self._global_dicts.pop(key)
+        for rk in entry[3]:
+            self.ctx.unref_remap(rk)
 
     # -- global group dictionaries --
     def global_dictionary(self, column: str, segments: Sequence[GpuSegment]):
@@ -498,6 +509,7 @@ class GpuPlanMaker:
     def set_global_dictionary(self, column: str, segments: Sequence[GpuSegment], glob):
         key = (column, tuple(s.uid for s in segments))
         remaps = []
+        rkeys = []
         digest = dictionary_digest(glob)
         if isinstance(glob, list):
             pos = {v: i for i, v in enumerate(glob)}
@@ -511,8 +523,11 @@ class GpuPlanMaker:
             else:
                 t = np.searchsorted(glob, d).astype(np.int32)
             remaps.append(self.ctx.remap((s.uid, column, digest), t))
+            rkeys.append((s.uid, column, digest))
+        if key in self._global_dicts:
+            self._evict_global(key)  # replaced (a wider dictionary installed): its remap references go
         # the entry holds the segments themselves, so their uids stay theirs while it is cached
-        self._global_dicts[key] = (glob, remaps, tuple(segments))
+        self._global_dicts[key] = (glob, remaps, tuple(segments), rkeys)
         return glob, remaps
 
     def filter_expr(self, query: QueryContext, segments: Sequence[GpuSegment]):

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes as C
 import itertools
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Union
 
@@ -120,12 +121,50 @@ class GpuContext:
         self.handle = _handle
         self.device = device
         self._remap_cache: Dict[tuple, "DeviceBuffer"] = {}
+        self._remap_refs: Dict[tuple, int] = {}  # holders of each cached remap table (remap / unref_remap)
+        self._remap_bytes = 0
+        # caches of per-segment derived state (plan makers' global dictionaries, executors' agreements) that must
+        # forget a segment when it is released: objects with a segment_released(uid) method, held weakly
+        self._listeners: "weakref.WeakSet" = weakref.WeakSet()
+
+    def add_listener(self, obj) -> None:
+        self._listeners.add(obj)
+
+    def segment_released(self, uid: int) -> None:
+        """A segment left HBM: drop its remap tables and every cache entry naming it (bounded host / HBM state
+        in a server whose pruning yields a different segment set per query)."""
+        for k in [k for k in self._remap_cache if k[0] == uid]:
+            self._drop_remap(k)
+        for obj in list(self._listeners):
+            obj.segment_released(uid)
+
+    def _drop_remap(self, key: tuple) -> None:
+        buf = self._remap_cache.pop(key)
+        self._remap_refs.pop(key, None)
+        self._remap_bytes -= buf.nbytes
+        buf.release()
+
+    def unref_remap(self, key: tuple) -> None:
+        """One holder of a remap table (a cached global dictionary) let it go: freed when none is left."""
+        n = self._remap_refs.get(key)
+        if n is None:
+            return  # already dropped with its segment
+        if n <= 1:
+            self._drop_remap(key)
+        else:
+            self._remap_refs[key] = n - 1
+
+    def remap_bytes(self) -> int:
+        """HBM held by cached group-key remap tables."""
+        return self._remap_bytes
 
     def close(self) -> None:
         if self.handle:
             for b in self._remap_cache.values():
                 b.release()
             self._remap_cache.clear()
+            self._remap_refs.clear()
+            self._remap_bytes = 0
             if self.owned:
                 self._lib.pgpu_shutdown(self.handle)
             self.handle = None
@@ -142,17 +181,25 @@ class GpuContext:
         return g.value, t.value, b.value
 
     def remap(self, key: tuple, table: np.ndarray) -> "DeviceBuffer":
+        """The remap table cached under `key` (uploaded on first use); the caller holds a reference until
+        unref_remap(key) or the release of the segment key[0]."""
         buf = self._remap_cache.get(key)
         if buf is None:
-            buf = DeviceBuffer.upload_int32(self, table)
+            buf = self._upload_remap(table)
             self._remap_cache[key] = buf
+            self._remap_bytes += buf.nbytes
+        self._remap_refs[key] = self._remap_refs.get(key, 0) + 1
         return buf
+
+    def _upload_remap(self, table: np.ndarray) -> "DeviceBuffer":
+        return DeviceBuffer.upload_int32(self, table)
 
 
 class DeviceBuffer:
-    def __init__(self, ctx: GpuContext, handle: C.c_void_p):
+    def __init__(self, ctx: GpuContext, handle: C.c_void_p, nbytes: int = 0):
         self.ctx = ctx
         self.handle = handle
+        self.nbytes = nbytes
 
     @staticmethod
     def upload_int32(ctx: GpuContext, arr: np.ndarray) -> "DeviceBuffer":
@@ -160,7 +207,7 @@ class DeviceBuffer:
         h = C.c_void_p()
         _lib.check(ctx._lib.pgpu_remap_upload(ctx.handle, a.ctypes.data_as(C.POINTER(C.c_int32)), len(a),
                                               C.byref(h)))
-        return DeviceBuffer(ctx, h)
+        return DeviceBuffer(ctx, h, 4 * len(a))
 
     def release(self) -> None:
         if self.handle:
@@ -336,5 +383,6 @@ class GpuSegment:
 
     def release(self) -> None:
         if self.handle:
+            self.ctx.segment_released(self.uid)
             self.ctx._lib.pgpu_segment_release(self.handle)
             self.handle = None
