@@ -339,64 +339,45 @@ def parity_check(ctx, w, q, opts):
 def cpu_baseline(ctx, w, q, opts, args, seconds):
     """The CPU leg: (1) Pinot's per-segment operators restated in C (oracle/pinot_cpu.c) timed on this host,
     the sample's segments queried repeatedly until ~`seconds` of wall time, at Pinot's default task count and
-    with every available core; workloads the C port's generator does not cover (skewed keys) time the numpy
-    restatement (oracle/engine.py) instead; (2) the GPU-vs-oracle parity check (parity_check)."""
+    with every available core; (2) the GPU-vs-oracle parity check (parity_check)."""
     check = None if args.no_check else parity_check(ctx, w, q, opts)
-    if any(c.dist != "uniform" for c in w.columns):
-        return engine_baseline(w, q, opts, args, seconds), check
     return c_baseline(w, q, args, seconds), check
 
 
-def engine_baseline(w, q, opts, args, seconds):
-    from oracle import engine
-    from oracle.segment_writer import pack_fixed_bit
-    from pinot_amd.synth import build_segment_cpu
-
-    nseg, n = 2, 1 << 21
-    segs = [build_segment_cpu(w, s, n, pack_fixed_bit) for s in range(nseg)]
-    total, runs = 0.0, 0
-    while runs == 0 or total < seconds:
-        t = time.perf_counter()
-        engine.execute(q, segs, num_groups_limit=opts.get("num_groups_limit", 100_000))
-        total += time.perf_counter() - t
-        runs += 1
-    return {"value": runs * nseg * n / total, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{runs} run(s) over {nseg} segment(s) x {n} docs of the same workload, oracle/engine.py "
-                      f"(numpy restatement of the filter operator tree; the C port's generator covers uniform "
-                      f"columns only), 1 thread",
-            "seconds": total}
-
-
 def c_baseline(w, q, args, seconds):
+    """the C port at Pinot's default parallelism (one task per segment, min(#segments,
+    min(10, nproc/2)) threads, CombineOperatorUtils.getNumTasksForQuery) over `cpu_sample_segments` segments, then
+    with every core this process may use over as many segments as cores (one task per segment, so the sample
+    must hold at least that many for every core to work)."""
     from oracle.cpu import CpuBaseline, synth_segment
 
-    nseg = args.cpu_sample_segments
-    segs = [synth_segment(w, s, args.docs) for s in range(nseg)]
     nproc = os.cpu_count() or 1
+    cores = available_cores()
+    nseg = args.cpu_sample_segments
+    segs = [synth_segment(w, s, args.docs) for s in range(max(nseg, cores))]
     threads = args.cpu_threads or max(1, min(nseg, min(10, nproc // 2)))
-    cb = CpuBaseline(q, segs)
+    cb = CpuBaseline(q, segs[:nseg])
     filt = ("doc-id set algebra of AndDocIdSet / OrDocIdSet over Roaring / sorted / scan leaves" if cb.q.num_nodes
             else "AndDocIdIterator over SVScanDocIdIterators")
 
-    def timed(th, budget):
+    def timed(c, th, n, budget):
         total, runs = 0.0, 0
         while runs == 0 or total < budget:
-            dt, matched, _, _, _ = cb.run(th)
+            dt, matched, _, _, _ = c.run(th)
             total += dt
             runs += 1
-        return runs * nseg * args.docs / total, runs, total
+        return runs * n * args.docs / total, runs, total
 
-    value, runs, total = timed(threads, seconds)
-    # BASELINE.md section 2: the same operators with every core this process may use (one task per segment, so
-    # at most #segments of them run at once)
-    cores = available_cores()
-    all_value, all_runs, all_total = timed(cores, max(1.0, seconds / 2))
+    value, runs, total = timed(cb, threads, nseg, seconds)
+    all_cb = cb if len(segs) == nseg else CpuBaseline(q, segs)
+    all_value, all_runs, all_total = timed(all_cb, cores, len(segs), max(1.0, seconds / 2))
+    skew = "" if all(c.dist == "uniform" for c in w.columns) else ", Zipf keys from the same CDF as the GPU's"
     return {"value": value, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload, "
+            "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload{skew}, "
                       f"oracle/pinot_cpu.c ({filt}, 10k-doc blocks, double SUM), "
                       f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
             "seconds": total,
-            "all_cores": {"value": all_value, "cores": min(cores, nseg), "available_cores": cores,
+            "all_cores": {"value": all_value, "cores": cores, "available_cores": cores, "segments": len(segs),
                           "runs": all_runs, "seconds": all_total}}
 
 

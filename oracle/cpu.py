@@ -256,11 +256,11 @@ def synth_segment(w, segment: int, num_docs: int) -> SegmentData:
     host builder, sorted columns from their closed form): same bytes, ~100x faster."""
     from pinot_amd._lib import PGPU_INT
     from pinot_amd.segment import ColumnIndexes
-    from pinot_amd.synth import SynthLib, column_seed, sorted_index_bytes
+    from pinot_amd.synth import SynthLib, column_seed, sorted_index_bytes, zipf_cdf
 
     lib = C.CDLL(LIB)
     lib.pc_synth_fixed_bit.restype = None
-    lib.pc_synth_fixed_bit.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_uint32, C.c_uint64]
+    lib.pc_synth_fixed_bit.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_uint32, C.c_uint64, C.c_void_p]
     seg = SegmentData(f"{w.name}_{segment}", num_docs)
     sl = None
     for c in w.columns:
@@ -269,12 +269,16 @@ def synth_segment(w, segment: int, num_docs: int) -> SegmentData:
             seg.columns[c.name] = ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=d,
                                                 sorted_index=sorted_index_bytes(num_docs, c.cardinality))
             continue
-        if c.dist != "uniform":
-            raise ValueError("C generator covers uniform columns")
+        cdf = None
+        if c.dist == "zipf":
+            cdf = np.ascontiguousarray(zipf_cdf(c.cardinality, c.zipf_s), dtype=np.uint32)
+        elif c.dist != "uniform":
+            raise ValueError(f"C generator covers uniform and zipf columns, not {c.dist}")
         bits = 1 if c.cardinality - 1 <= 1 else int(c.cardinality - 1).bit_length()
         n = (num_docs * bits + 7) // 8
         buf = C.create_string_buffer(n + 8)
-        lib.pc_synth_fixed_bit(buf, num_docs, bits, c.cardinality, column_seed(w.seed, segment, c.name))
+        lib.pc_synth_fixed_bit(buf, num_docs, bits, c.cardinality, column_seed(w.seed, segment, c.name),
+                               None if cdf is None else cdf.ctypes.data)
         fwd = buf.raw[:n]
         inv = None
         if c.index == "inv":

@@ -597,14 +597,26 @@ static inline uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-/* FixedBitSVForwardIndexWriter layout of ids(doc) = ((splitmix64(seed ^ doc*K) >> 32) * card) >> 32. */
-void pc_synth_fixed_bit(uint8_t* out, int64_t num_docs, int32_t bits, uint32_t card, uint64_t seed) {
+/* FixedBitSVForwardIndexWriter layout of ids(doc) = ((splitmix64(seed ^ doc*K) >> 32) * card) >> 32, or with a
+ * CDF table (Zipf keys, pinot_amd.synth.zipf_cdf) the first k with cdf[k] > u(doc), as synth.hip's synth_id. */
+void pc_synth_fixed_bit(uint8_t* out, int64_t num_docs, int32_t bits, uint32_t card, uint64_t seed,
+                        const uint32_t* cdf) {
   uint64_t acc = 0;  /* pending bits, MSB-aligned count `have` */
   int have = 0;
   int64_t pos = 0;
   for (int64_t d = 0; d < num_docs; ++d) {
     const uint32_t u = (uint32_t)(splitmix64(seed ^ ((uint64_t)d * 0xD1B54A32D192ED03ull)) >> 32);
-    const uint64_t v = ((uint64_t)u * card) >> 32;
+    uint64_t v;
+    if (!cdf) {
+      v = ((uint64_t)u * card) >> 32;
+    } else {
+      uint32_t lo = 0, hi = card - 1;
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+      }
+      v = lo;
+    }
     acc = (acc << bits) | v;
     have += bits;
     while (have >= 8) {
