@@ -5,7 +5,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd $R
 O=gpurun_out/r3check; mkdir -p $O
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $O/tests.log 2>&1 \
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -x --timeout 120 --timeout-method thread > $O/tests.log 2>&1 \
   || { echo "tests failed rc=$?"; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 fi

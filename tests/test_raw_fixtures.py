@@ -128,7 +128,7 @@ def test_gpu_queries_reference_file(gpu_ctx, name, n, start, version, codec):
         for sql, _ in _queries(n, start):
             res = GpuPlanMaker(gpu_ctx).execute(parse_sql(sql), [g])
             _check_analytic(sql, res.aggregation_result, res.group_rows, res.stats.num_docs_scanned, vals, n, start)
-            ref = engine.execute(parse_sql(sql), [seg])
+            ref = engine.execute(parse_sql(sql), [seg], iterator_stats=True)
             assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter, sql
     finally:
         g.release()
