@@ -781,7 +781,8 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
                            for a in query.aggregations]
         return res
     if any(ds.seg.column(g).mv_forward is not None for g in query.group_by):
-        raise NotImplementedError("GROUP BY a multi-value column")
+        res.groups = _group_multi_value(query, ds, docs, num_groups_limit, max_init_group_holder_capacity)
+        return res
     # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long)
     cards = [ds.seg.column(g).cardinality for g in query.group_by]
     prod = 1
@@ -814,6 +815,62 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
                                for a in query.aggregations]
     res.groups = groups
     return res
+
+
+def _group_multi_value(query: QueryContext, ds: DecodedSegment, docs: np.ndarray, num_groups_limit: int,
+                       max_init_group_holder_capacity: int) -> Dict[tuple, list]:
+    """GROUP BY with multi-value group columns: every matched doc contributes to one group per element of the
+    cartesian product of its group columns' values (duplicates within a row kept), in the order
+    DictionaryBasedGroupKeyGenerator.getIntRawKeys builds them (columns from last to first, a multi-value column's
+    values outermost: DictionaryBasedGroupKeyGenerator.java:472-544); the holders' processMultiValue
+    (:325-336, :417-431, :616-630) assign group ids first-seen in that order, and each aggregation's
+    aggregateGroupByMV adds the doc's value(s) once per key (e.g. SumAggregationFunction.java:105-114)."""
+    cols = list(query.group_by)
+    src = []
+    for g in cols:
+        if ds.seg.column(g).mv_forward is not None:
+            off, ids = ds.mv(g)
+            src.append((off, ids))
+        else:
+            src.append(ds.ids(g))
+    exp_docs: List[int] = []
+    exp_keys: List[tuple] = []
+    for d in docs.tolist():
+        keys: List[tuple] = [()]
+        for j in range(len(cols) - 1, -1, -1):
+            s = src[j]
+            if isinstance(s, tuple):
+                vals = s[1][s[0][d]:s[0][d + 1]].tolist()
+                keys = [(v,) + k for v in vals for k in keys]
+            else:
+                v = int(s[d])
+                keys = [(v,) + k for k in keys]
+        for k in keys:
+            exp_docs.append(d)
+            exp_keys.append(k)
+    prod = 1
+    for g in cols:
+        prod *= ds.seg.column(g).cardinality
+    order: Dict[tuple, List[int]] = {}
+    for d, k in zip(exp_docs, exp_keys):
+        lst = order.get(k)
+        if lst is None:
+            if prod > max_init_group_holder_capacity and len(order) >= num_groups_limit:
+                continue  # map-based holder full: new keys get no group id (INVALID_ID)
+            lst = order[k] = []
+        lst.append(d)
+    dicts = [ds.dictionary(g) for g in cols]
+    groups: Dict[tuple, list] = {}
+    for k, dl in order.items():
+        vals = []
+        for j, dct in enumerate(dicts):
+            v = dct[k[j]]
+            vals.append(v.item() if hasattr(v, "item") else v)
+        part = np.asarray(dl, dtype=np.int64)
+        groups[tuple(vals)] = [aggregate(a.function, None if a.column is None else
+                                         _as_float_values(ds, a.column, part, a.function), len(part))
+                               for a in query.aggregations]
+    return groups
 
 
 @dataclass

@@ -352,6 +352,8 @@ struct DevParams {
   int32_t segmask_rows;
   int32_t cancel_poll;            // self-loading waves: tiles between cancel polls (PGPU_CANCEL_POLL, env override)
   int32_t rd_planes;              // register-direct: planes per tile held in VGPRs (>= every leaf's width; 8/10/12/16)
+  int32_t mv_gmask;               // bit g: group column g is multi-value (sparse_agg_mv expands each doc's values)
+  int32_t pad_mv_;
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

@@ -1313,11 +1313,73 @@ FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], co
       if ((spill >> r) & 1u) part_spill(p, key[r], raw[r]);
 }
 
+// GROUP BY with multi-value group columns (p.mv_gmask): every survivor adds to one cell per element of the
+// cartesian product of its group columns' values, duplicates included (DictionaryBasedGroupKeyGenerator
+// processMultiValue / getIntRawKeys, DictionaryBasedGroupKeyGenerator.java:325-336, 472-544; every aggregation's
+// aggregateGroupByMV adds the doc's value once per key, e.g. SumAggregationFunction.java:105-114).  A multi-value
+// column's DevColumn holds the values' packed ids in `fwd` and the rows' offsets into them in `sorted`.  Dense key
+// spaces (LDS / GLOBAL tables), one lane per doc, table atomics per expanded key.
+template <int MODE>
+FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, const int32_t (&doc)[U], uint32_t m) {
+  int64_t* tab = table_base<MODE>(p, L);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!((m >> u) & 1u)) continue;
+    const int32_t d = doc[u];
+    uint32_t base = 0, total = 1;
+    for (int g = 0; g < p.ngcols; ++g) {
+      const DevColumn c = col_of(ss, p.gcols[g]);
+      if ((p.mv_gmask >> g) & 1) {
+        total *= (uint32_t)(gld(c.sorted, d + 1) - gld(c.sorted, d));
+        continue;
+      }
+      const int32_t dd[1] = {d};
+      uint32_t id[1];
+      gather_ids(colref(c), dd, id);
+      remap_ids(cld(ss.remaps, g), id);
+      base += id[0] * p.gstride[g];
+    }
+    for (uint32_t j = 0; j < total; ++j) {
+      uint32_t key = base, r = j;
+      for (int g = 0; g < p.ngcols; ++g) {
+        if (!((p.mv_gmask >> g) & 1)) continue;
+        const DevColumn c = col_of(ss, p.gcols[g]);
+        const int32_t s0 = gld(c.sorted, d), n = gld(c.sorted, d + 1) - s0;
+        const int32_t vi[1] = {s0 + (int32_t)(r % (uint32_t)n)};
+        r /= (uint32_t)n;
+        uint32_t id[1];
+        gather_ids(ColRef{c.fwd, nullptr, PGPU_COL_FIXED_BIT, c.bits, c.card}, vi, id);
+        remap_ids(cld(ss.remaps, g), id);
+        key += id[0] * p.gstride[g];
+      }
+      atomicAdd((unsigned long long*)&tab[key], 1ull);
+      for (int a = 0; a < p.nagg; ++a) {
+        const DevAgg ag = p.aggs[a];
+        if (ag.fn == PGPU_AGG_COUNT) continue;
+        const DevColumn c = col_of(ss, ag.col);
+        const int32_t dd[1] = {d};
+        uint32_t id[1];
+        gather_ids(colref(c), dd, id);
+        int64_t v[1];
+        gather_cells(c.dict, ag.vtype, ag.op, id, v);
+        apply_part(v, ag.part);
+        cell_atomic(tab + (size_t)ag.sec * p.G + key, ag.op, v[0]);
+      }
+    }
+  }
+}
+
 // Sparse (per-doc) aggregation of the survivors `m` among this lane's U docs: group key = mixed radix of the
 // remapped group ids, COUNT into section 0, every other aggregation gathers its id and dictionary value.
 template <int MODE>
 FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                    const int32_t (&doc)[U], uint32_t m) {
+  if constexpr (MODE == PGPU_MODE_LDS || MODE == PGPU_MODE_GLOBAL) {
+    if (p.mv_gmask) {
+      sparse_agg_mv<MODE>(p, L, ss, doc, m);
+      return;
+    }
+  }
   uint32_t key[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) key[u] = 0;

@@ -981,7 +981,8 @@ int pgpu_segment_seal(pgpu_segment* seg) {
     DevColumn d{};
     d.sliced = (const uint32_t*)c.sliced.p;
     d.fwd = (const uint32_t*)c.fwd.p;
-    d.sorted = (const int32_t*)c.sorted.p;
+    // a multi-value column's row offsets take the sorted-index slot (sparse_agg_mv; a MV column has no sorted index)
+    d.sorted = (const int32_t*)(c.kind == PGPU_COL_MV ? c.mv_off.p : c.sorted.p);
     d.dict = c.dict.p;
     d.inv_dir = (const uint32_t*)c.inv_dir.p;
     d.inv_ct = (const DevContainer*)c.inv_ct.p;
@@ -1724,7 +1725,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   int agg_mode;
   if (aggcols.empty()) {
     agg_mode = PGPU_AM_COUNT;
-  } else if (residual) {
+  } else if (residual || p.mv_gmask) {  // multi-value group keys: expanded per candidate doc (sparse_agg_mv)
     agg_mode = PGPU_AM_SPARSE;
   } else {
     // the hash group-by computes 64-bit keys and slots per doc in the candidate path only
@@ -1948,6 +1949,21 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       d.part = parts == 3 ? k + 1 : 0;
     }
   }
+  // multi-value group columns (every segment's column of one schema: multi-value everywhere or nowhere)
+  p.mv_gmask = 0;
+  for (int g = 0; g < q->num_group_columns; ++g) {
+    int nmv = 0;
+    for (int s = 0; s < q->num_segments; ++s) {
+      const pgpu_segment_plan& sp = q->segments[s];
+      const int32_t slot = sp.column_map[q->group_columns[g]];
+      if (slot >= 0 && slot < (int32_t)sp.segment->dev.size() && sp.segment->dev[slot].kind == PGPU_COL_MV) ++nmv;
+    }
+    if (nmv && nmv != q->num_segments)
+      return fail(PGPU_E_INVALID, "group column %d is multi-value in %d of %d segments", g, nmv, q->num_segments);
+    if (nmv) p.mv_gmask |= 1 << g;
+  }
+  if (p.mv_gmask && p.mode == PGPU_MODE_HASH)
+    return fail(PGPU_E_UNSUPPORTED, "GROUP BY on a multi-value column over a hashed key space (map-based holder)");
   int64_t tiles = 0;
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
@@ -1973,8 +1989,6 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       if (c.kind == PGPU_COL_NONE) return fail(PGPU_E_INVALID, "segment %d: group column without forward index", s);
       if (c.kind == PGPU_COL_RAW)  // NoDictionary*GroupKeyGenerator: a value-hash path the GPU does not run
         return fail(PGPU_E_UNSUPPORTED, "segment %d: GROUP BY on a raw (no-dictionary) column", s);
-      if (c.kind == PGPU_COL_MV)  // one group key per value of the row (DictionaryBasedGroupKeyGenerator MV path)
-        return fail(PGPU_E_UNSUPPORTED, "segment %d: GROUP BY on a multi-value column", s);
       const pgpu_buffer* rb = sp.group_remap ? sp.group_remap[g] : nullptr;
       if (rb && rb->length < c.card) return fail(PGPU_E_INVALID, "segment %d: remap shorter than cardinality", s);
       if (!rb && c.card > q->group_cardinalities[g])
@@ -2086,7 +2100,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   while ((8ull * L.num_sections << (pshift + 1)) <= PGPU_PART_LDS_BYTES) ++pshift;
   uint64_t nparts = (L.num_keys + (1ull << pshift) - 1) >> pshift;
   part_ok = part_ok && nparts <= PGPU_PART_MAX_PARTS && L.num_keys < (1ull << 31) &&
-            L.num_sections <= PGPU_PART_MAX_SECTIONS;
+            L.num_sections <= PGPU_PART_MAX_SECTIONS && !p.mv_gmask;  // one record per doc: no value expansion
   if (q->num_group_columns == 0) p.mode = PGPU_MODE_AGG;
   else if (L.key_kind == PGPU_KEYS_HASH) p.mode = PGPU_MODE_HASH;
   else if (tbytes <= PGPU_LDS_TABLE_BYTES && many && !(q->flags & PGPU_Q_PARTITION) &&

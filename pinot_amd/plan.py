@@ -272,9 +272,6 @@ def check_group_columns(query: QueryContext, segments: Sequence[GpuSegment]) -> 
             if s.column(g).is_raw:
                 raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
                                            f"GROUP BY on raw (no-dictionary) column {g!r} of segment {s.name}")
-            if s.column(g).is_mv:  # one group key per value of the row: not on the GPU path
-                raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
-                                           f"GROUP BY on multi-value column {g!r} of segment {s.name}")
     for a in query.aggregations:
         if a.column is None or not segments:
             continue

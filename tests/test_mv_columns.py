@@ -120,10 +120,93 @@ def test_oracle_mv_aggregations_brute_force():
     assert r.aggregation_result[5] == len(sel)
 
 
-def test_oracle_rejects_mv_group_by_and_sv_functions():
+MV_GROUP_QUERIES = [
+    "SELECT tags, COUNT(*), SUM(s), MAX(s), MIN(s) FROM t WHERE s < 60 GROUP BY tags",
+    "SELECT g, tags, COUNT(*), SUMMV(lv), AVG(s) FROM t GROUP BY g, tags",
+    "SELECT tags, g, COUNT(*), MAXMV(fv), COUNTMV(lv) FROM t WHERE tags IN (7, 14, 21) OR s > 90 GROUP BY tags, g",
+    "SELECT tags, lv, COUNT(*), SUM(s) FROM t WHERE g = 2 GROUP BY tags, lv",
+    "SELECT tags, COUNT(*), SUMMV(tags) FROM t WHERE tags <> 0 GROUP BY tags ORDER BY COUNT(*) DESC LIMIT 5",
+]
+
+
+def _brute_mv_groups(seg, sql):
+    """Plain loops over the rows: each matched doc adds to every element of the cartesian product of its group
+    columns' values (duplicates kept) -- DictionaryBasedGroupKeyGenerator's multi-value keys."""
+    q = parse_sql(sql)
+    ds = engine.DecodedSegment(seg)
+    # the filter's doc set from the oracle's (separately pinned) filter path; the expansion below is brute force
+    where = " WHERE " + sql.split(" WHERE ")[1].split(" GROUP BY")[0] if " WHERE " in sql else ""
+    mask = np.zeros(seg.num_docs, bool)
+    mask[engine.execute_segment(parse_sql("SELECT COUNT(*) FROM t" + where), seg).matched] = True
+    def vals(col, d):
+        c = seg.column(col)
+        if c.is_mv:
+            off, ids = ds.mv(col)
+            return list(ds.dictionary(col)[ids[off[d]:off[d + 1]]])
+        return [ds.dictionary(col)[ds.ids(col)[d]]]
+    groups = {}
+    for d in np.flatnonzero(mask):
+        keys = [()]
+        for col in q.group_by:
+            keys = [k + (v.item(),) for k in keys for v in vals(col, d)]
+        for k in keys:
+            acc = groups.setdefault(k, [])
+            acc.append(d)
+    out = {}
+    for k, docs in groups.items():
+        row = []
+        for a in q.aggregations:
+            if a.function == "COUNT":
+                row.append(len(docs))
+                continue
+            vs = [x for d in docs for x in vals(a.column, d)]
+            f = a.function.replace("MV", "") if a.function.endswith("MV") else a.function
+            if a.function == "COUNTMV":
+                row.append(len(vs))
+            elif f == "SUM":
+                row.append(float(np.sum(np.asarray(vs, dtype=np.float64))))
+            elif f == "MIN":
+                row.append(float(min(vs)))
+            elif f == "MAX":
+                row.append(float(max(vs)))
+            else:
+                row.append(float(np.sum(np.asarray(vs, dtype=np.float64))) / len(vs))
+        out[k] = row
+    return out
+
+
+@pytest.mark.parametrize("sql", MV_GROUP_QUERIES[:4])
+def test_oracle_mv_group_by_brute_force(sql):
+    seg = _segment(2, n=700)
+    want = _brute_mv_groups(seg, sql)
+    got = {r[:len(parse_sql(sql).group_by)]: r[len(parse_sql(sql).group_by):]
+           for r in engine.execute(parse_sql(sql), [seg]).group_rows}
+    assert got.keys() == want.keys()
+    for k in got:
+        assert all(_close(a, b) for a, b in zip(got[k], want[k])), (k, got[k], want[k])
+
+
+def test_oracle_mv_group_by_limit_keeps_first_seen():
+    """Map-based holder with numGroupsLimit: only the first keys in (doc, value) order get group ids."""
+    seg = _segment(4, n=300)
+    q = parse_sql("SELECT tags, g, COUNT(*) FROM t GROUP BY tags, g")
+    full = engine.execute(q, [seg], num_groups_limit=10**9, max_init_group_holder_capacity=10).group_rows
+    lim = engine.execute(q, [seg], num_groups_limit=17, max_init_group_holder_capacity=10).group_rows
+    ds = engine.DecodedSegment(seg)
+    off, ids = ds.mv("tags")
+    first = []
+    for d in range(seg.num_docs):
+        for v in ids[off[d]:off[d + 1]]:
+            k = (int(ds.dictionary("tags")[v]), int(ds.dictionary("g")[ds.ids("g")[d]]))
+            if k not in first:
+                first.append(k)
+    assert sorted(r[:2] for r in lim) == sorted(first[:17])
+    fd = {r[:2]: r[2] for r in full}
+    assert all(fd[r[:2]] == r[2] for r in lim)
+
+
+def test_oracle_rejects_sv_functions_on_mv_and_back():
     seg = _segment(2, n=500)
-    with pytest.raises(NotImplementedError):
-        engine.execute(parse_sql("SELECT tags, COUNT(*) FROM t GROUP BY tags"), [seg])
     with pytest.raises(ValueError):
         engine.execute(parse_sql("SELECT SUM(tags) FROM t"), [seg])
     with pytest.raises(ValueError):
@@ -226,8 +309,7 @@ def test_gpu_mv_unsupported_shapes(gpu_ctx):
     g = GpuSegment(gpu_ctx, _segment(21, n=1000))
     try:
         pm = GpuPlanMaker(gpu_ctx)
-        for sql in ("SELECT tags, COUNT(*) FROM t GROUP BY tags", "SELECT SUM(tags) FROM t",
-                    "SELECT COUNTMV(s) FROM t"):
+        for sql in ("SELECT SUM(tags) FROM t", "SELECT COUNTMV(s) FROM t"):
             with pytest.raises(UnsupportedPlanError):
                 pm.execute(parse_sql(sql), [g])
     finally:
@@ -250,3 +332,33 @@ def test_gpu_loaded_mv_segment(gpu_ctx, tmp_path):
         assert sorted(res.group_rows) == sorted(ref.group_rows)
     finally:
         g.release()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql", MV_GROUP_QUERIES)
+@pytest.mark.parametrize("inverted", [(), ("tags",)])
+def test_gpu_mv_group_by_matches_oracle(gpu_ctx, sql, inverted):
+    """GROUP BY on multi-value columns (one key per value, cartesian product over several): GPU vs oracle over
+    three segments whose dictionaries differ (global dictionary + remap tables), every group compared."""
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    from tests.helpers import check_groups
+    segs = [_segment(30 + k, n=[6000, 4097, 2048][k], inverted=inverted, name=f"mvg{k}") for k in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(sql)
+        res = GpuPlanMaker(gpu_ctx).execute(q, gs)
+        ref = engine.execute(q, segs)
+        check_groups(res, ref, 1e-9)
+        got = {r[:len(q.group_by)]: r for r in res.group_rows}
+        for r in ref.group_rows:
+            if r[:len(q.group_by)] in got:
+                assert _close(tuple(got[r[:len(q.group_by)]]), tuple(r)), (sql, r)
+        assert res.stats.num_docs_scanned == ref.num_docs_scanned
+        assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
+        if q.order_by:
+            assert [tuple(r) for r in res.rows] == [tuple(r) for r in ref.rows] or \
+                all(_close(tuple(a), tuple(b)) for a, b in zip(res.rows, ref.rows))
+    finally:
+        for g in gs:
+            g.release()
