@@ -15,7 +15,7 @@
 #include <memory>
 #include <vector>
 
-#include "../../include/pinot_gpu.h"
+#include "pgpu_host.h"
 
 namespace {
 
@@ -254,8 +254,10 @@ struct Node {
   std::vector<Node> kids;
 };
 
-int parse(const pgpu_filter_node* nd, int n, int i, int* leaf, Node* out) {
-  if (i >= n) return -1;
+constexpr int kMaxDepth = 256;  // nesting bound: a malformed program fails, it never exhausts the stack
+
+int parse(const pgpu_filter_node* nd, int n, int i, int* leaf, Node* out, int depth = 0) {
+  if (i < 0 || i >= n || depth > kMaxDepth) return -1;
   const int op = nd[i].op;
   out->op = op;
   switch (op) {
@@ -270,7 +272,7 @@ int parse(const pgpu_filter_node* nd, int n, int i, int* leaf, Node* out) {
       return i + 1;
     case PGPU_F_NOT: {
       out->kids.emplace_back();
-      return parse(nd, n, i + 1, leaf, &out->kids.back());
+      return parse(nd, n, i + 1, leaf, &out->kids.back(), depth + 1);
     }
     case PGPU_F_AND_BEGIN:
     case PGPU_F_OR_BEGIN: {
@@ -278,7 +280,7 @@ int parse(const pgpu_filter_node* nd, int n, int i, int* leaf, Node* out) {
       int j = i + 1;
       while (j < n && nd[j].op != (a ? PGPU_F_AND_END : PGPU_F_OR_END)) {
         out->kids.emplace_back();
-        j = parse(nd, n, j, leaf, &out->kids.back());
+        j = parse(nd, n, j, leaf, &out->kids.back(), depth + 1);
         if (j < 0 || j >= n || nd[j].op != (a ? PGPU_F_AND_CHILD_END : PGPU_F_OR_CHILD_END)) return -1;
         ++j;
       }

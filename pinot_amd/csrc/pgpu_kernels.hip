@@ -1317,16 +1317,18 @@ FI void part_emit(const DevParams& p, const Lds& L, const uint32_t (&key)[N], co
 // cartesian product of its group columns' values, duplicates included (DictionaryBasedGroupKeyGenerator
 // processMultiValue / getIntRawKeys, DictionaryBasedGroupKeyGenerator.java:325-336, 472-544; every aggregation's
 // aggregateGroupByMV adds the doc's value once per key, e.g. SumAggregationFunction.java:105-114).  A multi-value
-// column's DevColumn holds the values' packed ids in `fwd` and the rows' offsets into them in `sorted`.  Dense key
-// spaces (LDS / GLOBAL tables), one lane per doc, table atomics per expanded key.
+// column's DevColumn holds the values' packed ids in `fwd` and the rows' offsets into them in `sorted`.  Dense
+// (LDS / GLOBAL) or hashed key spaces; one lane per doc, table atomics per expanded key.
 template <int MODE>
 FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, const int32_t (&doc)[U], uint32_t m) {
+  constexpr bool HASH = MODE == PGPU_MODE_HASH;
   int64_t* tab = table_base<MODE>(p, L);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!((m >> u) & 1u)) continue;
     const int32_t d = doc[u];
-    uint32_t base = 0, total = 1;
+    uint64_t b0 = 0, b1 = 0;  // the single-value columns' part of the key (dense: b0 only; HASH: two key words)
+    uint32_t total = 1;
     for (int g = 0; g < p.ngcols; ++g) {
       const DevColumn c = col_of(ss, p.gcols[g]);
       if ((p.mv_gmask >> g) & 1) {
@@ -1337,10 +1339,12 @@ FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, cons
       uint32_t id[1];
       gather_ids(colref(c), dd, id);
       remap_ids(cld(ss.remaps, g), id);
-      base += id[0] * p.gstride[g];
+      if (HASH) (g < p.key_split ? b0 : b1) += (uint64_t)id[0] * p.gstride64[g];
+      else b0 += (uint64_t)(id[0] * p.gstride[g]);
     }
     for (uint32_t j = 0; j < total; ++j) {
-      uint32_t key = base, r = j;
+      uint64_t k0 = b0, k1 = b1;
+      uint32_t r = j;
       for (int g = 0; g < p.ngcols; ++g) {
         if (!((p.mv_gmask >> g) & 1)) continue;
         const DevColumn c = col_of(ss, p.gcols[g]);
@@ -1350,7 +1354,17 @@ FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, cons
         uint32_t id[1];
         gather_ids(ColRef{c.fwd, nullptr, PGPU_COL_FIXED_BIT, c.bits, c.card}, vi, id);
         remap_ids(cld(ss.remaps, g), id);
-        key += id[0] * p.gstride[g];
+        if (HASH) (g < p.key_split ? k0 : k1) += (uint64_t)id[0] * p.gstride64[g];
+        else k0 += (uint64_t)(id[0] * p.gstride[g]);
+      }
+      uint32_t key;
+      if (HASH) {
+        const uint64_t a0[1] = {k0}, a1[1] = {k1};
+        uint32_t slot[1];
+        hash_slots(p, a0, a1, 1u, ss.track, slot);
+        key = slot[0];
+      } else {
+        key = (uint32_t)k0;
       }
       atomicAdd((unsigned long long*)&tab[key], 1ull);
       for (int a = 0; a < p.nagg; ++a) {
@@ -1374,7 +1388,7 @@ FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, cons
 template <int MODE>
 FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                    const int32_t (&doc)[U], uint32_t m) {
-  if constexpr (MODE == PGPU_MODE_LDS || MODE == PGPU_MODE_GLOBAL) {
+  if constexpr (MODE == PGPU_MODE_LDS || MODE == PGPU_MODE_GLOBAL || MODE == PGPU_MODE_HASH) {
     if (p.mv_gmask) {
       sparse_agg_mv<MODE>(p, L, ss, doc, m);
       return;

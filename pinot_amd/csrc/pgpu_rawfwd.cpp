@@ -17,11 +17,12 @@
 // not decoded here (PGPU_E_UNSUPPORTED: the server keeps its CPU reader for such a segment).
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
 
-#include "../../include/pinot_gpu.h"
+#include "pgpu_host.h"
 
 namespace {
 
@@ -33,7 +34,8 @@ inline uint64_t rd_be64(const uint8_t* p) { return ((uint64_t)rd_be32(p) << 32) 
 // Snappy raw block: varint uncompressed length, then elements.  Tag low 2 bits: 00 literal (length-1 in the upper 6
 // bits, or 60..63 = 1..4 little-endian length bytes follow), 01 copy with 1-byte offset (len 4 + 3 bits, offset 3
 // high bits << 8 | next byte), 10 copy with 2-byte LE offset (len 1 + 6 bits), 11 copy with 4-byte LE offset.
-bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
+// `cap`: the most bytes a chunk may decode to (its values); a longer declared or produced output is malformed.
+bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out, uint64_t cap) {
   size_t i = 0;
   uint64_t len = 0;
   for (int shift = 0;; shift += 7) {
@@ -42,8 +44,9 @@ bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
     len |= (uint64_t)(b & 0x7F) << shift;
     if (!(b & 0x80)) break;
   }
+  if (len > cap) return false;
   out->clear();
-  out->reserve(len);
+  out->reserve((size_t)std::min<uint64_t>(len, 32ull * n + 64));  // a snappy element expands at most ~22x
   while (i < n) {
     const uint8_t tag = in[i++];
     const int type = tag & 3;
@@ -57,7 +60,7 @@ bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
         i += nb;
       }
       ++l;
-      if (i + l > n) return false;
+      if (l > n - i || out->size() + l > len) return false;
       out->insert(out->end(), in + i, in + i + l);
       i += l;
       continue;
@@ -78,7 +81,7 @@ bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
       off = (uint64_t)in[i] | ((uint64_t)in[i + 1] << 8) | ((uint64_t)in[i + 2] << 16) | ((uint64_t)in[i + 3] << 24);
       i += 4;
     }
-    if (off == 0 || off > out->size()) return false;
+    if (off == 0 || off > out->size() || out->size() + l > len) return false;
     const size_t from = out->size() - off;
     for (uint64_t k = 0; k < l; ++k) out->push_back((*out)[from + k]);  // overlapping copies repeat the pattern
   }
@@ -87,7 +90,7 @@ bool snappy_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
 
 // LZ4 block: sequences of token (literal length high nibble, match length - 4 low nibble; 15 = extended by 255-run
 // bytes), literals, 2-byte LE match offset, extended match length.  The last sequence has literals only.
-bool lz4_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
+bool lz4_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out, uint64_t cap) {
   out->clear();
   size_t i = 0;
   while (i < n) {
@@ -101,7 +104,7 @@ bool lz4_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
         lit += b;
       } while (b == 255);
     }
-    if (i + lit > n) return false;
+    if (lit > n - i || out->size() + lit > cap) return false;
     out->insert(out->end(), in + i, in + i + lit);
     i += lit;
     if (i == n) break;  // last sequence
@@ -118,7 +121,7 @@ bool lz4_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
       } while (b == 255);
     }
     ml += 4;
-    if (off == 0 || off > out->size()) return false;
+    if (off == 0 || off > out->size() || out->size() + ml > cap) return false;
     const size_t from = out->size() - off;
     for (uint64_t k = 0; k < ml; ++k) out->push_back((*out)[from + k]);
   }
@@ -173,15 +176,15 @@ int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t
     if (codec == 0) {  // PASS_THROUGH: the chunk's values as they are
       buf.assign(src, src + std::min(len, chunk_bytes));
     } else if (codec == 1) {
-      if (!snappy_decode(src, len, &buf)) return bad(PGPU_E_INVALID, "bad SNAPPY chunk " + std::to_string(c));
+      if (!snappy_decode(src, len, &buf, chunk_bytes)) return bad(PGPU_E_INVALID, "bad SNAPPY chunk " + std::to_string(c));
     } else {
       if (codec == 4) {  // LZ4_LENGTH_PREFIXED
         if (len < 4) return bad(PGPU_E_INVALID, "bad LZ4 chunk " + std::to_string(c));
         const uint32_t dl = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
         src += 4;
         len -= 4;
-        if (!lz4_decode(src, len, &buf) || buf.size() != dl) return bad(PGPU_E_INVALID, "bad LZ4 chunk " + std::to_string(c));
-      } else if (!lz4_decode(src, len, &buf)) {
+        if (dl > chunk_bytes || !lz4_decode(src, len, &buf, dl) || buf.size() != dl) return bad(PGPU_E_INVALID, "bad LZ4 chunk " + std::to_string(c));
+      } else if (!lz4_decode(src, len, &buf, chunk_bytes)) {
         return bad(PGPU_E_INVALID, "bad LZ4 chunk " + std::to_string(c));
       }
     }

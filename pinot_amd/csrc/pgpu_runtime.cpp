@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/pinot_gpu.h"
+#include "pgpu_host.h"
 #include "pgpu_internal.h"
 
 // kernels (pgpu_kernels.hip)
@@ -49,13 +50,6 @@ hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, 
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
-// pgpu_iterstats.cpp
-int64_t reference_entries_scanned(const pgpu_filter_node* nodes, int num_nodes, const uint32_t* const* leaf_words,
-                                  int num_leaves, int32_t num_docs, const int32_t* const* leaf_offsets = nullptr);
-bool pgpu_filter_count_is_reference(const pgpu_filter_node* nodes, int num_nodes);
-// pgpu_rawfwd.cpp
-int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t num_docs, std::vector<uint8_t>* out,
-                            std::string* err);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
@@ -337,72 +331,14 @@ void release_ws(pgpu_context* ctx, Workspace* w) {
   w->busy = false;
 }
 
-// ---- Roaring portable format (RoaringBitmap 0.9.26 serialize / ImmutableRoaringBitmap) ----------------------
-// cookie 12346: int32 cookie, int32 size, (key, card-1) uint16 pairs, int32 offsets, containers.
-// cookie 12347: low 16 bits = 12347, high 16 bits = size-1, run-flag bitset ceil(size/8) bytes, (key, card-1)
-//               pairs, int32 offsets only when size >= 4, containers.  Container: run (flag set) = uint16 n +
-//               n (start, length-1) pairs; else card > 4096 = bitmap 1024 x uint64; else array card x uint16.
-struct ParsedContainer {
-  uint32_t key, type, card;
-  const uint8_t* payload;
-  size_t payload_bytes;
-};
-
-int parse_roaring(const uint8_t* p, size_t n, std::vector<ParsedContainer>* out) {
-  if (n < 4) return fail(PGPU_E_INVALID, "roaring bitmap truncated");
-  const uint32_t cookie = le32(p);
-  size_t pos;
-  uint32_t size;
-  bool has_run = false;
-  const uint8_t* runflags = nullptr;
-  if ((cookie & 0xFFFFu) == 12347u) {
-    has_run = true;
-    size = (cookie >> 16) + 1;
-    runflags = p + 4;
-    pos = 4 + (size + 7) / 8;
-  } else if (cookie == 12346u) {
-    if (n < 8) return fail(PGPU_E_INVALID, "roaring bitmap truncated");
-    size = le32(p + 4);
-    pos = 8;
-  } else {
-    return fail(PGPU_E_INVALID, "bad roaring cookie %u", cookie);
-  }
-  if (size > 65536u) return fail(PGPU_E_INVALID, "bad roaring container count %u", size);
-  if (pos + 4ull * size > n) return fail(PGPU_E_INVALID, "roaring header truncated");
-  const uint8_t* kc = p + pos;
-  pos += 4ull * size;
-  if (!has_run || size >= 4) pos += 4ull * size;  // offsets
-  for (uint32_t i = 0; i < size; ++i) {
-    ParsedContainer c;
-    c.key = le16(kc + 4 * i);
-    const uint32_t card = (uint32_t)le16(kc + 4 * i + 2) + 1;
-    const bool run = has_run && ((runflags[i / 8] >> (i % 8)) & 1);
-    if (run) {
-      if (pos + 2 > n) return fail(PGPU_E_INVALID, "roaring run container truncated");
-      const uint32_t nruns = le16(p + pos);
-      pos += 2;
-      c.type = PGPU_CT_RUN;
-      c.card = nruns;
-      c.payload = p + pos;
-      c.payload_bytes = 4ull * nruns;
-    } else if (card > 4096) {
-      c.type = PGPU_CT_BITMAP;
-      c.card = card;
-      c.payload = p + pos;
-      c.payload_bytes = 8192;
-    } else {
-      c.type = PGPU_CT_ARRAY;
-      c.card = card;
-      c.payload = p + pos;
-      c.payload_bytes = 2ull * card;
-    }
-    if (pos + c.payload_bytes > n) return fail(PGPU_E_INVALID, "roaring container %u truncated", i);
-    if (i > 0 && c.key <= out->back().key) return fail(PGPU_E_INVALID, "roaring keys not ascending");
-    pos += c.payload_bytes;
-    out->push_back(c);
-  }
-  return PGPU_OK;
+// Roaring portable format: pgpu_roaring.cpp (pgpu_parse_roaring)
+int parse_roaring(const uint8_t* p, size_t n, std::vector<PgpuRoaringContainer>* out) {
+  std::string err;
+  const int rc = pgpu_parse_roaring(p, n, out, &err);
+  return rc ? fail(rc, "%s", err.c_str()) : PGPU_OK;
 }
+using ParsedContainer = PgpuRoaringContainer;
+static_assert(PGPU_CT_ARRAY == 0 && PGPU_CT_BITMAP == 1 && PGPU_CT_RUN == 2, "pgpu_parse_roaring container types");
 
 int check_column(pgpu_segment* seg, int32_t column) {
   if (!seg) return fail(PGPU_E_INVALID, "null segment");
@@ -1962,8 +1898,6 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       return fail(PGPU_E_INVALID, "group column %d is multi-value in %d of %d segments", g, nmv, q->num_segments);
     if (nmv) p.mv_gmask |= 1 << g;
   }
-  if (p.mv_gmask && p.mode == PGPU_MODE_HASH)
-    return fail(PGPU_E_UNSUPPORTED, "GROUP BY on a multi-value column over a hashed key space (map-based holder)");
   int64_t tiles = 0;
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
