@@ -54,6 +54,10 @@ def lower(query: QueryContext) -> Tuple[QueryContext, List[List[int]]]:
     return low, parts
 
 
+def lowered_columns(query: QueryContext) -> List[str]:
+    return lower(query)[0].projected_columns
+
+
 def _raise_values(query: QueryContext, parts: List[List[int]], fin: list, inter: list):
     """Final and intermediate values of the original aggregations from the lowered ones."""
     out_f, out_i = [], []
@@ -77,6 +81,12 @@ def raise_result(query: QueryContext, parts: List[List[int]], low_res):
     from .plan import QueryResult, order_and_limit, to_select_order
 
     res = QueryResult(query=query, stats=low_res.stats)
+    # numEntriesScannedPostFilter = scanned docs x the ORIGINAL query's projected columns (the row columns the
+    # lowered query reads stand in for their multi-value column: AggregationGroupByOrderByOperator.java:97-137)
+    low_cols = len(lowered_columns(query))
+    if low_cols:
+        st = res.stats
+        st.num_entries_scanned_post_filter = st.num_entries_scanned_post_filter // low_cols * len(query.projected_columns)
     if not query.group_by:
         fin, inter = _raise_values(query, parts, low_res.aggregation_result, low_res.intermediate[()])
         res.aggregation_result = fin

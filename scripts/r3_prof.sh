@@ -18,4 +18,11 @@ for wl in ${PMC_WLS:-}; do
       python3 $BENCH --workload $wl --steps 3 --warmup 1 > "$OUT/pmc_${wl}_$c.log" 2>&1 || { echo "pmc $wl $c failed rc=$?"; exit 1; }
   done
 done
+
+# phase counters of the profiling build (PGPU_PROFILE=1: libpinotgpu_prof.so) for $PROF_WLS
+for wl in ${PROF_WLS:-}; do
+  PGPU_PROFILE=1 timeout -k 10 200 python3 $BENCH --workload $wl --steps 3 --warmup 1 > "$OUT/phase_$wl.log" 2>&1 \
+    || { echo "phase $wl failed rc=$?"; tail -5 "$OUT/phase_$wl.log"; exit 1; }
+  grep "pgpu profile" "$OUT/phase_$wl.log" | tail -2
+done
 echo done
