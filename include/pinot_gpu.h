@@ -102,8 +102,8 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
 /* Raw (no-dictionary) single-value column of a fixed-width type (INT / LONG / FLOAT / DOUBLE): the file
  * FixedByteChunkSVForwardIndexWriter writes (`<column>.sv.raw.fwd`, seglocal/io/writer/impl/
  * FixedByteChunkSVForwardIndexWriter.java:39-104, header BaseChunkSVForwardIndexWriter.java:125-160), versions 1-4,
- * chunks PASS_THROUGH / SNAPPY / LZ4 / LZ4_LENGTH_PREFIXED (ChunkCompressionType ordinals 0, 1, 3, 4; ZSTANDARD
- * returns PGPU_E_UNSUPPORTED).  Decoded once into HBM as the values by doc id, replacing FixedByteChunkSVForwardIndexReader /
+ * chunks PASS_THROUGH / SNAPPY / ZSTANDARD / LZ4 / LZ4_LENGTH_PREFIXED (ChunkCompressionType ordinals 0-4; ZSTANDARD
+ * frames are decoded by the system's libzstd.so.1, and return PGPU_E_UNSUPPORTED when it cannot be loaded).  Decoded once into HBM as the values by doc id, replacing FixedByteChunkSVForwardIndexReader /
  * FixedBytePower2ChunkSVForwardIndexReader (seglocal/segment/index/readers/forward/BaseChunkSVForwardIndexReader.java:56-157).
  * Such a column has no dictionary (do not call pgpu_segment_add_dictionary); it may be aggregated (SUM / MIN / MAX /
  * AVG) and filtered through PGPU_F_RAW_SCAN / PGPU_F_RANGE_INDEX leaves, but not grouped on (the reference groups raw

@@ -10,6 +10,9 @@
   SNAPPY 1, ZSTANDARD 2, LZ4 3, LZ4_LENGTH_PREFIXED 4).  SNAPPY and LZ4 are third-party (snappy-java, lz4-java;
   not vendored, not importable here): their published raw block formats are restated below, encoder and decoder.
   The encoders are simple greedy matchers -- any valid block decodes the same, which is all the readers rely on.
+  ZSTANDARD (ZstandardCompressor / ZstandardDecompressor: zstd-jni 1.4.9-5, one zstd frame per chunk) is too large
+  a format to restate; it goes through pyarrow's bundled zstd codec, an implementation independent of the system
+  libzstd.so.1 the product decodes with.
 * The reader half mirrors BaseChunkSVForwardIndexReader (seglocal/segment/index/readers/forward/
   BaseChunkSVForwardIndexReader.java:56-157) / FixedByteChunkSVForwardIndexReader.getInt/Long/Float/Double.
 """
@@ -210,6 +213,8 @@ def _compress(chunk: bytes, codec: int) -> bytes:
         return lz4_compress(chunk)
     if codec == LZ4_LENGTH_PREFIXED:  # LZ4CompressorWithLength: 4-byte little-endian length, then the block
         return struct.pack("<I", len(chunk)) + lz4_compress(chunk)
+    if codec == ZSTANDARD:  # Zstd.compress(dst, src) at the default level: one frame with its content size
+        return _zstd().compress(chunk, asbytes=True)
     raise ValueError(f"codec {codec} is not restated here")
 
 
@@ -225,7 +230,28 @@ def _decompress(chunk: bytes, codec: int) -> bytes:
         out = lz4_decompress(chunk[4:])
         assert len(out) == n
         return out
+    if codec == ZSTANDARD:
+        import pyarrow as pa
+        n = _zstd_content_size(chunk)
+        return _zstd().decompress(pa.py_buffer(chunk), decompressed_size=n, asbytes=True)
     raise ValueError(f"codec {codec} is not restated here")
+
+
+def _zstd():
+    import pyarrow as pa
+    return pa.Codec("zstd", compression_level=3)  # zstd-jni's Zstd.compress default level (3)
+
+
+def _zstd_content_size(frame: bytes) -> int:
+    """Frame_Content_Size of a zstd frame header (RFC 8878 3.1.1.1): what Zstd.decompressedSize returns."""
+    assert frame[:4] == b"\x28\xb5\x2f\xfd", "not a zstd frame"
+    fhd = frame[4]
+    fcs_flag, single, did_flag = fhd >> 6, (fhd >> 5) & 1, fhd & 3
+    pos = 5 + (0 if single else 1) + (0, 1, 2, 4)[did_flag]
+    size = (1 if single else 0, 2, 4, 8)[fcs_flag]
+    assert size, "frame without a content size"
+    v = int.from_bytes(frame[pos:pos + size], "little")
+    return v + 256 if size == 2 else v
 
 
 # ---- file ---------------------------------------------------------------------------------------------------------

@@ -13,8 +13,11 @@
 // Codecs (seglocal/io/compression/ChunkCompressorFactory.java): PASS_THROUGH, SNAPPY (snappy-java raw block format),
 // LZ4 (lz4-java fastCompressor: raw LZ4 block), LZ4_LENGTH_PREFIXED (lz4-java LZ4CompressorWithLength: 4-byte
 // little-endian decompressed length, then a raw LZ4 block).  The snappy and LZ4 libraries are third-party
-// dependencies of the reference (not vendored); their published block formats are restated below.  ZSTANDARD is
-// not decoded here (PGPU_E_UNSUPPORTED: the server keeps its CPU reader for such a segment).
+// dependencies of the reference (not vendored); their published block formats are restated below.  ZSTANDARD
+// (seglocal/io/compression/ZstandardDecompressor.java: zstd-jni 1.4.9-5 `Zstd.decompress`, one zstd frame per chunk)
+// is decoded by the system's libzstd.so.1, loaded on first use; without it such a segment returns PGPU_E_UNSUPPORTED
+// and the server keeps its CPU reader.
+#include <dlfcn.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -128,6 +131,35 @@ bool lz4_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out, uint64_t
   return true;
 }
 
+// ZSTANDARD chunk: one zstd frame (RFC 8878) decoded by libzstd's ZSTD_decompress into at most `cap` bytes.  The
+// library is resolved once; its two entry points have been ABI-stable since zstd 1.0.
+struct Zstd {
+  size_t (*decompress)(void*, size_t, const void*, size_t) = nullptr;
+  unsigned (*is_error)(size_t) = nullptr;
+};
+const Zstd& zstd_lib() {
+  static const Zstd z = [] {
+    Zstd r;
+    void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return r;
+    r.decompress = (size_t(*)(void*, size_t, const void*, size_t))dlsym(h, "ZSTD_decompress");
+    r.is_error = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
+    if (!r.decompress || !r.is_error) r.decompress = nullptr;
+    return r;
+  }();
+  return z;
+}
+// 1: decoded, 0: malformed (or longer than `cap`), -1: no zstd library
+int zstd_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out, uint64_t cap) {
+  const Zstd& z = zstd_lib();
+  if (!z.decompress) return -1;
+  out->resize((size_t)cap);
+  const size_t r = z.decompress(out->data(), (size_t)cap, in, n);
+  if (z.is_error(r)) return 0;
+  out->resize(r);
+  return 1;
+}
+
 }  // namespace
 
 // Decodes the file into num_docs little-endian values of `width` bytes (out is resized to num_docs * width).
@@ -157,7 +189,8 @@ int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t
   }
   const int off_size = version >= 3 ? 8 : 4;
   if (data_header + (uint64_t)num_chunks * off_size > n) return bad(PGPU_E_INVALID, "raw forward index chunk offsets truncated");
-  if (codec == 2) return bad(PGPU_E_UNSUPPORTED, "ZSTANDARD raw forward index chunks are not decoded on this path");
+  if (codec == 2 && !zstd_lib().decompress)
+    return bad(PGPU_E_UNSUPPORTED, "ZSTANDARD raw forward index chunks need libzstd.so.1, which is not loadable");
   if (codec < 0 || codec > 4) return bad(PGPU_E_INVALID, "raw forward index compression type " + std::to_string(codec));
   auto chunk_pos = [&](int32_t c) -> uint64_t {
     const uint8_t* p = b + data_header + (uint64_t)c * off_size;
@@ -177,6 +210,8 @@ int pgpu_decode_raw_forward(const uint8_t* b, uint64_t n, int32_t width, int32_t
       buf.assign(src, src + std::min(len, chunk_bytes));
     } else if (codec == 1) {
       if (!snappy_decode(src, len, &buf, chunk_bytes)) return bad(PGPU_E_INVALID, "bad SNAPPY chunk " + std::to_string(c));
+    } else if (codec == 2) {
+      if (zstd_decode(src, len, &buf, chunk_bytes) != 1) return bad(PGPU_E_INVALID, "bad ZSTANDARD chunk " + std::to_string(c));
     } else {
       if (codec == 4) {  // LZ4_LENGTH_PREFIXED
         if (len < 4) return bad(PGPU_E_INVALID, "bad LZ4 chunk " + std::to_string(c));

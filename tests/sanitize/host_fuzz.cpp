@@ -1,6 +1,6 @@
 // Sanitizer harness for libpinotgpu's host-side parsers of untrusted segment bytes (built with
 // -fsanitize=address,undefined by tests/test_host_sanitize.py, CPU only): pgpu_decode_raw_forward (raw forward
-// index chunks: PASS_THROUGH / SNAPPY / LZ4 / LZ4_LENGTH_PREFIXED), pgpu_parse_roaring (inverted-index bitmaps)
+// index chunks: PASS_THROUGH / SNAPPY / LZ4 / LZ4_LENGTH_PREFIXED / ZSTANDARD), pgpu_parse_roaring (inverted-index bitmaps)
 // and reference_entries_scanned (filter programs replayed over leaf bitmaps).
 //
 // Usage: host_fuzz <kind> <file> [variants]   kind = raw:<width>:<num_docs> | roaring | program

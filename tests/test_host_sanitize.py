@@ -31,7 +31,7 @@ pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not ava
 def fuzz(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("sanitize") / "host_fuzz")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-           "-fno-omit-frame-pointer"] + SOURCES + ["-o", out]
+           "-fno-omit-frame-pointer"] + SOURCES + ["-o", out, "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail(r.stderr[-4000:])
@@ -60,7 +60,7 @@ def test_raw_forward_reference_files(fuzz, tmp_path, name, n):
 
 
 @pytest.mark.parametrize("codec,version", [(rawfwd.PASS_THROUGH, 2), (rawfwd.SNAPPY, 3), (rawfwd.LZ4, 3),
-                                           (rawfwd.LZ4_LENGTH_PREFIXED, 4)])
+                                           (rawfwd.LZ4_LENGTH_PREFIXED, 4), (rawfwd.ZSTANDARD, 2)])
 @pytest.mark.parametrize("dt,width", [(PGPU_INT, 4), (PGPU_LONG, 8)])
 def test_raw_forward_codecs(fuzz, tmp_path, codec, version, dt, width):
     rng = np.random.default_rng(codec * 10 + version)

@@ -15,7 +15,8 @@ from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, Unsuppo
 from pinot_amd.query import parse_sql
 from tests.helpers import check_groups, close, rows_close
 
-CODECS = [(rawfwd.PASS_THROUGH, 2), (rawfwd.SNAPPY, 2), (rawfwd.LZ4, 3), (rawfwd.LZ4_LENGTH_PREFIXED, 4)]
+CODECS = [(rawfwd.PASS_THROUGH, 2), (rawfwd.SNAPPY, 2), (rawfwd.LZ4, 3), (rawfwd.LZ4_LENGTH_PREFIXED, 4),
+          (rawfwd.ZSTANDARD, 3)]
 
 
 def _data(rng, n):
