@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 5
+#define PGPU_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -106,8 +106,8 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
  * frames are decoded by the system's libzstd.so.1, and return PGPU_E_UNSUPPORTED when it cannot be loaded).  Decoded once into HBM as the values by doc id, replacing FixedByteChunkSVForwardIndexReader /
  * FixedBytePower2ChunkSVForwardIndexReader (seglocal/segment/index/readers/forward/BaseChunkSVForwardIndexReader.java:56-157).
  * Such a column has no dictionary (do not call pgpu_segment_add_dictionary); it may be aggregated (SUM / MIN / MAX /
- * AVG) and filtered through PGPU_F_RAW_SCAN / PGPU_F_RANGE_INDEX leaves, but not grouped on (the reference groups raw
- * columns with NoDictionary*GroupKeyGenerator, a value-hash path outside this one: PGPU_E_UNSUPPORTED). */
+ * AVG), filtered through PGPU_F_RAW_SCAN / PGPU_F_RANGE_INDEX leaves, and grouped on through its on-the-fly group
+ * dictionary (pgpu_segment_add_group_dictionary). */
 int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_t data_type, const void* bytes,
                                        uint64_t num_bytes);
 /* Range index of a column (`<column>.bitmap.range`): only its header is read -- version 2 is the exact bit-sliced
@@ -136,6 +136,20 @@ int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const v
 int pgpu_segment_add_mv_row_columns(pgpu_segment* seg, int32_t column, int32_t len_column, int32_t sum_column,
                                     int32_t min_column, int32_t max_column);
 int pgpu_segment_seal(pgpu_segment* seg);
+/* GROUP BY on a raw (no-dictionary) column: its on-the-fly dictionary, the replacement of the value -> id maps of
+ * NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator
+ * (core/query/aggregation/groupby/NoDictionarySingleColumnGroupKeyGenerator.java:70-118, 199-235;
+ * NoDictionaryMultiColumnGroupKeyGenerator.java:90-150).  Built on the GPU from `raw_column`'s values into the empty
+ * slot `dict_column` (callable before or after seal, once): the distinct values sorted ascending (Float.compare order;
+ * FLOAT / DOUBLE values distinct by floatToIntBits / doubleToLongBits, as the reference's primitive maps key them:
+ * -0.0 and 0.0 apart, one NaN) as a numeric dictionary, and every doc's id as a fixed-bit forward index.  The slot then
+ * groups like any dictionary-encoded column; *out_cardinality = its distinct values. */
+int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int32_t dict_column,
+                                      int32_t* out_cardinality);
+/* The little-endian numeric dictionary of a column (pgpu_segment_add_dictionary or _add_group_dictionary):
+ * *out_bytes = its size; copied into `out` when non-NULL (capacity_bytes >= *out_bytes). */
+int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void* out, uint64_t capacity_bytes,
+                                   uint64_t* out_bytes);
 /* HBM bytes held by the segment (all columns, including padding and container directories). */
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);
 int pgpu_segment_release(pgpu_segment* seg);

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import bisect
 import math
+import struct
 from dataclasses import dataclass, field
 from fractions import Fraction
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -783,18 +784,25 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
     if any(ds.seg.column(g).mv_forward is not None for g in query.group_by):
         res.groups = _group_multi_value(query, ds, docs, num_groups_limit, max_init_group_holder_capacity)
         return res
-    # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long)
-    cards = [ds.seg.column(g).cardinality for g in query.group_by]
+    # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long); a raw
+    # (no-dictionary) group column keys by value (_raw_group_ids)
+    gsrc = [_raw_group_ids(ds, g) if ds.seg.column(g).raw_forward is not None else (ds.ids(g), ds.dictionary(g))
+            for g in query.group_by]
+    cards = [len(d) for _, d in gsrc]
     prod = 1
     for c in cards:
         prod *= c
-    idmat = np.stack([ds.ids(g)[docs].astype(np.int64) for g in query.group_by], axis=1) if len(docs) else \
+    # NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator (any raw group column):
+    # a value -> id map capped at numGroupsLimit whatever the key space (:199-235 / :295-330)
+    raw_group = [ds.seg.column(g).raw_forward is not None for g in query.group_by]
+    no_dict = any(raw_group)
+    idmat = np.stack([ids[docs].astype(np.int64) for ids, _ in gsrc], axis=1) if len(docs) else \
         np.zeros((0, len(cards)), dtype=np.int64)
     uniq, first, inv = (np.unique(idmat, axis=0, return_index=True, return_inverse=True) if len(docs)
                         else (np.zeros((0, len(cards)), np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64)))
     inv = np.asarray(inv).reshape(-1)
     keep_groups = np.ones(len(uniq), dtype=bool)
-    if prod > max_init_group_holder_capacity and len(uniq) > num_groups_limit:
+    if (no_dict or prod > max_init_group_holder_capacity) and len(uniq) > num_groups_limit:
         # map-based holder: only the first `limit` distinct keys (in doc order) get group ids
         keep_groups[:] = False
         keep_groups[np.argsort(first, kind="stable")[:num_groups_limit]] = True
@@ -802,19 +810,59 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
     inv_s, docs_s = inv[order], docs[order]
     bounds = np.flatnonzero(np.diff(inv_s)) + 1
     groups: Dict[tuple, list] = {}
-    dicts = [ds.dictionary(g) for g in query.group_by]
+    dicts = [d for _, d in gsrc]
     for part_docs, part_g in zip(np.split(docs_s, bounds), np.split(inv_s, bounds)):
         if part_docs.size == 0 or not keep_groups[part_g[0]]:
             continue
         vals = []
         for j, d in enumerate(dicts):
             v = d[int(uniq[part_g[0], j])]
-            vals.append(v.item() if hasattr(v, "item") else v)
+            v = v.item() if hasattr(v, "item") else v
+            vals.append(JavaFloatKey(v) if isinstance(v, float) and raw_group[j] else v)
         groups[tuple(vals)] = [aggregate(a.function, None if a.column is None else
                                          _as_float_values(ds, a.column, part_docs, a.function), len(part_docs))
                                for a in query.aggregations]
     res.groups = groups
     return res
+
+
+def float_bits_key(v: np.ndarray) -> np.ndarray:
+    """Java's map key of FLOAT / DOUBLE values -- Float.floatToIntBits / Double.doubleToLongBits (one NaN; -0.0 and
+    0.0 apart) -- as an order-preserving int64 (Float.compare order)."""
+    if v.dtype == np.float32:
+        b = v.view(np.int32).astype(np.int64)
+        b = np.where(np.isnan(v), np.int64(0x7FC00000), b)
+        return np.where(b >= 0, b, b ^ np.int64(0x7FFFFFFF))
+    b = v.view(np.int64)
+    b = np.where(np.isnan(v), np.int64(0x7FF8000000000000), b)
+    return np.where(b >= 0, b, b ^ np.int64(0x7FFFFFFFFFFFFFFF))
+
+
+class JavaFloatKey(float):
+    """A FLOAT / DOUBLE group value compared and hashed as the reference's map keys are: by floatToIntBits /
+    doubleToLongBits (-0.0 != 0.0, NaN == NaN), so that Python dicts keep -0.0 and 0.0 as two groups."""
+
+    def _bits(self):
+        return b"nan" if math.isnan(self) else struct.pack(">d", self)
+
+    def __eq__(self, other):
+        return isinstance(other, float) and JavaFloatKey._bits(self) == JavaFloatKey._bits(other)
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    def __hash__(self):
+        return hash(JavaFloatKey._bits(self))
+
+
+def _raw_group_ids(ds: DecodedSegment, col: str):
+    """Per doc an id of its value among the segment's distinct values of a raw column, and those values ascending:
+    the keys of NoDictionary*GroupKeyGenerator's value -> id maps (Int2Int / Long2Int / Float2Int / Double2Int
+    OpenHashMap: INT / LONG by value, FLOAT / DOUBLE by floatToIntBits / doubleToLongBits)."""
+    v = ds.raw_values(col)
+    keys = float_bits_key(v) if v.dtype.kind == "f" else v.astype(np.int64)
+    uniq, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    return np.asarray(inv).reshape(-1), v[first]
 
 
 def _group_multi_value(query: QueryContext, ds: DecodedSegment, docs: np.ndarray, num_groups_limit: int,

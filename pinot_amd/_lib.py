@@ -37,7 +37,7 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class PinotGpuError(RuntimeError):
@@ -140,6 +140,8 @@ SIGNATURES = [
     ("pgpu_segment_add_mv_forward_index", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.c_int32, C.c_int32, C.c_int64]),
     ("pgpu_segment_add_mv_row_columns", C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     ("pgpu_segment_seal", C.c_int, [_P]),
+    ("pgpu_segment_add_group_dictionary", C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+    ("pgpu_segment_dictionary_values", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_device_bytes", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_release", C.c_int, [_P]),
     ("pgpu_remap_upload", C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),

@@ -33,7 +33,7 @@ from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I6
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
 from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
                    has_mv_aggregations, key_words_out, merge_filtered, mv_lower, mv_raise, table_capacity,
-                   topk_spec)
+                   topk_spec, union_sorted)
 from .query import QueryContext, split_filtered_aggregations
 from .segment import GpuSegment
 
@@ -147,7 +147,7 @@ def union_dictionaries(local: Sequence, group=None, device=None):
     parts = [_decode_dictionary(b[:sz].cpu().numpy(), kind) for b, sz in zip(bufs, sizes)]
     if kind == "s":
         return sorted(set().union(*[set(p) for p in parts]))
-    vals = np.unique(np.concatenate(parts)) if parts else np.zeros(0)
+    vals = union_sorted(parts)
     if kind == "i":
         return vals.astype(np.int64)
     return vals

@@ -1385,10 +1385,13 @@ FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, cons
 
 // Sparse (per-doc) aggregation of the survivors `m` among this lane's U docs: group key = mixed radix of the
 // remapped group ids, COUNT into section 0, every other aggregation gathers its id and dictionary value.
-template <int MODE>
+// MV: the kernel may meet multi-value group columns (only the ring kernel: the expansion's loops and gathers would
+// cost the self-loading kernels' register budget -- 1.1 KB of scratch and a wave per SIMD -- the runtime never
+// sends such a query to them).
+template <int MODE, bool MV>
 FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                    const int32_t (&doc)[U], uint32_t m) {
-  if constexpr (MODE == PGPU_MODE_LDS || MODE == PGPU_MODE_GLOBAL || MODE == PGPU_MODE_HASH) {
+  if constexpr (MV && (MODE == PGPU_MODE_LDS || MODE == PGPU_MODE_GLOBAL || MODE == PGPU_MODE_HASH)) {
     if (p.mv_gmask) {
       sparse_agg_mv<MODE>(p, L, ss, doc, m);
       return;
@@ -1515,7 +1518,7 @@ FI int new_sectors(uint32_t b, int32_t doc, bool live, int32_t prev_doc, bool pr
 }
 
 // Flush the candidate queue (doc ids of one segment, ascending): residual filter per doc, then sparse aggregation.
-template <int MODE, int NCONS>
+template <int MODE, int NCONS, bool MV = false>
 FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss, int n,
                     int64_t& matched, int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
   const int lane = lane_id();
@@ -1573,7 +1576,7 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
       const int tot = wave_sum_i32(sec);
       if (lane == 0) sector_bytes += 32ll * tot;
     }
-    if (nm && ss.agg_mode == PGPU_AM_SPARSE) sparse_agg<MODE>(p, L, cv, la, ss, d.doc, m);
+    if (nm && ss.agg_mode == PGPU_AM_SPARSE) sparse_agg<MODE, MV>(p, L, cv, la, ss, d.doc, m);
   }
   // a wait hipcc sees: its scoreboard then holds no pending gather, so it does not guard the next tile's LDS reads
   // with vmcnt(0) (which would also drain the direct kernel's prefetched tiles)
@@ -1845,7 +1848,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
   for (;;) {
     if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES)) {
       const int64_t tq = now(pf);
-      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+      flush_queue<MODE, NCONS, true>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
       PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
       qn = qt = 0;
     }
@@ -1867,7 +1870,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     const bool segchg = !end && cur.seg != cseg;
     if (qn && (end || segchg)) {
       const int64_t tq = now(pf);
-      flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+      flush_queue<MODE, NCONS, true>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
       PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
       qn = qt = 0;
     }
@@ -1962,7 +1965,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
         // a dense tile does not fit behind the queued entries: flush them, then queue and flush the tile in two
         // halves (lanes 0-31, 32-63: <= 1024 entries each)
         if (qn) {
-          flush_queue<MODE, NCONS>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+          flush_queue<MODE, NCONS, true>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
           qn = qt = 0;
         }
         if (lane == 0) cv.qtiles[0] = cur.tile_in_seg;
@@ -1973,7 +1976,7 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
           int k = wave_excl_scan(__popc(mh));
           for (uint32_t left = mh; left; left &= left - 1)
             cv.queue[k++] = (uint16_t)(32 * lane + __builtin_ctz(left));
-          flush_queue<MODE, NCONS>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
+          flush_queue<MODE, NCONS, true>(p, L, cv, la, ss, nh, matched, scanned, sector_bytes, dense_bytes, pf);
         }
       }
     }

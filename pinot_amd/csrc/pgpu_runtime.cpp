@@ -53,6 +53,12 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
+// on-the-fly group dictionaries of raw columns (pgpu_gdict.hip)
+size_t pgpu_gdict_temp_bytes(int64_t n);
+hipError_t pgpu_gdict_sort_unique(const void* vals, int32_t dtype, int64_t n, uint64_t* keys, uint64_t* sorted,
+                                  uint64_t* uniq, uint32_t* d_card, void* temp, size_t temp_bytes, hipStream_t st);
+hipError_t pgpu_gdict_encode(const uint64_t* keys, int64_t n, const uint64_t* uniq, int32_t card, int32_t dtype,
+                             int bits, void* dict, uint32_t* ids, uint32_t* words, int64_t nwords, hipStream_t st);
 
 namespace {
 
@@ -106,6 +112,16 @@ struct DevMem {
   DevMem(const DevMem&) = delete;
   DevMem& operator=(const DevMem&) = delete;
   DevMem(DevMem&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevMem& operator=(DevMem&& o) noexcept {
+    if (this != &o) {
+      reset();
+      p = o.p;
+      n = o.n;
+      o.p = nullptr;
+      o.n = 0;
+    }
+    return *this;
+  }
   ~DevMem() { reset(); }
   void reset() {
     if (p) (void)hipFree(p);
@@ -345,6 +361,18 @@ int check_column(pgpu_segment* seg, int32_t column) {
   if (seg->sealed) return fail(PGPU_E_INVALID, "segment already sealed");
   if (column < 0 || column >= (int32_t)seg->cols.size()) return fail(PGPU_E_INVALID, "bad column %d", column);
   return PGPU_OK;
+}
+
+// Two independent 64-bit hashes of a little-endian dictionary (shared-dictionary checks).
+void dictionary_hash(const std::vector<uint8_t>& le, uint64_t* out) {
+  uint64_t h1 = 1469598103934665603ull, h2 = 0x9E3779B97F4A7C15ull;  // FNV-1a, and a multiply-xorshift mix
+  for (uint8_t x : le) {
+    h1 = (h1 ^ x) * 1099511628211ull;
+    h2 = (h2 + x + 1) * 0xBF58476D1CE4E5B9ull;
+    h2 ^= h2 >> 29;
+  }
+  out[0] = h1;
+  out[1] = h2;
 }
 
 hipError_t upload(DevMem& m, const void* src, size_t bytes, size_t alloc_bytes, int mem_kind) {
@@ -656,14 +684,7 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
       c.for_nblk = nblk;
     }
   }
-  uint64_t h1 = 1469598103934665603ull, h2 = 0x9E3779B97F4A7C15ull;  // FNV-1a, and a multiply-xorshift mix
-  for (uint8_t x : le) {
-    h1 = (h1 ^ x) * 1099511628211ull;
-    h2 = (h2 + x + 1) * 0xBF58476D1CE4E5B9ull;
-    h2 ^= h2 >> 29;
-  }
-  c.dict_hash[0] = h1;
-  c.dict_hash[1] = h2;
+  dictionary_hash(le, c.dict_hash);
   c.hdict = std::move(le);
   c.max_abs = max_abs;
   return PGPU_OK;
@@ -900,42 +921,136 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
   return PGPU_OK;
 }
 
+namespace {
+// The kernels' view of column i (DevColumn), with its bit-sliced copy built first (fixed-bit columns).
+int seal_column(pgpu_segment* seg, size_t i) {
+  static const bool no_slice = getenv("PGPU_NO_SLICE") && atoi(getenv("PGPU_NO_SLICE")) != 0;
+  HostColumn& c = seg->cols[i];
+  if (c.kind == PGPU_COL_FIXED_BIT && !no_slice && !c.sliced.p) {
+    // bit planes of every 2048-doc tile of the padded stream (same byte count as the packed copy)
+    const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
+    HIP_TRY(c.sliced.alloc(c.fwd.n));
+    HIP_TRY(hipMemset(c.sliced.p, 0, c.sliced.n));
+    HIP_TRY(pgpu_launch_bitslice((const uint32_t*)c.fwd.p, (uint32_t*)c.sliced.p, c.bits, ntiles, nullptr));
+  }
+  DevColumn d{};
+  d.sliced = (const uint32_t*)c.sliced.p;
+  d.fwd = (const uint32_t*)c.fwd.p;
+  // a multi-value column's row offsets take the sorted-index slot (sparse_agg_mv; a MV column has no sorted index)
+  d.sorted = (const int32_t*)(c.kind == PGPU_COL_MV ? c.mv_off.p : c.sorted.p);
+  d.dict = c.dict.p;
+  d.inv_dir = (const uint32_t*)c.inv_dir.p;
+  d.inv_ct = (const DevContainer*)c.inv_ct.p;
+  d.inv_data = (const uint8_t*)c.inv_data.p;
+  d.kind = c.kind;
+  d.bits = c.bits;
+  d.card = c.fwd_card ? c.fwd_card : (c.dict_card ? c.dict_card : c.inv_card);
+  d.dict_type = c.dict_type;
+  c.card = d.card;
+  if (c.dict_card && c.fwd_card && c.dict_card != c.fwd_card)
+    return fail(PGPU_E_INVALID, "column %zu: dictionary cardinality %d != index cardinality %d", i, c.dict_card,
+                c.fwd_card);
+  seg->dev[i] = d;
+  std::vector<uint8_t>().swap(c.mv_raw);
+  return PGPU_OK;
+}
+}  // namespace
+
 int pgpu_segment_seal(pgpu_segment* seg) {
   if (!seg) return fail(PGPU_E_INVALID, "null segment");
   seg->dev.resize(seg->cols.size());
   HIP_TRY(hipSetDevice(seg->ctx->device));
-  static const bool no_slice = getenv("PGPU_NO_SLICE") && atoi(getenv("PGPU_NO_SLICE")) != 0;
   for (size_t i = 0; i < seg->cols.size(); ++i) {
-    HostColumn& c = seg->cols[i];
-    if (c.kind == PGPU_COL_FIXED_BIT && !no_slice && !c.sliced.p) {
-      // bit planes of every 2048-doc tile of the padded stream (same byte count as the packed copy)
-      const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
-      HIP_TRY(c.sliced.alloc(c.fwd.n));
-      HIP_TRY(hipMemset(c.sliced.p, 0, c.sliced.n));
-      HIP_TRY(pgpu_launch_bitslice((const uint32_t*)c.fwd.p, (uint32_t*)c.sliced.p, c.bits, ntiles, nullptr));
-    }
-    DevColumn d{};
-    d.sliced = (const uint32_t*)c.sliced.p;
-    d.fwd = (const uint32_t*)c.fwd.p;
-    // a multi-value column's row offsets take the sorted-index slot (sparse_agg_mv; a MV column has no sorted index)
-    d.sorted = (const int32_t*)(c.kind == PGPU_COL_MV ? c.mv_off.p : c.sorted.p);
-    d.dict = c.dict.p;
-    d.inv_dir = (const uint32_t*)c.inv_dir.p;
-    d.inv_ct = (const DevContainer*)c.inv_ct.p;
-    d.inv_data = (const uint8_t*)c.inv_data.p;
-    d.kind = c.kind;
-    d.bits = c.bits;
-    d.card = c.fwd_card ? c.fwd_card : (c.dict_card ? c.dict_card : c.inv_card);
-    d.dict_type = c.dict_type;
-    c.card = d.card;
-    if (c.dict_card && c.fwd_card && c.dict_card != c.fwd_card)
-      return fail(PGPU_E_INVALID, "column %zu: dictionary cardinality %d != index cardinality %d", i, c.dict_card,
-                  c.fwd_card);
-    seg->dev[i] = d;
-    std::vector<uint8_t>().swap(c.mv_raw);
+    const int rc = seal_column(seg, i);
+    if (rc) return rc;
   }
   HIP_TRY(hipDeviceSynchronize());
   seg->sealed = true;
+  return PGPU_OK;
+}
+
+int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int32_t dict_column,
+                                      int32_t* out_cardinality) {
+  if (!seg || !out_cardinality) return fail(PGPU_E_INVALID, "null argument");
+  const int32_t nc = (int32_t)seg->cols.size();
+  if (raw_column < 0 || raw_column >= nc || dict_column < 0 || dict_column >= nc || raw_column == dict_column)
+    return fail(PGPU_E_INVALID, "bad columns %d -> %d", raw_column, dict_column);
+  const HostColumn& r = seg->cols[raw_column];
+  HostColumn& c = seg->cols[dict_column];
+  if (r.kind != PGPU_COL_RAW) return fail(PGPU_E_INVALID, "column %d is not a raw (no-dictionary) column", raw_column);
+  if (c.kind != PGPU_COL_NONE || c.dict_card) return fail(PGPU_E_INVALID, "group dictionary slot %d is not empty", dict_column);
+  const int64_t n = seg->num_docs;
+  if (n < 1) return fail(PGPU_E_UNSUPPORTED, "group dictionary of an empty segment");
+  const int32_t t = r.dict_type;
+  const int w = type_width(t);
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  DevMem keys, sorted, uniq, dcard, temp, ids, fwd, dict;
+  const size_t tb = pgpu_gdict_temp_bytes(n);
+  HIP_TRY(keys.alloc(8 * (size_t)n));
+  HIP_TRY(sorted.alloc(8 * (size_t)n));
+  HIP_TRY(uniq.alloc(8 * (size_t)n));
+  HIP_TRY(dcard.alloc(16));
+  HIP_TRY(temp.alloc(tb));
+  HIP_TRY(pgpu_gdict_sort_unique(r.dict.p, t, n, (uint64_t*)keys.p, (uint64_t*)sorted.p, (uint64_t*)uniq.p,
+                                 (uint32_t*)dcard.p, temp.p, tb, nullptr));
+  uint32_t card = 0;
+  HIP_TRY(hipMemcpy(&card, dcard.p, 4, hipMemcpyDeviceToHost));
+  if (card < 1 || (int64_t)card > n) return fail(PGPU_E_INVALID, "group dictionary of column %d: cardinality %u", raw_column, card);
+  sorted.reset();
+  temp.reset();
+  int bits = 1;  // PinotDataBitSet.getNumBitsPerValue(card - 1)
+  while (bits < 31 && (1ll << bits) < (int64_t)card) ++bits;
+  const uint64_t ntiles = ((uint64_t)n + PGPU_TILE - 1) / PGPU_TILE;
+  const uint64_t need = ((uint64_t)n * bits + 7) / 8;
+  const uint64_t alloc = std::max<uint64_t>(ntiles * PGPU_TILE / 8 * bits, need) + 16;
+  HIP_TRY(fwd.alloc(alloc));
+  HIP_TRY(hipMemset(fwd.p, 0, alloc));
+  HIP_TRY(ids.alloc(4 * (size_t)n));
+  HIP_TRY(dict.alloc((size_t)w * card));
+  const int64_t nwords = (int64_t)((need + 3) / 4);
+  HIP_TRY(pgpu_gdict_encode((const uint64_t*)keys.p, n, (const uint64_t*)uniq.p, (int32_t)card, t, bits, dict.p,
+                            (uint32_t*)ids.p, (uint32_t*)fwd.p, nwords, nullptr));
+  std::vector<uint8_t> le((size_t)w * card);
+  HIP_TRY(hipMemcpy(le.data(), dict.p, le.size(), hipMemcpyDeviceToHost));
+  double max_abs = 0;
+  for (uint32_t i = 0; i < card && (t == PGPU_INT || t == PGPU_LONG); ++i) {
+    int64_t v;
+    if (w == 4) { int32_t x; memcpy(&x, &le[4 * (size_t)i], 4); v = x; }
+    else memcpy(&v, &le[8 * (size_t)i], 8);
+    max_abs = std::max(max_abs, std::fabs((double)v));
+  }
+  c.dict = std::move(dict);
+  c.fwd = std::move(fwd);
+  c.dict_type = t;
+  c.dict_card = (int32_t)card;
+  c.dict_bytes = le.size();
+  c.kind = PGPU_COL_FIXED_BIT;
+  c.bits = bits;
+  c.fwd_card = (int32_t)card;
+  c.fwd_bytes = need;
+  c.max_abs = max_abs;
+  dictionary_hash(le, c.dict_hash);
+  c.hdict = std::move(le);
+  if (seg->sealed) {
+    const int rc = seal_column(seg, (size_t)dict_column);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  *out_cardinality = (int32_t)card;
+  return PGPU_OK;
+}
+
+int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void* out, uint64_t capacity_bytes,
+                                   uint64_t* out_bytes) {
+  if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
+  if (column < 0 || column >= (int32_t)seg->cols.size()) return fail(PGPU_E_INVALID, "bad column %d", column);
+  const HostColumn& c = seg->cols[column];
+  if (c.hdict.empty()) return fail(PGPU_E_INVALID, "column %d has no numeric dictionary", column);
+  *out_bytes = c.hdict.size();
+  if (!out) return PGPU_OK;
+  if (capacity_bytes < c.hdict.size()) return fail(PGPU_E_INVALID, "dictionary of column %d: %zu bytes > capacity", column,
+                                                   c.hdict.size());
+  memcpy(out, c.hdict.data(), c.hdict.size());
   return PGPU_OK;
 }
 
@@ -2071,7 +2186,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // candidate gathers' latency
   bool index_only = true;
   for (const DevSeg& ds : pk.segs) index_only &= ds.ntiles == 0 || (ds.nstage == 0 && ds.fast == 0);
-  if (!no_direct && !p.dense && p.mode != PGPU_MODE_PART && (pk.tile_bytes > 0 || index_only)) {
+  // (multi-value group keys expand per candidate in the ring kernel only: sparse_agg<MODE, MV>)
+  if (!no_direct && !p.dense && p.mode != PGPU_MODE_PART && !p.mv_gmask && (pk.tile_bytes > 0 || index_only)) {
     bool ok = true;
     for (const DevSeg& ds : pk.segs)
       ok &= ds.ntiles == 0 || ((ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&

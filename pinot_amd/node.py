@@ -16,17 +16,17 @@ import numpy as np
 from . import _lib
 from ._lib import QueryDesc, QueryStats, TableLayout
 from .plan import (ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, check_group_columns, finish,
-                   has_mv_aggregations, key_words_out, mv_lower, mv_raise)
+                   has_mv_aggregations, key_words_out, mv_lower, mv_raise, union_sorted)
 from .query import QueryContext
 from .segment import GpuContext, GpuSegment
 
 
 def union_dictionary(column: str, segments: Sequence[GpuSegment]):
     """Sorted union of the segments' dictionaries of one group column (host data only)."""
-    dicts = [s.dictionaries[column] for s in segments]
+    dicts = [s.dictionaries[s.group_view(column)] for s in segments]
     if isinstance(dicts[0], list):
         return sorted(set().union(*[set(d) for d in dicts]))
-    return np.unique(np.concatenate([np.asarray(d) for d in dicts]))
+    return union_sorted(dicts)
 
 
 class GpuNode:

@@ -265,13 +265,8 @@ def emit_program(op: FilterOp, col_index: Dict[str, int], nodes: list, ids: list
 
 
 def check_group_columns(query: QueryContext, segments: Sequence[GpuSegment]) -> None:
-    """GROUP BY on a raw (no-dictionary) column is the reference's NoDictionary*GroupKeyGenerator (a value-hash
-    path): not run on the GPU."""
-    for g in query.group_by:
-        for s in segments:
-            if s.column(g).is_raw:
-                raise UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
-                                           f"GROUP BY on raw (no-dictionary) column {g!r} of segment {s.name}")
+    """Aggregation functions must match their columns' arity (*MV functions on multi-value columns only).  GROUP BY
+    on a raw (no-dictionary) column reads its on-the-fly group dictionary (GpuSegment.group_view)."""
     for a in query.aggregations:
         if a.column is None or not segments:
             continue
@@ -429,6 +424,29 @@ def to_select_order(query: QueryContext, row: tuple) -> tuple:
     return tuple(out)
 
 
+def order_key(v: np.ndarray) -> np.ndarray:
+    """Sort / equality key of dictionary values: the values themselves, or for FLOAT / DOUBLE their bits as an
+    order-preserving int64 (Float.compare order: -0.0 before 0.0, one NaN last) -- the identity of a map key in the
+    reference's no-dictionary group-key generators (floatToIntBits / doubleToLongBits)."""
+    v = np.asarray(v)
+    if v.dtype.kind != "f":
+        return v
+    if v.dtype == np.float32:
+        b = np.where(np.isnan(v), np.int32(0x7FC00000), v.view(np.int32)).astype(np.int64)
+        return np.where(b >= 0, b, b ^ np.int64(0x7FFFFFFF))
+    b = np.where(np.isnan(v), np.int64(0x7FF8000000000000), v.view(np.int64))
+    return np.where(b >= 0, b, b ^ np.int64(0x7FFFFFFFFFFFFFFF))
+
+
+def union_sorted(parts: Sequence[np.ndarray]) -> np.ndarray:
+    """Sorted union of numeric dictionaries; FLOAT / DOUBLE values distinct by bits (order_key)."""
+    allv = np.concatenate([np.asarray(p) for p in parts]) if len(parts) else np.zeros(0)
+    if allv.dtype.kind != "f":
+        return np.unique(allv)
+    _, idx = np.unique(order_key(allv), return_index=True)
+    return allv[idx]
+
+
 def dictionary_digest(glob) -> str:
     """Content digest of a global dictionary: remap tables are cached per (segment, column, digest), so two
     different global dictionaries of the same length never share one."""
@@ -489,18 +507,21 @@ class GpuPlanMaker:
 
     # -- global group dictionaries --
     def global_dictionary(self, column: str, segments: Sequence[GpuSegment]):
-        """Global dictionary of a group column (sorted union of the segments' dictionaries unless a wider one was
-        installed by set_global_dictionary) and per-segment remap buffers (None = identity)."""
+        """Global dictionary of a group column (sorted union of the segments' dictionaries -- a raw column's
+        on-the-fly group dictionaries -- unless a wider one was installed by set_global_dictionary) and per-segment
+        remap buffers (None = identity)."""
         key = (column, tuple(s.uid for s in segments))
         hit = self._global_dicts.get(key)
         if hit is not None:
             return hit[:2]
-        dicts = [s.dictionaries[column] for s in segments]
+        dicts = [s.dictionaries[s.group_view(column)] for s in segments]
         first = dicts[0]
         if isinstance(first, list):
             glob = sorted(set().union(*[set(d) for d in dicts]))
+        elif len(dicts) == 1:
+            glob = np.asarray(first)
         else:
-            glob = np.unique(np.concatenate(dicts)) if len(dicts) > 1 else np.asarray(first)
+            glob = union_sorted(dicts)
         return self.set_global_dictionary(column, segments, glob)
 
     def set_global_dictionary(self, column: str, segments: Sequence[GpuSegment], glob):
@@ -511,14 +532,17 @@ class GpuPlanMaker:
         if isinstance(glob, list):
             pos = {v: i for i, v in enumerate(glob)}
         for s in segments:
-            d = s.dictionaries[column]
-            if len(d) == len(glob) and (list(d) == list(glob) if isinstance(d, list) else np.array_equal(d, glob)):
+            d = s.dictionaries[s.group_view(column)]
+            if not isinstance(glob, list):
+                d = np.asarray(d, dtype=glob.dtype)  # exact widening (FLOAT -> DOUBLE keeps -0.0 and NaN)
+            if len(d) == len(glob) and (list(d) == list(glob) if isinstance(d, list) else
+                                        np.array_equal(order_key(d), order_key(glob))):
                 remaps.append(None)
                 continue
             if isinstance(glob, list):
                 t = np.array([pos[v] for v in d], dtype=np.int32)
             else:
-                t = np.searchsorted(glob, d).astype(np.int32)
+                t = np.searchsorted(order_key(glob), order_key(d)).astype(np.int32)
             remaps.append(self.ctx.remap((s.uid, column, digest), t))
             rkeys.append((s.uid, column, digest))
         if key in self._global_dicts:
@@ -599,11 +623,25 @@ class GpuPlanMaker:
         points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array).
         plan_filters=False leaves the per-segment filter programs empty (the library plans them from
         filter_expr)."""
-        columns = query.columns
+        columns = list(query.columns)
         col_index = {c: i for i, c in enumerate(columns)}
         nseg = len(segments)
         check_group_columns(query, segments)
         globals_ = [self.global_dictionary(g, segments) for g in query.group_by]
+        # a group column that is raw (no-dictionary) in some segment is read through its on-the-fly group dictionary
+        # there (GpuSegment.group_view): one more descriptor column per such group column, mapped per segment, so
+        # that filters and aggregations on the same column keep reading its values
+        group_col = {}
+        views: Dict[int, str] = {}
+        no_dict = False
+        for g in query.group_by:
+            if any(s.column(g).is_raw for s in segments):
+                no_dict = True
+                views[len(columns)] = g
+                group_col[g] = len(columns)
+                columns.append(f"{g}$group")
+            else:
+                group_col[g] = col_index[g]
         nodes: list = []
         ids: list = []
         vals: list = []
@@ -612,7 +650,8 @@ class GpuPlanMaker:
         flt = query.filter if plan_filters else None
         for seg in segments:
             slots = seg.slots
-            cmaps.append([slots[c] for c in columns] if columns else [0])
+            cmaps.append([slots[seg.group_view(views[i])] if i in views else slots[c] for i, c in enumerate(columns)]
+                         if columns else [0])
             starts.append(len(nodes))
             if flt is not None:
                 op = SegmentFilterPlanner(seg).build(flt)
@@ -644,7 +683,7 @@ class GpuPlanMaker:
             plans["group_remap"] = remap.ctypes.data + remap.strides[0] * np.arange(nseg, dtype=np.uint64)
         aggs = (Agg * len(query.aggregations))(
             *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
-        gcols = (C.c_int32 * max(1, ng))(*[col_index[g] for g in query.group_by])
+        gcols = (C.c_int32 * max(1, ng))(*[group_col[g] for g in query.group_by])
         gcards = (C.c_int32 * max(1, ng))(*[len(g[0]) for g in globals_])
         keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards]
         desc = QueryDesc(num_columns=len(columns), num_segments=nseg,
@@ -654,7 +693,9 @@ class GpuPlanMaker:
                          flags=(_lib.PGPU_Q_STATS if self.collect_stats else 0) | self.query_flags | extra_flags |
                          (_lib.PGPU_Q_EXACT_FILTER_STATS if self.exact_filter_stats else 0),
                          reduce_docs=reduce_docs, num_groups_limit=self.num_groups_limit,
-                         array_based_threshold=self.max_init_group_holder_capacity,
+                         # NoDictionary*GroupKeyGenerator caps every key space at numGroupsLimit: with a raw group
+                         # column no segment is array-based (a segment meeting more keys goes back to the CPU)
+                         array_based_threshold=0 if no_dict else self.max_init_group_holder_capacity,
                          deadline_ms=0 if self.timeout_ms is None else int(time.time() * 1000) + int(self.timeout_ms))
         return desc, keep, globals_
 

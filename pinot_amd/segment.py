@@ -225,6 +225,11 @@ def mv_row_column(column: str, kind: str) -> str:
     return f"{column}$mv{kind}"
 
 
+def group_dict_column(column: str) -> str:
+    """Slot name of a raw column's on-the-fly group dictionary (GpuSegment.group_view)."""
+    return f"{column}$gdict"
+
+
 class GpuSegment:
     """An immutable segment resident in HBM plus the host-side dictionaries used for predicate evaluation.
 
@@ -244,12 +249,15 @@ class GpuSegment:
         # multi-value columns' per-row reductions (mv_row_columns): raw columns of their own slots
         self.derived: Dict[str, ColumnIndexes] = {}
         nmv = 0 if _incremental else sum(1 for n in names if data.column(n).is_mv)
+        # one spare slot per raw column for its on-the-fly group dictionary (group_view), filled on first use
+        nraw = 0 if _incremental else sum(1 for n in names if data.column(n).is_raw)
         lib = ctx._lib
         h = C.c_void_p()
-        _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, len(names) + len(MV_ROW_COLUMNS) * nmv,
-                                           C.byref(h)))
+        nslots = len(names) + len(MV_ROW_COLUMNS) * nmv + nraw
+        _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, nslots, C.byref(h)))
         self.handle = h
-        self._capacity = len(names) + len(MV_ROW_COLUMNS) * nmv
+        self._capacity = nslots
+        self._gdict_free = list(range(nslots - nraw, nslots))  # spare slots (after every column's own)
         if _incremental:
             return
         try:
@@ -337,6 +345,35 @@ class GpuSegment:
             _lib.check(lib.pgpu_segment_add_inverted_index(seg, slot, inv, len(inv), card))
         if col.range_index is not None:
             _lib.check(lib.pgpu_segment_add_range_index(seg, slot, col.range_index, len(col.range_index)))
+
+    def group_view(self, name: str) -> str:
+        """The column a GROUP BY on `name` reads in this segment: the column itself when it is dictionary-encoded;
+        for a raw (no-dictionary) column its on-the-fly group dictionary (pgpu_segment_add_group_dictionary: the
+        distinct values as a sorted dictionary + a fixed-bit id per doc, built on the GPU on first use and kept
+        with the segment), the analogue of NoDictionary*GroupKeyGenerator's value -> id maps."""
+        col = self.column(name)
+        if not col.is_raw:
+            return name
+        gname = group_dict_column(name)
+        if gname in self.slots:
+            return gname
+        if not self._gdict_free:
+            raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                            f"no spare slot for the group dictionary of raw column {name!r}")
+        slot = self._gdict_free.pop(0)
+        lib = self.ctx._lib
+        card = C.c_int32()
+        _lib.check(lib.pgpu_segment_add_group_dictionary(self.handle, self.slots[name], slot, C.byref(card)))
+        nb = C.c_uint64()
+        _lib.check(lib.pgpu_segment_dictionary_values(self.handle, slot, None, 0, C.byref(nb)))
+        buf = np.empty(nb.value, dtype=np.uint8)
+        _lib.check(lib.pgpu_segment_dictionary_values(self.handle, slot, buf.ctypes.data, nb.value, C.byref(nb)))
+        vals = buf.view(_NATIVE[col.data_type]).copy()
+        self.slots[gname] = slot
+        self.dictionaries[gname] = vals
+        self.derived[gname] = ColumnIndexes(gname, col.data_type, card.value,
+                                            dictionary=vals.astype(_BE_DTYPE[col.data_type]).tobytes())
+        return gname
 
     def column(self, name: str) -> ColumnIndexes:
         c = self.derived.get(name)

@@ -32,6 +32,9 @@ class _Seg:
         self.ctx, self.uid = ctx, next(_uid)
         self.dictionaries = {"k": np.unique(rng.integers(0, 1000, 50)).astype(np.int32)}
 
+    def group_view(self, name):
+        return name
+
     def release(self):
         self.ctx.segment_released(self.uid)
 

@@ -68,6 +68,9 @@ class HostSegment:
     def column(self, name):
         return self.data.column(name)
 
+    def group_view(self, name):
+        return name  # dictionary-encoded columns only (no device to build an on-the-fly group dictionary)
+
     def sorted_dictionary(self, name):
         return self._gs.sorted_dictionary(self, name)
 

@@ -193,15 +193,92 @@ def test_gpu_raw_aggregation_group_modes(gpu_ctx, flags):
     _gpu_vs_oracle(gpu_ctx, segs, "SELECT d, k, SUM(ri), COUNT(*) FROM t GROUP BY d, k", query_flags=qf)
 
 
+GROUP_RAW = [
+    "SELECT ri, COUNT(*), SUM(rd) FROM t GROUP BY ri",
+    "SELECT rf, COUNT(*), MAX(ri), SUM(ri) FROM t WHERE d < 25 GROUP BY rf",
+    "SELECT rl, SUM(rl), MIN(rd) FROM t WHERE ri BETWEEN -50 AND 50 GROUP BY rl",
+    "SELECT k, ri, COUNT(*), SUM(rf) FROM t WHERE rd > 0 GROUP BY k, ri",
+    "SELECT ri, d, COUNT(*) FROM t GROUP BY ri, d ORDER BY COUNT(*) DESC, ri, d LIMIT 20",
+]
+
+
+@pytest.mark.parametrize("sql", GROUP_RAW)
+def test_oracle_group_by_raw_equals_dictionary_encoded(sql):
+    """NoDictionary*GroupKeyGenerator keys by value: the same groups as the dictionary-encoded twin below the
+    numGroupsLimit (at it, the no-dictionary generators cap every key space -- test_oracle_group_by_raw_limit)."""
+    segs, dense = _segments(73, [3000, 2500])
+    q = parse_sql(sql)
+    a, b = engine.execute(q, segs), engine.execute(q, dense)
+    assert a.num_docs_scanned == b.num_docs_scanned
+    assert rows_close(sorted(a.group_rows), sorted(b.group_rows))
+
+
+def test_oracle_group_by_raw_float_keys():
+    """FLOAT / DOUBLE group keys are Float.floatToIntBits / Double.doubleToLongBits: -0.0 and 0.0 are two groups,
+    every NaN one (fastutil Float2IntOpenHashMap / Double2IntOpenHashMap)."""
+    n = 12
+    vals = np.array([0.0, -0.0, 1.5, np.nan, -0.0, np.float32(np.nan), 1.5, 0.0, -2.0, np.nan, 3.0, 0.0],
+                    dtype=np.float32)
+    vals[5] = np.frombuffer(np.uint32(0x7FC00001).tobytes(), dtype=np.float32)[0]  # a second NaN pattern
+    cols = {"d": (PGPU_INT, np.arange(n) % 3), "rf": (PGPU_FLOAT, vals)}
+    seg = build_segment("f", cols, raw=("rf",), sorted_columns=())
+    r = engine.execute_segment(parse_sql("SELECT rf, COUNT(*) FROM t GROUP BY rf"), seg)
+    got = {}
+    for k, v in r.groups.items():
+        got[np.float32(k[0]).tobytes() if not np.isnan(k[0]) else b"nan"] = v[0]
+    assert got[np.float32(0.0).tobytes()] == 3 and got[np.float32(-0.0).tobytes()] == 2
+    assert got[b"nan"] == 3 and got[np.float32(1.5).tobytes()] == 2 and len(got) == 6
+
+
+def test_oracle_group_by_raw_limit():
+    """A raw group column caps the segment's groups at numGroupsLimit, first seen in doc order, whatever the key
+    space (NoDictionarySingleColumnGroupKeyGenerator.java:199-235) -- a dictionary column of the same cardinality
+    below maxInitialResultHolderCapacity would not."""
+    n = 500
+    cols = {"ri": (PGPU_INT, (np.arange(n) * 7919) % 97), "d": (PGPU_INT, np.arange(n) % 5)}
+    raw = build_segment("r", cols, raw=("ri",), sorted_columns=())
+    dense = build_segment("r", cols, sorted_columns=())
+    q = parse_sql("SELECT ri, COUNT(*) FROM t GROUP BY ri")
+    a = engine.execute_segment(q, raw, num_groups_limit=10, max_init_group_holder_capacity=10_000)
+    b = engine.execute_segment(q, dense, num_groups_limit=10, max_init_group_holder_capacity=10_000)
+    first = list(dict.fromkeys(((np.arange(n) * 7919) % 97).tolist()))[:10]
+    assert sorted(k[0] for k in a.groups) == sorted(first)
+    assert len(b.groups) == 97
+
+
 @pytest.mark.gpu
-def test_gpu_group_by_raw_column_unsupported(gpu_ctx):
+@pytest.mark.parametrize("qi", range(len(GROUP_RAW)))
+@pytest.mark.parametrize("flags", ["default", "hash", "partition"])
+def test_gpu_group_by_raw_vs_oracle(gpu_ctx, qi, flags):
+    """GROUP BY on raw columns through their on-the-fly group dictionaries (pgpu_segment_add_group_dictionary), one
+    segment holding the column dictionary-encoded beside raw ones."""
+    from pinot_amd import _lib
+    qf = {"partition": _lib.PGPU_Q_PARTITION, "hash": _lib.PGPU_Q_HASH, "default": 0}[flags]
+    segs, dense = _segments(75 + qi, [5000, 70000, 2049])
+    _gpu_vs_oracle(gpu_ctx, segs[:2] + dense[2:], GROUP_RAW[qi], query_flags=qf)
+
+
+@pytest.mark.gpu
+def test_gpu_group_by_raw_float_keys_and_limit(gpu_ctx):
+    """-0.0 / 0.0 apart and NaNs as one group on the GPU too; a segment meeting more raw keys than numGroupsLimit goes
+    back to the CPU plan (PGPU_E_UNSUPPORTED), as the reference would truncate it."""
     from pinot_amd.plan import GpuPlanMaker
     from pinot_amd.segment import GpuSegment
-    segs, _ = _segments(71, [1000])
-    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    rng = np.random.default_rng(77)
+    n = 9000
+    vals = rng.choice(np.array([0.0, -0.0, 1.5, np.nan, -2.25, 7.0], dtype=np.float64), n)
+    cols = {"d": (PGPU_INT, rng.integers(0, 9, n)), "rd": (PGPU_DOUBLE, vals), "ri": (PGPU_INT, rng.integers(0, 500, n))}
+    seg = build_segment("f", cols, raw=("rd", "ri"), sorted_columns=())
+    gs = [GpuSegment(gpu_ctx, seg)]
     try:
+        q = parse_sql("SELECT rd, COUNT(*), SUM(d) FROM t GROUP BY rd")
+        res = GpuPlanMaker(gpu_ctx).execute(q, gs)
+        ref = engine.execute_segment(q, seg)
+        got = {np.float64(r[0]).tobytes() if not np.isnan(r[0]) else b"nan": tuple(r[1:]) for r in res.group_rows}
+        exp = {np.float64(k[0]).tobytes() if not np.isnan(k[0]) else b"nan": (v[0], v[1]) for k, v in ref.groups.items()}
+        assert len(got) == 6 and got == exp
         with pytest.raises(UnsupportedPlanError):
-            GpuPlanMaker(gpu_ctx).execute(parse_sql("SELECT ri, COUNT(*) FROM t GROUP BY ri"), gs)
+            GpuPlanMaker(gpu_ctx, num_groups_limit=100).execute(parse_sql("SELECT ri, COUNT(*) FROM t GROUP BY ri"), gs)
     finally:
         for g in gs:
             g.release()
