@@ -794,8 +794,7 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
         prod *= c
     # NoDictionarySingleColumnGroupKeyGenerator / NoDictionaryMultiColumnGroupKeyGenerator (any raw group column):
     # a value -> id map capped at numGroupsLimit whatever the key space (:199-235 / :295-330)
-    raw_group = [ds.seg.column(g).raw_forward is not None for g in query.group_by]
-    no_dict = any(raw_group)
+    no_dict = any(ds.seg.column(g).raw_forward is not None for g in query.group_by)
     idmat = np.stack([ids[docs].astype(np.int64) for ids, _ in gsrc], axis=1) if len(docs) else \
         np.zeros((0, len(cards)), dtype=np.int64)
     uniq, first, inv = (np.unique(idmat, axis=0, return_index=True, return_inverse=True) if len(docs)
@@ -818,7 +817,7 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
         for j, d in enumerate(dicts):
             v = d[int(uniq[part_g[0], j])]
             v = v.item() if hasattr(v, "item") else v
-            vals.append(JavaFloatKey(v) if isinstance(v, float) and raw_group[j] else v)
+            vals.append(JavaFloatKey(v) if isinstance(v, float) else v)
         groups[tuple(vals)] = [aggregate(a.function, None if a.column is None else
                                          _as_float_values(ds, a.column, part_docs, a.function), len(part_docs))
                                for a in query.aggregations]
@@ -839,8 +838,9 @@ def float_bits_key(v: np.ndarray) -> np.ndarray:
 
 
 class JavaFloatKey(float):
-    """A FLOAT / DOUBLE group value compared and hashed as the reference's map keys are: by floatToIntBits /
-    doubleToLongBits (-0.0 != 0.0, NaN == NaN), so that Python dicts keep -0.0 and 0.0 as two groups."""
+    """A FLOAT / DOUBLE group value compared as the broker's group keys are (Float.equals / Double.equals: by
+    floatToIntBits / doubleToLongBits, so -0.0 != 0.0 and NaN == NaN), so that Python dicts keep -0.0 and 0.0 as two
+    groups and merge NaNs.  Hashes agree with plain floats' (NaN: one constant)."""
 
     def _bits(self):
         return b"nan" if math.isnan(self) else struct.pack(">d", self)
@@ -852,7 +852,7 @@ class JavaFloatKey(float):
         return not self.__eq__(other)
 
     def __hash__(self):
-        return hash(JavaFloatKey._bits(self))
+        return 0x7FF8 if math.isnan(self) else hash(float(self))
 
 
 def _raw_group_ids(ds: DecodedSegment, col: str):

@@ -2603,10 +2603,10 @@ FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, u
 // `final`).  A lane first settles its partition's range [H, E) and head.  Whole lines below the region's end go
 // out eight partitions per step: 8 lanes per line, one 16-B ds_read_b128 / global_store_dwordx4 each, offsets in
 // 32 bits from the workgroup's region block.  The rest -- a line's head or tail piece (after a ring overflow, and
-// at the end) and records past a full region -- take a per-record walk, two partitions per step.
+// at the end) and records past a full region -- are walked one flagged partition at a time.
 FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring,
                     const uint32_t* lcap, const uint32_t* loff, uint32_t RC, int wave, bool final) {
-  const int lane = lane_id(), np = p.nparts, half = lane >> 5, j = lane & 31, g = lane >> 3, sub = lane & 7;
+  const int lane = lane_id(), np = p.nparts, g = lane >> 3, sub = lane & 7;
   const uint32_t rw = (uint32_t)p.rw, lsh = rw == 1 ? 5u : 4u, line = 1u << lsh;  // records per 128-B line
   uint32_t* wrec = p.recs + (size_t)blockIdx.x * p.pblock * rw;  // this workgroup's block (part_base)
   for (int qb = wave * 64; qb < np; qb += 64 * PGPU_PSCAN_WAVES) {
@@ -2644,35 +2644,43 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
         *(u32x4*)(wrec + (of + s) * rw + 4 * sub) = v;
       }
     }
-    if (!__ballot(rest)) continue;
-    // head / tail pieces and records past the region's end: lane j of a half takes dword j of a line
-    bool spill = false;
-    for (int pp = 0; pp < 32; ++pp) {
-      const int src = 2 * pp + half;
-      const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
-      const uint32_t lo = (uint32_t)__shfl((int)FL, src, 64) << lsh, hi = (uint32_t)__shfl((int)LL, src, 64) << lsh;
-      const uint32_t cp = (uint32_t)__shfl((int)cap, src, 64), of = (uint32_t)__shfl((int)off, src, 64);
+    // head / tail pieces and records past the region's end, one flagged partition at a time (a ring overflows in a
+    // few partitions per step: walking every partition here cost half of phase 1): its values in SGPRs, lane l takes
+    // dword l of the 256 bytes from the piece's first line on
+    uint64_t todo = __ballot(rest);
+    uint64_t spill = 0;
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)H, src);
+      const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)E, src);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)FL, src) << lsh;
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)LL, src) << lsh;
+      const uint32_t cp = (uint32_t)__builtin_amdgcn_readlane((int)cap, src);
+      const uint32_t of = (uint32_t)__builtin_amdgcn_readlane((int)off, src);
       const uint32_t qq = (uint32_t)(qb + src);
-      for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
-        const uint32_t s = s0 + j / rw;
+      bool full = false;
+      for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += 64u / rw) {
+        const uint32_t s = s0 + (uint32_t)lane / rw;
         if (s < h || s >= e || (s >= lo && s < hi)) continue;
-        if (s < cp) wrec[(of + s) * rw + (j & (rw - 1))] = ring[(qq * RC + (s & (RC - 1))) * rw + (j & (rw - 1))];
-        else spill = true;
+        if (s < cp) wrec[(of + s) * rw + (lane & (rw - 1))] = ring[(qq * RC + (s & (RC - 1))) * rw + (lane & (rw - 1))];
+        else full = true;
       }
+      if (__ballot(full)) spill |= 1ull << src;
     }
-    // region full (rare): the same walk again, HBM-table atomics for the records past the region's end
-    if (__ballot(spill)) {
-      for (int pp = 0; pp < 32; ++pp) {
-        const int src = 2 * pp + half;
-        const uint32_t h = (uint32_t)__shfl((int)H, src, 64), e = (uint32_t)__shfl((int)E, src, 64);
-        const uint32_t cp = (uint32_t)__shfl((int)cap, src, 64);
-        const uint32_t qq = (uint32_t)(qb + src);
-        for (uint32_t s0 = h & ~(line - 1u); s0 < e; s0 += line) {
-          const uint32_t s = s0 + j / rw;
-          if (s < h || s >= e || s < cp || (j & (rw - 1))) continue;
-          const uint32_t* r = ring + (qq * RC + (s & (RC - 1))) * rw;
-          pscan_put(p, qq, s, cp, r[0], rw == 2 ? r[1] : 0u);
-        }
+    // region full (rare): the records past the region's end go to the HBM table with atomics
+    while (spill) {
+      const int src = __builtin_ctzll(spill);
+      spill &= spill - 1;
+      const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)H, src);
+      const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)E, src);
+      const uint32_t cp = (uint32_t)__builtin_amdgcn_readlane((int)cap, src);
+      const uint32_t qq = (uint32_t)(qb + src);
+      for (uint32_t s0 = std::max(h, cp); s0 < e; s0 += 64u) {
+        const uint32_t s = s0 + (uint32_t)lane;
+        if (s >= e) continue;
+        const uint32_t* r = ring + (qq * RC + (s & (RC - 1))) * rw;
+        pscan_put(p, qq, s, cp, r[0], rw == 2 ? r[1] : 0u);
       }
       __builtin_amdgcn_s_waitcnt(0);  // nothing of this rare path stays pending into the store loops above
     }

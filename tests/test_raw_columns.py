@@ -209,8 +209,10 @@ def test_oracle_group_by_raw_equals_dictionary_encoded(sql):
     segs, dense = _segments(73, [3000, 2500])
     q = parse_sql(sql)
     a, b = engine.execute(q, segs), engine.execute(q, dense)
-    assert a.num_docs_scanned == b.num_docs_scanned
+    c = engine.execute(q, segs[:1] + dense[1:])  # the column raw in one segment, dictionary-encoded in the other
+    assert a.num_docs_scanned == b.num_docs_scanned == c.num_docs_scanned
     assert rows_close(sorted(a.group_rows), sorted(b.group_rows))
+    assert rows_close(sorted(c.group_rows), sorted(b.group_rows))
 
 
 def test_oracle_group_by_raw_float_keys():
