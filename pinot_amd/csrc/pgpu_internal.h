@@ -141,7 +141,14 @@ struct DevSeg {
   int32_t nbits;
   int32_t pad2_;
   const uint32_t* bits_w[PGPU_PREBITS];
+  // register-direct prefix pre-filter (DevParams::rd_pfx planes): the residual SCAN leaf's query column (-1: none)
+  // and the ranges [lo, hi) of its ids' top rd_pfx bits that can match, OR-ed -- a candidate outside them cannot
+  // match the leaf, so it is never gathered
+  int32_t pfx_col;
+  int32_t pfx_nr;
+  uint32_t pfx_rng[PGPU_SLICE_RANGES][2];
 };
+#define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 
 // Filter instruction with statically resolved mask slots.
 #define PGPU_I_ALL 0
@@ -353,7 +360,7 @@ struct DevParams {
   int32_t cancel_poll;            // self-loading waves: tiles between cancel polls (PGPU_CANCEL_POLL, env override)
   int32_t rd_planes;              // register-direct: planes per tile held in VGPRs (>= every leaf's width; 8/10/12/16)
   int32_t mv_gmask;               // bit g: group column g is multi-value (sparse_agg_mv expands each doc's values)
-  int32_t pad_mv_;
+  int32_t rd_pfx;                 // register-direct: prefix planes of every segment's residual leaf (0 or PGPU_PFX_PLANES)
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

@@ -2315,9 +2315,11 @@ FI void direct_epilogue(const DevParams& p, const Lds& L, const Stats& st, int w
 // streamed 3.8 TB/s (its in-flight bytes are bounded by the LDS slots).  Candidate handling as in direct_consumer.
 // ================================================================================================================
 #define PGPU_RDIRECT_DEPTH 2
-struct RdIssue {  // the issue cursor's segment: its sliced column
+struct RdIssue {  // the issue cursor's segment: its sliced column (and the prefix column's)
   const uint32_t* sliced;
   int bits;
+  const uint32_t* psliced;
+  int pbits;
 };
 FI void rd_load_issue(const DevParams& p, int seg, RdIssue& is) {
   const DevSeg* sg = p.segs + seg;
@@ -2325,6 +2327,9 @@ FI void rd_load_issue(const DevParams& p, int seg, RdIssue& is) {
   const int qc = cld(&sg->stage_col[0]);
   is.sliced = (const uint32_t*)cld(&cols[qc].sliced);
   is.bits = cld(&cols[qc].bits);
+  const int pc = cld(&sg->pfx_col);
+  is.psliced = pc >= 0 ? (const uint32_t*)cld(&cols[pc].sliced) : nullptr;
+  is.pbits = pc >= 0 ? cld(&cols[pc].bits) : 0;
 }
 template <int PL>
 FI void rd_load_tile(const RdIssue& is, int tile_in_seg, uint32_t (&x)[PL]) {
@@ -2332,6 +2337,13 @@ FI void rd_load_tile(const RdIssue& is, int tile_in_seg, uint32_t (&x)[PL]) {
 #pragma unroll
   for (int k = 0; k < PL; ++k)
     x[k] = k < is.bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;  // planes past the width: 0 (inert below)
+}
+// The residual column's top PK planes (plane j of the prefix = bit pbits - PK + j of the id)
+template <int PK>
+FI void rd_load_prefix(const RdIssue& is, int tile_in_seg, uint32_t (&y)[PK]) {
+  const uint32_t* src = is.psliced + ((size_t)tile_in_seg * is.pbits + (is.pbits - PK)) * 64 + lane_id();
+#pragma unroll
+  for (int k = 0; k < PK; ++k) y[k] = __builtin_nontemporal_load(src + 64 * k);
 }
 // The fast leaf on register planes: OR of dict-id ranges [lo, hi) (x < c as a borrow chain; planes past the
 // column's width are 0 and leave the chain unchanged, and c = 2^bits sets the borrow there), then negated.
@@ -2354,8 +2366,22 @@ FI uint32_t rd_filter(const SegState& ss, const uint32_t (&x)[PL], uint32_t vali
   }
   return valid & (ss.f_sneg[0] ? ~m : m);
 }
+// Prefix pre-filter of the candidates `mm`: those whose residual-column id has its top PK bits in a matching range.
+// The rest are rejected here, never gathered; each still counts as one entry the residual leaf scans
+// (SVScanDocIdIterator over the AND's candidates).
+template <int PK>
+FI uint32_t rd_prefix(const SegState& ss, const uint32_t (&y)[PK], uint32_t mm, uint32_t& lane_scanned) {
+  uint32_t pm = 0;
+  const int nr = cld(&ss.sg->pfx_nr);
+  for (int r = 0; r < nr; ++r) {
+    const uint32_t lo = cld(&ss.sg->pfx_rng[r][0]), hi = cld(&ss.sg->pfx_rng[r][1]);
+    pm |= rd_lt(y, hi) & ~rd_lt(y, lo);
+  }
+  lane_scanned += __popc(mm & ~pm);
+  return mm & pm;
+}
 
-template <int MODE, int PL>
+template <int MODE, int PL, int PK>
 FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
   constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH;
   const int64_t t_start = now(pf);
@@ -2386,11 +2412,13 @@ FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
     RdIssue is;
     rd_load_issue(p, ci.seg, is);
     uint32_t x[RD][PL];
+    uint32_t y[RD][PK > 0 ? PK : 1];
 #pragma unroll
     for (int s = 0; s < RD; ++s) {
       if (s < own) {
         if (s > 0 && cursor_advance(p, ci, NW)) rd_load_issue(p, ci.seg, is);
         rd_load_tile(is, ci.tile_in_seg, x[s]);
+        if constexpr (PK > 0) rd_load_prefix<PK>(is, ci.tile_in_seg, y[s]);
       }
     }
     int poll = p.cancel_poll;
@@ -2428,13 +2456,15 @@ FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
           const int ndocs = min(WT, ss.num_docs - doc0);
           const int rem = ndocs - 32 * lane;
           valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
-          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * ss.f_bits[0] + 7) / 8;
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * (ss.f_bits[0] + PK) + 7) / 8;
         }
-        const uint32_t mm = rd_filter(ss, x[s], valid, lane_scanned);
+        uint32_t mm = rd_filter(ss, x[s], valid, lane_scanned);
+        if constexpr (PK > 0) mm = rd_prefix<PK>(ss, y[s], mm, lane_scanned);
         // refill this register slot with the tile RD ahead (its loads overlap this tile's candidate handling)
         if (k + RD < own) {
           if (cursor_advance(p, ci, NW)) rd_load_issue(p, ci.seg, is);
           rd_load_tile(is, ci.tile_in_seg, x[s]);
+          if constexpr (PK > 0) rd_load_prefix<PK>(is, ci.tile_in_seg, y[s]);
         }
         PROF_ADD(pf, PGPU_P_C_FILTER, tf);
         const int64_t ta = now(pf);
@@ -2466,7 +2496,7 @@ FI Stats rdirect_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
   return st;
 }
 
-template <int MODE, int PL>
+template <int MODE, int PL, int PK>
 __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevParams p) {
   constexpr int NT = PGPU_DIRECT_THREADS, NWAVES = PGPU_DIRECT_WAVES;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
@@ -2489,7 +2519,7 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevP
 #pragma unroll
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
-  const Stats st = rdirect_consumer<MODE, PL>(p, L, wave, t0, t1 - t0, pf);
+  const Stats st = rdirect_consumer<MODE, PL, PK>(p, L, wave, t0, t1 - t0, pf);
   direct_epilogue<MODE>(p, L, st, wave, lane, pf);
 }
 
@@ -3411,10 +3441,31 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
 }  // namespace
 
 // ---- host-side launch helpers (called by pgpu_runtime.cpp) --------------------------------------------------------
-template <int M, int PL>
+template <int M, int PL, int PK>
 static hipError_t rd_attr(size_t lds_bytes) {
-  return hipFuncSetAttribute((const void*)query_kernel_rdirect<M, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  return hipFuncSetAttribute((const void*)query_kernel_rdirect<M, PL, PK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds_bytes);
+}
+// (the prefix variants stop at 12 planes: 16 + 3 planes per tile in flight would pass 128 VGPRs -- one wave per
+// SIMD less -- so the runtime sets rd_pfx only for fast leaves of <= 12 bits)
+template <int M, int PK>
+static void rd_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+  if (p.rd_planes <= 8)
+    hipLaunchKernelGGL((query_kernel_rdirect<M, 8, PK>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);
+  else if (p.rd_planes <= 10)
+    hipLaunchKernelGGL((query_kernel_rdirect<M, 10, PK>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);
+  else if (PK > 0 || p.rd_planes <= 12)
+    hipLaunchKernelGGL((query_kernel_rdirect<M, 12, PK>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);
+  else
+    hipLaunchKernelGGL((query_kernel_rdirect<M, 16, 0>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);
+}
+template <int M, int PK>
+static hipError_t rd_attrs(size_t lds_bytes) {
+  hipError_t e = rd_attr<M, 8, PK>(lds_bytes);
+  if (e == hipSuccess) e = rd_attr<M, 10, PK>(lds_bytes);
+  if (e == hipSuccess) e = rd_attr<M, 12, PK>(lds_bytes);
+  if (e == hipSuccess && PK == 0) e = rd_attr<M, 16, 0>(lds_bytes);
+  return e;
 }
 // Per aggregation mode (one translation unit each): launch the ring or direct query kernel, set its LDS attribute.
 #define PGPU_MODE_FUNCS(M, NAME)                                                                                  \
@@ -3425,14 +3476,8 @@ static hipError_t rd_attr(size_t lds_bytes) {
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
     if (p.direct == 2) {                                                                                        \
-      if (p.rd_planes <= 8)                                                                                     \
-        hipLaunchKernelGGL((query_kernel_rdirect<M, 8>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
-      else if (p.rd_planes <= 10)                                                                               \
-        hipLaunchKernelGGL((query_kernel_rdirect<M, 10>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
-      else if (p.rd_planes <= 12)                                                                               \
-        hipLaunchKernelGGL((query_kernel_rdirect<M, 12>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
-      else                                                                                                      \
-        hipLaunchKernelGGL((query_kernel_rdirect<M, 16>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p); \
+      if (p.rd_pfx) rd_launch<M, PGPU_PFX_PLANES>(p, grid, dyn_smem, st);                                       \
+      else rd_launch<M, 0>(p, grid, dyn_smem, st);                                                              \
     } else                                                                                                      \
       hipLaunchKernelGGL((query_kernel_direct<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);     \
     return hipGetLastError();                                                                                   \
@@ -3446,10 +3491,8 @@ static hipError_t rd_attr(size_t lds_bytes) {
     if (e == hipSuccess)                                                                                        \
       e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                               (int)lds_bytes);                                                                  \
-    if (e == hipSuccess) e = rd_attr<M, 8>(lds_bytes);                                                          \
-    if (e == hipSuccess) e = rd_attr<M, 10>(lds_bytes);                                                         \
-    if (e == hipSuccess) e = rd_attr<M, 12>(lds_bytes);                                                         \
-    if (e == hipSuccess) e = rd_attr<M, 16>(lds_bytes);                                                         \
+    if (e == hipSuccess) e = rd_attrs<M, 0>(lds_bytes);                                                         \
+    if (e == hipSuccess) e = rd_attrs<M, PGPU_PFX_PLANES>(lds_bytes);                                           \
     return e;                                                                                                   \
   }
 #define PGPU_MODE_DECLS(NAME)                                                                   \

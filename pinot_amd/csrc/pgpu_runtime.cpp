@@ -1718,6 +1718,60 @@ constexpr double kDenseTouch = 0.5;
 constexpr double kDenseAggTouch = 0.95;
 constexpr int kMaxSlotBytes = 27 * 1024;  // keeps >= 3 ring slots next to the consumer areas
 
+// Prefix pre-filter for the register-direct kernel (DevSeg::pfx_*): when the residual program is one SCAN leaf on a
+// fixed-bit column with a bit-sliced copy, the top PGPU_PFX_PLANES planes of that column can be streamed beside the
+// fast leaf, and a candidate whose id's top bits fall outside every matching id run is rejected without its
+// gather.  Each gather moves a whole 128-B line (tools/gather_policy_bench.hip: ~50 G random 4-B loads/s = 6.5 TB/s
+// of lines, whatever the cache policy), a plane 256 B per 2048-doc tile: worth it when the candidates per tile x
+// 128 B x the rejected share exceed the planes' bytes.  Config 5 (16 candidates per tile, accountId EQ): 4.6 ->
+// 3.6 KB of DRAM traffic per tile.
+void plan_prefix(const SegView& v, const Packer& pk, double rho_dense, DevSeg& ds) {
+  ds.pfx_col = -1;
+  ds.pfx_nr = 0;
+  for (int r = 0; r < PGPU_SLICE_RANGES; ++r) ds.pfx_rng[r][0] = ds.pfx_rng[r][1] = 0;
+  static const bool no_pfx = getenv("PGPU_NO_PREFIX") && atoi(getenv("PGPU_NO_PREFIX")) != 0;
+  if (no_pfx || ds.rprog_len != 1) return;
+  const DevInstr& in = pk.instrs[ds.rprog_begin];
+  if (in.op != PGPU_I_SCAN || in.kind != PGPU_COL_FIXED_BIT || in.negate || in.nostat) return;
+  const DevColumn* dc = v.dev(in.col);
+  const int K = PGPU_PFX_PLANES;
+  if (!dc->sliced || dc->bits <= K || dc->bits > 31) return;
+  std::vector<std::pair<uint64_t, uint64_t>> runs;  // matching ids [a, b)
+  if (in.pred == 0) {
+    if (in.hi > in.lo) runs.emplace_back((uint64_t)(uint32_t)in.lo, (uint64_t)(uint32_t)in.hi);
+  } else if (in.pred == 2) {
+    for (int k = 0; k < 8; ++k)
+      if (in.ids[k] != 0xFFFFFFFFu) runs.emplace_back((uint64_t)in.ids[k], (uint64_t)in.ids[k] + 1);
+  } else if (in.pred == 3) {
+    const uint64_t mask = (uint64_t)(uint32_t)in.lo | ((uint64_t)(uint32_t)in.hi << 32);
+    for (int i = 0; i < 64; ++i)
+      if ((mask >> i) & 1u) runs.emplace_back((uint64_t)i, (uint64_t)i + 1);
+  } else {
+    return;
+  }
+  const int sh = dc->bits - K;
+  std::vector<std::pair<uint32_t, uint32_t>> pr;  // prefix ranges, merged
+  for (auto& r : runs) pr.emplace_back((uint32_t)(r.first >> sh), (uint32_t)(((r.second - 1) >> sh) + 1));
+  std::sort(pr.begin(), pr.end());
+  std::vector<std::pair<uint32_t, uint32_t>> merged;
+  for (auto& r : pr) {
+    if (!merged.empty() && r.first <= merged.back().second) merged.back().second = std::max(merged.back().second, r.second);
+    else merged.push_back(r);
+  }
+  if (merged.empty() || (int)merged.size() > PGPU_SLICE_RANGES) return;
+  double covered = 0;
+  for (auto& r : merged) covered += r.second - r.first;
+  covered /= (double)(1u << K);
+  const double cand = rho_dense * PGPU_WT;  // candidates per 2048-doc tile
+  if (cand * 128.0 * (1.0 - covered) <= 256.0 * K) return;
+  ds.pfx_col = in.col;
+  ds.pfx_nr = (int32_t)merged.size();
+  for (size_t r = 0; r < merged.size(); ++r) {
+    ds.pfx_rng[r][0] = merged[r].first;
+    ds.pfx_rng[r][1] = merged[r].second;
+  }
+}
+
 int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pgpu_segment* seg,
                  const DevParams& p, Packer& pk, DevSeg& ds) {
   SegView v{q, &sp, seg, sp.filter, sp.num_filter_nodes};
@@ -1740,7 +1794,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     }
   }
   // dense prefix of the children: every scan column of a dense child is read with >= kDenseTouch sector density
-  double rho = 1.0;
+  double rho = 1.0, rho_dense = 1.0;
   bool residual = false;
   std::vector<int> dense_kids, resid_kids, staged;
   auto add_stage = [&](int qc) {
@@ -1763,6 +1817,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       resid_kids.push_back((int)k);
     }
     rho *= s;
+    if (dense) rho_dense *= s;
   }
   const size_t nfilter_stage = staged.size();
   // aggregation plan
@@ -1846,6 +1901,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   rc = convert_filter(q, sp, rn.data(), (int)rn.size(), seg, pk);
   if (rc) return rc;
   ds.rprog_len = (int32_t)pk.instrs.size() - ds.rprog_begin;
+  plan_prefix(v, pk, rho_dense, ds);
   auto stage_index = [&](int qc) {
     for (size_t j = 0; j < staged.size(); ++j)
       if (staged[j] == qc) return (int)j;
@@ -2247,6 +2303,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       if (g >= 8) g &= ~7;
       p.direct = 2;
       p.rd_planes = rd_bits <= 8 ? 8 : rd_bits <= 10 ? 10 : rd_bits <= 12 ? 12 : 16;
+      // prefix pre-filter when every segment's residual leaf has one (plan_prefix)
+      bool pfx = true;
+      for (const DevSeg& ds : pk.segs) pfx &= ds.ntiles == 0 || ds.pfx_col >= 0;
+      p.rd_pfx = pfx && p.rd_planes <= 12 ? PGPU_PFX_PLANES : 0;  // (no 16 + 3-plane variant: > 128 VGPRs)
       p.dslots = 0;
       grid = std::max(1, g);
       dyn = rdyn;
