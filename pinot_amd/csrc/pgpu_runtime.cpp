@@ -2110,6 +2110,9 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     }
     int rc = plan_segment(q, sp, seg, p, pk, ds);
     if (rc) return rc;
+    // a filter folded to EMPTY (a literal absent from the dictionary under an AND, ...) matches nothing: the
+    // reference's EmptyFilterOperator scans no doc, so the segment gets no tiles
+    if (ds.prog_len == 1 && ds.rprog_len == 0 && pk.instrs[ds.prog_begin].op == PGPU_I_EMPTY) ds.ntiles = 0;
     ds.track = 0;
     if (p.mode == PGPU_MODE_HASH && segment_needs_count(q, sp)) {
       pk.tracked.push_back(s);
