@@ -1068,8 +1068,23 @@ FI uint32_t leaf_bits(const DocCtx& t, const DevInstr& in) {
   for (int u = 0; u < U; ++u) m |= ((w[u] >> (t.doc[u] & 31)) & 1u) << u;
   return m;
 }
+// The lane's 32 docs against doc ranges [s, e] inline in the instruction (n <= 4, pgpu_runtime convert_filter).
+FI uint32_t inline_ranges_word(const DevInstr& in, int32_t doc0) {
+  const int32_t d0 = doc0 + 32 * lane_id(), d1 = d0 + 31;
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= in.n) break;
+    const int32_t s = (int32_t)in.ids[2 * k], e = (int32_t)in.ids[2 * k + 1];
+    if (e >= d0 && s <= d1) {
+      const int32_t bs = s > d0 ? s - d0 : 0, be = e < d1 ? e - d0 : 31;
+      w |= (0xFFFFFFFFu >> (31 - be)) & (0xFFFFFFFFu << bs);
+    }
+  }
+  return w;
+}
 FI uint32_t leaf_sorted(const DevParams& p, const TileCtx& t, const DevInstr& in) {
-  const uint32_t m = sorted_ranges_word(p.pool + in.pool_off, in.n, t.doc0);
+  const uint32_t m = in.n <= 4 ? inline_ranges_word(in, t.doc0) : sorted_ranges_word(p.pool + in.pool_off, in.n, t.doc0);
   return in.negate ? ~m : m;
 }
 FI uint32_t leaf_sorted(const DevParams& p, const DocCtx& t, const DevInstr& in) {
@@ -2161,7 +2176,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
         load_seg(p, cseg, ss);
       }
       const int64_t tw = now(pf);
-      wait_vmcnt(next_instrs);  // this tile's DMAs have landed (later tiles' may still be in flight)
+      if (ss.nstage > 0) wait_vmcnt(next_instrs);  // this tile's DMAs have landed (later tiles' may be in flight)
       PROF_ADD(pf, PGPU_P_C_FULL, tw);
       const int64_t tf = now(pf);
 #ifdef PGPU_PROFILE_BUILD

@@ -1547,6 +1547,13 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
           }
         }
         in.n = n;
+        // up to four ranges also inline in the instruction (ids[2k], ids[2k + 1]): the per-tile leaf then reads no
+        // memory beyond the instruction's scalar loads
+        for (int k = 0; k < 8; ++k) in.ids[k] = 0xFFFFFFFFu;
+        for (int k = 0; k < n && k < 4; ++k) {
+          in.ids[2 * k] = (uint32_t)pk.pool[in.pool_off + 2 * k];
+          in.ids[2 * k + 1] = (uint32_t)pk.pool[in.pool_off + 2 * k + 1];
+        }
         emit(in);
         close_nots();
         break;
