@@ -174,7 +174,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
 # Secondary workloads measured after the headline in the default run (BASELINE.json configs 2-4 and the SURVEY 8(d)
 # variants): (name, steps, warmup, segments per GPU or 0 = the workload's own, CPU sample seconds)
 SECONDARY = [("range_in", 10, 2, 0, 3.0), ("groupby1m", 5, 1, 0, 3.0), ("bitmap5", 10, 2, 0, 3.0),
-             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 8, 3.0)]
+             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 8, 3.0), ("adanalytics_exact", 10, 2, 0, 2.0)]
 
 
 def main():
@@ -282,14 +282,16 @@ def inverted_bytes_read(q, segs):
 
 
 # Looser variants of the bench queries (same plan shapes) so the parity sample matches rows, not only zero.
-PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789")}
+PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789"),
+                   "adanalytics_exact": ("accountId IN (123456789)", "accountId < 123456789")}
 
 
 def plan_options(opts):
     """GpuPlanMaker settings of a workload: numGroupsLimit and the server's ORDER BY trim (config 4 runs with
     minServerGroupTrimSize = -1, SURVEY.md 8(d): every group comes back, so the result is exact)."""
     return {"num_groups_limit": opts.get("num_groups_limit", 100_000),
-            "min_server_group_trim_size": opts.get("min_server_group_trim_size", 5000)}
+            "min_server_group_trim_size": opts.get("min_server_group_trim_size", 5000),
+            "exact_filter_stats": opts.get("exact_filter_stats", False)}
 
 
 def parity_check(ctx, w, q, opts):
@@ -317,7 +319,8 @@ def parity_check(ctx, w, q, opts):
     try:
         for qq in queries:
             res = GpuPlanMaker(ctx, **po).execute(qq, gs)
-            ref = engine.execute(qq, segs, num_groups_limit=po["num_groups_limit"])
+            ref = engine.execute(qq, segs, num_groups_limit=po["num_groups_limit"],
+                                 iterator_stats=po["exact_filter_stats"])
             if qq.group_by:
                 got, exp = res.group_rows, ref.group_rows
                 if po["min_server_group_trim_size"] <= 0:
@@ -328,6 +331,8 @@ def parity_check(ctx, w, q, opts):
             else:
                 ok = list(res.aggregation_result) == list(ref.aggregation_result)
             ok = ok and res.stats.num_docs_scanned == ref.num_docs_scanned
+            if po["exact_filter_stats"]:  # the reference's numEntriesScannedInFilter (iterator replay)
+                ok = ok and res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
             out["matched"].append(ref.num_docs_scanned)
             out["ok"] = bool(out["ok"] and ok)
         return out

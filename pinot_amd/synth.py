@@ -160,6 +160,18 @@ WORKLOADS: Dict[str, Workload] = {
          SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
         "SELECT COUNT(*) FROM adAnalytics WHERE daysSinceEpoch BETWEEN 17849 AND 17856",
         {}, 5, "config 5's filter stream alone (FETCH_SIZE calibration of the register-direct stream)"),
+    # config 5 with the reference's numEntriesScannedInFilter (PGPU_Q_EXACT_FILTER_STATS: one more pass over every
+    # filter leaf and the host iterator replay): the cost of pinot.server.query.executor.gpu.exact.filter.stats
+    "adanalytics_exact": Workload(
+        "adanalytics_exact", "adAnalytics",
+        [SynthColumn("daysSinceEpoch", 1024, _days),
+         SynthColumn("accountId", 1 << 20, _accounts),
+         SynthColumn("clicks", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 11)),
+         SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
+        "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
+        "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
+        "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
+        {"exact_filter_stats": True}, 5, "config 5 with the reference's exact numEntriesScannedInFilter"),
     "adanalytics_inv": Workload(
         "adanalytics_inv", "adAnalytics",
         [SynthColumn("daysSinceEpoch", 1024, _days),
