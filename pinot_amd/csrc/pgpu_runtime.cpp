@@ -1351,7 +1351,7 @@ int convert_filter(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const 
   int care = -1;   // care slot of the next node
   auto emit = [&](DevInstr in) {
     in.stage_off = -1;
-    if (in.pred != 2)
+    if (in.pred != 2 && in.op != PGPU_I_SORTED)  // LIST ids and SORTED inline ranges keep theirs
       for (int k = 0; k < 8; ++k) in.ids[k] = 0xFFFFFFFFu;
     pk.instrs.push_back(in);
     return (int)pk.instrs.size() - 1 - base;
