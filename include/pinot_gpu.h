@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 6
+#define PGPU_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -48,6 +48,12 @@ extern "C" {
 /* pgpu_query_cancel was called before the query finished (the reference cancels the segment tasks' futures,
  * BaseCombineOperator.getNextBlock); results and stats are partial and must be discarded. */
 #define PGPU_E_CANCELLED (-6)
+/* A segment whose group-key holder is map-based met more distinct keys than pgpu_query_desc.num_groups_limit: the
+ * reference keeps only the first-seen keys in doc order (DictionaryBasedGroupKeyGenerator.java:384-463, 991-1016;
+ * new keys beyond the limit get INVALID_ID and their docs are not aggregated).  The launch's table is discarded; the
+ * caller re-runs such segments with MIN over the doc-id column (pgpu_segment_add_docid_column) and keeps the
+ * num_groups_limit keys of smallest first doc (pinot_amd/plan.py), or keeps the CPU plan. */
+#define PGPU_E_GROUPS_LIMIT (-7)
 
 /* ---- stored data types (spi/data/FieldSpec.java DataType, stored type) -------------------------------------- */
 #define PGPU_INT 0
@@ -150,6 +156,10 @@ int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int
  * *out_bytes = its size; copied into `out` when non-NULL (capacity_bytes >= *out_bytes). */
 int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void* out, uint64_t capacity_bytes,
                                    uint64_t* out_bytes);
+/* The doc-id column: fills the empty slot `column` (before or after seal, once) with a raw INT column whose value at
+ * doc d is d.  MIN over it is each group's first doc, the order in which the reference's map-based group-key holders
+ * assign group ids (first-seen truncation at numGroupsLimit, PGPU_E_GROUPS_LIMIT).  4 bytes of HBM per doc. */
+int pgpu_segment_add_docid_column(pgpu_segment* seg, int32_t column);
 /* HBM bytes held by the segment (all columns, including padding and container directories). */
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);
 int pgpu_segment_release(pgpu_segment* seg);

@@ -23,6 +23,7 @@ PGPU_E_UNSUPPORTED = -3
 PGPU_E_NOT_FOUND = -4
 PGPU_E_TIMEOUT = -5
 PGPU_E_CANCELLED = -6
+PGPU_E_GROUPS_LIMIT = -7
 
 PGPU_INT, PGPU_LONG, PGPU_FLOAT, PGPU_DOUBLE, PGPU_STRING = range(5)
 PGPU_MEM_HOST, PGPU_MEM_DEVICE = 0, 1
@@ -37,7 +38,7 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class PinotGpuError(RuntimeError):
@@ -50,6 +51,12 @@ class PinotGpuError(RuntimeError):
 
 class UnsupportedPlanError(PinotGpuError):
     """PGPU_E_UNSUPPORTED: the server keeps the reference CPU plan for this query."""
+
+
+class GroupsLimitError(UnsupportedPlanError):
+    """PGPU_E_GROUPS_LIMIT: a segment met more distinct group keys than numGroupsLimit; the reference keeps its
+    first-seen keys only (GpuPlanMaker.execute re-runs such segments with their first docs, or the server keeps the
+    CPU plan -- an UnsupportedPlanError to callers that know no better)."""
 
 
 class QueryTimeoutError(PinotGpuError):
@@ -141,6 +148,7 @@ SIGNATURES = [
     ("pgpu_segment_add_mv_row_columns", C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     ("pgpu_segment_seal", C.c_int, [_P]),
     ("pgpu_segment_add_group_dictionary", C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+    ("pgpu_segment_add_docid_column", C.c_int, [_P, C.c_int32]),
     ("pgpu_segment_dictionary_values", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_device_bytes", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_release", C.c_int, [_P]),
@@ -214,6 +222,8 @@ def check(rc: int) -> None:
         msg = last_error()
         if rc == PGPU_E_UNSUPPORTED:
             raise UnsupportedPlanError(rc, msg)
+        if rc == PGPU_E_GROUPS_LIMIT:
+            raise GroupsLimitError(rc, msg)
         if rc == PGPU_E_TIMEOUT:
             raise QueryTimeoutError(rc, msg)
         if rc == PGPU_E_CANCELLED:

@@ -2649,7 +2649,7 @@ FI void pscan_put(const DevParams& p, uint32_t q, uint32_t slot, uint32_t cap, u
 // out eight partitions per step: 8 lanes per line, one 16-B ds_read_b128 / global_store_dwordx4 each, offsets in
 // 32 bits from the workgroup's region block.  The rest -- a line's head or tail piece (after a ring overflow, and
 // at the end) and records past a full region -- are walked one flagged partition at a time.
-FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, const uint32_t* ring,
+FI void pscan_flush(const DevParams& p, uint32_t* ht, const uint32_t* ring,
                     const uint32_t* lcap, const uint32_t* loff, uint32_t RC, int wave, bool final) {
   const int lane = lane_id(), np = p.nparts, g = lane >> 3, sub = lane & 7;
   const uint32_t rw = (uint32_t)p.rw, lsh = rw == 1 ? 5u : 4u, line = 1u << lsh;  // records per 128-B line
@@ -2658,17 +2658,17 @@ FI void pscan_flush(const DevParams& p, uint32_t* head, const uint32_t* tail, co
     const int q = qb + lane;
     uint32_t H = 0, E = 0, cap = 0, off = 0;
     if (q < np) {
-      H = head[q];
+      H = ht[2 * q + 1];
       cap = lcap[q];
       off = loff[q];
-      const uint32_t T = tail[q];
+      const uint32_t T = ht[2 * q];
       if (T - H > RC) {  // the ring overflowed this step: it holds [H, H + RC), the rest went straight to HBM
         E = H + RC;
-        head[q] = T;
+        ht[2 * q + 1] = T;
       } else {
         E = final ? T : (T & ~(line - 1u));
         if (E < H) E = H;
-        head[q] = E;
+        ht[2 * q + 1] = E;
       }
     }
     if (!__ballot(E > H)) continue;
@@ -2740,11 +2740,12 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int np = p.nparts;
   const uint32_t RC = (uint32_t)p.pscan;  // ring records per partition (power of two)
-  // [np + 64]: first slot not yet written out; the 64 lanes' dummy partitions follow the real ones
   const int npad = (np + 64 + 2) & ~1;   // + the cancel word; keeps the ring 16-B aligned
-  uint32_t* head = (uint32_t*)dyn_smem;
-  uint32_t* tail = head + npad;           // [np + 64] slots taken (= records of this workgroup in the partition)
-  uint32_t* lcap = tail + npad;           // [npad] region capacity / offset in the block per partition
+  // [npad] pairs {tail, head} (one 8-B word per partition: a record's slot and the partition's head come back from
+  // one 64-bit LDS atomic): tail = slots taken (records of this workgroup in the partition), head = first slot not
+  // yet written out; the 64 lanes' dummy partitions follow the real ones, then the cancel word (head of np + 64)
+  uint32_t* ht = (uint32_t*)dyn_smem;
+  uint32_t* lcap = ht + 2 * npad;         // [npad] region capacity / offset in the block per partition
   uint32_t* loff = lcap + npad;
   uint32_t* ring = loff + npad;           // [np][RC * rw], then one dummy record per lane
   Cons cv;
@@ -2753,7 +2754,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   cv.klist = cv.vlist = nullptr;
   cv.acc = nullptr;
   cv.qtiles = nullptr;
-  for (int i = threadIdx.x; i < 2 * npad; i += PGPU_PSCAN_THREADS) head[i] = 0u;
+  for (int i = threadIdx.x; i < 2 * npad; i += PGPU_PSCAN_THREADS) ht[i] = 0u;
   if (!COUNT)
     for (int i = threadIdx.x; i < np; i += PGPU_PSCAN_THREADS) {
       lcap[i] = part_cap(p, i);
@@ -2826,7 +2827,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
         if (COUNT) {
 #pragma unroll
           for (int i = 0; i < 32; ++i)
-            if (lane_bit(mm, i)) atomicAdd(&tail[key[i] >> p.pshift], 1u);
+            if (lane_bit(mm, i)) atomicAdd(&ht[2 * (key[i] >> p.pshift)], 1u);
         } else {
         if (p.pcol >= 0) {
           const DevColumn c = col_of(ss, p.pcol);
@@ -2854,9 +2855,11 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             qq[j] = lane_bit(mm, i) ? (key[i] >> p.pshift) : dq;
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) slot[j] = atomicAdd(&tail[qq[j]], 1u);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) hd[j] = head[qq[j]];
+          for (int j = 0; j < 8; ++j) {
+            const uint64_t o = atomicAdd((unsigned long long*)(ht + 2 * qq[j]), 1ull);
+            slot[j] = (uint32_t)o;
+            hd[j] = (uint32_t)(o >> 32);
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int i = 8 * g8 + j;
@@ -2894,21 +2897,21 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
     __syncthreads();
     PROF_ADD(pf, PGPU_P_C_FULL, tp);  // barrier waits
     tp = now(pf);
-    pscan_flush(p, head, tail, ring, lcap, loff, RC, wave, false);
-    if (wave == 0 && step % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p) && lane == 0) head[np + 64] = 1u;
+    pscan_flush(p, ht, ring, lcap, loff, RC, wave, false);
+    if (wave == 0 && step % PGPU_CANCEL_POLL == PGPU_CANCEL_POLL - 1 && query_cancelled(p) && lane == 0) ht[2 * (np + 64) + 1] = 1u;
     PROF_ADD(pf, PGPU_P_C_FLUSH, tp);
     tp = now(pf);
     __syncthreads();
     PROF_ADD(pf, PGPU_P_C_FULL, tp);
-    if (head[np + 64]) break;  // cancelled: the workgroup stops together (the word was set before the barrier)
+    if (ht[2 * (np + 64) + 1]) break;  // cancelled: the workgroup stops together (the word was set before the barrier)
   }
   if (COUNT) {
     __syncthreads();
     for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
-      if (tail[q]) atomicAdd(&p.pcount[q], tail[q]);
+      if (ht[2 * q]) atomicAdd(&p.pcount[q], ht[2 * q]);
     return;
   }
-  pscan_flush(p, head, tail, ring, lcap, loff, RC, wave, true);
+  pscan_flush(p, ht, ring, lcap, loff, RC, wave, true);
   const size_t w = (size_t)blockIdx.x * PGPU_PSCAN_WAVES + wave;
   PROF_ADD(pf, PGPU_P_C_TOTAL, t_all);
 #ifdef PGPU_PROFILE_BUILD
@@ -2926,7 +2929,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
     o[PGPU_STAT_DENSE_BYTES] = dense_bytes;
   }
   for (int q = threadIdx.x; q < np; q += PGPU_PSCAN_THREADS)
-    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = tail[q] < lcap[q] ? tail[q] : lcap[q];
+    p.rcount[(size_t)q * gridDim.x + blockIdx.x] = ht[2 * q] < lcap[q] ? ht[2 * q] : lcap[q];
 }
 
 // Region sizing and phase-2 work split from the sampled counts (one 1024-thread workgroup):

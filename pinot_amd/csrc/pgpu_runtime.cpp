@@ -1040,6 +1040,30 @@ int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int
   return PGPU_OK;
 }
 
+int pgpu_segment_add_docid_column(pgpu_segment* seg, int32_t column) {
+  if (!seg) return fail(PGPU_E_INVALID, "null segment");
+  if (column < 0 || column >= (int32_t)seg->cols.size()) return fail(PGPU_E_INVALID, "bad column %d", column);
+  HostColumn& c = seg->cols[column];
+  if (c.kind != PGPU_COL_NONE || c.dict_card) return fail(PGPU_E_INVALID, "doc-id slot %d is not empty", column);
+  const int32_t n = seg->num_docs;
+  // padded to whole PGPU_TILE-doc tiles (+16 B) like any raw column: the kernels read whole tiles of "ids"
+  const uint64_t ntiles = ((uint64_t)std::max(n, 1) + PGPU_TILE - 1) / PGPU_TILE;
+  std::vector<int32_t> iota((size_t)ntiles * PGPU_TILE + 4, 0);
+  for (int32_t i = 0; i < n; ++i) iota[(size_t)i] = i;
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(upload(c.dict, iota.data(), 4ull * iota.size(), 4ull * iota.size(), PGPU_MEM_HOST));
+  c.kind = PGPU_COL_RAW;
+  c.dict_type = PGPU_INT;
+  c.fwd_card = n;
+  c.dict_bytes = 4ull * (uint64_t)n;
+  c.max_abs = n > 0 ? (double)(n - 1) : 0.0;
+  if (seg->sealed) {
+    const int rc = seal_column(seg, (size_t)column);
+    if (rc) return rc;
+  }
+  return PGPU_OK;
+}
+
 int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void* out, uint64_t capacity_bytes,
                                    uint64_t* out_bytes) {
   if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
@@ -2806,16 +2830,21 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
     int32_t flag = 0;
     memcpy(&flag, (const char*)qq->ws->h_stats.p + 8 * PGPU_NSTATS, 4);
     if (flag) {
+      // the table holds every segment's bound (its key space, docs, and numGroupsLimit for a map-based holder): an
+      // overflow means a tracked segment met more keys than numGroupsLimit
       if (out_stats) *out_stats = qq->stats;
+      if (!qq->tracked.empty())
+        return fail(PGPU_E_GROUPS_LIMIT, "hash group-by table overflow: a segment meets more distinct group keys than "
+                    "numGroupsLimit %lld (the reference keeps the first-seen keys only)", (long long)qq->groups_limit);
       return fail(PGPU_E_UNSUPPORTED, "hash group-by table overflow (more distinct keys than the holder limits allow)");
     }
     const int64_t* cnt = (const int64_t*)qq->ws->h_segcnt.p;
     for (size_t i = 0; i < qq->tracked.size(); ++i)
       if (cnt[i] > qq->groups_limit) {
         if (out_stats) *out_stats = qq->stats;
-        return fail(PGPU_E_UNSUPPORTED,
+        return fail(PGPU_E_GROUPS_LIMIT,
                     "segment %d meets %lld distinct group keys > numGroupsLimit %lld: the reference keeps the "
-                    "first-seen keys only (DictionaryBasedGroupKeyGenerator); served by the CPU plan",
+                    "first-seen keys only (DictionaryBasedGroupKeyGenerator)",
                     qq->tracked[i], (long long)cnt[i], (long long)qq->groups_limit);
       }
   }

@@ -24,6 +24,7 @@ the server keeps its CPU plan for it.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 import time
 import hashlib
 import math
@@ -40,8 +41,8 @@ from ._lib import (ExprNode, Literal, PGPU_AGG_AVG, PGPU_AGG_COUNT, PGPU_AGG_MAX
                    UnsupportedPlanError)
 from .predicate import (DictPredicateEvaluator, RawPredicateEvaluator, SortedDictionary, get_predicate_evaluator,
                         get_raw_predicate_evaluator)
-from .query import MV_AGGS, UNBOUNDED, FilterContext, QueryContext, split_filtered_aggregations
-from .segment import GpuContext, GpuSegment
+from .query import MV_AGGS, UNBOUNDED, AggregationSpec, FilterContext, QueryContext, split_filtered_aggregations
+from .segment import DOCID_COLUMN, GpuContext, GpuSegment
 
 AGG_FN = {"COUNT": PGPU_AGG_COUNT, "SUM": PGPU_AGG_SUM, "MIN": PGPU_AGG_MIN, "MAX": PGPU_AGG_MAX,
           "AVG": PGPU_AGG_AVG}
@@ -778,7 +779,72 @@ class GpuPlanMaker:
             rest = [s for s, ns in zip(segments, non_scan) if not ns]
             res = self.collect(self.submit(query, rest)) if rest else None
             return merge_non_scan(query, res, [s for s, ns in zip(segments, non_scan) if ns])
-        return self.collect(self.submit(query, segments))
+        try:
+            return self.collect(self.submit(query, segments))
+        except _lib.GroupsLimitError:
+            return self.first_seen_groups(query, segments)
+
+    def first_seen_groups(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
+        """A segment met more distinct group keys than numGroupsLimit (PGPU_E_GROUPS_LIMIT).  The reference's
+        map-based holders give group ids in doc order and drop every key past the limit, with its docs
+        (DictionaryBasedGroupKeyGenerator.java:384-463, IntGroupIdMap.getGroupId :991-1016; NoDictionary*
+        GroupKeyGenerator likewise).  Segments whose key space cannot exceed the limit run together as usual; each
+        other segment runs alone with no limit plus MIN over its doc-id column (GpuSegment.docid_view), i.e. every
+        group's first doc, and keeps the num_groups_limit groups of smallest first doc.  The partial results merge
+        as the combine merges segment results (AggregationFunction.merge)."""
+        from .datatable import _final, _merge
+        if any(s.column(g).is_mv for s in segments for g in query.group_by):
+            raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
+                                            "numGroupsLimit on a multi-value group key (first-seen order per value)")
+        limit = self.num_groups_limit
+        no_dict = any(s.column(g).is_raw for s in segments for g in query.group_by)
+        thr = 0 if no_dict else self.max_init_group_holder_capacity
+
+        def key_space(s):
+            P = 1
+            for g in query.group_by:
+                P *= max(1, s.column(s.group_view(g)).cardinality)
+            return P
+
+        capped = [key_space(s) > max(0, thr) and key_space(s) > limit for s in segments]
+        free = [s for s, c in zip(segments, capped) if not c]
+        parts = []
+        if free:
+            r = self.execute(query, free)
+            parts.append((r.intermediate, r.stats))
+        sub = GpuPlanMaker(self.ctx, num_groups_limit=0, max_init_group_holder_capacity=self.max_init_group_holder_capacity,
+                           collect_stats=self.collect_stats, query_flags=self.query_flags,
+                           host_planning=self.host_planning, exact_filter_stats=self.exact_filter_stats,
+                           timeout_ms=self.timeout_ms, gpu_topk=False, min_server_group_trim_size=-1)
+        probe = dataclasses.replace(query, aggregations=list(query.aggregations) + [AggregationSpec("MIN", DOCID_COLUMN)])
+        for s, c in zip(segments, capped):
+            if not c:
+                continue
+            s.docid_view()
+            r = sub.execute(probe, [s])
+            items = list(r.intermediate.items())
+            if len(items) > limit:
+                items = sorted(items, key=lambda kv: kv[1][-1])[:limit]
+            parts.append(({k: v[:-1] for k, v in items}, r.stats))
+        fns = [a.function for a in query.aggregations]
+        merged: Dict[tuple, list] = {}
+        st = ExecutionStats()
+        for inter, rs in parts:
+            for k, v in inter.items():
+                cur = merged.get(k)
+                merged[k] = list(v) if cur is None else [_merge(fn, x, y) for fn, x, y in zip(fns, cur, v)]
+            for f in ("num_docs_scanned", "num_entries_scanned_in_filter", "num_total_docs", "num_segments_processed",
+                      "kernel_ms", "sparse_sector_bytes", "dense_bytes"):
+                setattr(st, f, getattr(st, f) + getattr(rs, f))
+            st.filter_stats_exact = st.filter_stats_exact and rs.filter_stats_exact
+        st.num_entries_scanned_post_filter = st.num_docs_scanned * len(query.projected_columns)
+        ng = len(query.group_by)
+        finals = [k + tuple(_final(fn, x) for fn, x in zip(fns, v)) for k, v in merged.items()]
+        res = QueryResult(query=query, stats=st)
+        res._intermediate = merged
+        res._group_rows = sorted(finals, key=lambda r: r[:ng])
+        res.rows = [to_select_order(query, r) for r in order_and_limit(query, finals)]
+        return res
 
     def non_scan_segments(self, query: QueryContext, segments: Sequence[GpuSegment]) -> List[bool]:
         """Per segment, AggregationPlanNode.buildNonFilteredAggOperator's choice (core/plan/AggregationPlanNode.java

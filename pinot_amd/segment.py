@@ -225,6 +225,9 @@ def mv_row_column(column: str, kind: str) -> str:
     return f"{column}$mv{kind}"
 
 
+DOCID_COLUMN = "$docId"  # GpuSegment.docid_view
+
+
 def group_dict_column(column: str) -> str:
     """Slot name of a raw column's on-the-fly group dictionary (GpuSegment.group_view)."""
     return f"{column}$gdict"
@@ -253,11 +256,13 @@ class GpuSegment:
         nraw = 0 if _incremental else sum(1 for n in names if data.column(n).is_raw)
         lib = ctx._lib
         h = C.c_void_p()
-        nslots = len(names) + len(MV_ROW_COLUMNS) * nmv + nraw
+        # + the doc-id column's slot (docid_view), filled on first use
+        nslots = len(names) + len(MV_ROW_COLUMNS) * nmv + nraw + (0 if _incremental else 1)
         _lib.check(lib.pgpu_segment_create(ctx.handle, data.num_docs, nslots, C.byref(h)))
         self.handle = h
         self._capacity = nslots
-        self._gdict_free = list(range(nslots - nraw, nslots))  # spare slots (after every column's own)
+        self._gdict_free = list(range(nslots - nraw - 1, nslots - 1))  # spare slots (after every column's own)
+        self._docid_slot = None if _incremental else nslots - 1
         if _incremental:
             return
         try:
@@ -374,6 +379,20 @@ class GpuSegment:
         self.derived[gname] = ColumnIndexes(gname, col.data_type, card.value,
                                             dictionary=vals.astype(_BE_DTYPE[col.data_type]).tobytes())
         return gname
+
+    def docid_view(self) -> str:
+        """The doc-id column (pgpu_segment_add_docid_column: a raw INT column whose value at doc d is d), added on
+        first use: MIN over it is each group's first doc, the order of the reference's first-seen group ids."""
+        if DOCID_COLUMN in self.slots:
+            return DOCID_COLUMN
+        if self._docid_slot is None:
+            raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED, "no doc-id slot (incrementally built segment)")
+        _lib.check(self.ctx._lib.pgpu_segment_add_docid_column(self.handle, self._docid_slot))
+        self.slots[DOCID_COLUMN] = self._docid_slot
+        self.dictionaries[DOCID_COLUMN] = None
+        self.derived[DOCID_COLUMN] = ColumnIndexes(DOCID_COLUMN, PGPU_INT, self.num_docs, raw_forward=b"",
+                                                   min_value=0.0, max_value=float(max(self.num_docs - 1, 0)))
+        return DOCID_COLUMN
 
     def column(self, name: str) -> ColumnIndexes:
         c = self.derived.get(name)

@@ -3,15 +3,15 @@
 The reference picks a holder per segment from its cardinality product (DictionaryBasedGroupKeyGenerator.java:
 100-170): array (<= max.init.group.holder.capacity), IntMap (<= 2^31), LongMap (<= 2^63), ArrayMap (beyond);
 map holders stop at num.groups.limit distinct keys, keeping the first-seen ones.  The GPU keys any space by hash
-slots, counts the distinct keys of every segment that could pass the limit, and declines (PGPU_E_UNSUPPORTED) only
-a query where a segment really does."""
+slots and counts the distinct keys of every segment that could pass the limit; a segment that really does keeps its
+first-seen keys (GpuPlanMaker.first_seen_groups: MIN over the doc-id column per group, then the limit smallest)."""
 import numpy as np
 import pytest
 
 from oracle import engine
 from oracle.segment_writer import build_segment
 from pinot_amd._lib import PGPU_DOUBLE, PGPU_INT, PGPU_KEYS_DENSE, PGPU_KEYS_HASH, PGPU_LONG, PGPU_Q_HASH, \
-    PGPU_STRING, UnsupportedPlanError
+    PGPU_STRING, GroupsLimitError, UnsupportedPlanError
 from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
@@ -121,10 +121,57 @@ def test_group_limit_counts_actual_keys(gpu_ctx):
     res, layout = _run(gpu_ctx, sql, small, num_groups_limit=5_000)
     assert layout.key_kind == PGPU_KEYS_HASH
     _same(res, engine.execute(parse_sql(sql), small, num_groups_limit=5_000))
-    # ~1800 distinct pairs per segment (1000 seed pairs + 800): above a limit of 1,500
+    # ~1800 distinct pairs per segment (1000 seed pairs + 800): above a limit of 1,500.  The launch reports it
+    # (PGPU_E_GROUPS_LIMIT, a GroupsLimitError to submit / collect callers); execute() keeps every such segment's
+    # first-seen 1,500 keys like the reference's holders (GpuPlanMaker.first_seen_groups)
     big = small + [_sparse_pairs(rng, 100_000, "g9", groups=800)]
-    with pytest.raises(UnsupportedPlanError, match="numGroupsLimit"):
-        _run(gpu_ctx, sql, big, num_groups_limit=1_500)
+    gs = [GpuSegment(gpu_ctx, s) for s in big]
+    try:
+        pm = GpuPlanMaker(gpu_ctx, num_groups_limit=1_500)
+        with pytest.raises(GroupsLimitError, match="numGroupsLimit"):
+            pm.collect(pm.submit(parse_sql(sql), gs))
+        res = pm.execute(parse_sql(sql), gs)
+    finally:
+        for g in gs:
+            g.release()
+    ref = engine.execute(parse_sql(sql), big, num_groups_limit=1_500)
+    assert len(res.group_rows) == len(ref.group_rows) < 3 * 1_800
+    _same(res, ref)
+    assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
+
+
+@pytest.mark.parametrize("sql,limit", [
+    # one group column of 30,000 values (IntMapBasedHolder), filtered: docs of dropped keys are not aggregated
+    ("SELECT k, COUNT(*), SUM(m), MIN(m), AVG(m) FROM t WHERE f < 70 GROUP BY k ORDER BY COUNT(*) DESC, k LIMIT 20",
+     2_000),
+    # two columns, the truncation ordered by MAX
+    ("SELECT k, f, MAX(m), COUNT(*) FROM t GROUP BY k, f ORDER BY MAX(m) DESC LIMIT 15", 7_000),
+    # a raw (no-dictionary) group column: NoDictionarySingleColumnGroupKeyGenerator caps at the limit too
+    ("SELECT r, COUNT(*), SUM(m) FROM t GROUP BY r ORDER BY SUM(m) DESC LIMIT 10", 3_000),
+])
+def test_first_seen_truncation_at_num_groups_limit(gpu_ctx, sql, limit):
+    """Segments beyond numGroupsLimit keep their first-seen keys (smallest first doc), the others all of theirs;
+    the merged result equals the reference's (oracle: DictionaryBasedGroupKeyGenerator's first-seen group ids)."""
+    rng = np.random.default_rng(31)
+    segs = []
+    for i, (n, card) in enumerate([(40_000, 30_000), (25_000, 30_000), (8_000, 500)]):
+        k = np.concatenate([np.arange(card), rng.integers(0, card, n - card if n > card else 0)])[:n]
+        rng.shuffle(k)
+        cols = {"k": (PGPU_INT, (k * 5 + 2).astype(np.int32)), "f": (PGPU_INT, rng.integers(0, 100, n)),
+                "m": (PGPU_INT, rng.integers(-1000, 50_000, n)), "r": (PGPU_LONG, rng.integers(0, 9_000, n) * 11)}
+        segs.append(build_segment(f"fs{i}", cols, sorted_columns=(), raw=("r",)))
+    q = parse_sql(sql)
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=limit).execute(q, gs)
+    finally:
+        for g in gs:
+            g.release()
+    ref = engine.execute(q, segs, num_groups_limit=limit)
+    full = engine.execute(q, segs, num_groups_limit=10 ** 9)
+    assert len(ref.group_rows) < len(full.group_rows)  # the limit really truncates
+    _same(res, ref)
+    assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
 
 
 def test_dense_layout_kept_for_dense_key_spaces(gpu_ctx):
