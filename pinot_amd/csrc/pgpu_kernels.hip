@@ -2755,6 +2755,25 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   cv.acc = nullptr;
   cv.qtiles = nullptr;
   for (int i = threadIdx.x; i < 2 * npad; i += PGPU_PSCAN_THREADS) ht[i] = 0u;
+  // the hottest partition of the sampling pass (skewed keys): its records take their slots with one atomic per wave
+  // instruction (a ballot over the lanes that hit it) instead of 64 atomics on one LDS address
+  uint32_t hq = 0xFFFFFFFFu;
+  if (!COUNT && p.pcap) {  // every wave reduces the sampled counts itself (no LDS: the rings have it all)
+    uint64_t best = 0;     // (count << 32 | partition): the largest count wins
+    for (int q = lane; q < np; q += 64) best = std::max(best, ((uint64_t)p.pcount[q] << 32) | (uint32_t)q);
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t x = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), o, 64) << 32) |
+                         (uint32_t)__shfl_xor((int)(uint32_t)best, o, 64);
+      best = std::max(best, x);
+    }
+    uint64_t tot = 0;
+    for (int q = lane; q < np; q += 64) tot += p.pcount[q];
+    tot = (uint64_t)wave_sum_i64((int64_t)tot);
+    // only a really hot partition (>= 4x the mean: skewed keys) -- for even keys the ballots cost more than the
+    // same-address atomics they save
+    if ((best >> 32) && (best >> 32) * (uint64_t)np >= 4 * tot)
+      hq = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)best);
+  }
   if (!COUNT)
     for (int i = threadIdx.x; i < np; i += PGPU_PSCAN_THREADS) {
       lcap[i] = part_cap(p, i);
@@ -2854,11 +2873,38 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             const int i = 8 * g8 + j;
             qq[j] = lane_bit(mm, i) ? (key[i] >> p.pshift) : dq;
           }
+          uint64_t o[8], hm[8];
+          if (hq == 0xFFFFFFFFu) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint64_t o = atomicAdd((unsigned long long*)(ht + 2 * qq[j]), 1ull);
-            slot[j] = (uint32_t)o;
-            hd[j] = (uint32_t)(o >> 32);
+            for (int j = 0; j < 8; ++j) o[j] = atomicAdd((unsigned long long*)(ht + 2 * qq[j]), 1ull);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              slot[j] = (uint32_t)o[j];
+              hd[j] = (uint32_t)(o[j] >> 32);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hm[j] = __ballot(qq[j] == hq);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const bool hot = (hm[j] >> lane) & 1u;
+              const int leader = hm[j] ? __builtin_ctzll(hm[j]) : 0;
+              o[j] = 0;
+              if (!hot || lane == leader)
+                o[j] = atomicAdd((unsigned long long*)(ht + 2 * qq[j]), hot ? (unsigned long long)__popcll(hm[j]) : 1ull);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              if (hm[j]) {  // the hot lanes' slots: the leader's base + their rank among the hot lanes
+                const int leader = __builtin_ctzll(hm[j]);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o[j], leader);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(o[j] >> 32), leader);
+                if ((hm[j] >> lane) & 1u)
+                  o[j] = ((uint64_t)hi << 32) | (lo + (uint32_t)__popcll(hm[j] & ((1ull << lane) - 1ull)));
+              }
+              slot[j] = (uint32_t)o[j];
+              hd[j] = (uint32_t)(o[j] >> 32);
+            }
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -3054,6 +3100,15 @@ FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 
   }
 }
 
+// A value of the frame-of-reference dictionary image in LDS: block base + the id's fbits-bit offset (it may straddle
+// two words).
+FI uint32_t for_value(const uint32_t* fimg, int fnblk, int fbits, uint32_t id) {
+  const uint32_t blk = id >> 5, bit = (id & 31u) * (uint32_t)fbits;
+  const uint32_t* wds = fimg + fnblk + (size_t)blk * fbits + (bit >> 5);
+  const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
+  return fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
+}
+
 template <int NS, bool ONE, int LDM>
 __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
@@ -3132,12 +3187,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               if (!ok[r]) continue;
-              // value = block base + the id's fbits-bit offset (it may straddle two words)
-              const uint32_t blk = id[r] >> 5, bit = (id[r] & 31u) * (uint32_t)fbits;
-              const uint32_t* wds = fimg + fnblk + (size_t)blk * fbits + (bit >> 5);
-              const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
-              const uint32_t val = fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
-              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)val);
+              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)for_value(fimg, fnblk, fbits, id[r]));
             }
           } else {
             uint32_t* sec = (uint32_t*)(base + soff[s]);

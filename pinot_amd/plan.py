@@ -842,8 +842,8 @@ class GpuPlanMaker:
         finals = [k + tuple(_final(fn, x) for fn, x in zip(fns, v)) for k, v in merged.items()]
         res = QueryResult(query=query, stats=st)
         res._intermediate = merged
-        res._group_rows = sorted(finals, key=lambda r: r[:ng])
-        res.rows = [to_select_order(query, r) for r in order_and_limit(query, finals)]
+        res._group_rows = sorted(finals, key=lambda r: r[:ng])  # ascending keys: ORDER BY ties as the one-launch path
+        res.rows = [to_select_order(query, r) for r in order_and_limit(query, res._group_rows)]
         return res
 
     def non_scan_segments(self, query: QueryContext, segments: Sequence[GpuSegment]) -> List[bool]:

@@ -144,10 +144,10 @@ def test_group_limit_counts_actual_keys(gpu_ctx):
     # one group column of 30,000 values (IntMapBasedHolder), filtered: docs of dropped keys are not aggregated
     ("SELECT k, COUNT(*), SUM(m), MIN(m), AVG(m) FROM t WHERE f < 70 GROUP BY k ORDER BY COUNT(*) DESC, k LIMIT 20",
      2_000),
-    # two columns, the truncation ordered by MAX
-    ("SELECT k, f, MAX(m), COUNT(*) FROM t GROUP BY k, f ORDER BY MAX(m) DESC LIMIT 15", 7_000),
+    # two columns, ordered by MAX (ties broken by the keys: the reference leaves tie order to its table)
+    ("SELECT k, f, MAX(m), COUNT(*) FROM t GROUP BY k, f ORDER BY MAX(m) DESC, k, f LIMIT 15", 7_000),
     # a raw (no-dictionary) group column: NoDictionarySingleColumnGroupKeyGenerator caps at the limit too
-    ("SELECT r, COUNT(*), SUM(m) FROM t GROUP BY r ORDER BY SUM(m) DESC LIMIT 10", 3_000),
+    ("SELECT r, COUNT(*), SUM(m) FROM t GROUP BY r ORDER BY SUM(m) DESC, r LIMIT 10", 3_000),
 ])
 def test_first_seen_truncation_at_num_groups_limit(gpu_ctx, sql, limit):
     """Segments beyond numGroupsLimit keep their first-seen keys (smallest first doc), the others all of theirs;

@@ -290,14 +290,19 @@ def test_partitioned_groupby_large_key_space(gpu_ctx):
             g.release()
 
 
-def test_group_limit_unsupported(gpu_ctx):
+def test_group_limit_first_seen(gpu_ctx):
     rng = np.random.default_rng(9)
     seg = _random_segment(rng, 200_000)  # column d: ~66k distinct values present -> IntMap holder
     g = GpuSegment(gpu_ctx, seg)
+    q = parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d")
     try:
-        with pytest.raises(UnsupportedPlanError):
-            GpuPlanMaker(gpu_ctx, num_groups_limit=50_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
-        res = GpuPlanMaker(gpu_ctx, num_groups_limit=100_000).execute(parse_sql("SELECT d, COUNT(*) FROM t GROUP BY d"), [g])
+        # beyond the limit: the first-seen 50,000 keys (GpuPlanMaker.first_seen_groups), as the reference keeps them
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=50_000).execute(q, [g])
+        ref = engine.execute(q, [seg], num_groups_limit=50_000)
+        assert len(res.group_rows) == len(ref.group_rows) == 50_000
+        _assert_same(res, ref)
+        assert sum(r[1] for r in res.group_rows) < 200_000
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=100_000).execute(q, [g])
         assert sum(r[1] for r in res.group_rows) == 200_000
     finally:
         g.release()

@@ -11,7 +11,7 @@ import pytest
 
 from oracle import engine, rawfwd
 from oracle.segment_writer import build_segment
-from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, UnsupportedPlanError
+from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG
 from pinot_amd.query import parse_sql
 from tests.helpers import check_groups, close, rows_close
 
@@ -262,8 +262,8 @@ def test_gpu_group_by_raw_vs_oracle(gpu_ctx, qi, flags):
 
 @pytest.mark.gpu
 def test_gpu_group_by_raw_float_keys_and_limit(gpu_ctx):
-    """-0.0 / 0.0 apart and NaNs as one group on the GPU too; a segment meeting more raw keys than numGroupsLimit goes
-    back to the CPU plan (PGPU_E_UNSUPPORTED), as the reference would truncate it."""
+    """-0.0 / 0.0 apart and NaNs as one group on the GPU too; a segment meeting more raw keys than numGroupsLimit keeps
+    its first-seen keys, as the reference truncates it."""
     from pinot_amd.plan import GpuPlanMaker
     from pinot_amd.segment import GpuSegment
     rng = np.random.default_rng(77)
@@ -279,8 +279,13 @@ def test_gpu_group_by_raw_float_keys_and_limit(gpu_ctx):
         got = {np.float64(r[0]).tobytes() if not np.isnan(r[0]) else b"nan": tuple(r[1:]) for r in res.group_rows}
         exp = {np.float64(k[0]).tobytes() if not np.isnan(k[0]) else b"nan": (v[0], v[1]) for k, v in ref.groups.items()}
         assert len(got) == 6 and got == exp
-        with pytest.raises(UnsupportedPlanError):
-            GpuPlanMaker(gpu_ctx, num_groups_limit=100).execute(parse_sql("SELECT ri, COUNT(*) FROM t GROUP BY ri"), gs)
+        # ~500 raw keys past a limit of 100: the first-seen 100 (NoDictionarySingleColumnGroupKeyGenerator caps its
+        # map at numGroupsLimit), through GpuPlanMaker.first_seen_groups
+        q = parse_sql("SELECT ri, COUNT(*) FROM t GROUP BY ri")
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=100).execute(q, gs)
+        ref = engine.execute(q, [seg], num_groups_limit=100)
+        assert len(res.group_rows) == len(ref.group_rows) == 100
+        assert sorted(res.group_rows) == sorted(ref.group_rows)
     finally:
         for g in gs:
             g.release()
