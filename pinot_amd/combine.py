@@ -87,13 +87,21 @@ def reduce_scatter_sections(table, layout: TableLayout, world: int, rank: int, g
     K = (G + world - 1) // world
     view = table.view(len(ops), G)
     out = torch.empty((len(ops), K), dtype=torch.int64, device=table.device)
+    native = hasattr(dist, "reduce_scatter_tensor") and dist.get_backend(group) != "gloo"
+    pad = None  # one padded staging row for all sections, only when G does not split evenly (or under gloo)
     for s, op in enumerate(ops):
-        src = torch.full((K * world,), section_identity(op), dtype=torch.int64, device=table.device)
-        src[:G] = view[s]
+        if native and K * world == G:
+            src = view[s]  # a contiguous row of the table: reduced in place of a copy
+        else:
+            if pad is None:
+                pad = torch.empty((K * world,), dtype=torch.int64, device=table.device)
+            pad[G:].fill_(section_identity(op))
+            pad[:G].copy_(view[s])
+            src = pad
         dst = out[s]
         if op == PGPU_RED_SUM_F64:
             src, dst = src.view(torch.float64), out[s].view(torch.float64)
-        if hasattr(dist, "reduce_scatter_tensor") and dist.get_backend(group) != "gloo":
+        if native:
             dist.reduce_scatter_tensor(dst, src, op=_dist_op(op), group=group)
         else:  # gloo has no reduce_scatter: all_reduce, keep this rank's slice
             dist.all_reduce(src, op=_dist_op(op), group=group)
