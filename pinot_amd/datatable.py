@@ -306,6 +306,8 @@ def server_data_table(query: QueryContext, result, group_types: Sequence[int] = 
           "numSegmentsProcessed": str(st.num_segments_processed),
           "numSegmentsMatched": str(st.num_segments_processed if st.num_docs_scanned else 0),
           "numResizes": "0", "resizeTimeMs": "0", "totalDocs": str(st.num_total_docs)}
+    if getattr(st, "num_groups_limit_reached", False):  # DataTable.MetadataKey.NUM_GROUPS_LIMIT_REACHED
+        md["numGroupsLimitReached"] = "true"
     return DataTable(schema, rows, md)
 
 
@@ -346,6 +348,7 @@ class BrokerResult:
     num_segments_processed: int = 0
     num_segments_matched: int = 0
     total_docs: int = 0
+    num_groups_limit_reached: bool = False
     exceptions: Dict[int, str] = field(default_factory=dict)
 
 
@@ -361,6 +364,7 @@ def reduce_data_tables(query: QueryContext, tables: Sequence[DataTable]) -> Brok
         res.num_segments_processed += int(md.get("numSegmentsProcessed", 0))
         res.num_segments_matched += int(md.get("numSegmentsMatched", 0))
         res.total_docs += int(md.get("totalDocs", 0))
+        res.num_groups_limit_reached |= md.get("numGroupsLimitReached") == "true"
         res.exceptions.update(t.exceptions)
     fns = [a.function for a in query.aggregations]
     ng = len(query.group_by)

@@ -289,6 +289,7 @@ class ExecutionStats:
     filter_stats_exact: bool = True          # num_entries_scanned_in_filter is the reference's figure
     sparse_sector_bytes: int = 0
     dense_bytes: int = 0
+    num_groups_limit_reached: bool = False   # some segment's holder stopped at numGroupsLimit (first_seen_groups)
 
 
 def key_words_out(L: TableLayout) -> int:
@@ -809,6 +810,7 @@ class GpuPlanMaker:
         capped = [key_space(s) > max(0, thr) and key_space(s) > limit for s in segments]
         free = [s for s, c in zip(segments, capped) if not c]
         parts = []
+        st = ExecutionStats()
         if free:
             r = self.execute(query, free)
             parts.append((r.intermediate, r.stats))
@@ -825,10 +827,10 @@ class GpuPlanMaker:
             items = list(r.intermediate.items())
             if len(items) > limit:
                 items = sorted(items, key=lambda kv: kv[1][-1])[:limit]
+                st.num_groups_limit_reached = True
             parts.append(({k: v[:-1] for k, v in items}, r.stats))
         fns = [a.function for a in query.aggregations]
         merged: Dict[tuple, list] = {}
-        st = ExecutionStats()
         for inter, rs in parts:
             for k, v in inter.items():
                 cur = merged.get(k)

@@ -171,6 +171,7 @@ def test_first_seen_truncation_at_num_groups_limit(gpu_ctx, sql, limit):
     full = engine.execute(q, segs, num_groups_limit=10 ** 9)
     assert len(ref.group_rows) < len(full.group_rows)  # the limit really truncates
     _same(res, ref)
+    assert res.stats.num_groups_limit_reached
     assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
 
 
