@@ -93,25 +93,35 @@ def measure(ex, q, segs, steps, warmup, inflight, world, barrier):
     return elapsed * 1000.0 / steps, sum(kernel_ms) / len(kernel_ms), result
 
 
-def algorithmic_bytes(ex, pm, q, segs):
-    """forward-index bytes (dense tiles + 32-B sectors of sparse reads, exact from the kernel's
-    stats pass) + dictionary bytes read once per segment per query (bounded by one 32-B sector per matched doc when
-    few docs match) + inverted-index bitmap bytes + output bytes."""
+def algorithmic_bytes(ex, pm, q, segs, w, seg_ids, num_docs):
+    """SURVEY.md 8(d) algorithmic bytes of the workload (tools/bytemodel.py: from the segments' dict ids and the
+    reference's filter tree, the same figure whatever strategy the kernels pick), plus `bytes_read_model`: what this
+    build's kernels read by their own stats pass (streamed tiles + 32-B sectors of their gathers + dictionaries +
+    bitmaps + output), which moves with the strategy."""
+    import torch
+
+    from tools.bytemodel import output_bytes, workload_bytes
+
     pm.collect_stats = True
     r = ex.execute(q, segs)
     st = ex.last_stats
     pm.collect_stats = False
+    ngroups = len(r.group_rows or []) if r is not None else 1  # ranks != 0 return no rows
     dict_bytes = 0
     for c in sorted(set(a.column for a in q.aggregations if a.column)):
         width = {0: 4, 1: 8, 2: 4, 3: 8}.get(segs[0].column(c).data_type, 4)
         full = sum(s.column(c).cardinality * width for s in segs)
         dict_bytes += min(full, 32 * st.num_docs_scanned)
-    ngroups = len(r.group_rows or []) if r is not None else 1  # ranks != 0 return no rows
-    out_bytes = 8 * max(1, ngroups) * (1 + len(q.aggregations))
+    out_bytes = output_bytes(ngroups, len(q.aggregations))
     bitmap_bytes = inverted_bytes_read(q, segs)
-    total = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
-    return total, st, {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
-                       "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes, "output": out_bytes}
+    read = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
+    read_parts = {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
+                  "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes, "output": out_bytes}
+    algo, parts, matched = workload_bytes(w, q, segs, num_docs, seg_ids, torch.device("cuda", torch.cuda.current_device()),
+                                          ngroups=ngroups)
+    if matched != st.num_docs_scanned:  # the model regenerates the ids: it must see the docs the GPU matched
+        raise RuntimeError(f"byte model matched {matched} docs, the GPU {st.num_docs_scanned}")
+    return algo, st, parts, read, read_parts
 
 
 def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier):
@@ -136,9 +146,10 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
     pm = GpuPlanMaker(ctx, **plan_options(opts))
     ex = DistributedExecutor(pm)
     try:
-        algo_bytes, st, breakdown = algorithmic_bytes(ex, pm, q, segs)
+        algo_bytes, st, breakdown, read_bytes, read_breakdown = algorithmic_bytes(ex, pm, q, segs, w, seg_ids,
+                                                                                  args.docs)
         log(f"{name}: stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, "
-            f"{st.kernel_ms:.3f} ms")
+            f"{read_bytes / 1e9:.3f} GB read by the kernels, {st.kernel_ms:.3f} ms")
         ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight, world, barrier)
         rows_per_gpu = nseg * args.docs
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
@@ -158,7 +169,9 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
-                         "kernel_ms_avg": avg_kernel_ms, "bytes_breakdown": breakdown},
+                         "kernel_ms_avg": avg_kernel_ms, "bytes_breakdown": breakdown,
+                         "bytes_definition": "SURVEY 8(d) workload bytes (tools/bytemodel.py), strategy-independent",
+                         "bytes_read_model": read_bytes, "bytes_read_breakdown": read_breakdown},
             "cpu_baseline": cpu,
             "result": {"matched_docs_per_gpu": st.num_docs_scanned,
                        "groups": (len(result.group_rows) if result and result.group_rows is not None else None),
@@ -174,7 +187,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
 # Secondary workloads measured after the headline in the default run (BASELINE.json configs 2-4 and the SURVEY 8(d)
 # variants): (name, steps, warmup, segments per GPU or 0 = the workload's own, CPU sample seconds)
 SECONDARY = [("range_in", 10, 2, 0, 3.0), ("groupby1m", 5, 1, 0, 3.0), ("bitmap5", 10, 2, 0, 3.0),
-             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 8, 3.0), ("adanalytics_exact", 10, 2, 0, 2.0)]
+             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 0, 3.0), ("adanalytics_exact", 10, 2, 0, 2.0)]
 
 
 def main():
