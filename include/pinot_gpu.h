@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 7
+#define PGPU_ABI_VERSION 8
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -356,11 +356,13 @@ typedef struct {
   int64_t num_docs_scanned;              /* docs matching the filter (AggregationOperator.java:82-87) */
   int64_t num_entries_scanned_in_filter; /* GPU-evaluated forward-index entries, or the reference's count */
   int64_t num_total_docs;
-  int64_t num_segments_matched;          /* reserved (0): per-segment match counts are not tracked */
+  int64_t num_segments_matched;          /* segments with at least one matching doc (CombineOperatorUtils.java:64-67) */
   int64_t sparse_sector_bytes;           /* PGPU_Q_STATS: 32-B sectors touched by sparse reads * 32 */
   int64_t dense_bytes;                   /* forward-index bytes streamed in dense (staged) mode */
   double kernel_ms;                      /* main query kernel time (HIP events on the query stream) */
   int64_t filter_stats_exact;            /* 1: num_entries_scanned_in_filter is the reference's figure */
+  int64_t num_groups_limit_reached;      /* 1: a segment met >= num_groups_limit distinct group keys
+                                            (AggregationGroupByOrderByOperator.java:111) */
 } pgpu_query_stats;
 
 /* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the partial table in
@@ -379,6 +381,12 @@ int pgpu_query_release(pgpu_query* query);
  * regions) and skips the rest of its work; the wait then returns PGPU_E_CANCELLED (PGPU_E_TIMEOUT when the
  * deadline fired it), and the query must still be released / collected. */
 int pgpu_query_cancel(pgpu_query* query);
+/* Per-segment numDocsScanned > 0 flags of a launched / submitted query: when the query's stats become valid
+ * (pgpu_query_wait / _collect) out[i] = 1 if segment i of the descriptor matched at least one doc, else 0.  `out`
+ * must hold the descriptor's num_segments bytes and outlive the wait.  Replaces the per-operator test of
+ * CombineOperatorUtils.setExecutionStatistics (:64-67) where several passes (filtered aggregations) share the
+ * segments and their numSegmentsMatched is the union, not the sum. */
+int pgpu_query_matched_segments(pgpu_query* query, uint8_t* out, int32_t num_segments);
 
 /* Compact a (reduced) table: copy every key with count > 0 to the host (dense: ascending by key; hash: in slot
  * order).

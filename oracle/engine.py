@@ -748,6 +748,7 @@ class SegmentResult:
     num_entries_scanned_post_filter: int = 0
     num_total_docs: int = 0
     matched: Optional[np.ndarray] = None
+    num_groups: int = 0                              # GroupByExecutor.getNumGroups (group-by only)
 
 
 def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int = 100_000,
@@ -783,6 +784,7 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
         return res
     if any(ds.seg.column(g).mv_forward is not None for g in query.group_by):
         res.groups = _group_multi_value(query, ds, docs, num_groups_limit, max_init_group_holder_capacity)
+        res.num_groups = len(res.groups)
         return res
     # group keys: the tuple of dict ids (raw key = sum_j dictId_j * prod_{k<j} card_k when it fits a long); a raw
     # (no-dictionary) group column keys by value (_raw_group_ids)
@@ -805,6 +807,8 @@ def execute_segment(query: QueryContext, seg: SegmentData, num_groups_limit: int
         # map-based holder: only the first `limit` distinct keys (in doc order) get group ids
         keep_groups[:] = False
         keep_groups[np.argsort(first, kind="stable")[:num_groups_limit]] = True
+    # the holder's key count: every distinct key (array-based) or at most the limit (map-based)
+    res.num_groups = int(np.count_nonzero(keep_groups))
     order = np.argsort(inv, kind="stable")  # stable: docs stay in doc order inside each group
     inv_s, docs_s = inv[order], docs[order]
     bounds = np.flatnonzero(np.diff(inv_s)) + 1
@@ -931,6 +935,9 @@ class OracleResult:
     num_entries_scanned_in_filter: int = 0
     num_entries_scanned_post_filter: int = 0
     num_total_docs: int = 0
+    num_segments_matched: int = 0                    # CombineOperatorUtils.java:64-67: numDocsScanned > 0
+    num_groups_limit_reached: bool = False           # AggregationGroupByOrderByOperator.java:111 (any segment)
+    segment_matched: Optional[List[bool]] = None     # per segment, for the union over filtered-aggregation passes
 
 
 def execute(query, segments: Sequence[SegmentData], num_groups_limit: int = 100_000,
@@ -946,9 +953,14 @@ def execute(query, segments: Sequence[SegmentData], num_groups_limit: int = 100_
     decoded: Dict[int, DecodedSegment] = {}
     agg = None
     groups: Dict[tuple, list] = {}
+    out.segment_matched = []
     for s in segments:
         ds = decoded.setdefault(id(s), DecodedSegment(s))
         r = execute_segment(query, ds, num_groups_limit, max_init_group_holder_capacity, iterator_stats)
+        out.segment_matched.append(r.num_docs_scanned > 0)
+        out.num_segments_matched += int(r.num_docs_scanned > 0)
+        if query.group_by and num_groups_limit > 0 and r.num_groups >= num_groups_limit:
+            out.num_groups_limit_reached = True
         out.num_docs_scanned += r.num_docs_scanned
         out.num_entries_scanned_in_filter += r.num_entries_scanned_in_filter
         out.num_entries_scanned_post_filter += r.num_entries_scanned_post_filter
@@ -996,8 +1008,11 @@ def _execute_filtered(query: QueryContext, segments, num_groups_limit, max_init,
     out = OracleResult()
     n = len(query.aggregations)
     fin, inter = [None] * n, [None] * n
+    out.segment_matched = [False] * len(segments)
     for sq, idx in _split_filtered(query):
         r = execute(sq, segments, num_groups_limit, max_init, iterator_stats)
+        # one FilteredAggregationOperator per segment sums its passes' numDocsScanned
+        out.segment_matched = [a or b for a, b in zip(out.segment_matched, r.segment_matched)]
         for j, i in enumerate(idx):
             fin[i] = r.aggregation_result[j]
             inter[i] = r.intermediate[()][j]
@@ -1005,6 +1020,7 @@ def _execute_filtered(query: QueryContext, segments, num_groups_limit, max_init,
         out.num_entries_scanned_in_filter += r.num_entries_scanned_in_filter
         out.num_entries_scanned_post_filter += r.num_entries_scanned_post_filter
         out.num_total_docs = r.num_total_docs
+    out.num_segments_matched = sum(out.segment_matched)
     out.aggregation_result = fin
     out.intermediate = {(): inter}
     out.rows = [tuple(fin[query.aggregations.index(s)] for s in query.select)]

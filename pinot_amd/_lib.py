@@ -38,7 +38,7 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class PinotGpuError(RuntimeError):
@@ -103,7 +103,7 @@ class QueryStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_total_docs", C.c_int64), ("num_segments_matched", C.c_int64),
                 ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double),
-                ("filter_stats_exact", C.c_int64)]
+                ("filter_stats_exact", C.c_int64), ("num_groups_limit_reached", C.c_int64)]
 
 
 PGPU_TOPK_AGG, PGPU_TOPK_GROUP = 0, 1
@@ -160,6 +160,7 @@ SIGNATURES = [
     ("pgpu_query_wait", C.c_int, [_P, C.POINTER(QueryStats)]),
     ("pgpu_query_release", C.c_int, [_P]),
     ("pgpu_query_cancel", C.c_int, [_P]),
+    ("pgpu_query_matched_segments", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32]),
     ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_table_topk", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(TopK), C.POINTER(C.c_int64),

@@ -196,7 +196,11 @@ def merge_rows(keys: np.ndarray, cells: np.ndarray, L: TableLayout):
 
 
 STAT_FIELDS = ("num_docs_scanned", "num_entries_scanned_in_filter", "num_entries_scanned_post_filter",
-               "num_total_docs", "num_segments_processed", "sparse_sector_bytes", "dense_bytes")
+               "num_total_docs", "num_segments_processed", "num_segments_matched", "sparse_sector_bytes",
+               "dense_bytes")
+
+# local wait outcomes agreed by every rank before any collective touches the tables (collect)
+_WAIT_OK, _WAIT_GROUPS_LIMIT, _WAIT_FAILED = 0, 1, 2
 
 
 def _uids_of(key) -> tuple:
@@ -346,6 +350,8 @@ class DistributedExecutor:
             lib.pgpu_query_release(handle)
         return {"num_docs_scanned": st.num_docs_scanned, "num_entries_scanned_in_filter":
                 st.num_entries_scanned_in_filter, "num_total_docs": st.num_total_docs,
+                "num_segments_matched": st.num_segments_matched,
+                "num_groups_limit_reached": st.num_groups_limit_reached,
                 "sparse_sector_bytes": st.sparse_sector_bytes, "dense_bytes": st.dense_bytes,
                 "kernel_ms": st.kernel_ms, "filter_stats_exact": st.filter_stats_exact}
 
@@ -399,7 +405,7 @@ class DistributedExecutor:
             table.view(len(ops), -1).copy_(torch.tensor([[section_identity(o)] for o in ops], dtype=torch.int64)
                                            .expand(len(ops), int(L.num_keys)))
         return _DistPending(query, L, table, handle, globals_,
-                            [s for s, ns in zip(segments, non_scan) if ns], len(segments))
+                            [s for s, ns in zip(segments, non_scan) if ns], len(segments), segments)
 
     def _fold_non_scan(self, p: "_DistPending", stats: dict) -> None:
         """NonScanBasedAggregationOperator answers (NonScanBasedAggregationOperator.java:85-101,253-256) folded
@@ -421,6 +427,7 @@ class DistributedExecutor:
                 view[sec, 0] = min(cur, k) if a.function == "MIN" else max(cur, k)
         stats["num_docs_scanned"] += cnt
         stats["num_total_docs"] += cnt
+        stats["num_segments_matched"] += sum(1 for s in p.non_scan if s.num_docs > 0)
 
     def collect(self, pending) -> Optional[QueryResult]:
         """Wait for this rank's launch, merge the partial tables over the collectives; rank 0 finishes."""
@@ -430,20 +437,37 @@ class DistributedExecutor:
             return res
         p = pending
         stats = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
+                 "num_segments_matched": 0, "num_groups_limit_reached": 0,
                  "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
+        # the local wait may fail on some ranks only (a segment past numGroupsLimit, a deadline): every rank learns
+        # the worst outcome before the next collective, so no rank is left waiting in one
+        status, err = _WAIT_OK, None
         if p.handle is not None:
             h, p.handle = p.handle, None
-            stats.update(self._wait_local(h))
+            try:
+                stats.update(self._wait_local(h))
+            except _lib.GroupsLimitError as e:
+                status, err = _WAIT_GROUPS_LIMIT, e
+            except _lib.PinotGpuError as e:
+                status, err = _WAIT_FAILED, e
+        worst = self._allreduce_i64([status], "max")[0]
+        if worst != _WAIT_OK:
+            self._tables.setdefault(int(p.table.numel()), []).append(p.table)
+            if worst == _WAIT_FAILED:
+                raise err if status == _WAIT_FAILED else _lib.PinotGpuError(
+                    _lib.PGPU_E_INVALID, "the query failed on another rank")
+            return self._collect_first_seen(p)
         self._fold_non_scan(p, stats)
         query, L, table = p.query, p.layout, p.table
         scan_docs = stats["num_docs_scanned"] - sum(s.num_docs for s in p.non_scan)
         local = [stats["num_docs_scanned"], stats["num_entries_scanned_in_filter"],
                  scan_docs * len(query.projected_columns), stats["num_total_docs"], p.num_segments,
-                 stats["sparse_sector_bytes"], stats["dense_bytes"], 0 if stats.get("filter_stats_exact", 1) else 1]
+                 stats["num_segments_matched"], stats["sparse_sector_bytes"], stats["dense_bytes"],
+                 int(bool(stats["num_groups_limit_reached"])), 0 if stats.get("filter_stats_exact", 1) else 1]
         sums = self._allreduce_i64(local)
         tot = dict(zip(STAT_FIELDS, sums))
         st = ExecutionStats(kernel_ms=stats["kernel_ms"], filter_stats_exact=sums[-1] == 0,  # this rank's kernel
-                            **tot)
+                            num_groups_limit_reached=sums[-2] > 0, **tot)
         self.last_stats = st
         try:
             big = query.group_by and 8 * int(table.numel()) >= self.SCATTER_MIN_BYTES
@@ -465,6 +489,35 @@ class DistributedExecutor:
             return finish(query, GroupTable.sorted(keys, cells, L), p.globals_, st)
         finally:
             self._tables.setdefault(int(table.numel()), []).append(table)
+
+    def _collect_first_seen(self, p: "_DistPending") -> Optional[QueryResult]:
+        """Some rank's segment met more distinct group keys than numGroupsLimit: every rank answers its own
+        segments by the first-seen path (GpuPlanMaker.first_seen_groups: the reference's map-based holders keep
+        the first `limit` keys of each segment), and rank 0 merges the ranks' intermediate groups per aggregation
+        function (GroupByOrderByCombineOperator's per-key merge) and finishes.  The rare path, so the exchange is
+        one object all-gather rather than the table collectives."""
+        import torch.distributed as dist
+
+        from .datatable import _merge
+        from .plan import result_from_intermediate
+        r = self.pm.first_seen_groups(p.query, p.segments)
+        mine = (r.intermediate, {f: getattr(r.stats, f) for f in STAT_FIELDS},
+                bool(r.stats.num_groups_limit_reached), bool(r.stats.filter_stats_exact), r.stats.kernel_ms)
+        every = [None] * self.world
+        dist.all_gather_object(every, mine, group=self.group)
+        tot = {f: sum(e[1][f] for e in every) for f in STAT_FIELDS}
+        st = ExecutionStats(kernel_ms=r.stats.kernel_ms, num_groups_limit_reached=any(e[2] for e in every),
+                            filter_stats_exact=all(e[3] for e in every), **tot)
+        self.last_stats = st
+        if self.rank != 0:
+            return None
+        fns = [a.function for a in p.query.aggregations]
+        merged: Dict[tuple, list] = {}
+        for inter, *_ in every:
+            for k, v in inter.items():
+                cur = merged.get(k)
+                merged[k] = list(v) if cur is None else [_merge(fn, x, y) for fn, x, y in zip(fns, cur, v)]
+        return result_from_intermediate(p.query, merged, st)
 
     def _trim_cap(self, query) -> int:
         """GroupByUtils.getTableCapacity(limit, min.server.group.trim.size) of the plan maker (TOPK_MIN without
@@ -577,9 +630,10 @@ class DistributedExecutor:
 class _DistPending:
     """A launched, not yet collected multi-GPU query of this rank."""
 
-    def __init__(self, query, layout, table, handle, globals_, non_scan, num_segments):
+    def __init__(self, query, layout, table, handle, globals_, non_scan, num_segments, segments=()):
         self.query, self.layout, self.table, self.handle = query, layout, table, handle
         self.globals_, self.non_scan, self.num_segments = globals_, non_scan, num_segments
+        self.segments = list(segments)
 
     def __del__(self):
         if self.handle is not None and getattr(self.handle, "value", None):

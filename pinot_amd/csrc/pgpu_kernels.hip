@@ -942,6 +942,12 @@ struct SegState {
   int32_t f_sneg[2];
   uint32_t f_lo[2], f_span[2];
 };
+// numSegmentsMatched (CombineOperatorUtils.java:64-67: a segment counts when its numDocsScanned > 0): a plain store of
+// 1 by lane 0 of any wave that matched docs of the segment (same value from every writer, no atomic needed).  `any`
+// must be wave-uniform.
+FI void mark_seg(const DevParams& p, const SegState& ss, bool any) {
+  if (any && lane_id() == 0) p.segany[ss.sg - p.segs] = 1u;
+}
 FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   const DevSeg* sg = p.segs + seg;
   ss.sg = sg;
@@ -1555,6 +1561,7 @@ FI void flush_queue(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& l
     if (ss.rprog_len > 0) m = run_program(p, cv, ss.rprog_begin, ss.rprog_len, d, scanned, dense_bytes, pf);
     const int nm = wave_sum_i32(__popc(m));
     if (lane == 0) matched += nm;
+    mark_seg(p, ss, nm != 0);
     if (stats) {
       // 32-B sectors of every gathered forward index: residual scan columns over the candidates,
       // aggregation / group columns over the survivors
@@ -1964,9 +1971,11 @@ FI Stats consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles
     if (nm) {
       if (DENSE && dense) {
         if (lane == 0) matched += nm;
+        mark_seg(p, ss, true);
         dense_agg<MODE>(p, L, cv, la, ss, t, mm, ra, rb);
       } else if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
         if (lane == 0) matched += nm;
+        mark_seg(p, ss, true);
       } else if (qn + nm <= PGPU_CQ_CAP) {
         // queue the candidates (ascending: lane order, then bit order) as queue-tile index << 11 | doc in tile
         if (lane == 0) cv.qtiles[qt] = cur.tile_in_seg;
@@ -2084,6 +2093,7 @@ FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, Lane
   const int lane = lane_id();
   if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
     lane_matched += __popc(mm);
+    mark_seg(p, ss, __builtin_amdgcn_ballot_w64(mm != 0) != 0);
   } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
     const int cnt = __popc(mm);
     const int ex = wave_excl_scan(cnt);
@@ -2824,6 +2834,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
       if (ss.prog_len > 0) mm = run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned, dense_bytes, pf);
       const int nm = wave_sum_i32(__popc(mm));
       if (lane == 0) matched += nm;
+      if (!COUNT) mark_seg(p, ss, nm != 0);
       if (nm) {
         // group keys (mixed radix of remapped ids) and the carried value / dict id, in registers
         uint32_t key[32], val[32];
@@ -3409,6 +3420,14 @@ __global__ __launch_bounds__(256) void segcount_kernel(DevParams p, int64_t* out
   }
   if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
+// numSegmentsMatched: the per-segment match words into pinned host memory (one byte per segment), each word reset to
+// 0 for the workspace's next query.
+__global__ __launch_bounds__(256) void segflags_kernel(uint32_t* segany, uint8_t* out, int32_t n) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    out[i] = segany[i] != 0u ? 1 : 0;
+    segany[i] = 0u;
+  }
+}
 // Copy `words` int64 of a finished table into pinned host memory.
 __global__ __launch_bounds__(256) void export_kernel(const int64_t* __restrict__ src, int64_t* dst, uint64_t words) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) dst[i] = src[i];
@@ -3907,6 +3926,12 @@ hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_sme
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
   if (p.total_tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(leafbits_kernel, dim3((p.total_tiles + 3) / 4), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st) {
+  if (p.nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(segflags_kernel, dim3(std::min(64, (p.nseg + 255) / 256)), dim3(256), 0, st, p.segany, out, p.nseg);
   return hipGetLastError();
 }
 

@@ -280,6 +280,8 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
     tot.num_docs_scanned += st.num_docs_scanned;
     tot.num_entries_scanned_in_filter += st.num_entries_scanned_in_filter;
     tot.num_total_docs += st.num_total_docs;
+    tot.num_segments_matched += st.num_segments_matched;  // the devices' segments are disjoint
+    tot.num_groups_limit_reached |= st.num_groups_limit_reached;
     tot.sparse_sector_bytes += st.sparse_sector_bytes;
     tot.dense_bytes += st.dense_bytes;
     tot.kernel_ms = std::max(tot.kernel_ms, st.kernel_ms);

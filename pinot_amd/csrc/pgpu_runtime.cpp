@@ -48,6 +48,7 @@ hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, i
 hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, uint64_t* okey, TopkState* ts,
                             uint32_t* hist, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
+hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
@@ -197,9 +198,10 @@ struct Workspace {
   DevMem pcount, pcap, poff, p2work;   // PART region sizing / phase-2 plan (part_plan_kernel)
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
+  DevMem segany;                       // per-segment matched words (DevParams::segany), zero between queries
   DevMem rawbits;                      // match bitmaps of the raw-value leaves (rawpred_kernel)
   DevMem tk_keys, tk_state;            // pgpu_table_topk: per-row order keys, radix-select state + histogram
-  PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits;
+  PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits, h_segany;
   DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
   PinnedMem h_cancel;                  // its source for pgpu_query_cancel's copy-engine write
   uint32_t cancel_gen = 0;
@@ -300,6 +302,7 @@ struct pgpu_query {
   bool eager_ordered = false;  // ... restricted to the best groups by the order given at submit
   // HASH mode: tracked segments (query segment index) whose distinct keys are checked against the limit
   std::vector<int32_t> tracked;
+  std::vector<uint8_t> tracked_map;  // per tracked segment: its holder is map-based (keys past the limit dropped)
   int64_t groups_limit = 0;
   // PGPU_Q_EXACT_FILTER_STATS: each segment's program (ids copied) and where its leaf bitmaps are
   struct FilterReplay {
@@ -309,6 +312,7 @@ struct pgpu_query {
     int64_t bits_off = 0;
     std::vector<const int32_t*> leaf_off;  // per leaf: row offsets of a multi-value SCAN leaf, else null
   };
+  uint8_t* matched_out = nullptr;  // pgpu_query_matched_segments: caller's per-segment flags, filled by the wait
   int64_t mv_entries = 0;  // entries of multi-value SCAN leaves that are a segment's whole filter (kernel: nostat)
   std::vector<FilterReplay> replay;
   bool exact_filter = false;
@@ -401,11 +405,16 @@ unsigned __int128 local_key_space(const pgpu_query_desc* q, const pgpu_segment_p
 // DictionaryBasedGroupKeyGenerator's holder choice for one segment (DictionaryBasedGroupKeyGenerator.java:137-164):
 // a map-based holder (product above the array threshold) stops at num_groups_limit distinct keys, so such a
 // segment whose product also exceeds the limit must have its distinct keys counted.
+// numGroupsLimit: a segment's distinct group keys are counted on the GPU when they can reach the limit -- for the
+// numGroupsLimitReached flag (AggregationGroupByOrderByOperator.java:111: numGroups >= numGroupsLimit) and, when
+// its holder is map-based (key space above the array-based threshold, DictionaryBasedGroupKeyGenerator.java:137-164),
+// for the first-seen cut of the keys past the limit (PGPU_E_GROUPS_LIMIT).
 bool segment_needs_count(const pgpu_query_desc* q, const pgpu_segment_plan& sp) {
   if (q->num_group_columns == 0 || q->num_groups_limit <= 0) return false;
-  const unsigned __int128 P = local_key_space(q, sp);
-  return P > (unsigned __int128)std::max(0, q->array_based_threshold) &&
-         P > (unsigned __int128)q->num_groups_limit;
+  return local_key_space(q, sp) >= (unsigned __int128)q->num_groups_limit;
+}
+bool segment_map_based(const pgpu_query_desc* q, const pgpu_segment_plan& sp) {
+  return local_key_space(q, sp) > (unsigned __int128)std::max(0, q->array_based_threshold);
 }
 
 // Table shape of the group keys: dense (cell = mixed-radix key) or hash slots (key words stored per slot).
@@ -2575,6 +2584,17 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "filter-statistics bitmaps: %s", hipGetErrorString(e)));
     p.leaf_bits = (uint32_t*)ws->leafbits.p;
   }
+  {
+    // numSegmentsMatched words: grown in stream order and zeroed once; segflags_kernel resets them after each query
+    const size_t want = 4ull * std::max(1, p.nseg);
+    if (ws->segany.n < want) {
+      e = ws->segany.ensure(want, ctx->mpool, st);
+      if (e == hipSuccess) e = hipMemsetAsync(ws->segany.p, 0, ws->segany.n, st);
+    }
+    if (e == hipSuccess) e = ws->h_segany.ensure((size_t)std::max(1, p.nseg));
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "segment match words: %s", hipGetErrorString(e)));
+    p.segany = (uint32_t*)ws->segany.p;
+  }
   if (p.mode == PGPU_MODE_HASH) {
     p.segmask_rows = (int32_t)pk.tracked.size();
     e = ws->hflag.ensure(16, ctx->mpool, st);
@@ -2659,6 +2679,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
+  if (e == hipSuccess) {
+    void* h_seg_dev = nullptr;
+    e = hipHostGetDevicePointer(&h_seg_dev, ws->h_segany.p, 0);
+    if (e == hipSuccess) e = pgpu_launch_segflags(p, (uint8_t*)h_seg_dev, st);
+  }
   if (e == hipSuccess && p.mode == PGPU_MODE_HASH) {
     // probe-overflow flag and the tracked segments' distinct-key counts, into pinned host memory
     void* h_cnt_dev = nullptr;
@@ -2694,6 +2719,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   for (int s = 0; s < q->num_segments; ++s) tot_docs += q->segments[s].segment->num_docs;
   qq->stats.num_total_docs = tot_docs;
   qq->tracked = pk.tracked;
+  for (int32_t s : pk.tracked) qq->tracked_map.push_back(segment_map_based(q, q->segments[s]) ? 1 : 0);
   qq->groups_limit = q->num_groups_limit;
   qq->exact_filter = pk.leaf_words > 0;
   bool exact = true;
@@ -2766,6 +2792,14 @@ static int signal_cancel(pgpu_query* qq) {
   return PGPU_OK;
 }
 
+int pgpu_query_matched_segments(pgpu_query* qq, uint8_t* out, int32_t num_segments) {
+  if (!qq || !out) return fail(PGPU_E_INVALID, "null argument");
+  if (num_segments != qq->params.nseg)
+    return fail(PGPU_E_INVALID, "matched-segment flags: %d entries for a %d-segment query", num_segments, qq->params.nseg);
+  qq->matched_out = out;
+  return PGPU_OK;
+}
+
 int pgpu_query_cancel(pgpu_query* qq) {
   if (!qq) return fail(PGPU_E_INVALID, "null query");
   int none = 0;
@@ -2803,6 +2837,13 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   qq->stats.num_entries_scanned_in_filter = s[PGPU_STAT_SCANNED] + qq->mv_entries;
   qq->stats.sparse_sector_bytes = s[PGPU_STAT_SECTOR_BYTES];
   qq->stats.dense_bytes = s[PGPU_STAT_DENSE_BYTES];
+  {
+    const uint8_t* f = (const uint8_t*)qq->ws->h_segany.p;
+    int64_t nm = 0;
+    for (int i = 0; i < qq->params.nseg; ++i) nm += f[i] != 0;
+    qq->stats.num_segments_matched = nm;
+    if (qq->matched_out) memcpy(qq->matched_out, f, (size_t)qq->params.nseg);
+  }
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
@@ -2840,7 +2881,9 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
     }
     const int64_t* cnt = (const int64_t*)qq->ws->h_segcnt.p;
     for (size_t i = 0; i < qq->tracked.size(); ++i)
-      if (cnt[i] > qq->groups_limit) {
+      if (cnt[i] >= qq->groups_limit) qq->stats.num_groups_limit_reached = 1;
+    for (size_t i = 0; i < qq->tracked.size(); ++i)
+      if (cnt[i] > qq->groups_limit && qq->tracked_map[i]) {
         if (out_stats) *out_stats = qq->stats;
         return fail(PGPU_E_GROUPS_LIMIT,
                     "segment %d meets %lld distinct group keys > numGroupsLimit %lld: the reference keeps the "

@@ -250,6 +250,8 @@ class DataTable:
             (n,), pos = struct.unpack_from(">i", b, pos), pos + 4
             for _ in range(n):
                 (ordinal,), pos = struct.unpack_from(">i", b, pos), pos + 4
+                # MetadataKey.getByOrdinal clamps to the last key, as the reference does (DataTable.java:128-130;
+                # its "null" branch at DataTableImplV3.java:351-355 is unreachable)
                 name, kind = METADATA_KEYS[min(ordinal, len(METADATA_KEYS) - 1)]
                 if kind == "I":
                     metadata[name] = str(struct.unpack_from(">i", b, pos)[0])
@@ -304,7 +306,7 @@ def server_data_table(query: QueryContext, result, group_types: Sequence[int] = 
           "numEntriesScannedInFilter": str(st.num_entries_scanned_in_filter),
           "numEntriesScannedPostFilter": str(st.num_entries_scanned_post_filter),
           "numSegmentsProcessed": str(st.num_segments_processed),
-          "numSegmentsMatched": str(st.num_segments_processed if st.num_docs_scanned else 0),
+          "numSegmentsMatched": str(st.num_segments_matched),
           "numResizes": "0", "resizeTimeMs": "0", "totalDocs": str(st.num_total_docs)}
     if getattr(st, "num_groups_limit_reached", False):  # DataTable.MetadataKey.NUM_GROUPS_LIMIT_REACHED
         md["numGroupsLimitReached"] = "true"

@@ -289,7 +289,9 @@ class ExecutionStats:
     filter_stats_exact: bool = True          # num_entries_scanned_in_filter is the reference's figure
     sparse_sector_bytes: int = 0
     dense_bytes: int = 0
-    num_groups_limit_reached: bool = False   # some segment's holder stopped at numGroupsLimit (first_seen_groups)
+    num_groups_limit_reached: bool = False   # some segment met >= numGroupsLimit distinct group keys
+    num_segments_matched: int = 0            # segments with numDocsScanned > 0 (CombineOperatorUtils.java:64-67)
+    segment_matched: Optional[np.ndarray] = None  # per segment of the launch (uint8), for unions over passes
 
 
 def key_words_out(L: TableLayout) -> int:
@@ -730,6 +732,9 @@ class GpuPlanMaker:
             C.byref(order) if order is not None else None, C.byref(h)))
         pq = PendingQuery(self, query, len(segments), h, L, globals_)
         pq.order = order
+        pq.matched = np.zeros(max(1, len(segments)), dtype=np.uint8)
+        _lib.check(self.ctx._lib.pgpu_query_matched_segments(h, pq.matched.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                             len(segments)))
         return pq
 
     def trim_order(self, query: QueryContext, globals_) -> Optional[_lib.TopK]:
@@ -767,7 +772,10 @@ class GpuPlanMaker:
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
                                num_total_docs=st.num_total_docs, num_segments_processed=pending.num_segments,
                                kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
-                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact))
+                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact),
+                               num_groups_limit_reached=bool(st.num_groups_limit_reached),
+                               num_segments_matched=st.num_segments_matched,
+                               segment_matched=pending.matched[:pending.num_segments].copy())
         return finish(query, table, [g[0] for g in pending.globals_], stats)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
@@ -793,7 +801,7 @@ class GpuPlanMaker:
         other segment runs alone with no limit plus MIN over its doc-id column (GpuSegment.docid_view), i.e. every
         group's first doc, and keeps the num_groups_limit groups of smallest first doc.  The partial results merge
         as the combine merges segment results (AggregationFunction.merge)."""
-        from .datatable import _final, _merge
+        from .datatable import _merge
         if any(s.column(g).is_mv for s in segments for g in query.group_by):
             raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
                                             "numGroupsLimit on a multi-value group key (first-seen order per value)")
@@ -825,7 +833,7 @@ class GpuPlanMaker:
             s.docid_view()
             r = sub.execute(probe, [s])
             items = list(r.intermediate.items())
-            if len(items) > limit:
+            if len(items) >= limit:  # numGroups >= numGroupsLimit (AggregationGroupByOrderByOperator.java:111)
                 items = sorted(items, key=lambda kv: kv[1][-1])[:limit]
                 st.num_groups_limit_reached = True
             parts.append(({k: v[:-1] for k, v in items}, r.stats))
@@ -836,17 +844,12 @@ class GpuPlanMaker:
                 cur = merged.get(k)
                 merged[k] = list(v) if cur is None else [_merge(fn, x, y) for fn, x, y in zip(fns, cur, v)]
             for f in ("num_docs_scanned", "num_entries_scanned_in_filter", "num_total_docs", "num_segments_processed",
-                      "kernel_ms", "sparse_sector_bytes", "dense_bytes"):
+                      "num_segments_matched", "kernel_ms", "sparse_sector_bytes", "dense_bytes"):
                 setattr(st, f, getattr(st, f) + getattr(rs, f))
             st.filter_stats_exact = st.filter_stats_exact and rs.filter_stats_exact
+            st.num_groups_limit_reached = st.num_groups_limit_reached or rs.num_groups_limit_reached
         st.num_entries_scanned_post_filter = st.num_docs_scanned * len(query.projected_columns)
-        ng = len(query.group_by)
-        finals = [k + tuple(_final(fn, x) for fn, x in zip(fns, v)) for k, v in merged.items()]
-        res = QueryResult(query=query, stats=st)
-        res._intermediate = merged
-        res._group_rows = sorted(finals, key=lambda r: r[:ng])  # ascending keys: ORDER BY ties as the one-launch path
-        res.rows = [to_select_order(query, r) for r in order_and_limit(query, res._group_rows)]
-        return res
+        return result_from_intermediate(query, merged, st)
 
     def non_scan_segments(self, query: QueryContext, segments: Sequence[GpuSegment]) -> List[bool]:
         """Per segment, AggregationPlanNode.buildNonFilteredAggOperator's choice (core/plan/AggregationPlanNode.java
@@ -871,6 +874,7 @@ class PendingQuery:
     layout: TableLayout
     globals_: list
     mv: Optional[tuple] = None  # (original query, lowered aggregation indexes) when *MV aggregations were lowered
+    matched: Optional[np.ndarray] = None  # per-segment matched flags, filled by the wait (pgpu_query_matched_segments)
     order: Optional[object] = None  # the pgpu_topk given at submit (collect passes the same one)
 
     def cancel(self) -> None:
@@ -883,6 +887,19 @@ class PendingQuery:
         if self.handle is not None and self.handle.value:
             self.maker.ctx._lib.pgpu_query_release(self.handle)
             self.handle = None
+
+
+def result_from_intermediate(query: QueryContext, merged: Dict[tuple, list], st: ExecutionStats) -> QueryResult:
+    """A GROUP BY result from merged intermediate values per group key (the first-seen paths)."""
+    from .datatable import _final
+    fns = [a.function for a in query.aggregations]
+    ng = len(query.group_by)
+    finals = [k + tuple(_final(fn, x) for fn, x in zip(fns, v)) for k, v in merged.items()]
+    res = QueryResult(query=query, stats=st)
+    res._intermediate = merged
+    res._group_rows = sorted(finals, key=lambda r: r[:ng])  # ascending keys: ORDER BY ties as the one-launch path
+    res.rows = [to_select_order(query, r) for r in order_and_limit(query, res._group_rows)]
+    return res
 
 
 def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats: ExecutionStats) -> QueryResult:
@@ -940,10 +957,12 @@ def merge_non_scan(query: QueryContext, scanned: Optional[QueryResult], segments
                 v = min(v, lo) if a.function in ("MIN", "MINMV") else max(v, hi)
         vals.append(v)
     st = res.stats
+    st.segment_matched = None  # the launch's per-segment flags no longer line up with the caller's segments
     for s in segments:
         st.num_docs_scanned += s.num_docs
         st.num_total_docs += s.num_docs
         st.num_segments_processed += 1
+        st.num_segments_matched += int(s.num_docs > 0)  # numDocsScanned = numTotalDocs
     res.aggregation_result = vals
     res._intermediate = {(): list(vals)}
     res.rows = [to_select_order(query, tuple(vals))]
@@ -968,6 +987,13 @@ def merge_filtered(query: QueryContext, parts, results: Sequence[QueryResult]) -
         st.filter_stats_exact = st.filter_stats_exact and r.stats.filter_stats_exact
     st.num_total_docs = results[-1].stats.num_total_docs
     st.num_segments_processed = results[-1].stats.num_segments_processed
+    # one operator per segment sums its passes' numDocsScanned: a segment matched when any pass matched in it
+    flags = [r.stats.segment_matched for r in results]
+    if all(f is not None and len(f) == len(flags[0]) for f in flags):
+        st.segment_matched = np.bitwise_or.reduce(np.stack(flags), axis=0)
+        st.num_segments_matched = int(np.count_nonzero(st.segment_matched))
+    else:
+        st.num_segments_matched = max(r.stats.num_segments_matched for r in results)
     res.aggregation_result = fin
     res._intermediate = {(): inter}
     res.rows = [to_select_order(query, tuple(fin))]

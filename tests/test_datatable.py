@@ -107,7 +107,8 @@ class _Res:
         self.stats = ExecutionStats(num_docs_scanned=o.num_docs_scanned,
                                     num_entries_scanned_in_filter=o.num_entries_scanned_in_filter,
                                     num_entries_scanned_post_filter=o.num_entries_scanned_post_filter,
-                                    num_total_docs=o.num_total_docs, num_segments_processed=1)
+                                    num_total_docs=o.num_total_docs, num_segments_processed=1,
+                                    num_segments_matched=o.num_segments_matched)
 
 
 def _segments(seed, sizes):
@@ -148,6 +149,25 @@ def test_broker_reduce_of_server_tables_equals_oracle(sql):
     ref = engine.execute(q, segs)
     _rows_match(got.rows, ref.rows)
     assert got.num_docs_scanned == ref.num_docs_scanned and got.total_docs == ref.num_total_docs
+    assert got.num_segments_matched == ref.num_segments_matched
+
+
+def test_num_segments_matched_counts_segments_with_docs():
+    """CombineOperatorUtils.setExecutionStatistics (:64-67): numSegmentsMatched counts the segments whose operator
+    scanned a doc -- one server whose first segment matches and whose second does not reports 1."""
+    segs = _segments(5, [3000, 2000])
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE k < 30 AND m > 499")  # m < 500: nothing, unless the seed says so
+    o = engine.execute(q, segs)
+    q2 = parse_sql("SELECT COUNT(*) FROM t WHERE k < 30")
+    o2 = engine.execute(q2, segs[:1])
+    assert o.num_segments_matched == sum(o.segment_matched) == 0
+    assert o2.num_segments_matched == 1
+    mixed = engine.execute(parse_sql("SELECT COUNT(*) FROM t WHERE m > 490"), segs)
+    assert mixed.num_segments_matched == sum(mixed.segment_matched)
+    dt = DataTable.from_bytes(server_data_table(q2, _Res(o2)).to_bytes())
+    assert dt.metadata["numSegmentsMatched"] == "1"
+    assert reduce_data_tables(q2, [dt, DataTable.from_bytes(server_data_table(q, _Res(o)).to_bytes())]
+                              ).num_segments_matched == 1
 
 
 # ---- GPU -----------------------------------------------------------------------------------------------------------
@@ -172,4 +192,5 @@ def test_gpu_servers_through_datatables(gpu_ctx, sql):
     ref = engine.execute(q, segs)
     _rows_match(got.rows, ref.rows)
     assert got.num_docs_scanned == ref.num_docs_scanned
+    assert got.num_segments_matched == ref.num_segments_matched
     assert not any(isinstance(v, float) and math.isnan(v) for r in got.rows for v in r)

@@ -46,6 +46,9 @@ def _assert_same(res, ref, rel=1e-9):
     assert res.stats.num_docs_scanned == ref.num_docs_scanned
     assert res.stats.num_entries_scanned_post_filter == ref.num_entries_scanned_post_filter
     assert res.stats.num_total_docs == ref.num_total_docs
+    assert res.stats.num_segments_matched == ref.num_segments_matched
+    if res.query.group_by:
+        assert res.stats.num_groups_limit_reached == ref.num_groups_limit_reached
     if res.stats.filter_stats_exact and getattr(ref, "_iterator_stats", False):
         assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
 
