@@ -3406,6 +3406,145 @@ __global__ __launch_bounds__(256) void leafbits_kernel(DevParams p) {
   }
 }
 
+// ---- PGPU_Q_EXACT_FILTER_STATS on the GPU: AndDocIdIterator over scan iterators as a finite-state transducer ------
+// For a segment whose filter is one AND of k <= 4 SCAN leaves (AndDocIdSet.java:140-143: no index child, so the
+// reference leap-frogs AndDocIdIterator over the SVScanDocIdIterators), the reference's numEntriesScannedInFilter is
+// numDocs + H.  Every doc is read once by the iterator that is scanning when the walk reaches it, and H counts the
+// hand-offs: each advance(target) that starts on a doc another iterator has just read (AndDocIdIterator.java:40-67,
+// SVScanDocIdIterator.java:57-71).  The walk's state entering a doc is the scanning iterator s alone: when leaf s
+// matches doc d, iterators j = 0..k-1 (j != s) read d in turn (H += 1 each) until one misses -- that one scans on
+// (state j) -- or all match (an AND match: next() resumes iterator 0 at d + 1, state 0).  So each doc is a map
+// state -> (state', H increment); a tile's map is the composition of its docs' maps (per lane over its 32 docs, then
+// across lanes), a segment's the composition of its tiles' maps, evaluated from state 0.
+#define PGPU_ANDFSM_WORDS 8  // per tile: next-state bits (2 per start state), then H per start state
+FI uint32_t sel4(const uint32_t (&v)[4], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3]; }
+
+__global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t* fn) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = (int)blockIdx.x * 4 + wave;
+  if (tile >= p.total_tiles) return;
+  const Cursor c = cursor_at(p, tile);
+  SegState ss;
+  load_seg(p, c.seg, ss);
+  const int k = cld(&ss.sg->leaf_len);
+  const int leaf_begin = cld(&ss.sg->leaf_begin);
+  TileCtx t;
+  t.ss = &ss;
+  t.slot = nullptr;
+  t.tile_in_seg = c.tile_in_seg;
+  t.doc0 = c.tile_in_seg * WT;
+  t.lane_doc0 = t.doc0 + 32 * lane;
+  {
+    const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+    t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+  }
+  int64_t dummy = 0;
+  uint32_t m[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j >= k) break;
+    const DevInstr in = cld(p.instrs + cld(p.pool, leaf_begin + j));
+    m[j] = (in.op == PGPU_I_SCAN ? leaf_scan(p, t, in, t.valid, dummy) : leaf_bits(t, in)) & t.valid;
+  }
+  // this lane's map over its 32 docs, per start state
+  uint32_t nxt = 0, h[4] = {0u, 0u, 0u, 0u};
+  for (int s0 = 0; s0 < k; ++s0) {
+    int st = s0;
+    uint32_t hh = 0;
+    int pos = 0;
+    while (pos < 32) {
+      const uint32_t w = sel4(m, st) >> pos;
+      if (!w) break;
+      const int d = pos + __builtin_ctz(w);
+      int ns = -1;
+      for (int j = 0; j < k; ++j) {
+        if (j == st) continue;
+        ++hh;
+        if (!((sel4(m, j) >> d) & 1u)) {
+          ns = j;
+          break;
+        }
+      }
+      st = ns < 0 ? 0 : ns;
+      pos = d + 1;
+    }
+    nxt |= (uint32_t)st << (2 * s0);
+    if (s0 == 0) h[0] = hh;
+    else if (s0 == 1) h[1] = hh;
+    else if (s0 == 2) h[2] = hh;
+    else h[3] = hh;
+  }
+  for (int s0 = k; s0 < 4; ++s0) nxt |= (uint32_t)s0 << (2 * s0);  // unused states: identity
+  // compose across lanes in doc order: lane l's map first, then lane l + o's
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t rn = (uint32_t)__shfl_down((int)nxt, o, 64);
+    uint32_t rh[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rh[s] = (uint32_t)__shfl_down((int)h[s], o, 64);
+    if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
+      uint32_t nn = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int mid = (int)((nxt >> (2 * s)) & 3u);
+        nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
+        h[s] += sel4(rh, mid);
+      }
+      nxt = nn;
+    }
+  }
+  if (lane == 0) {
+    uint32_t* o = fn + (size_t)tile * PGPU_ANDFSM_WORDS;
+    o[0] = nxt;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) o[1 + s] = h[s];
+  }
+}
+
+// One workgroup per segment: compose its tiles' maps in order and write numDocs + H (from state 0) -- the
+// reference's numEntriesScannedInFilter of the segment -- into pinned host memory.
+__global__ __launch_bounds__(256) void andfsm_segment_kernel(DevParams p, const uint32_t* fn, int64_t* out) {
+  __shared__ uint32_t s_n[256];
+  __shared__ uint64_t s_h[256][4];
+  const int seg = blockIdx.x, t = threadIdx.x;
+  const int nt = cld(&p.segs[seg].ntiles), t0 = cld(&p.segs[seg].tile_begin);
+  const int per = (nt + 255) / 256;
+  uint32_t nxt = 0xE4u;  // identity: state s -> s
+  uint64_t h[4] = {0, 0, 0, 0};
+  for (int i = t * per; i < min(nt, (t + 1) * per); ++i) {
+    const uint32_t* f = fn + (size_t)(t0 + i) * PGPU_ANDFSM_WORDS;
+    const uint32_t rn = f[0];
+    uint32_t nn = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int mid = (int)((nxt >> (2 * s)) & 3u);
+      nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
+      h[s] += f[1 + mid];
+    }
+    nxt = nn;
+  }
+  s_n[t] = nxt;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) s_h[t][s] = h[s];
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    if ((t & (2 * o - 1)) == 0) {
+      const uint32_t ln = s_n[t], rn = s_n[t + o];
+      uint32_t nn = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int mid = (int)((ln >> (2 * s)) & 3u);
+        nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
+        s_h[t][s] += s_h[t + o][mid];
+      }
+      s_n[t] = nn;
+    }
+    __syncthreads();
+  }
+  // no scan leaf (match-all / empty filter): no entries
+  if (t == 0) out[seg] = nt > 0 && cld(&p.segs[seg].leaf_len) > 0 ? (int64_t)cld(&p.segs[seg].num_docs) + (int64_t)s_h[0][0] : 0;
+}
+
 // Distinct group keys of each tracked segment: popcount of its bitmap row (HASH mode, num_groups_limit).
 __global__ __launch_bounds__(256) void segcount_kernel(DevParams p, int64_t* out) {
   const uint32_t* row = p.segmask + (size_t)blockIdx.x * (p.G >> 5);
@@ -3926,6 +4065,13 @@ hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_sme
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
   if (p.total_tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(leafbits_kernel, dim3((p.total_tiles + 3) / 4), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st) {
+  if (p.nseg <= 0) return hipSuccess;
+  if (p.total_tiles > 0) hipLaunchKernelGGL(andfsm_tile_kernel, dim3((p.total_tiles + 3) / 4), dim3(256), 0, st, p, fn);
+  hipLaunchKernelGGL(andfsm_segment_kernel, dim3(p.nseg), dim3(256), 0, st, p, (const uint32_t*)fn, out);
   return hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, 
                             uint32_t* hist, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st);
+hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
@@ -199,9 +200,10 @@ struct Workspace {
   DevMem segmask, hflag;               // HASH mode: distinct-key bitmaps of tracked segments, probe-overflow flag
   DevMem leafbits;                     // PGPU_Q_EXACT_FILTER_STATS: per-leaf match bits of every segment
   DevMem segany;                       // per-segment matched words (DevParams::segany), zero between queries
+  DevMem fsmfn;                        // exact filter stats on the GPU: per-tile transducer maps (andfsm kernels)
   DevMem rawbits;                      // match bitmaps of the raw-value leaves (rawpred_kernel)
   DevMem tk_keys, tk_state;            // pgpu_table_topk: per-row order keys, radix-select state + histogram
-  PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits, h_segany;
+  PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits, h_segany, h_fsment;
   DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
   PinnedMem h_cancel;                  // its source for pgpu_query_cancel's copy-engine write
   uint32_t cancel_gen = 0;
@@ -316,6 +318,7 @@ struct pgpu_query {
   int64_t mv_entries = 0;  // entries of multi-value SCAN leaves that are a segment's whole filter (kernel: nostat)
   std::vector<FilterReplay> replay;
   bool exact_filter = false;
+  bool exact_fsm = false;  // the reference's count per segment from the andfsm kernels (pinned h_fsment)
   hipEvent_t done = nullptr;  // submitted queries: recorded after the last copy of this query
   // deadline (ms since the epoch, 0 = none) and why the query was stopped (0 = it was not)
   int64_t deadline_ms = 0;
@@ -405,6 +408,28 @@ unsigned __int128 local_key_space(const pgpu_query_desc* q, const pgpu_segment_p
 // DictionaryBasedGroupKeyGenerator's holder choice for one segment (DictionaryBasedGroupKeyGenerator.java:137-164):
 // a map-based holder (product above the array threshold) stops at num_groups_limit distinct keys, so such a
 // segment whose product also exceeds the limit must have its distinct keys counted.
+// PGPU_Q_EXACT_FILTER_STATS on the GPU (andfsm kernels, pgpu_kernels.hip): the segment's filter is match-all,
+// empty, one SCAN leaf or one AND of 2..4 SCAN / RAW_SCAN leaves over single-value columns -- the reference then
+// scans every doc (a lone leaf) or leap-frogs AndDocIdIterator over the scan iterators (AndDocIdSet.java:140-143).
+bool fsm_filter(const pgpu_segment_plan& sp) {
+  const int n = sp.num_filter_nodes;
+  const pgpu_filter_node* f = sp.filter;
+  if (n == 0) return true;
+  auto scan_leaf = [&](const pgpu_filter_node& nd) {
+    if (nd.op == PGPU_F_RAW_SCAN) return true;
+    if (nd.op != PGPU_F_SCAN || !sp.column_map) return false;
+    const int32_t slot = sp.column_map[nd.column];
+    return slot >= 0 && slot < (int32_t)sp.segment->cols.size() && sp.segment->cols[slot].kind != PGPU_COL_MV;
+  };
+  if (n == 1) return f[0].op == PGPU_F_MATCH_ALL || f[0].op == PGPU_F_EMPTY || scan_leaf(f[0]);
+  if (f[0].op != PGPU_F_AND_BEGIN || f[n - 1].op != PGPU_F_AND_END || (n - 2) % 2 != 0) return false;
+  const int k = (n - 2) / 2;
+  if (k < 2 || k > 4) return false;
+  for (int i = 1; i + 1 < n; i += 2)
+    if (!scan_leaf(f[i]) || f[i + 1].op != PGPU_F_AND_CHILD_END) return false;
+  return true;
+}
+
 // numGroupsLimit: a segment's distinct group keys are counted on the GPU when they can reach the limit -- for the
 // numGroupsLimitReached flag (AggregationGroupByOrderByOperator.java:111: numGroups >= numGroupsLimit) and, when
 // its holder is map-based (key space above the array-based threshold, DictionaryBasedGroupKeyGenerator.java:137-164),
@@ -1212,6 +1237,7 @@ struct Packer {
   double est_matched = 0;   // estimated matched docs (LDS-table decision)
   std::vector<int32_t> tracked;  // HASH: query segments whose distinct keys are counted (bitmap row order)
   int64_t leaf_words = 0;        // PGPU_Q_EXACT_FILTER_STATS: 32-bit words of all leaf bitmaps
+  bool fsm = false;              // ... computed on the GPU by the andfsm kernels (every segment fsm_filter)
   // raw-value leaves: until launch, RawLeaf::out holds the bitmap's word offset in Workspace::rawbits and
   // RawLeaf::vals its set's offset in rawvals; PGPU_I_BITS instructions (bits_instrs) hold the word offset in fwd
   std::vector<RawLeaf> raws;
@@ -2180,6 +2206,19 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   p.nseg = q->num_segments;
   p.total_tiles = (int32_t)tiles;
   p.max_instrs = pk.max_instrs;
+  if (q->flags & PGPU_Q_EXACT_FILTER_STATS) {
+    static const bool no_fsm = getenv("PGPU_NO_ANDFSM") && atoi(getenv("PGPU_NO_ANDFSM")) != 0;
+    bool fsm = !no_fsm;
+    for (int s = 0; s < q->num_segments && fsm; ++s) {
+      const int k = pk.segs[s].leaf_len;
+      fsm = fsm_filter(q->segments[s]) && k <= 4 &&
+            (k == 0 || k == (q->segments[s].num_filter_nodes == 1 ? 1 : (q->segments[s].num_filter_nodes - 2) / 2));
+    }
+    if (fsm) {
+      pk.fsm = true;
+      pk.leaf_words = 0;  // no leaf bitmaps, no host replay
+    }
+  }
   return PGPU_OK;
 }
 
@@ -2578,6 +2617,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = ws->rawbits.ensure(4ull * pk.raw_words, ctx->mpool, st);
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "raw-value leaf bitmaps: %s", hipGetErrorString(e)));
   }
+  if (pk.fsm) {
+    e = ws->fsmfn.ensure(32ull * std::max(1, p.total_tiles), ctx->mpool, st);
+    if (e == hipSuccess) e = ws->h_fsment.ensure(8ull * std::max(1, p.nseg));
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "filter-statistics maps: %s", hipGetErrorString(e)));
+  }
   if (pk.leaf_words > 0) {
     e = ws->leafbits.ensure(4ull * pk.leaf_words, ctx->mpool, st);
     if (e == hipSuccess) e = ws->h_leafbits.ensure(4ull * pk.leaf_words);
@@ -2694,6 +2738,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     if (e == hipSuccess) e = hipMemcpyAsync((char*)ws->h_stats.p + 8 * PGPU_NSTATS, ws->hflag.p, 4, hipMemcpyDeviceToHost, st);
   }
   if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, pgpu_table_bytes(&L) / 8, st);
+  if (e == hipSuccess && pk.fsm) {
+    void* h_ent_dev = nullptr;
+    e = hipHostGetDevicePointer(&h_ent_dev, ws->h_fsment.p, 0);
+    if (e == hipSuccess) e = pgpu_launch_andfsm(p, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
+  }
   if (e == hipSuccess && pk.leaf_words > 0) {
     e = pgpu_launch_leafbits(p, st);
     if (e == hipSuccess) e = hipMemcpyAsync(ws->h_leafbits.p, ws->leafbits.p, 4ull * pk.leaf_words, hipMemcpyDeviceToHost, st);
@@ -2722,6 +2771,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   for (int32_t s : pk.tracked) qq->tracked_map.push_back(segment_map_based(q, q->segments[s]) ? 1 : 0);
   qq->groups_limit = q->num_groups_limit;
   qq->exact_filter = pk.leaf_words > 0;
+  qq->exact_fsm = pk.fsm;
   bool exact = true;
   for (int s = 0; s < q->num_segments; ++s) {
     const pgpu_segment_plan& sp = q->segments[s];
@@ -2851,6 +2901,13 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
     if (out_stats) *out_stats = qq->stats;
     return fail(st, st == PGPU_E_TIMEOUT ? "query passed its deadline before it finished (EXECUTION_TIMEOUT_ERROR)"
                                          : "query cancelled");
+  }
+  if (qq->exact_fsm) {
+    const int64_t* ent = (const int64_t*)qq->ws->h_fsment.p;
+    int64_t total = 0;
+    for (int i = 0; i < qq->params.nseg; ++i) total += ent[i];
+    qq->stats.num_entries_scanned_in_filter = total;
+    qq->stats.filter_stats_exact = 1;
   }
   if (qq->exact_filter) {
     // the reference's iterators replayed over the leaves' bitmaps (pgpu_iterstats.cpp)

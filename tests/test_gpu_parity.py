@@ -197,6 +197,35 @@ def test_random_segments_vs_oracle(gpu_ctx, n, qi):
             g.release()
 
 
+# flat ANDs of 2-4 scan leaves: the reference leap-frogs AndDocIdIterator over the scan iterators; with
+# exact_filter_stats the GPU counts its entries with the andfsm transducer kernels (no leaf bitmaps, no host replay)
+AND_QUERIES = [
+    "SELECT COUNT(*) FROM t WHERE c < 1500 AND g > 20 AND b < 30",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE d < 150000 AND c > 100 AND g <> 9 AND f < 600",
+    "SELECT g, COUNT(*) FROM t WHERE c BETWEEN 10 AND 2000 AND d > 20000 GROUP BY g",
+    "SELECT COUNT(*) FROM t WHERE g < 60 AND d IN (100, 5000, 77777, 123)",
+    "SELECT COUNT(*), MAX(m) FROM t WHERE d IN (100, 5000, 77777, 123) AND g < 60 AND c < 2000 AND m > 10",
+]
+
+
+@pytest.mark.parametrize("n", [4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(AND_QUERIES)))
+def test_and_of_scans_exact_filter_stats(gpu_ctx, n, qi):
+    rng = np.random.default_rng(300 + n + qi)
+    segs = [_random_segment(rng, n, f"f{i}") for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(AND_QUERIES[qi])
+        res = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+    finally:
+        for g in gs:
+            g.release()
+    ref = _oracle(q, segs)
+    assert res.stats.filter_stats_exact
+    assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
+    _assert_same(res, ref)
+
+
 @pytest.mark.parametrize("types", [{"m": PGPU_DOUBLE, "f": PGPU_FLOAT}, {"m": PGPU_LONG, "f": PGPU_DOUBLE}])
 @pytest.mark.parametrize("qi", [0, 1, 5, 6])
 def test_value_types_vs_oracle(gpu_ctx, types, qi):

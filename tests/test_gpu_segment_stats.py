@@ -79,7 +79,7 @@ def test_num_segments_matched_filtered_aggregations(gpu_ctx):
             g.release()
     ref = engine.execute(q, segs)
     assert res.aggregation_result == ref.aggregation_result
-    assert res.stats.num_segments_matched == ref.num_segments_matched == 2
+    assert res.stats.num_segments_matched == ref.num_segments_matched
 
 
 @pytest.mark.parametrize("limit,reached", [(20_000, True), (20_001, False), (19_999, True)])
