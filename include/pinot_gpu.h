@@ -130,10 +130,18 @@ int pgpu_segment_add_range_index(pgpu_segment* seg, int32_t column, const void* 
  * leaf on such a column has applyMV semantics (BaseDictionaryBasedPredicateEvaluator.java:133-149): a row matches
  * when any of its values is in the leaf's dict-id set / range, and `negate` keeps the rows none of whose values is
  * (the exclusive NEQ / NOT IN forms); it counts each row's length towards numEntriesScannedInFilter
- * (MVScanDocIdIterator.java:56-100).  The column cannot be grouped on or aggregated directly (PGPU_E_UNSUPPORTED):
- * the *MV aggregation functions read its row columns (below). */
+ * (MVScanDocIdIterator.java:56-100).  GROUP BY on the column expands each matched doc into one key per value
+ * (DictionaryBasedGroupKeyGenerator.java:472-544, processMultiValue), with first-seen numGroupsLimit truncation as in
+ * the single-value case.  It cannot be aggregated directly (PGPU_E_UNSUPPORTED): the *MV aggregation functions read
+ * its row columns (below). */
 int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const void* bytes, uint64_t num_bytes,
                                       int32_t bits_per_value, int32_t cardinality, int64_t num_values);
+/* Dict ids of one row of a multi-value column, in value order (*out_len = the row's length; at most `capacity` ids
+ * are written).  The host side of the first-seen numGroupsLimit cut on multi-value group keys: the new keys of the
+ * doc where the limit is reached get ids in the order DictionaryBasedGroupKeyGenerator.processMultiValue meets
+ * them (DictionaryBasedGroupKeyGenerator.java:186-199, IntGroupIdMap.getGroupId :991-1016). */
+int pgpu_segment_mv_row(pgpu_segment* seg, int32_t column, int32_t doc, int32_t* out_ids, int32_t capacity,
+                        int32_t* out_len);
 /* Per-row reductions of a multi-value column, installed as raw columns in other slots of the same segment (-1 skips
  * one): len_column = values per row (INT), sum_column = the row's sum (LONG for INT / LONG, DOUBLE for FLOAT /
  * DOUBLE values), min_column / max_column = the row's smallest / largest value (the column's type).  COUNTMV /

@@ -161,6 +161,8 @@ SIGNATURES = [
     ("pgpu_query_release", C.c_int, [_P]),
     ("pgpu_query_cancel", C.c_int, [_P]),
     ("pgpu_query_matched_segments", C.c_int, [_P, C.POINTER(C.c_uint8), C.c_int32]),
+    ("pgpu_segment_mv_row", C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                      C.POINTER(C.c_int32)]),
     ("pgpu_table_compact", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(C.c_int64),
                                      C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_table_topk", C.c_int, [_P, C.POINTER(TableLayout), _P, _P, C.POINTER(TopK), C.POINTER(C.c_int64),

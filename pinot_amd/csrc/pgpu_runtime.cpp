@@ -819,6 +819,33 @@ int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const v
   return PGPU_OK;
 }
 
+int pgpu_segment_mv_row(pgpu_segment* seg, int32_t column, int32_t doc, int32_t* out_ids, int32_t capacity,
+                        int32_t* out_len) {
+  int rc = check_column(seg, column);
+  if (rc) return rc;
+  const HostColumn& c = seg->cols[column];
+  if (c.kind != PGPU_COL_MV) return fail(PGPU_E_INVALID, "column %d is not multi-value", column);
+  if (doc < 0 || doc >= seg->num_docs || !out_len || (capacity > 0 && !out_ids))
+    return fail(PGPU_E_INVALID, "doc %d of a %d-doc segment", doc, seg->num_docs);
+  const int64_t v0 = c.mv_offsets[doc], v1 = c.mv_offsets[doc + 1];
+  *out_len = (int32_t)(v1 - v0);
+  const int64_t nv = std::min<int64_t>(v1 - v0, std::max(0, capacity));
+  if (nv <= 0) return PGPU_OK;
+  // the row's bits [v0 * b, (v0 + nv) * b) of the MSB-first packed ids (PinotDataBitSet.readInt)
+  const int b = c.bits;
+  const uint64_t byte0 = (uint64_t)(v0 * b) >> 3, byte1 = ((uint64_t)((v0 + nv) * b) + 7) >> 3;
+  std::vector<uint8_t> raw(byte1 - byte0 + 8, 0);
+  HIP_TRY(hipSetDevice(seg->ctx->device));
+  HIP_TRY(hipMemcpy(raw.data(), (const uint8_t*)c.fwd.p + byte0, byte1 - byte0, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < nv; ++i) {
+    const uint64_t bit = (uint64_t)((v0 + i) * b) - byte0 * 8;
+    uint64_t w = 0;
+    for (int k = 0; k < 8; ++k) w = (w << 8) | raw[(bit >> 3) + k];
+    out_ids[i] = (int32_t)((w >> (64 - (bit & 7) - b)) & ((1ull << b) - 1));
+  }
+  return PGPU_OK;
+}
+
 namespace {
 // Install host little-endian values as a raw column in `slot` (padded like a decoded raw forward index).
 int install_raw(pgpu_segment* seg, int32_t slot, int32_t data_type, std::vector<uint8_t>& le, double max_abs) {

@@ -802,9 +802,6 @@ class GpuPlanMaker:
         group's first doc, and keeps the num_groups_limit groups of smallest first doc.  The partial results merge
         as the combine merges segment results (AggregationFunction.merge)."""
         from .datatable import _merge
-        if any(s.column(g).is_mv for s in segments for g in query.group_by):
-            raise _lib.UnsupportedPlanError(_lib.PGPU_E_UNSUPPORTED,
-                                            "numGroupsLimit on a multi-value group key (first-seen order per value)")
         limit = self.num_groups_limit
         no_dict = any(s.column(g).is_raw for s in segments for g in query.group_by)
         thr = 0 if no_dict else self.max_init_group_holder_capacity
@@ -834,8 +831,12 @@ class GpuPlanMaker:
             r = sub.execute(probe, [s])
             items = list(r.intermediate.items())
             if len(items) >= limit:  # numGroups >= numGroupsLimit (AggregationGroupByOrderByOperator.java:111)
-                items = sorted(items, key=lambda kv: kv[1][-1])[:limit]
                 st.num_groups_limit_reached = True
+                items = sorted(items, key=lambda kv: kv[1][-1])
+                if len(items) > limit and any(s.column(g).is_mv for g in query.group_by):
+                    items = first_seen_multi_value(query, s, items, limit)
+                else:
+                    items = items[:limit]
             parts.append(({k: v[:-1] for k, v in items}, r.stats))
         fns = [a.function for a in query.aggregations]
         merged: Dict[tuple, list] = {}
@@ -887,6 +888,32 @@ class PendingQuery:
         if self.handle is not None and self.handle.value:
             self.maker.ctx._lib.pgpu_query_release(self.handle)
             self.handle = None
+
+
+def first_seen_multi_value(query: QueryContext, seg: GpuSegment, items: List[tuple], limit: int) -> List[tuple]:
+    """The first `limit` group keys in the order the reference's holders give them ids when a group column is
+    multi-value.  `items` = (group values, intermediate values + [first doc]) sorted by first doc.  Every doc expands
+    into one key per element of the cartesian product of its group columns' values, column 0 outermost
+    (DictionaryBasedGroupKeyGenerator.getIntRawKeys, :472-544), and processMultiValue (:186-199) gives each new key
+    the next id until the limit: the keys first met before the doc where the limit is reached are all kept, and that
+    doc's new keys are kept in its own expansion order (single-value columns are constant within a doc, so only the
+    multi-value columns' value order matters)."""
+    import itertools
+    d_cut = items[limit - 1][1][-1]
+    before = [kv for kv in items if kv[1][-1] < d_cut]
+    tie = {kv[0]: kv for kv in items if kv[1][-1] == d_cut}
+    need = limit - len(before)
+    mv_pos = [i for i, g in enumerate(query.group_by) if seg.column(g).is_mv]
+    per_col = []
+    for i in mv_pos:
+        g = query.group_by[i]
+        d = seg.dictionaries[g]
+        per_col.append([d[int(x)].item() if hasattr(d[int(x)], "item") else d[int(x)] for x in seg.mv_row(g, d_cut)])
+    rank = {}
+    for combo in itertools.product(*per_col):
+        rank.setdefault(tuple(combo), len(rank))
+    new = sorted(tie.values(), key=lambda kv: rank.get(tuple(kv[0][i] for i in mv_pos), len(rank)))
+    return before + new[:need]
 
 
 def result_from_intermediate(query: QueryContext, merged: Dict[tuple, list], st: ExecutionStats) -> QueryResult:

@@ -394,6 +394,18 @@ class GpuSegment:
                                                    min_value=0.0, max_value=float(max(self.num_docs - 1, 0)))
         return DOCID_COLUMN
 
+    def mv_row(self, name: str, doc: int) -> np.ndarray:
+        """Dict ids of doc `doc` of a multi-value column, in value order (pgpu_segment_mv_row)."""
+        cap = max(1, self.column(name).max_values or 64)
+        while True:
+            out = np.empty(cap, dtype=np.int32)
+            n = C.c_int32()
+            _lib.check(self.ctx._lib.pgpu_segment_mv_row(self.handle, self.slots[name], int(doc),
+                                                         out.ctypes.data_as(C.POINTER(C.c_int32)), cap, C.byref(n)))
+            if n.value <= cap:
+                return out[: n.value]
+            cap = n.value
+
     def column(self, name: str) -> ColumnIndexes:
         c = self.derived.get(name)
         return c if c is not None else self.data.column(name)

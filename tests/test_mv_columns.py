@@ -362,3 +362,30 @@ def test_gpu_mv_group_by_matches_oracle(gpu_ctx, sql, inverted):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sql,limit", [("SELECT tags, g, COUNT(*), SUM(s) FROM t GROUP BY tags, g", 17),
+                                       ("SELECT tags, COUNT(*), MAX(s) FROM t WHERE s < 80 GROUP BY tags", 23),
+                                       ("SELECT g, tags, COUNT(*) FROM t GROUP BY g, tags", 100)])
+def test_gpu_mv_group_by_first_seen_limit(gpu_ctx, sql, limit):
+    """numGroupsLimit on multi-value group keys: the GPU keeps the first `limit` keys in the order
+    processMultiValue gives them ids ((doc, expansion) order, DictionaryBasedGroupKeyGenerator.java:186-199), the
+    limit's doc cut by its own key expansion (GpuPlanMaker.first_seen_groups, pgpu_segment_mv_row)."""
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.segment import GpuSegment
+    from tests.helpers import check_groups
+    segs = [_segment(40 + k, n=[300, 450][k], name=f"mvl{k}") for k in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(sql)
+        res = GpuPlanMaker(gpu_ctx, num_groups_limit=limit, max_init_group_holder_capacity=10).execute(q, gs)
+    finally:
+        for g in gs:
+            g.release()
+    ref = engine.execute(q, segs, num_groups_limit=limit, max_init_group_holder_capacity=10)
+    full = engine.execute(q, segs, num_groups_limit=10 ** 9)
+    assert len(ref.group_rows) < len(full.group_rows)  # the limit really cuts
+    check_groups(res, ref, 1e-9)
+    assert sorted(r[:len(q.group_by)] for r in res.group_rows) == sorted(r[:len(q.group_by)] for r in ref.group_rows)
+    assert res.stats.num_groups_limit_reached and ref.num_groups_limit_reached
