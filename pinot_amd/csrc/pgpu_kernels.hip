@@ -3419,6 +3419,57 @@ __global__ __launch_bounds__(256) void leafbits_kernel(DevParams p) {
 #define PGPU_ANDFSM_WORDS 8  // per tile: next-state bits (2 per start state), then H per start state
 FI uint32_t sel4(const uint32_t (&v)[4], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3]; }
 
+// A SCAN leaf's words for the transducer from the column's bit-sliced copy (plane k of lane l at dword
+// (tile * B + k) * 64 + l): a dict-id range is lt(hi) & ~lt(lo) (sliced_lt), an id list an OR of [id, id + 1).  A
+// single id on a wide column is compared MSB first, four planes at a time, and stops once no doc of the wave can
+// still match (accountId = x in config 5: ~12 of its 20 planes are read).
+template <int B>
+FI uint32_t fsm_sliced_b(const uint32_t* sl, int tile, const DevInstr& in) {
+  const uint32_t* src = sl + (size_t)tile * 64 * B + lane_id();
+  uint32_t m;
+  if (in.pred == PRED_LIST && in.n == 1 && B >= 12) {
+    const uint32_t id = in.ids[0];
+    m = ~0u;
+    for (int k0 = B - 1; k0 >= 0; k0 -= 4) {
+      uint32_t x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = k0 - j >= 0 ? __builtin_nontemporal_load(src + 64 * (k0 - j)) : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k0 - j >= 0) m &= ((id >> (k0 - j)) & 1u) ? x[j] : ~x[j];
+      if (__builtin_amdgcn_ballot_w64(m != 0) == 0) break;
+    }
+  } else {
+    uint32_t x[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) x[k] = __builtin_nontemporal_load(src + 64 * k);
+    if (in.pred == PRED_RANGE) {
+      m = sliced_lt<B>(x, (uint32_t)in.hi) & ~sliced_lt<B>(x, (uint32_t)in.lo);
+    } else if (in.pred == PRED_MASK) {  // <= 64 ids: one [id, id + 1) per member of the mask
+      m = 0;
+      for (uint64_t mk = ((uint64_t)(uint32_t)in.hi << 32) | (uint32_t)in.lo; mk; mk &= mk - 1) {
+        const uint32_t id = (uint32_t)__builtin_ctzll(mk);
+        m |= sliced_lt<B>(x, id + 1u) & ~sliced_lt<B>(x, id);
+      }
+    } else {
+      m = 0;
+      for (int j = 0; j < in.n && j < 8; ++j) m |= sliced_lt<B>(x, in.ids[j] + 1u) & ~sliced_lt<B>(x, in.ids[j]);
+    }
+  }
+  return in.negate ? ~m : m;
+}
+FI bool fsm_sliced_ok(const DevInstr& in, const DevColumn& c) {
+  return in.op == PGPU_I_SCAN && in.kind == PGPU_COL_FIXED_BIT && c.sliced && in.bits >= 1 && in.bits <= 31 &&
+         (in.pred == PRED_RANGE || in.pred == PRED_MASK || (in.pred == PRED_LIST && in.n >= 1 && in.n <= 4));
+}
+FI uint32_t fsm_sliced(const uint32_t* sl, int bits, int tile, const DevInstr& in) {
+  uint32_t m = 0;
+#define FS_CALL(B) m = fsm_sliced_b<B>(sl, tile, in)
+  PGPU_DISPATCH_B(bits, FS_CALL)
+#undef FS_CALL
+  return m;
+}
+
 __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t* fn) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tile = (int)blockIdx.x * 4 + wave;
@@ -3444,7 +3495,9 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
   for (int j = 0; j < 4; ++j) {
     if (j >= k) break;
     const DevInstr in = cld(p.instrs + cld(p.pool, leaf_begin + j));
-    m[j] = (in.op == PGPU_I_SCAN ? leaf_scan(p, t, in, t.valid, dummy) : leaf_bits(t, in)) & t.valid;
+    const DevColumn col = col_of(ss, in.col);
+    if (fsm_sliced_ok(in, col)) m[j] = fsm_sliced(col.sliced, in.bits, t.tile_in_seg, in) & t.valid;
+    else m[j] = (in.op == PGPU_I_SCAN ? leaf_scan(p, t, in, t.valid, dummy) : leaf_bits(t, in)) & t.valid;
   }
   // this lane's map over its 32 docs, per start state
   uint32_t nxt = 0, h[4] = {0u, 0u, 0u, 0u};

@@ -10,6 +10,8 @@ Inputs (data files the reference's tests hold; nothing here executes reference c
       -> baseball.npz (playerID, yearID, teamID, playerName, runs; schema
       pinot-tools/src/main/resources/examples/batch/baseballStats/baseballStats_schema.json, nulls replaced by the
       FieldSpec defaults spi/data/FieldSpec.java:49-59: STRING dimension "null", INT metric 0)
+  pinot-core/src/test/resources/data/simpleData200001.avro -> simple_data_200001.npz (dim0, dim1, met;
+      QueryExecutorTest.java:150-185)
 The known-answer values themselves are transcribed into kat.json with their file:line.
 """
 from __future__ import annotations
@@ -80,7 +82,16 @@ def make_baseball():
     print("baseball.npz", t.num_rows, "rows")
 
 
+def make_simple():
+    """QueryExecutorTest.java:150-185: simpleData200001.avro (dim0, dim1, met INT columns)."""
+    rows = read_avro(os.path.join(REF, "pinot-core/src/test/resources/data/simpleData200001.avro"))
+    out = {c: np.array([r[c] for r in rows], dtype=np.int32) for c in ("dim0", "dim1", "met")}
+    np.savez_compressed(os.path.join(HERE, "simple_data_200001.npz"), **out)
+    print("simple_data_200001.npz", len(rows), "rows")
+
+
 if __name__ == "__main__":
+    make_simple()
     make_sv()
     make_padding()
     make_baseball()

@@ -32,6 +32,16 @@ def sv_segment():
     return build_segment("testTable_126164076_167572854", sv_columns())
 
 
+def simple_data_segments():
+    """QueryExecutorTest.java:84-103: two segments of simpleData200001.avro (dim0, dim1, met; default segment
+    generator config, no sorted / inverted index configured -- dim0 is generated in sorted order by the creator
+    only when the data is sorted, so the columns are plain fixed-bit here)."""
+    from oracle.segment_writer import build_segment
+    d = np.load(os.path.join(GOLDEN, "simple_data_200001.npz"))
+    cols = {c: (PGPU_INT, d[c]) for c in ("dim0", "dim1", "met")}
+    return [build_segment(f"testTable_{k}", cols, sorted_columns=()) for k in range(2)]
+
+
 def fast_count_segment():
     """FastFilteredCountTest.java:104-134: 1000 rows; class/sorted with inverted indexes, sorted column sorted."""
     from oracle.segment_writer import build_segment

@@ -16,7 +16,7 @@ from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
 from pinot_amd.segment import GpuSegment
 from tests.helpers import (baseball_segment, check_groups, close, fast_count_segment, load_kat, rows_close,
-                           sv_segment)
+                           simple_data_segments, sv_segment)
 
 pytestmark = pytest.mark.gpu
 KAT = load_kat()
@@ -75,6 +75,21 @@ def test_inner_segment_kat_gpu(gpu_ctx, sv, case):
     v = res.intermediate[tuple(case["group"])] if case["group_by"] else res.intermediate[()]
     got = [v[0], int(v[1]), int(v[2]), int(v[3]), int(v[4][0]), v[4][1]]
     assert got == case["result"]
+
+
+@pytest.mark.parametrize("case", KAT["query_executor"]["cases"], ids=lambda c: c["sql"])
+def test_query_executor_kat_gpu(gpu_ctx, case):
+    """QueryExecutorTest.java:150-185: COUNT / SUM / MAX / MIN over two simpleData200001 segments (COUNT, MIN and
+    MAX from segment metadata and the dictionaries, SUM scanned on the GPU)."""
+    segs = simple_data_segments()
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        res = _gpu(gpu_ctx, parse_sql(case["sql"]), gs)
+    finally:
+        for g in gs:
+            g.release()
+    assert res.aggregation_result[0] == case["value"]
+    assert res.stats.num_total_docs == 400002 and res.stats.num_segments_matched == 2
 
 
 @pytest.mark.parametrize("case", KAT["inter_segment"]["cases"], ids=lambda c: c["sql"][:60])

@@ -10,7 +10,7 @@ from oracle import engine
 from oracle.segment_writer import build_segment
 from pinot_amd._lib import PGPU_INT
 from pinot_amd.query import parse_sql
-from tests.helpers import close, fast_count_segment, load_kat, rows_close, sv_segment
+from tests.helpers import close, fast_count_segment, load_kat, rows_close, simple_data_segments, sv_segment
 
 KAT = load_kat()
 
@@ -96,3 +96,11 @@ def test_baseball_quickstart_top10():
         ("Adrian", 1749), ("Jose Antonio", 1461), ("Brian Michael", 1445), ("Jose Alberto", 1426),
         ("Rafael", 1376), ("Alexander Emmanuel", 1292), ("Derek Sanderson", 1271), ("Ichiro", 1261),
         ("James Calvin", 1242), ("Carlos", 1207)]
+
+
+@pytest.mark.parametrize("case", load_kat()["query_executor"]["cases"], ids=lambda c: c["sql"])
+def test_query_executor_kat(case):
+    """QueryExecutorTest.java:150-185 over its two simpleData200001 segments."""
+    segs = simple_data_segments()
+    res = engine.execute(case["sql"], segs)
+    assert res.aggregation_result[0] == case["value"]
