@@ -156,7 +156,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
         log(f"{name}: timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
         cpu = check = None
         if rank == 0 and not args.no_cpu_baseline:
-            cpu, check = cpu_baseline(ctx, w, q, opts, args, cpu_seconds)
+            cpu, check = cpu_baseline(ctx, w, q, opts, args, cpu_seconds, segs)
         traffic, traffic_src = _pmc_traffic(name)
         return {
             "value": rows_per_gpu * world / (ms_per_step * 1e-3),
@@ -354,12 +354,65 @@ def parity_check(ctx, w, q, opts):
             g.release()
 
 
-def cpu_baseline(ctx, w, q, opts, args, seconds):
+def cpu_baseline(ctx, w, q, opts, args, seconds, gpu_segs):
     """The CPU leg: (1) Pinot's per-segment operators restated in C (oracle/pinot_cpu.c) timed on this host,
     the sample's segments queried repeatedly until ~`seconds` of wall time, at Pinot's default task count and
-    with every available core; (2) the GPU-vs-oracle parity check (parity_check)."""
+    with every available core; (2) the GPU-vs-oracle parity check (parity_check) on small segments, and (3) at full
+    size: the GPU over the same full-size segments the C port just timed, compared with the C port's results."""
     check = None if args.no_check else parity_check(ctx, w, q, opts)
-    return c_baseline(w, q, args, seconds), check
+    cpu, last = c_baseline(w, q, args, seconds)
+    if check is not None:
+        full = full_size_check(ctx, w, q, opts, args, gpu_segs, last)
+        check["full_size"] = bool(full.get("ok"))
+        check["full_size_detail"] = full
+        check["ok"] = bool(check["ok"] and full.get("ok"))
+    return cpu, check
+
+
+def full_size_check(ctx, w, q, opts, args, gpu_segs, cport):
+    """The GPU over the first `cpu_sample_segments` full-size segments of this rank (the ones the C port timed:
+    same generator, same seeds), against the C port's matched docs, per-key counts and sums (double
+    accumulators, exact for these integer inputs < 2^53): integers bit-exact, every group compared."""
+    import numpy as np
+
+    from pinot_amd.plan import GpuPlanMaker
+
+    nseg = min(args.cpu_sample_segments, len(gpu_segs))
+    matched, counts, sums = cport
+    res = GpuPlanMaker(ctx, **plan_options(opts)).execute(q, gpu_segs[:nseg])
+    out = {"segments": nseg, "docs": nseg * args.docs, "matched": int(matched),
+           "gpu_matched": int(res.stats.num_docs_scanned)}
+    ok = res.stats.num_docs_scanned == matched
+    aggs = q.aggregations
+
+    def expect(a, ai, key):
+        cnt = int(counts[key])
+        if a.function == "COUNT":
+            return cnt
+        v = float(sums[ai][key])
+        return v / cnt if a.function == "AVG" else v
+
+    if not q.group_by:
+        exp = [expect(a, ai, 0) for ai, a in enumerate(aggs)] if matched else None
+        got = list(res.aggregation_result)
+        ok = ok and (exp is None or all(float(g) == float(e) for g, e in zip(got, exp)))
+        out["compared"] = "aggregation values"
+    else:
+        values = {c.name: c.values() for c in w.columns}
+        gvals = values[q.group_by[0]]
+        live = np.flatnonzero(counts)
+        rows = {tuple(r[:1]): r[1:] for r in res.group_rows}
+        ok = ok and len(rows) == len(live) and len(q.group_by) == 1
+        bad = 0
+        for key in live.tolist():
+            r = rows.get((int(gvals[key]),))
+            if r is None or any(float(g) != float(expect(a, ai, key)) for ai, (a, g) in enumerate(zip(aggs, r))):
+                bad += 1
+        ok = ok and bad == 0
+        out.update({"groups": int(len(live)), "gpu_groups": len(rows), "mismatched_groups": bad,
+                    "compared": "every group"})
+    out["ok"] = bool(ok)
+    return out
 
 
 def c_baseline(w, q, args, seconds):
@@ -378,25 +431,29 @@ def c_baseline(w, q, args, seconds):
     filt = ("doc-id set algebra of AndDocIdSet / OrDocIdSet over Roaring / sorted / scan leaves" if cb.q.num_nodes
             else "AndDocIdIterator over SVScanDocIdIterators")
 
+    last = []
+
     def timed(c, th, n, budget):
         total, runs = 0.0, 0
         while runs == 0 or total < budget:
-            dt, matched, _, _, _ = c.run(th)
+            dt, matched, counts, sums, _ = c.run(th)
             total += dt
             runs += 1
+        last[:] = [matched, counts, sums]
         return runs * n * args.docs / total, runs, total
 
     value, runs, total = timed(cb, threads, nseg, seconds)
+    first = list(last)
     all_cb = cb if len(segs) == nseg else CpuBaseline(q, segs)
     all_value, all_runs, all_total = timed(all_cb, cores, len(segs), max(1.0, seconds / 2))
     skew = "" if all(c.dist == "uniform" for c in w.columns) else ", Zipf keys from the same CDF as the GPU's"
-    return {"value": value, "unit": "rows/s", "cores": threads, "kind": "port",
+    return ({"value": value, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload{skew}, "
                       f"oracle/pinot_cpu.c ({filt}, 10k-doc blocks, double SUM), "
                       f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
             "seconds": total,
             "all_cores": {"value": all_value, "cores": cores, "available_cores": cores, "segments": len(segs),
-                          "runs": all_runs, "seconds": all_total}}
+                          "runs": all_runs, "seconds": all_total}}, first)
 
 
 if __name__ == "__main__":

@@ -99,6 +99,8 @@ struct DevColumn {
 #define PGPU_AM_COUNT 0   // COUNT(*) only, no group-by: matched docs are only counted
 #define PGPU_AM_DENSE 1   // group / agg column ids decoded from the staged LDS slot
 #define PGPU_AM_SPARSE 2  // matched docs queued; ids gathered per doc
+#define PGPU_AM_SLICED 3  // aggregation-only: agg columns staged bit-sliced, matched docs' ids read from the planes
+                          // in registers, values gathered from the dictionary (query_kernel_direct only)
 
 #define PGPU_PREBITS 4
 #define PGPU_FOR_MAX_BITS 16  // frame-of-reference dictionaries: widest per-block offset

@@ -2084,16 +2084,94 @@ FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* 
   }
 }
 
+// PGPU_AM_SLICED (aggregation-only): each aggregated column's planes were DMAed into the tile's slot beside the
+// filter's (plane k of lane l at dword k * 64 + l, one coalesced 256-B row per plane: the column streams at the
+// filter's rate, not at a 128-B line per gathered value).  A matched doc's id is read bit by bit from the lane's
+// planes in registers, its value gathered from the dictionary (L2-resident), folded into the lane partials.
+template <int B>
+FI void sliced_agg_col(const Cons& cv, LaneAcc& la, const uint32_t* region, const DevColumn& c, const DevAgg& ag,
+                       int a, uint32_t mm) {
+  const LAS uint32_t* src = (const LAS uint32_t*)region + opaque_lane();
+  uint32_t x[B];
+#pragma unroll
+  for (int k = 0; k < B; ++k) x[k] = src[64 * k];
+  const bool mn = ag.op == PGPU_RED_MIN_I64, mx = ag.op == PGPU_RED_MAX_I64;
+  if (mn || mx) {  // sorted dictionary: the extreme matched id, one value gather per lane
+    uint32_t best = mn ? 0xFFFFFFFFu : 0u;
+    for (uint32_t left = mm; left; left &= left - 1) {
+      const int i = __builtin_ctz(left);
+      uint32_t id = 0;
+#pragma unroll
+      for (int k = 0; k < B; ++k) id |= ((x[k] >> i) & 1u) << k;
+      best = mn ? min(best, id) : max(best, id);
+    }
+    int64_t part = sec_identity(ag.op);
+    if (mm) {
+      const uint32_t idx[1] = {best};
+      int64_t v1[1];
+      gather_cells(c.dict, ag.vtype, ag.op, idx, v1);
+      part = v1[0];
+    }
+    lacc_add(la, cv, a, ag.op, part);
+    return;
+  }
+  int64_t part = sec_identity(ag.op);
+  uint32_t left = mm;
+  while (__builtin_amdgcn_ballot_w64(left != 0)) {
+    // four matched docs per round: their value gathers are in flight together
+    uint32_t idx[4];
+    uint32_t live = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      idx[r] = 0;
+      if (left) {
+        const int i = __builtin_ctz(left);
+        left &= left - 1;
+        uint32_t id = 0;
+#pragma unroll
+        for (int k = 0; k < B; ++k) id |= ((x[k] >> i) & 1u) << k;
+        idx[r] = id;
+        live |= 1u << r;
+      }
+    }
+    int64_t v[4];
+    gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+    apply_part(v, ag.part);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if ((live >> r) & 1u) part = cell_combine(ag.op, part, v[r]);
+  }
+  lacc_add(la, cv, a, ag.op, part);
+}
+FI void sliced_agg(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, const unsigned char* slot,
+                   uint32_t mm) {
+  for (int a = 0; a < p.nagg; ++a) {
+    const DevAgg ag = p.aggs[a];
+    if (ag.fn == PGPU_AGG_COUNT) continue;
+    const DevColumn c = col_of(ss, ag.col);
+    const uint32_t* region = staged_region(ss, slot, ag.col);
+#define SA_CALL(B) sliced_agg_col<B>(cv, la, region, c, ag, a, mm)
+    PGPU_DISPATCH_B(c.bits, SA_CALL)
+#undef SA_CALL
+  }
+}
+
 // A self-loading wave's filtered tile: count it (COUNT-only segment), or queue its candidate docs for the residual
 // filter and the sparse aggregation (a tile that does not fit behind the queued entries is flushed in two halves).
 template <int MODE, int NW>
 FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                           int tile_in_seg, uint32_t mm, int& qn, int& qt, uint32_t& lane_matched, int64_t& matched,
-                          int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf) {
+                          int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf,
+                          const unsigned char* slot = nullptr) {
   const int lane = lane_id();
   if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
     lane_matched += __popc(mm);
     mark_seg(p, ss, __builtin_amdgcn_ballot_w64(mm != 0) != 0);
+  } else if (MODE == PGPU_MODE_AGG && ss.agg_mode == PGPU_AM_SLICED) {  // planner: no residual program
+    lane_matched += __popc(mm);
+    const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
+    mark_seg(p, ss, any);
+    if (any) sliced_agg(p, cv, la, ss, slot, mm);
   } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
     const int cnt = __popc(mm);
     const int ex = wave_excl_scan(cnt);
@@ -2219,7 +2297,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);
       direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, mm, qn, qt, lane_matched, matched, scanned,
-                                  sector_bytes, dense_bytes, pf);
+                                  sector_bytes, dense_bytes, pf, t.slot);
       PROF_ADD(pf, PGPU_P_C_AGG, ta);
     }
     if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);

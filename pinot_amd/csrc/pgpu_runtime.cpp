@@ -821,8 +821,8 @@ int pgpu_segment_add_mv_forward_index(pgpu_segment* seg, int32_t column, const v
 
 int pgpu_segment_mv_row(pgpu_segment* seg, int32_t column, int32_t doc, int32_t* out_ids, int32_t capacity,
                         int32_t* out_len) {
-  int rc = check_column(seg, column);
-  if (rc) return rc;
+  if (!seg) return fail(PGPU_E_INVALID, "null segment");
+  if (column < 0 || column >= (int32_t)seg->cols.size()) return fail(PGPU_E_INVALID, "bad column %d", column);
   const HostColumn& c = seg->cols[column];
   if (c.kind != PGPU_COL_MV) return fail(PGPU_E_INVALID, "column %d is not multi-value", column);
   if (doc < 0 || doc >= seg->num_docs || !out_len || (capacity > 0 && !out_ids))
@@ -1809,6 +1809,16 @@ constexpr double kDenseTouch = 0.5;
 // self-loading kernels' candidate gathers win (config 2, 9.4 % of docs, 16-bit metric, 79 % of sectors touched:
 // dense 2.37 ms, candidates 1.40 ms; 50 % of docs: dense 3.0 ms, candidates 3.8 ms).  PGPU_DENSE_TOUCH overrides.
 constexpr double kDenseAggTouch = 0.95;
+// Aggregation-only queries: the aggregated columns are streamed bit-sliced beside the filter (PGPU_AM_SLICED) when
+// at least this share of their 128-B lines holds a matched doc -- a gathered 4-B value moves a whole line
+// (tools/gather_policy_bench.hip), so the candidate gathers would read those lines anyway, at gather speed.
+// PGPU_SLICED_TOUCH overrides; PGPU_NO_SLICED_AGG=1 turns the mode off.
+constexpr double kSlicedAggTouch = 0.5;
+double line_touch(double rho, int bits) {
+  if (rho >= 1.0) return 1.0;
+  if (rho <= 0.0) return 0.0;
+  return 1.0 - std::pow(1.0 - rho, 1024.0 / bits);
+}
 constexpr int kMaxSlotBytes = 27 * 1024;  // keeps >= 3 ring slots next to the consumer areas
 
 // Prefix pre-filter for the register-direct kernel (DevSeg::pfx_*): when the residual program is one SCAN leaf on a
@@ -1922,8 +1932,19 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   for (int a = 0; a < q->num_aggs; ++a)
     if (q->aggs[a].fn != PGPU_AGG_COUNT) add_agg(q->aggs[a].column);
   int agg_mode;
+  static const bool no_sliced = getenv("PGPU_NO_SLICED_AGG") && atoi(getenv("PGPU_NO_SLICED_AGG")) != 0;
+  static const double sliced_touch = getenv("PGPU_SLICED_TOUCH") ? atof(getenv("PGPU_SLICED_TOUCH")) : kSlicedAggTouch;
+  bool sliced = !no_sliced && !aggcols.empty() && !residual && p.mode == PGPU_MODE_AGG && !p.mv_gmask;
+  for (int qc : aggcols) {
+    const DevColumn* dc = v.dev(qc);
+    sliced = sliced && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced && dc->bits >= 1 && dc->bits <= 31 &&
+             line_touch(rho, dc->bits) >= sliced_touch;
+  }
   if (aggcols.empty()) {
     agg_mode = PGPU_AM_COUNT;
+  } else if (sliced) {
+    agg_mode = PGPU_AM_SLICED;
+    for (int qc : aggcols) add_stage(qc);
   } else if (residual || p.mv_gmask) {  // multi-value group keys: expanded per candidate doc (sparse_agg_mv)
     agg_mode = PGPU_AM_SPARSE;
   } else {
@@ -1948,7 +1969,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     }
     return staged.size() <= PGPU_MAX_STAGE && instrs <= PGPU_MAX_STAGE_INSTRS && bytes <= kMaxSlotBytes;
   };
-  if (!fits() && agg_mode == PGPU_AM_DENSE) {
+  if (!fits() && (agg_mode == PGPU_AM_DENSE || agg_mode == PGPU_AM_SLICED)) {
     staged.resize(nfilter_stage);
     agg_mode = PGPU_AM_SPARSE;
   }
@@ -2066,6 +2087,24 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       ds.f_rng[j][r][1] = rng[r].second;
     }
     ds.stage_sliced |= 1 << stage_index(in.col);
+  }
+  // sliced aggregation: the aggregated columns' staged regions are plain copies of their bit-sliced tiles; the
+  // dense program must then read staged columns only as fast sliced leaves (run_program would decode a staged
+  // region as the packed layout)
+  if (agg_mode == PGPU_AM_SLICED) {
+    bool prog_ok = true;
+    for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+      const DevInstr& in = pk.instrs[i];
+      if (in.op == PGPU_I_SCAN && ds.fast == 0) prog_ok = false;
+    }
+    for (int j = 0; j < ds.fast; ++j)
+      prog_ok = prog_ok && ds.f_nr[j] > 0;  // each fast leaf evaluated on its planes
+    if (prog_ok) {
+      for (int qc : aggcols) ds.stage_sliced |= 1 << stage_index(qc);
+    } else {
+      staged.resize(nfilter_stage);
+      agg_mode = PGPU_AM_SPARSE;
+    }
   }
   // staging layout
   std::vector<int> stage_offs;
@@ -2357,7 +2396,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     for (const DevSeg& ds : pk.segs)
       ok &= ds.ntiles == 0 || ((ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&
                                ((ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1) ||
-                                (ds.nstage == 0 && ds.fast == 0)));
+                                (ds.nstage == 0 && ds.fast == 0))) ||
+            (ds.agg_mode == PGPU_AM_SLICED && ds.stage_sliced == (1 << ds.nstage) - 1);
     // up to five 4-wave workgroups per CU (more waves hide the per-tile latency better than deeper prefetch, which
     // measured flat); each wave keeps D - 1 tiles in flight, aiming at ~12 KiB (HBM latency
     // x per-CU bandwidth), within the 6-bit vmcnt and the LDS
@@ -2395,7 +2435,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     int rd_bits = 1;
     for (const DevSeg& ds : pk.segs)
       if (ds.ntiles) {
-        if (!(ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1)) {  // stage_col[0] is set only when staged
+        if (!(ds.nstage == 1 && ds.fast == 1 && ds.stage_sliced == 1) || ds.agg_mode == PGPU_AM_SLICED) {
           rd = false;
           continue;
         }
@@ -2421,6 +2461,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       dyn = rdyn;
     }
   }
+  // sliced aggregation runs in query_kernel_direct only: elsewhere its segments gather per candidate (their staged
+  // aggregation planes are then only extra DMA, never read)
+  if (p.direct != 1)
+    for (DevSeg& ds : pk.segs)
+      if (ds.agg_mode == PGPU_AM_SLICED) ds.agg_mode = PGPU_AM_SPARSE;
   // one-word PART records (in-partition key, dict id) when every segment holds the same dictionary for the
   // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
   int part_idbits = 0;

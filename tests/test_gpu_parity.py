@@ -241,6 +241,33 @@ def test_and_of_scans_exact_filter_stats(gpu_ctx, n, qi):
     _assert_same(res, ref)
 
 
+# aggregation-only queries whose aggregated columns are streamed bit-sliced beside the filter (PGPU_AM_SLICED,
+# query_kernel_direct): every value type, narrow and wide columns, an aggregated column that is also the filter's,
+# index-only filters
+SLICED_QUERIES = [
+    "SELECT COUNT(*), SUM(m), MIN(m), MAX(f), AVG(d) FROM t WHERE c < 2000 AND b > 3",
+    "SELECT SUM(d), MAX(m), COUNT(*) FROM t WHERE d BETWEEN 1000 AND 150000",
+    "SELECT SUM(m), MIN(c), AVG(g) FROM t WHERE a <> 0",
+    "SELECT SUM(m), MAX(d), MIN(f) FROM t WHERE a = 3 OR b IN (0, 3, 6)",
+]
+
+
+@pytest.mark.parametrize("types", [None, {"m": PGPU_DOUBLE, "f": PGPU_FLOAT}, {"m": PGPU_LONG, "f": PGPU_DOUBLE}])
+@pytest.mark.parametrize("n", [4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(SLICED_QUERIES)))
+def test_sliced_aggregation_vs_oracle(gpu_ctx, qi, n, types):
+    rng = np.random.default_rng(500 + qi + n)
+    inv = ["a", "b"] if qi == 3 else []
+    segs = [_random_segment(rng, n, f"sl{i}", inverted=inv, types=types) for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(SLICED_QUERIES[qi])
+        _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
+
+
 @pytest.mark.parametrize("types", [{"m": PGPU_DOUBLE, "f": PGPU_FLOAT}, {"m": PGPU_LONG, "f": PGPU_DOUBLE}])
 @pytest.mark.parametrize("qi", [0, 1, 5, 6])
 def test_value_types_vs_oracle(gpu_ctx, types, qi):
