@@ -89,10 +89,15 @@ struct DevColumn {
   const DevContainer* inv_ct;     // containers
   const uint8_t* inv_data;        // Roaring payload bytes
   const uint32_t* sliced;         // FIXED_BIT: bit-sliced copy (pgpu_bitslice_kernel), nullptr = none
+  const uint32_t* vsliced;        // FIXED_BIT over an INT / LONG dictionary: bit planes of each doc's VALUE minus
+                                  // vmin (vbits planes per tile, same layout as `sliced`; vslice_kernel), or nullptr
+  int64_t vmin;
+  int32_t vbits;
   int32_t kind;                   // PGPU_COL_*
   int32_t bits;
   int32_t card;
   int32_t dict_type;              // PGPU_INT .. PGPU_STRING
+  int32_t pad_;
 };
 
 // Aggregation plan of a segment

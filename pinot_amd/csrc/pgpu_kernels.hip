@@ -2084,75 +2084,151 @@ FI void issue_tile_direct(const StageCache& sc, int tile_in_seg, unsigned char* 
   }
 }
 
-// PGPU_AM_SLICED (aggregation-only): each aggregated column's planes were DMAed into the tile's slot beside the
-// filter's (plane k of lane l at dword k * 64 + l, one coalesced 256-B row per plane: the column streams at the
-// filter's rate, not at a 128-B line per gathered value).  A matched doc's id is read bit by bit from the lane's
-// planes in registers, its value gathered from the dictionary (L2-resident), folded into the lane partials.
+// PGPU_AM_SLICED (aggregation-only): after the filter, each aggregated column's planes for the tile are loaded
+// straight into VGPRs from its bit-sliced copy (plane k of lane l at dword (tile * B + k) * 64 + l: one coalesced
+// 256-B row per plane, so the column streams at the filter's rate instead of one 128-B line per gathered value),
+// and each matched doc's id is read bit by bit from the lane's planes.  Ids of columns of <= 16 bits go to the
+// wave's LDS queue (the candidate queue's space, unused here: one sub-queue per column) and their dictionary values
+// are gathered in batches when it fills (many gathers in flight per lane); wider columns gather per tile.
 template <int B>
-FI void sliced_agg_col(const Cons& cv, LaneAcc& la, const uint32_t* region, const DevColumn& c, const DevAgg& ag,
-                       int a, uint32_t mm) {
-  const LAS uint32_t* src = (const LAS uint32_t*)region + opaque_lane();
-  uint32_t x[B];
+FI void sliced_load(const uint32_t* sl, int tile, uint32_t (&x)[B]) {
+  const uint32_t* src = sl + (size_t)tile * 64 * B + lane_id();
 #pragma unroll
-  for (int k = 0; k < B; ++k) x[k] = src[64 * k];
-  const bool mn = ag.op == PGPU_RED_MIN_I64, mx = ag.op == PGPU_RED_MAX_I64;
-  if (mn || mx) {  // sorted dictionary: the extreme matched id, one value gather per lane
-    uint32_t best = mn ? 0xFFFFFFFFu : 0u;
-    for (uint32_t left = mm; left; left &= left - 1) {
-      const int i = __builtin_ctz(left);
-      uint32_t id = 0;
-#pragma unroll
-      for (int k = 0; k < B; ++k) id |= ((x[k] >> i) & 1u) << k;
-      best = mn ? min(best, id) : max(best, id);
-    }
-    int64_t part = sec_identity(ag.op);
-    if (mm) {
-      const uint32_t idx[1] = {best};
-      int64_t v1[1];
-      gather_cells(c.dict, ag.vtype, ag.op, idx, v1);
-      part = v1[0];
-    }
-    lacc_add(la, cv, a, ag.op, part);
-    return;
-  }
-  int64_t part = sec_identity(ag.op);
-  uint32_t left = mm;
-  while (__builtin_amdgcn_ballot_w64(left != 0)) {
-    // four matched docs per round: their value gathers are in flight together
-    uint32_t idx[4];
-    uint32_t live = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      idx[r] = 0;
-      if (left) {
-        const int i = __builtin_ctz(left);
-        left &= left - 1;
-        uint32_t id = 0;
-#pragma unroll
-        for (int k = 0; k < B; ++k) id |= ((x[k] >> i) & 1u) << k;
-        idx[r] = id;
-        live |= 1u << r;
-      }
-    }
-    int64_t v[4];
-    gather_cells(c.dict, ag.vtype, ag.op, idx, v);
-    apply_part(v, ag.part);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if ((live >> r) & 1u) part = cell_combine(ag.op, part, v[r]);
-  }
-  lacc_add(la, cv, a, ag.op, part);
+  for (int k = 0; k < B; ++k) x[k] = __builtin_nontemporal_load(src + 64 * k);
 }
-FI void sliced_agg(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, const unsigned char* slot,
-                   uint32_t mm) {
+template <int B>
+FI uint32_t sliced_id(const uint32_t (&x)[B], int i) {
+  uint32_t id = 0;
+#pragma unroll
+  for (int k = 0; k < B; ++k) id |= ((x[k] >> i) & 1u) << k;
+  return id;
+}
+// ids of this lane's matched docs of column c into queue q at [at, ...)
+template <int B>
+FI void sliced_enqueue_b(const DevColumn& c, int tile, uint32_t mm, uint16_t* q, int at) {
+  uint32_t x[B];
+  sliced_load<B>(c.sliced, tile, x);
+  for (uint32_t left = mm; left; left &= left - 1) q[at++] = (uint16_t)sliced_id<B>(x, __builtin_ctz(left));
+}
+// Columns queued by the wave (<= 2 non-COUNT aggregations over <= 16-bit columns) and each one's queue capacity.
+FI int sliced_queued(const DevParams& p, const SegState& ss) {
+  int n = 0;
+  for (int a = 0; a < p.nagg; ++a) {
+    if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+    if (col_of(ss, p.aggs[a].col).bits > 16) return 0;
+    ++n;
+  }
+  return n <= 2 ? n : 0;
+}
+// Gather and fold the queued ids' values (segment `ss`'s dictionaries), eight per lane in flight.
+FI void sliced_flush(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, int n) {
+  if (n <= 0) return;
+  wave_sync();
+  const int cap = PGPU_CQ_CAP / 2;
+  int slot = 0;
   for (int a = 0; a < p.nagg; ++a) {
     const DevAgg ag = p.aggs[a];
     if (ag.fn == PGPU_AGG_COUNT) continue;
     const DevColumn c = col_of(ss, ag.col);
-    const uint32_t* region = staged_region(ss, slot, ag.col);
-#define SA_CALL(B) sliced_agg_col<B>(cv, la, region, c, ag, a, mm)
-    PGPU_DISPATCH_B(c.bits, SA_CALL)
-#undef SA_CALL
+    const uint16_t* q = cv.queue + slot++ * cap;
+    int64_t part = sec_identity(ag.op);
+    for (int base = 0; base < n; base += 8 * 64) {
+      uint32_t idx[8];
+      uint32_t live = 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = base + r * 64 + lane_id();
+        idx[r] = e < n ? (uint32_t)q[e] : 0u;
+        live |= (uint32_t)(e < n) << r;
+      }
+      int64_t v[8];
+      gather_cells(c.dict, ag.vtype, ag.op, idx, v);
+      apply_part(v, ag.part);
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if ((live >> r) & 1u) part = cell_combine(ag.op, part, v[r]);
+    }
+    lacc_add(la, cv, a, ag.op, part);
+  }
+  wave_sync();
+}
+// Aggregations answered from the value planes (bit-sliced index): SUM of whole int64 cells, MIN, MAX.
+#define BSI_MAXB 24  // value planes held in VGPRs per tile (wider values: the id path; the direct kernel stays spill-free)
+FI bool bsi_agg(const DevAgg& ag, const DevColumn& c) {
+  return c.vsliced && c.vbits >= 1 && c.vbits <= BSI_MAXB &&
+         ((ag.op == PGPU_RED_SUM_I64 && ag.part == 0) || ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64);
+}
+FI void bsi_tile(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& ag, int a, int tile, uint32_t mm) {
+  const int vb = c.vbits;
+  const uint32_t* src = c.vsliced + (size_t)tile * 64 * vb + lane_id();
+  uint32_t x[BSI_MAXB];
+#pragma unroll
+  for (int k = 0; k < BSI_MAXB; ++k) x[k] = k < vb ? __builtin_nontemporal_load(src + 64 * k) : 0u;
+  int64_t part;
+  if (ag.op == PGPU_RED_SUM_I64) {
+    uint64_t u = 0;
+#pragma unroll
+    for (int k = 0; k < BSI_MAXB; ++k)
+      if (k < vb) u += (uint64_t)__popc(x[k] & mm) << k;
+    part = (int64_t)u + (int64_t)__popc(mm) * c.vmin;
+  } else {
+    // MSB first: keep the matched docs whose value has the bit set (MAX) / clear (MIN) while any does
+    const bool mx = ag.op == PGPU_RED_MAX_I64;
+    uint32_t cand = mm, u = 0;
+#pragma unroll
+    for (int k = BSI_MAXB - 1; k >= 0; --k) {
+      if (k >= vb) continue;
+      const uint32_t t = cand & (mx ? x[k] : ~x[k]);
+      if (t) cand = t;
+      if ((t != 0) == mx) u |= 1u << k;
+    }
+    part = mm ? c.vmin + (int64_t)u : sec_identity(ag.op);
+  }
+  lacc_add(la, cv, a, ag.op, part);
+}
+
+FI void sliced_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, int tile, uint32_t mm,
+                    int& sn) {
+  bool all_bsi = true;
+  for (int a = 0; a < p.nagg; ++a)
+    if (p.aggs[a].fn != PGPU_AGG_COUNT) all_bsi = all_bsi && bsi_agg(p.aggs[a], col_of(ss, p.aggs[a].col));
+  if (all_bsi) {
+    for (int a = 0; a < p.nagg; ++a)
+      if (p.aggs[a].fn != PGPU_AGG_COUNT) bsi_tile(cv, la, col_of(ss, p.aggs[a].col), p.aggs[a], a, tile, mm);
+    return;
+  }
+  // (the planner sends a segment here only when its aggregations are all bit-sliced-index ones, or at most two over
+  // <= 16-bit columns: sliced_queued)
+  const int cap = PGPU_CQ_CAP / 2;
+  // a tile with more matches than a sub-queue holds goes in quarters of 16 lanes (<= 512 docs each)
+  const int cnt_all = __popc(mm);
+  const int nm_all = wave_sum_i32(cnt_all);
+  const int parts = nm_all <= cap ? 1 : 4;
+  for (int part = 0; part < parts; ++part) {
+    const uint32_t mp = parts == 1 ? mm : ((lane_id() >> 4) == part ? mm : 0u);
+    const int cnt = __popc(mp);
+    const int ex = wave_excl_scan(cnt);
+    const int nm = __builtin_amdgcn_readlane(ex + cnt, 63);
+    if (nm == 0) continue;
+    if (sn + nm > cap) {
+      sliced_flush(p, cv, la, ss, sn);
+      sn = 0;
+    }
+    int slot = 0;
+    for (int a = 0; a < p.nagg; ++a) {
+      if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+      const DevColumn c = col_of(ss, p.aggs[a].col);
+      uint16_t* q = cv.queue + slot++ * cap;
+#define SQ_CALL(B) sliced_enqueue_b<B>(c, tile, mp, q, sn + ex)
+      switch (c.bits) {
+        case 1: SQ_CALL(1); break;   case 2: SQ_CALL(2); break;   case 3: SQ_CALL(3); break;   case 4: SQ_CALL(4); break;
+        case 5: SQ_CALL(5); break;   case 6: SQ_CALL(6); break;   case 7: SQ_CALL(7); break;   case 8: SQ_CALL(8); break;
+        case 9: SQ_CALL(9); break;   case 10: SQ_CALL(10); break; case 11: SQ_CALL(11); break; case 12: SQ_CALL(12); break;
+        case 13: SQ_CALL(13); break; case 14: SQ_CALL(14); break; case 15: SQ_CALL(15); break; default: SQ_CALL(16); break;
+      }
+#undef SQ_CALL
+    }
+    sn += nm;
   }
 }
 
@@ -2162,7 +2238,7 @@ template <int MODE, int NW>
 FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                           int tile_in_seg, uint32_t mm, int& qn, int& qt, uint32_t& lane_matched, int64_t& matched,
                           int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf,
-                          const unsigned char* slot = nullptr) {
+                          int* sn = nullptr) {
   const int lane = lane_id();
   if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
     lane_matched += __popc(mm);
@@ -2171,7 +2247,13 @@ FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, Lane
     lane_matched += __popc(mm);
     const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
     mark_seg(p, ss, any);
-    if (any) sliced_agg(p, cv, la, ss, slot, mm);
+    if (any && sn) sliced_tile(p, cv, la, ss, tile_in_seg, mm, *sn);
+    if (any && (p.flags & PGPU_FLAG_STATS) && lane == 0)  // the aggregated columns' planes of this tile
+      for (int a = 0; a < p.nagg; ++a)
+        if (p.aggs[a].fn != PGPU_AGG_COUNT) {
+          const DevColumn c = col_of(ss, p.aggs[a].col);
+          dense_bytes += (int64_t)WT * (bsi_agg(p.aggs[a], c) ? c.vbits : c.bits) / 8;
+        }
   } else if (__builtin_amdgcn_ballot_w64(mm != 0) != 0) {
     const int cnt = __popc(mm);
     const int ex = wave_excl_scan(cnt);
@@ -2227,6 +2309,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
 #pragma unroll
   for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
   int qn = 0, qt = 0;
+  int sn = 0;  // PGPU_AM_SLICED: ids queued per column (sliced_tile)
   SegState ss;
   int cseg = -1;
   if (cidx < ntiles) {
@@ -2260,6 +2343,10 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
         qn = qt = 0;
       }
       if (cur.seg != cseg) {
+        if (MODE == PGPU_MODE_AGG && sn) {  // queued ids are the previous segment's
+          sliced_flush(p, cv, la, ss, sn);
+          sn = 0;
+        }
         cseg = cur.seg;
         load_seg(p, cseg, ss);
       }
@@ -2297,10 +2384,11 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);
       direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, mm, qn, qt, lane_matched, matched, scanned,
-                                  sector_bytes, dense_bytes, pf, t.slot);
+                                  sector_bytes, dense_bytes, pf, &sn);
       PROF_ADD(pf, PGPU_P_C_AGG, ta);
     }
     if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+    if (MODE == PGPU_MODE_AGG && sn) sliced_flush(p, cv, la, ss, sn);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   {
@@ -3497,53 +3585,87 @@ __global__ __launch_bounds__(256) void leafbits_kernel(DevParams p) {
 #define PGPU_ANDFSM_WORDS 8  // per tile: next-state bits (2 per start state), then H per start state
 FI uint32_t sel4(const uint32_t (&v)[4], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3]; }
 
+template <int B>
+FI void sliced_load_fsm(const uint32_t* sl, int tile, uint32_t (&x)[B]) {
+  const uint32_t* src = sl + (size_t)tile * 64 * B + lane_id();
+#pragma unroll
+  for (int k = 0; k < B; ++k) x[k] = __builtin_nontemporal_load(src + 64 * k);
+}
 // A SCAN leaf's words for the transducer from the column's bit-sliced copy (plane k of lane l at dword
 // (tile * B + k) * 64 + l): a dict-id range is lt(hi) & ~lt(lo) (sliced_lt), an id list an OR of [id, id + 1).  A
-// single id on a wide column is compared MSB first, four planes at a time, and stops once no doc of the wave can
-// still match (accountId = x in config 5: ~12 of its 20 planes are read).
+// (The MSB-first early exit of an EQ leaf -- a wave stops once no doc can match -- measured slower: its dependent
+// four-plane rounds leave each tile's loads latency-bound.)
 template <int B>
 FI uint32_t fsm_sliced_b(const uint32_t* sl, int tile, const DevInstr& in) {
-  const uint32_t* src = sl + (size_t)tile * 64 * B + lane_id();
+  uint32_t x[B];
+  sliced_load_fsm<B>(sl, tile, x);  // every plane in flight at once: one round trip per tile
   uint32_t m;
-  if (in.pred == PRED_LIST && in.n == 1 && B >= 12) {
-    const uint32_t id = in.ids[0];
-    m = ~0u;
-    for (int k0 = B - 1; k0 >= 0; k0 -= 4) {
-      uint32_t x[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = k0 - j >= 0 ? __builtin_nontemporal_load(src + 64 * (k0 - j)) : 0u;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (k0 - j >= 0) m &= ((id >> (k0 - j)) & 1u) ? x[j] : ~x[j];
-      if (__builtin_amdgcn_ballot_w64(m != 0) == 0) break;
+  if (in.pred == PRED_RANGE) {
+    m = sliced_lt<B>(x, (uint32_t)in.hi) & ~sliced_lt<B>(x, (uint32_t)in.lo);
+  } else if (in.pred == PRED_MASK) {  // <= 64 ids: one [id, id + 1) per member of the mask
+    m = 0;
+    for (uint64_t mk = ((uint64_t)(uint32_t)in.hi << 32) | (uint32_t)in.lo; mk; mk &= mk - 1) {
+      const uint32_t id = (uint32_t)__builtin_ctzll(mk);
+      m |= sliced_lt<B>(x, id + 1u) & ~sliced_lt<B>(x, id);
     }
   } else {
-    uint32_t x[B];
+    m = 0;
 #pragma unroll
-    for (int k = 0; k < B; ++k) x[k] = __builtin_nontemporal_load(src + 64 * k);
-    if (in.pred == PRED_RANGE) {
-      m = sliced_lt<B>(x, (uint32_t)in.hi) & ~sliced_lt<B>(x, (uint32_t)in.lo);
-    } else if (in.pred == PRED_MASK) {  // <= 64 ids: one [id, id + 1) per member of the mask
-      m = 0;
-      for (uint64_t mk = ((uint64_t)(uint32_t)in.hi << 32) | (uint32_t)in.lo; mk; mk &= mk - 1) {
-        const uint32_t id = (uint32_t)__builtin_ctzll(mk);
-        m |= sliced_lt<B>(x, id + 1u) & ~sliced_lt<B>(x, id);
-      }
-    } else {
-      m = 0;
-      for (int j = 0; j < in.n && j < 8; ++j) m |= sliced_lt<B>(x, in.ids[j] + 1u) & ~sliced_lt<B>(x, in.ids[j]);
+    for (int j = 0; j < 4; ++j)  // (fsm_sliced_ok: <= 4 ids; a constant index keeps ids[] out of scratch)
+      if (j < in.n) m |= sliced_lt<B>(x, in.ids[j] + 1u) & ~sliced_lt<B>(x, in.ids[j]);
+  }
+  return in.negate ? ~m : m;
+}
+// Runtime-width forms (FSM_MAXB planes, each guarded by k < bits: constant register indices, no dispatch), so that
+// the planes of several leaves can be in flight together.
+#define FSM_MAXB 24
+FI void fsm_load_planes(const uint32_t* sl, int bits, int tile, uint32_t (&x)[FSM_MAXB]) {
+  const uint32_t* src = sl + (size_t)tile * 64 * bits + lane_id();
+#pragma unroll
+  for (int k = 0; k < FSM_MAXB; ++k) x[k] = k < bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;
+}
+FI uint32_t fsm_lt(const uint32_t (&x)[FSM_MAXB], int bits, uint32_t c) {
+  if (c >> bits) return ~0u;  // past the largest id
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < FSM_MAXB; ++k)
+    if (k < bits) br = __builtin_amdgcn_bitop3_b32((uint32_t)-(int32_t)((c >> k) & 1u), x[k], br, 0xB2);
+  return br;
+}
+FI uint32_t fsm_eval_planes(const uint32_t (&x)[FSM_MAXB], const DevInstr& in) {
+  const int b = in.bits;
+  uint32_t m;
+  if (in.pred == PRED_RANGE) {
+    m = fsm_lt(x, b, (uint32_t)in.hi) & ~fsm_lt(x, b, (uint32_t)in.lo);
+  } else if (in.pred == PRED_MASK) {
+    m = 0;
+    for (uint64_t mk = ((uint64_t)(uint32_t)in.hi << 32) | (uint32_t)in.lo; mk; mk &= mk - 1) {
+      const uint32_t id = (uint32_t)__builtin_ctzll(mk);
+      m |= fsm_lt(x, b, id + 1u) & ~fsm_lt(x, b, id);
     }
+  } else {
+    m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < in.n) m |= fsm_lt(x, b, in.ids[j] + 1u) & ~fsm_lt(x, b, in.ids[j]);
   }
   return in.negate ? ~m : m;
 }
 FI bool fsm_sliced_ok(const DevInstr& in, const DevColumn& c) {
-  return in.op == PGPU_I_SCAN && in.kind == PGPU_COL_FIXED_BIT && c.sliced && in.bits >= 1 && in.bits <= 31 &&
+  return in.op == PGPU_I_SCAN && in.kind == PGPU_COL_FIXED_BIT && c.sliced && in.bits >= 1 && in.bits <= 24 &&
          (in.pred == PRED_RANGE || in.pred == PRED_MASK || (in.pred == PRED_LIST && in.n >= 1 && in.n <= 4));
 }
 FI uint32_t fsm_sliced(const uint32_t* sl, int bits, int tile, const DevInstr& in) {
   uint32_t m = 0;
 #define FS_CALL(B) m = fsm_sliced_b<B>(sl, tile, in)
-  PGPU_DISPATCH_B(bits, FS_CALL)
+  switch (bits) {
+    case 1: FS_CALL(1); break;   case 2: FS_CALL(2); break;   case 3: FS_CALL(3); break;   case 4: FS_CALL(4); break;
+    case 5: FS_CALL(5); break;   case 6: FS_CALL(6); break;   case 7: FS_CALL(7); break;   case 8: FS_CALL(8); break;
+    case 9: FS_CALL(9); break;   case 10: FS_CALL(10); break; case 11: FS_CALL(11); break; case 12: FS_CALL(12); break;
+    case 13: FS_CALL(13); break; case 14: FS_CALL(14); break; case 15: FS_CALL(15); break; case 16: FS_CALL(16); break;
+    case 17: FS_CALL(17); break; case 18: FS_CALL(18); break; case 19: FS_CALL(19); break; case 20: FS_CALL(20); break;
+    case 21: FS_CALL(21); break; case 22: FS_CALL(22); break; case 23: FS_CALL(23); break; default: FS_CALL(24); break;
+  }
 #undef FS_CALL
   return m;
 }
@@ -3569,9 +3691,29 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
   }
   int64_t dummy = 0;
   uint32_t m[4] = {0u, 0u, 0u, 0u};
+  // the first two leaves, when bit-sliced: every plane of both is loaded before either is evaluated (one round trip
+  // per tile instead of one per leaf)
+  uint32_t x0[FSM_MAXB], x1[FSM_MAXB];
+  bool sl0 = false, sl1 = false;
+  DevInstr in0, in1;
+  if (k > 0) {
+    in0 = cld(p.instrs + cld(p.pool, leaf_begin));
+    const DevColumn c0 = col_of(ss, in0.col);
+    sl0 = fsm_sliced_ok(in0, c0);
+    if (sl0) fsm_load_planes(c0.sliced, in0.bits, t.tile_in_seg, x0);
+  }
+  if (k > 1) {
+    in1 = cld(p.instrs + cld(p.pool, leaf_begin + 1));
+    const DevColumn c1 = col_of(ss, in1.col);
+    sl1 = fsm_sliced_ok(in1, c1);
+    if (sl1) fsm_load_planes(c1.sliced, in1.bits, t.tile_in_seg, x1);
+  }
+  if (sl0) m[0] = fsm_eval_planes(x0, in0) & t.valid;
+  if (sl1) m[1] = fsm_eval_planes(x1, in1) & t.valid;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (j >= k) break;
+    if ((j == 0 && sl0) || (j == 1 && sl1)) continue;
     const DevInstr in = cld(p.instrs + cld(p.pool, leaf_begin + j));
     const DevColumn col = col_of(ss, in.col);
     if (fsm_sliced_ok(in, col)) m[j] = fsm_sliced(col.sliced, in.bits, t.tile_in_seg, in) & t.valid;
@@ -3954,6 +4096,40 @@ __device__ void bitslice_b(const uint32_t* fwd, uint32_t* out, int64_t tile, int
     dst[(size_t)k * 64] = pl;
   }
 }
+// Value planes (DevColumn::vsliced): per tile and lane the 32 docs' dictionary values minus vmin, bit k of doc 32l+i
+// in bit i of dword k * 64 + l of the tile's 256 * vbits bytes.
+template <int B>
+__device__ void vslice_b(const uint32_t* fwd, const void* dict, int dict_type, int64_t vmin, int vbits, uint32_t* out,
+                         int64_t tile, int lane) {
+  uint32_t w[B], ids[32];
+  const uint32_t* src = fwd + ((size_t)tile * 64 + lane) * B;
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = bswap32(src[k]);
+  unpack_b<B>(w, ids);
+  uint32_t u[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int64_t v = dict_type == PGPU_INT ? (int64_t)gld((const int32_t*)dict, ids[i]) : gld((const int64_t*)dict, ids[i]);
+    u[i] = (uint32_t)((uint64_t)v - (uint64_t)vmin);
+  }
+  uint32_t* dst = out + (size_t)tile * vbits * 64 + lane;
+  for (int k = 0; k < vbits; ++k) {
+    uint32_t pl = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) pl |= ((u[i] >> k) & 1u) << i;
+    dst[(size_t)k * 64] = pl;
+  }
+}
+__global__ __launch_bounds__(256) void vslice_kernel(const uint32_t* fwd, const void* dict, int dict_type, int64_t vmin,
+                                                     int bits, int vbits, uint32_t* out, int64_t ntiles) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tile = g >> 6;
+  const int lane = (int)(g & 63);
+  if (tile >= ntiles) return;
+#define VS_CALL(B) vslice_b<B>(fwd, dict, dict_type, vmin, vbits, out, tile, lane)
+  PGPU_DISPATCH_B(bits, VS_CALL)
+#undef VS_CALL
+}
 __global__ __launch_bounds__(256) void bitslice_kernel(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles) {
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tile = g >> 6;
@@ -4141,6 +4317,15 @@ hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t m
   if (nleaves <= 0) return hipSuccess;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (max_words / 32 + 3) / 4));
   hipLaunchKernelGGL(rawpred_kernel, dim3((unsigned)blocks, (unsigned)nleaves), dim3(256), 0, st, dev_leaves);
+  return hipGetLastError();
+}
+
+hipError_t pgpu_launch_vslice(const uint32_t* fwd, const void* dict, int dict_type, int64_t vmin, int bits, int vbits,
+                              uint32_t* out, int64_t ntiles, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  const int64_t blocks = (ntiles * 64 + 255) / 256;
+  hipLaunchKernelGGL(vslice_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fwd, dict, dict_type, vmin, bits, vbits,
+                     out, ntiles);
   return hipGetLastError();
 }
 

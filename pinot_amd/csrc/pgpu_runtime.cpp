@@ -39,6 +39,8 @@ hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_sme
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
 hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st);
+hipError_t pgpu_launch_vslice(const uint32_t* fwd, const void* dict, int dict_type, int64_t vmin, int bits, int vbits,
+                              uint32_t* out, int64_t ntiles, hipStream_t st);
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
                                 bool init_table, hipStream_t st);
 hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
@@ -261,6 +263,10 @@ struct HostColumn {
   int32_t inv_card = 0;
   DevMem fwd, sorted, dict, inv_dir, inv_ct, inv_data;
   DevMem sliced;                       // bit-sliced copy of fwd (built at seal; PGPU_NO_SLICE=1 skips it)
+  DevMem vsliced;                      // bit planes of the docs' values - vmin (INT / LONG dictionaries, <= 32 bits;
+                                       // built at seal; PGPU_NO_VSLICE=1 skips it)
+  int64_t vmin = 0;
+  int32_t vbits = 0;
   uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
@@ -994,8 +1000,39 @@ int seal_column(pgpu_segment* seg, size_t i) {
     HIP_TRY(hipMemset(c.sliced.p, 0, c.sliced.n));
     HIP_TRY(pgpu_launch_bitslice((const uint32_t*)c.fwd.p, (uint32_t*)c.sliced.p, c.bits, ntiles, nullptr));
   }
+  // value planes (bit-sliced index of the values): SUM is then sum_k 2^k popcount(plane_k & matched) per tile and
+  // MIN / MAX an MSB-first selection -- no per-doc id extraction, no dictionary gather (PGPU_AM_SLICED)
+  static const bool no_vslice = getenv("PGPU_NO_VSLICE") && atoi(getenv("PGPU_NO_VSLICE")) != 0;
+  if (c.kind == PGPU_COL_FIXED_BIT && !no_vslice && !c.vsliced.p && c.dict.p && c.dict_card > 0 &&
+      (c.dict_type == PGPU_INT || c.dict_type == PGPU_LONG) && c.hdict.size() >= (size_t)c.dict_card * type_width(c.dict_type)) {
+    int64_t lo, hi;
+    if (c.dict_type == PGPU_INT) {
+      int32_t a, b;
+      memcpy(&a, c.hdict.data(), 4);
+      memcpy(&b, c.hdict.data() + 4 * (size_t)(c.dict_card - 1), 4);
+      lo = a;
+      hi = b;
+    } else {
+      memcpy(&lo, c.hdict.data(), 8);
+      memcpy(&hi, c.hdict.data() + 8 * (size_t)(c.dict_card - 1), 8);
+    }
+    const uint64_t range = (uint64_t)hi - (uint64_t)lo;  // ascending dictionary (checked at upload)
+    int vb = 0;
+    while (vb < 64 && (range >> vb)) ++vb;
+    if (hi >= lo && vb >= 1 && vb <= 32) {
+      const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
+      HIP_TRY(c.vsliced.alloc((size_t)ntiles * 256 * vb));
+      HIP_TRY(pgpu_launch_vslice((const uint32_t*)c.fwd.p, c.dict.p, c.dict_type, lo, c.bits, vb,
+                                 (uint32_t*)c.vsliced.p, ntiles, nullptr));
+      c.vmin = lo;
+      c.vbits = vb;
+    }
+  }
   DevColumn d{};
   d.sliced = (const uint32_t*)c.sliced.p;
+  d.vsliced = (const uint32_t*)c.vsliced.p;
+  d.vmin = c.vmin;
+  d.vbits = c.vbits;
   d.fwd = (const uint32_t*)c.fwd.p;
   // a multi-value column's row offsets take the sorted-index slot (sparse_agg_mv; a MV column has no sorted index)
   d.sorted = (const int32_t*)(c.kind == PGPU_COL_MV ? c.mv_off.p : c.sorted.p);
@@ -1143,7 +1180,7 @@ int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes) {
   if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
   uint64_t t = 0;
   for (const HostColumn& c : seg->cols)
-    t += c.fwd.n + c.sliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n + c.mv_off.n;
+    t += c.fwd.n + c.sliced.n + c.vsliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n + c.mv_off.n;
   *out_bytes = t;
   return PGPU_OK;
 }
@@ -1934,17 +1971,35 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   int agg_mode;
   static const bool no_sliced = getenv("PGPU_NO_SLICED_AGG") && atoi(getenv("PGPU_NO_SLICED_AGG")) != 0;
   static const double sliced_touch = getenv("PGPU_SLICED_TOUCH") ? atof(getenv("PGPU_SLICED_TOUCH")) : kSlicedAggTouch;
-  bool sliced = !no_sliced && !aggcols.empty() && !residual && p.mode == PGPU_MODE_AGG && !p.mv_gmask;
-  for (int qc : aggcols) {
-    const DevColumn* dc = v.dev(qc);
-    sliced = sliced && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced && dc->bits >= 1 && dc->bits <= 31 &&
-             line_touch(rho, dc->bits) >= sliced_touch;
+  // (aggregation-only: p.mode is still undecided for dense group-by tables here)
+  // every aggregation answered from value planes (SUM of whole int64 cells, MIN, MAX over an INT / LONG dictionary
+  // of <= 24 value bits: sliced_tile's bit-sliced index), or at most two over id planes of <= 16 bits (ids queued,
+  // values gathered in batches)
+  bool sliced = !no_sliced && !aggcols.empty() && !residual && q->num_group_columns == 0 && !p.mv_gmask;
+  bool all_bsi = true;
+  int nvalue = 0;
+  for (int a = 0; a < q->num_aggs; ++a) {
+    if (q->aggs[a].fn == PGPU_AGG_COUNT) continue;
+    ++nvalue;
+    const DevColumn* dc = v.dev(q->aggs[a].column);
+    const bool whole_sum = q->aggs[a].fn == PGPU_AGG_SUM || q->aggs[a].fn == PGPU_AGG_AVG;
+    bool split = false;  // a SUM split into 21-bit part sections (pgpu_table_layout.agg_sum_parts == 3)
+    for (int i = 0; i < p.nagg; ++i) split = split || (p.aggs[i].col == q->aggs[a].column && p.aggs[i].part != 0);
+    const bool bsi = dc->vsliced && dc->vbits >= 1 && dc->vbits <= 24 &&
+                     ((whole_sum && (dc->dict_type == PGPU_INT || dc->dict_type == PGPU_LONG) && !split) ||
+                      q->aggs[a].fn == PGPU_AGG_MIN || q->aggs[a].fn == PGPU_AGG_MAX);
+    all_bsi = all_bsi && bsi;
+    sliced = sliced && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced &&
+             line_touch(rho, bsi ? dc->vbits : dc->bits) >= sliced_touch;
+  }
+  if (sliced && !all_bsi) {
+    for (int qc : aggcols) sliced = sliced && v.dev(qc)->bits >= 1 && v.dev(qc)->bits <= 16;
+    sliced = sliced && nvalue <= 2;
   }
   if (aggcols.empty()) {
     agg_mode = PGPU_AM_COUNT;
   } else if (sliced) {
-    agg_mode = PGPU_AM_SLICED;
-    for (int qc : aggcols) add_stage(qc);
+    agg_mode = PGPU_AM_SLICED;  // the aggregated columns' planes load into VGPRs per matched tile: nothing staged
   } else if (residual || p.mv_gmask) {  // multi-value group keys: expanded per candidate doc (sparse_agg_mv)
     agg_mode = PGPU_AM_SPARSE;
   } else {
@@ -1969,7 +2024,7 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     }
     return staged.size() <= PGPU_MAX_STAGE && instrs <= PGPU_MAX_STAGE_INSTRS && bytes <= kMaxSlotBytes;
   };
-  if (!fits() && (agg_mode == PGPU_AM_DENSE || agg_mode == PGPU_AM_SLICED)) {
+  if (!fits() && agg_mode == PGPU_AM_DENSE) {
     staged.resize(nfilter_stage);
     agg_mode = PGPU_AM_SPARSE;
   }
@@ -2087,24 +2142,6 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       ds.f_rng[j][r][1] = rng[r].second;
     }
     ds.stage_sliced |= 1 << stage_index(in.col);
-  }
-  // sliced aggregation: the aggregated columns' staged regions are plain copies of their bit-sliced tiles; the
-  // dense program must then read staged columns only as fast sliced leaves (run_program would decode a staged
-  // region as the packed layout)
-  if (agg_mode == PGPU_AM_SLICED) {
-    bool prog_ok = true;
-    for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
-      const DevInstr& in = pk.instrs[i];
-      if (in.op == PGPU_I_SCAN && ds.fast == 0) prog_ok = false;
-    }
-    for (int j = 0; j < ds.fast; ++j)
-      prog_ok = prog_ok && ds.f_nr[j] > 0;  // each fast leaf evaluated on its planes
-    if (prog_ok) {
-      for (int qc : aggcols) ds.stage_sliced |= 1 << stage_index(qc);
-    } else {
-      staged.resize(nfilter_stage);
-      agg_mode = PGPU_AM_SPARSE;
-    }
   }
   // staging layout
   std::vector<int> stage_offs;
@@ -2397,7 +2434,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       ok &= ds.ntiles == 0 || ((ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&
                                ((ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1) ||
                                 (ds.nstage == 0 && ds.fast == 0))) ||
-            (ds.agg_mode == PGPU_AM_SLICED && ds.stage_sliced == (1 << ds.nstage) - 1);
+            (ds.agg_mode == PGPU_AM_SLICED &&
+             ((ds.fast >= 1 && ds.nstage == ds.fast && ds.stage_sliced == (1 << ds.nstage) - 1) ||
+              (ds.nstage == 0 && ds.fast == 0)));
     // up to five 4-wave workgroups per CU (more waves hide the per-tile latency better than deeper prefetch, which
     // measured flat); each wave keeps D - 1 tiles in flight, aiming at ~12 KiB (HBM latency
     // x per-CU bandwidth), within the 6-bit vmcnt and the LDS

@@ -244,7 +244,7 @@ def test_and_of_scans_exact_filter_stats(gpu_ctx, n, qi):
 # aggregation-only queries whose aggregated columns are streamed bit-sliced beside the filter (PGPU_AM_SLICED,
 # query_kernel_direct): every value type, narrow and wide columns, an aggregated column that is also the filter's,
 # index-only filters
-SLICED_QUERIES = [
+SLICED_AGG_QUERIES = [
     "SELECT COUNT(*), SUM(m), MIN(m), MAX(f), AVG(d) FROM t WHERE c < 2000 AND b > 3",
     "SELECT SUM(d), MAX(m), COUNT(*) FROM t WHERE d BETWEEN 1000 AND 150000",
     "SELECT SUM(m), MIN(c), AVG(g) FROM t WHERE a <> 0",
@@ -254,15 +254,37 @@ SLICED_QUERIES = [
 
 @pytest.mark.parametrize("types", [None, {"m": PGPU_DOUBLE, "f": PGPU_FLOAT}, {"m": PGPU_LONG, "f": PGPU_DOUBLE}])
 @pytest.mark.parametrize("n", [4097, 200_003])
-@pytest.mark.parametrize("qi", range(len(SLICED_QUERIES)))
+@pytest.mark.parametrize("qi", range(len(SLICED_AGG_QUERIES)))
 def test_sliced_aggregation_vs_oracle(gpu_ctx, qi, n, types):
     rng = np.random.default_rng(500 + qi + n)
     inv = ["a", "b"] if qi == 3 else []
     segs = [_random_segment(rng, n, f"sl{i}", inverted=inv, types=types) for i in range(3)]
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
-        q = parse_sql(SLICED_QUERIES[qi])
+        q = parse_sql(SLICED_AGG_QUERIES[qi])
         _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
+    finally:
+        for g in gs:
+            g.release()
+
+
+@pytest.mark.parametrize("n", [2048, 70_001])
+def test_value_planes_negative_and_long(gpu_ctx, n):
+    """Bit-sliced value planes (DevColumn::vsliced: value - vmin) over negative INT and LONG dictionaries of <= 24
+    value bits, and a constant column (no planes: the id path)."""
+    rng = np.random.default_rng(n)
+    cols = {"x": (PGPU_INT, rng.integers(0, 50, n).astype(np.int32)),
+            "neg": (PGPU_INT, rng.integers(-3_000_000, 3_000_000, n).astype(np.int32)),
+            "lg": (PGPU_LONG, (rng.integers(0, 1 << 20, n) - (1 << 40)).astype(np.int64)),
+            "one": (PGPU_INT, np.full(n, 7, dtype=np.int32))}
+    segs = [build_segment(f"vp{i}", cols, sorted_columns=()) for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        for sql in ("SELECT SUM(neg), MIN(neg), MAX(neg), COUNT(*) FROM t WHERE x < 40",
+                    "SELECT SUM(lg), MIN(lg), MAX(lg), AVG(neg) FROM t WHERE x >= 3",
+                    "SELECT SUM(one), MAX(one), SUM(neg) FROM t WHERE x <> 7"):
+            q = parse_sql(sql)
+            _assert_same(_gpu(gpu_ctx, q, gs), engine.execute(q, segs))
     finally:
         for g in gs:
             g.release()
