@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 8
+#define PGPU_ABI_VERSION 9
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -288,6 +288,11 @@ typedef struct {
    * at launch), the query is cancelled and pgpu_query_wait / _collect / _execute / pgpu_node_query return
    * PGPU_E_TIMEOUT. */
   int64_t deadline_ms;
+  /* Per aggregation (num_aggs entries), or NULL: a lower bound of the fixed-point exponent of each FLOAT / DOUBLE
+   * SUM / AVG (pgpu_table_layout.agg_sum_exp).  The layout takes the larger of it and the launch's own, so callers
+   * that combine tables across launches (ranks, devices) pass the max of their launches' agg_sum_exp and get one
+   * layout everywhere; PGPU_SUM_EXP_F64 forces the float64 section. */
+  const int32_t* sum_exp;
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
@@ -322,7 +327,15 @@ typedef struct {
  *                                  SUM = c[s] + c[s+1] * 2^21 + c[s+2] * 2^42, exact for < 2^42 docs
  *                                  (SumAggregationFunction.java:55-92 adds doubles in doc order and never
  *                                  wraps; an int64 cell would)
- *                              SUM of FLOAT/DOUBLE      -> float64 SUM
+ *                              SUM of FLOAT/DOUBLE      -> three 21-bit-part int64 SUM sections of the
+                                                          values in fixed point: v -> rint(v * 2^-e) with
+                                                          e = ilogb(max|value|) + 1 - 62 (agg_sum_exp), so that
+                                                          integer adds make the sum independent of the order
+                                                          the GPU adds in (a float64 SUM of atomics is not);
+                                                          value = round(exact part sum) * 2^e, within 2^-61 of
+                                                          max|value| per value of the exact sum.  A NaN or
+                                                          infinity in the column (or no section budget) keeps
+                                                          one float64 SUM section (agg_sum_exp = PGPU_SUM_EXP_F64)
  *                              MIN / MAX                -> int64 MIN / MAX of an order-preserving key
  *                              AVG                      -> as SUM (count comes from section 0)
  *                              COUNT                    -> no section (section 0)
@@ -333,6 +346,7 @@ typedef struct {
 #define PGPU_RED_SUM_F64 1
 #define PGPU_RED_MIN_I64 2
 #define PGPU_RED_MAX_I64 3
+#define PGPU_SUM_EXP_F64 32767 /* agg_sum_exp of a float64 SUM section */
 
 /* key_kind of a table layout */
 #define PGPU_KEYS_DENSE 0 /* cell index = global raw key: sum_j gid_j * prod_{k<j} card_k (< 2^31) */
@@ -344,7 +358,9 @@ typedef struct {
   int32_t section_op[PGPU_MAX_SECTIONS]; /* PGPU_RED_* per section (section 0 = count) */
   int32_t agg_section[16]; /* section of agg i, or 0 for COUNT */
   int32_t agg_value_type[16]; /* stored type of the agg column (PGPU_INT..), -1 for COUNT */
-  int32_t agg_sum_parts[16];  /* SUM / AVG of INT / LONG: 1 = one exact int64 section, 3 = 21-bit-part sections */
+  int32_t agg_sum_parts[16];  /* SUM / AVG: 1 = one int64 (or float64) section, 3 = 21-bit-part sections */
+  int32_t agg_sum_exp[16];    /* SUM / AVG of FLOAT / DOUBLE in fixed point: value = (exact part sum) * 2^exp;
+                                 PGPU_SUM_EXP_F64 = a float64 section; 0 for integer columns */
   /* Group keys.  Dense: the cell index is the key.  Hash: key_words int64 words per slot follow the sections
    * (word w of slot i at int64 index (num_sections + w) * num_keys + i; an empty slot holds -1).  Word 0 is the
    * mixed-radix key of group columns [0, key_split), word 1 (when key_words == 2, key spaces above 2^63, the
@@ -511,10 +527,18 @@ int pgpu_query_submit_ordered(pgpu_context* ctx, const pgpu_query_desc* q, const
  * For a server that drives all GPUs of a node from one process (a JVM): contexts for the given HIP ordinals and
  * one RCCL communicator clique over them (RCCL is loaded on first use).  Segments are uploaded through each
  * device's context (pgpu_node_context).  pgpu_node_query runs descs[i] (device i's segments, the same aggregations,
- * group columns and global group cardinalities on every device) on every device, merges the partial tables --
- * dense: grouped ncclReduce per section to device 0 over xGMI; hash: per-device compaction merged by key -- and
- * compacts the result like pgpu_query_collect (out_layout receives the layout the cells follow).  Replaces the
- * host-side combine (AggregationOnlyCombineOperator.java:47-57, GroupByOrderByCombineOperator.java:127-248). */
+ * group columns and global group cardinalities on every device) on every device and merges the partial tables over
+ * xGMI with the collectives of the one-process-per-GPU combine (pinot_amd/combine.py):
+ *   dense, aggregation only or < 1 MiB : grouped ncclReduce per run of same-op sections to device 0;
+ *   dense, larger                      : reduce-scatter -- device d owns the final cells of keys
+ *                                        pgpu_slice_of(G, n, d) -- and every device trims its own slice;
+ *   hash                               : each device's rows go to the device pgpu_key_owner names (peer copies)
+ *                                        and are merged there in a fresh hash table, then trimmed there.
+ * The rows come back like pgpu_query_collect's (out_layout receives the layout the cells follow); with `order`
+ * (pgpu_node_query_topk) each device keeps only its best order->k rows by the ORDER BY key, ties kept -- exact,
+ * because every row a device holds is final -- and the caller's ORDER BY ... LIMIT over the union equals the one
+ * over all groups.  Replaces the host-side combine (AggregationOnlyCombineOperator.java:47-57,
+ * GroupByOrderByCombineOperator.java:127-248, trim size GroupByUtils.getTableCapacity, GroupByUtils.java:24-41). */
 typedef struct pgpu_node pgpu_node;
 int pgpu_node_init(const int32_t* device_ordinals, int32_t num_devices, pgpu_node** out_node);
 int pgpu_node_context(pgpu_node* node, int32_t index, pgpu_context** out_ctx);
@@ -522,6 +546,15 @@ int pgpu_node_shutdown(pgpu_node* node);
 int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_t* out_keys, int64_t* out_cells,
                     uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
                     pgpu_table_layout* out_layout);
+int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_topk* order,
+                         int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups,
+                         pgpu_query_stats* out_stats, pgpu_table_layout* out_layout);
+/* The partition arithmetic both multi-GPU combines share (host only, no device needed): the key slice
+ * [first, first + count) of a dense table of num_keys keys that rank `rank` of `world` owns after the
+ * reduce-scatter (slices of ceil(num_keys / world) keys, the last one shorter), and the rank owning a hash-table
+ * group key of num_key_words words (-1 on bad arguments). */
+void pgpu_slice_of(uint64_t num_keys, int32_t world, int32_t rank, uint64_t* first, uint64_t* count);
+int32_t pgpu_key_owner(const int64_t* key_words, int32_t num_key_words, int32_t world);
 
 /* Convenience: submit + collect. */
 int pgpu_query_execute(pgpu_context* ctx, const pgpu_query_desc* q, int64_t* out_keys, int64_t* out_cells,

@@ -38,7 +38,8 @@ PGPU_Q_STATS, PGPU_Q_PARTITION, PGPU_Q_PART_SPILL, PGPU_Q_SUM_SPLIT, PGPU_Q_HASH
 PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
-ABI_VERSION = 8
+PGPU_SUM_EXP_F64 = 32767  # pgpu_table_layout.agg_sum_exp of a float64 SUM section
+ABI_VERSION = 9
 
 
 class PinotGpuError(RuntimeError):
@@ -89,13 +90,15 @@ class QueryDesc(C.Structure):
                 ("num_aggs", C.c_int32), ("num_group_columns", C.c_int32), ("aggs", C.POINTER(Agg)),
                 ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
                 ("flags", C.c_uint64), ("reduce_docs", C.c_int64), ("num_groups_limit", C.c_int32),
-                ("array_based_threshold", C.c_int32), ("deadline_ms", C.c_int64)]
+                ("array_based_threshold", C.c_int32), ("deadline_ms", C.c_int64),
+                ("sum_exp", C.POINTER(C.c_int32))]
 
 
 class TableLayout(C.Structure):
     _fields_ = [("num_keys", C.c_uint64), ("num_sections", C.c_int32), ("section_op", C.c_int32 * 17),
                 ("agg_section", C.c_int32 * 16), ("agg_value_type", C.c_int32 * 16),
-                ("agg_sum_parts", C.c_int32 * 16), ("key_kind", C.c_int32), ("key_words", C.c_int32),
+                ("agg_sum_parts", C.c_int32 * 16), ("agg_sum_exp", C.c_int32 * 16), ("key_kind", C.c_int32),
+                ("key_words", C.c_int32),
                 ("key_split", C.c_int32), ("reserved", C.c_int32)]
 
 
@@ -185,6 +188,11 @@ SIGNATURES = [
     ("pgpu_node_shutdown", C.c_int, [_P]),
     ("pgpu_node_query", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                   C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats), C.POINTER(TableLayout)]),
+    ("pgpu_node_query_topk", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(TopK), C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats),
+                                       C.POINTER(TableLayout)]),
+    ("pgpu_slice_of", None, [C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("pgpu_key_owner", C.c_int32, [C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
     ("pgpu_filter_entries_scanned", C.c_int, [C.POINTER(FilterNode), C.c_int32, C.POINTER(C.POINTER(C.c_uint32)),
                                              C.c_int32, C.c_int32, C.POINTER(C.c_int64)]),
     ("pgpu_kernel_geometry", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),

@@ -161,6 +161,28 @@ def union_dictionaries(local: Sequence, group=None, device=None):
     return vals
 
 
+def key_owners(keys: np.ndarray, world: int) -> np.ndarray:
+    """Rank owning each group key (rows of key words) in the hash-table merge: the key words chained with the
+    golden-ratio multiplier, two murmur3 fmix64 steps, modulo world -- the same routing as the node-level combine
+    (pgpu_key_owner, pgpu_internal.h pgpu_key_owner_of)."""
+    k2 = np.asarray(keys).reshape(len(keys), -1).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        h = k2[:, 0].copy()
+        for w in range(1, k2.shape[1]):
+            h = h * np.uint64(0x9E3779B97F4A7C15) + k2[:, w]
+        h ^= h >> np.uint64(33)
+        h *= np.uint64(0xff51afd7ed558ccd)
+        h ^= h >> np.uint64(33)
+    return (h % np.uint64(world)).astype(np.int64)
+
+
+def slice_of(num_keys: int, world: int, rank: int):
+    """(first, count) of the keys rank owns after reduce_scatter_sections (pgpu_slice_of)."""
+    K = (num_keys + world - 1) // world
+    first = min(num_keys, K * rank)
+    return first, min(K, num_keys - first)
+
+
 def minmax_key(value: float, vtype: int) -> int:
     """Order-preserving int64 key of a MIN / MAX value (the inverse of pgpu_decode_minmax_key)."""
     if vtype in (PGPU_INT, PGPU_LONG):
@@ -292,9 +314,11 @@ class DistributedExecutor:
             self._docs[key] = hit
         return hit[0]
 
-    def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int) -> int:
-        """Flags that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's integer-SUM bound
-        needs the split sections, PGPU_Q_HASH when any rank's key space takes the hash group-by."""
+    def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int):
+        """(flags, sum_exp) that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's
+        integer-SUM bound needs the split sections, PGPU_Q_HASH when any rank's key space takes the hash group-by,
+        and per aggregation the largest fixed-point exponent any rank's floating SUM needs
+        (pgpu_table_layout.agg_sum_exp; PGPU_SUM_EXP_F64 anywhere makes every rank keep float64 sections)."""
         key = (tuple((a.function, a.column) for a in query.aggregations), tuple(query.group_by),
                self._seg_key(segments))
         hit = self._split.get(key)
@@ -302,27 +326,31 @@ class DistributedExecutor:
             hit = None
         if hit is None:
             L = self._local_layout(query, segments, 0, reduce_docs)
-            split = any(L.agg_sum_parts[i] == 3 for i in range(len(query.aggregations)))
+            na = len(query.aggregations)
+            split = any(L.agg_sum_parts[i] == 3 and L.agg_value_type[i] in (_lib.PGPU_INT, _lib.PGPU_LONG)
+                        for i in range(na))
             hashed = L.key_kind == _lib.PGPU_KEYS_HASH
-            s_any, h_any = self._allreduce_i64([int(split), int(hashed)], "max")
-            hit = ((_lib.PGPU_Q_SUM_SPLIT if s_any else 0) | (_lib.PGPU_Q_HASH if h_any else 0), tuple(segments))
+            s_any, h_any, *exps = self._allreduce_i64([int(split), int(hashed)] + [L.agg_sum_exp[i] for i in range(na)],
+                                                      "max")
+            hit = (((_lib.PGPU_Q_SUM_SPLIT if s_any else 0) | (_lib.PGPU_Q_HASH if h_any else 0), tuple(exps)),
+                   tuple(segments))
             self._split[key] = hit
         return hit[0]
 
     # ---- local kernel step (libpinotgpu) -------------------------------------------------------------------------
-    def _local_layout(self, query, segments, flags, reduce_docs) -> TableLayout:
-        return self._prepare_local(query, segments, flags, reduce_docs)[0]
+    def _local_layout(self, query, segments, flags, reduce_docs, sum_exp=None) -> TableLayout:
+        return self._prepare_local(query, segments, flags, reduce_docs, sum_exp)[0]
 
     def _alloc_table(self, n: int):
         import torch
         pool = self._tables.setdefault(n, [])
         return pool.pop() if pool else torch.empty(n, dtype=torch.int64, device=self.device)
 
-    def _prepare_local(self, query, segments, flags, reduce_docs):
+    def _prepare_local(self, query, segments, flags, reduce_docs, sum_exp=None):
         """(table layout, launch(table) -> handle) for this rank's scanned segments."""
         expr = self.pm.filter_expr(query, segments)
         desc, keep, _ = self.pm.build_desc(query, segments, plan_filters=expr is None, extra_flags=flags,
-                                           reduce_docs=reduce_docs)
+                                           reduce_docs=reduce_docs, sum_exp=sum_exp)
         L = self.pm.layout(desc)
 
         def launch(table):
@@ -390,11 +418,12 @@ class DistributedExecutor:
             raise ValueError("every rank needs at least one segment")
         globals_ = self._global_dicts(query, segments) if query.group_by else []
         reduce_docs = self._reduce_docs(segments)
-        flags = self._layout_flags(query, segments, reduce_docs)
+        flags, sum_exp = self._layout_flags(query, segments, reduce_docs)
         non_scan = self.pm.non_scan_segments(query, segments)
         scan = [s for s, ns in zip(segments, non_scan) if not ns]
-        # the layout is the same on every rank: group cardinalities are global, the split-SUM choice agreed
-        L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs)
+        # the layout is the same on every rank: group cardinalities are global, the split-SUM choice and the
+        # fixed-point exponents agreed
+        L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs, sum_exp)
         n = _lib.table_bytes(L) // 8 if L.key_kind == _lib.PGPU_KEYS_HASH else int(L.num_sections * L.num_keys)
         table = self._alloc_table(n)
         handle = None
@@ -566,14 +595,7 @@ class DistributedExecutor:
         keys, cells = self._compact(L, p.table)
         kw = 1 if keys.ndim == 1 else keys.shape[1]
         n = len(keys)
-        k2 = keys.reshape(n, kw).astype(np.uint64)
-        h = k2[:, 0].copy()
-        for w in range(1, kw):
-            h = h * np.uint64(0x9E3779B97F4A7C15) + k2[:, w]
-        h ^= h >> np.uint64(33)
-        h *= np.uint64(0xff51afd7ed558ccd)
-        h ^= h >> np.uint64(33)
-        dest = (h % np.uint64(self.world)).astype(np.int64)
+        dest = key_owners(keys.reshape(n, kw), self.world)
         order = np.argsort(dest, kind="stable")
         width = kw + L.num_sections
         rows = np.concatenate([keys.reshape(n, kw), cells], axis=1)[order] if n else np.zeros((0, width), np.int64)

@@ -141,7 +141,8 @@ struct DevSeg {
   // k * ntiles * 64 + tile * 64 + lane] (leafbits_kernel)
   int32_t leaf_len;
   int32_t leaf_begin;
-  int32_t pad_;
+  int32_t single_bits;            // the dense program is one precomputed BITS leaf (progbits_kernel's output):
+                                  // a tile's match word is one load, no interpreter
   int64_t leaf_bits_off;
   // BITS leaves of the dense program (their instructions' n = slot): the query kernel loads their words for a
   // tile together before interpreting the program, one round trip instead of one per leaf
@@ -234,6 +235,18 @@ struct MvLeaf {
 
 // An inverted-index leaf expanded into a doc bitmap before the query kernel (invexp_kernel): one workgroup per
 // (leaf, 65,536-doc container key) ORs the key's container of every id, complemented within [0, num_docs) when negate.
+// An index-only dense program evaluated once per query over all of a segment's tiles (progbits_kernel), its
+// match words then read by the query kernel as one BITS leaf: the interpreter and the leaves' per-tile loads leave
+// the query kernel's critical path.
+struct ProgJob {
+  int32_t seg;                // query segment
+  int32_t prog_begin, prog_len;  // the original program (its BITS leaves load their words directly: n = -1)
+  int32_t tile0;              // first tile of this job in the progbits grid
+  int32_t ntiles;
+  int32_t pad_;
+  uint32_t* out;              // ntiles * 64 words (a workspace bitmap)
+};
+
 struct InvLeafX {
   const uint32_t* dir;     // DevColumn::inv_dir
   const DevContainer* ct;  // DevColumn::inv_ct
@@ -259,6 +272,7 @@ struct DevAgg {
   int32_t emit;     // PART mode: this aggregation's column is the one carried in the records (first such agg)
   int32_t part;     // split integer SUM (pgpu_table_layout.agg_sum_parts == 3): 0 whole value, 1 bits [0,21),
                     // 2 bits [21,42), 3 bits [42,64) (arithmetic) -- each a SUM_I64 section of its own
+  int32_t fxe;      // FLOAT / DOUBLE SUM_I64 (fixed point): the value's cell is rint(v * 2^-fxe) before the part split
 };
 #define PGPU_PART_BITS 21
 
@@ -279,6 +293,22 @@ struct DevAgg {
 // [0, key_split)) gets a slot s0 in a first table, then the slot of (s0 << 32 | word 1) is the cell index.
 #define PGPU_MODE_HASH 4
 #define PGPU_HASH_EMPTY (~0ull)
+
+// Owner of a group key in the node-level / multi-rank combine of hash tables: the key words chained with the
+// golden-ratio multiplier, two murmur3 fmix64 steps, modulo the device count -- bit for bit the routing of
+// pinot_amd/combine.py (_hash_merge_topk), so both combines send a key to the same rank.
+__host__ __device__ inline uint32_t pgpu_key_owner_of(const int64_t* key, int kw, int world) {
+  uint64_t h = (uint64_t)key[0];
+  for (int w = 1; w < kw; ++w) h = h * 0x9E3779B97F4A7C15ull + (uint64_t)key[w];
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return (uint32_t)(h % (uint64_t)world);
+}
+// Section ops of a table, by value (node merge kernel)
+struct NodeOps {
+  int32_t op[PGPU_MAX_SECTIONS];
+};
 
 #define PGPU_STAT_MATCHED 0
 #define PGPU_STAT_SCANNED 1
@@ -442,6 +472,8 @@ struct TopkDev {
   int32_t nsec;
   int32_t kw;        // 0 dense (cell index = key), 1 one hash key word, 2 two-level hash key
   uint64_t key_base; // dense: key of cell 0
+  int32_t fxe;       // SUM / AVG split of a fixed-point floating SUM: value = part sum * 2^fxe (0: integer)
+  int32_t pad_;
 };
 struct TopkState {  // radix-select state: the best-k threshold's high bits found so far
   uint64_t prefix, mask, kleft;
@@ -498,7 +530,7 @@ __host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDe
   switch (s.mode) {
     case PGPU_TK_COUNT: u = (uint64_t)cnt ^ 0x8000000000000000ull; break;
     case PGPU_TK_SUM_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row]); break;
-    case PGPU_TK_SUM_SPLIT: u = pgpu_tk_double(pgpu_tk_split_sum(t, G, s.sec, row)); break;
+    case PGPU_TK_SUM_SPLIT: u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, row), s.fxe)); break;
     case PGPU_TK_SUM_F64: {
       double d;
       __builtin_memcpy(&d, &t[(uint64_t)s.sec * G + row], 8);
@@ -515,7 +547,9 @@ __host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDe
       break;
     }
     case PGPU_TK_AVG_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row] / (double)cnt); break;
-    case PGPU_TK_AVG_SPLIT: u = pgpu_tk_double(pgpu_tk_split_sum(t, G, s.sec, row) / (double)cnt); break;
+    case PGPU_TK_AVG_SPLIT:
+      u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, row), s.fxe) / (double)cnt);
+      break;
     case PGPU_TK_AVG_F64: {
       double d;
       __builtin_memcpy(&d, &t[(uint64_t)s.sec * G + row], 8);

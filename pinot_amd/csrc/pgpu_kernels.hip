@@ -245,7 +245,7 @@ FI void gather_cells(const void* dict, int32_t vtype, int32_t op, const uint32_t
 #pragma unroll
       for (int r = 0; r < N; ++r) {
         const double d = (double)__uint_as_float(raw[r]);
-        out[r] = op == PGPU_RED_SUM_F64 ? __double_as_longlong(d) : key_of_double(d);
+        out[r] = op == PGPU_RED_MIN_I64 || op == PGPU_RED_MAX_I64 ? key_of_double(d) : __double_as_longlong(d);
       }
     }
   } else {
@@ -257,7 +257,8 @@ FI void gather_cells(const void* dict, int32_t vtype, int32_t op, const uint32_t
       for (int r = 0; r < N; ++r) out[r] = raw[r];
     } else {
 #pragma unroll
-      for (int r = 0; r < N; ++r) out[r] = op == PGPU_RED_SUM_F64 ? raw[r] : key_of_double(__longlong_as_double(raw[r]));
+      for (int r = 0; r < N; ++r)
+        out[r] = op == PGPU_RED_MIN_I64 || op == PGPU_RED_MAX_I64 ? key_of_double(__longlong_as_double(raw[r])) : raw[r];
     }
   }
 }
@@ -269,11 +270,21 @@ FI int64_t part_of(int64_t v, int32_t part) {
   if (part == 3) return v >> (2 * PGPU_PART_BITS);
   return v;
 }
+// Fixed-point floating SUM (DevAgg::fxe, pgpu_table_layout.agg_sum_exp): the double v as the integer
+// rint(v * 2^-fxe), |.| < 2^62 by the layout's choice of fxe; integer adds make the sums order-independent.
+FI int64_t fixed_of(int64_t bits, int32_t fxe) {
+  return (int64_t)__builtin_rint(__builtin_ldexp(__longlong_as_double(bits), -fxe));
+}
+// gather_cells' SUM values -> the agg's cells: the fixed-point integer of a floating value, then its part section
 template <int N>
-FI void apply_part(int64_t (&v)[N], int32_t part) {
-  if (part == 0) return;
+FI void apply_part(int64_t (&v)[N], const DevAgg& ag) {
+  if (ag.op == PGPU_RED_SUM_I64 && (ag.vtype == PGPU_FLOAT || ag.vtype == PGPU_DOUBLE)) {
 #pragma unroll
-  for (int r = 0; r < N; ++r) v[r] = part_of(v[r], part);
+    for (int r = 0; r < N; ++r) v[r] = fixed_of(v[r], ag.fxe);
+  }
+  if (ag.part == 0) return;
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = part_of(v[r], ag.part);
 }
 FI int64_t cell_combine(int32_t op, int64_t a, int64_t b) {
   if (op == PGPU_RED_SUM_I64) return a + b;
@@ -931,6 +942,7 @@ struct Cons {
 struct SegState {
   const DevSeg* sg;
   int32_t track;  // HASH: distinct-key bitmap row + 1 (0 = not counted)
+  int32_t single_bits;  // DevSeg::single_bits
   const DevColumn* cols;
   const int32_t* const* remaps;
   int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
@@ -965,6 +977,7 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   ss.reg_col1 = cld(&sg->reg_col[1]);
   ss.fast = cld(&sg->fast);
   ss.track = cld(&sg->track);
+  ss.single_bits = cld(&sg->single_bits);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
@@ -1397,7 +1410,7 @@ FI void sparse_agg_mv(const DevParams& p, const Lds& L, const SegState& ss, cons
         gather_ids(colref(c), dd, id);
         int64_t v[1];
         gather_cells(c.dict, ag.vtype, ag.op, id, v);
-        apply_part(v, ag.part);
+        apply_part(v, ag);
         cell_atomic(tab + (size_t)ag.sec * p.G + key, ag.op, v[0]);
       }
     }
@@ -1510,7 +1523,7 @@ FI void sparse_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la
     }
     int64_t v[U];
     gather_cells(c.dict, ag.vtype, ag.op, id, v);
-    apply_part(v, ag.part);
+    apply_part(v, ag);
     if (MODE == PGPU_MODE_AGG) {
       int64_t part = sec_identity(ag.op);
 #pragma unroll
@@ -1670,7 +1683,7 @@ FI void dense_agg_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const Se
       }
       int64_t v[8];
       gather_cells(c.dict, ag.vtype, ag.op, idx, v);
-      apply_part(v, ag.part);
+      apply_part(v, ag);
 #pragma unroll
       for (int r = 0; r < 8; ++r)
         if (b0 + lane + 64 * r < nt) part = cell_combine(ag.op, part, v[r]);
@@ -1812,7 +1825,7 @@ FI void dense_agg(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la,
         }
         int64_t v[8];
         gather_cells(c.dict, ag.vtype, ag.op, idx, v);
-        apply_part(v, ag.part);
+        apply_part(v, ag);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const int e = lane + 64 * (r0 + r);
@@ -2143,7 +2156,7 @@ FI void sliced_flush(const DevParams& p, const Cons& cv, LaneAcc& la, const SegS
       }
       int64_t v[8];
       gather_cells(c.dict, ag.vtype, ag.op, idx, v);
-      apply_part(v, ag.part);
+      apply_part(v, ag);
 #pragma unroll
       for (int r = 0; r < 8; ++r)
         if ((live >> r) & 1u) part = cell_combine(ag.op, part, v[r]);
@@ -2323,6 +2336,8 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
     int poll = p.cancel_poll;
     uint32_t voff16;
     asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(voff16) : "v"(opaque_lane()));  // lane * 16, kept live
+    uint32_t bw_next = 0;
+    bool bw_have = false;
     for (int k = 0; k < own; ++k) {
       while (issued < own && issued < k + D) {
         if (issued > 0 && cursor_advance(p, ci, NW)) load_stage(p, ci.seg, sc);
@@ -2374,9 +2389,26 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
             if (lane == 0) dense_bytes += ((int64_t)ndocs * b + 7) / 8;
           }
       }
+      // a segment whose index-only program was evaluated by progbits_kernel reads one word per lane; the next
+      // tile's word of the same segment is loaded one iteration ahead
+      uint32_t bits_word = 0;
+      if (ss.single_bits) {
+        const uint32_t* bw = (const uint32_t*)cld(&ss.sg->bits_w[0]);
+        bits_word = bw_have ? bw_next : gld(bw, (size_t)cur.tile_in_seg * 64 + lane);
+        bw_have = false;
+        if (k + 1 < own) {
+          Cursor nx = cur;
+          cursor_advance(p, nx, NW);
+          if (nx.seg == cseg) {
+            bw_next = gld(bw, (size_t)nx.tile_in_seg * 64 + lane);
+            bw_have = true;
+          }
+        }
+      }
       // fast sliced leaves in registers; a segment with nothing staged (bitmap / sorted / BITS leaves only) runs
       // its program through the interpreter -- no slot is read
       const uint32_t mm = ss.fast ? fast_filter(ss, t, lane_scanned)
+                                  : ss.single_bits ? bits_word & t.valid
                                   : (ss.prog_len > 0 ? run_program(p, cv, ss.prog_begin, ss.prog_len, t, scanned,
                                                                    dense_bytes, pf)
                                                      : t.valid);
@@ -3061,7 +3093,14 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             }
           } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) hm[j] = __ballot(qq[j] == hq);
+            for (int j = 0; j < 8; ++j) {
+              // the first live lane's partition when >= 4 lanes share it (skewed keys spread their hot partitions),
+              // else the sampled hottest one
+              const uint64_t lv = __ballot(lane_bit(mm, 8 * g8 + j));
+              const uint32_t cq = lv ? (uint32_t)__builtin_amdgcn_readlane((int)qq[j], __builtin_ctzll(lv)) : hq;
+              hm[j] = __ballot(qq[j] == cq);
+              if (cq != hq && __popcll(hm[j]) < 4) hm[j] = __ballot(qq[j] == hq);
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const bool hot = (hm[j] >> lane) & 1u;
@@ -3247,6 +3286,94 @@ __global__ __launch_bounds__(1024) void part_plan_kernel(DevParams p, int grid1)
 // Each wave walks its own regions in chunks of R x 64 records; loads are unconditional (clamped indices), so a
 // chunk's R loads are in flight together; section ops are uniform, so a chunk runs one branch-free atomic loop
 // per section.
+// A value of the frame-of-reference dictionary image in LDS: block base + the id's fbits-bit offset (it may straddle
+// two words).
+FI uint32_t for_value(const uint32_t* fimg, int fnblk, int fbits, uint32_t id) {
+  const uint32_t blk = id >> 5, bit = (id & 31u) * (uint32_t)fbits;
+  const uint32_t* wds = fimg + fnblk + (size_t)blk * fbits + (bit >> 5);
+  const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
+  return fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
+}
+
+// Skewed keys (Zipf): the records of one hot key arriving together would serialize on one LDS address per wave
+// instruction.  Before the per-lane atomics, the key of the first live lane is matched across the wave; when >= 4
+// lanes hold it, their cells are reduced in registers (wave reductions) and that lane applies the totals -- up to two
+// keys per record batch.  For even keys the match is nearly always one lane and the check costs two ballots.
+#define PGPU_P2_COMBINE 4
+template <int NS>
+FI void part_combine(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS : 1], int32_t vt, int idbits,
+                     uint32_t k, uint32_t raw, uint32_t val, bool& ok) {
+  const int lane = lane_id();
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const uint64_t live = __ballot(ok);
+    if (!live) return;
+    const int ld = __builtin_ctzll(live);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k, ld);
+    const uint64_t m = __ballot(ok && k == k0);
+    const int c = __popcll(m);
+    if (c < PGPU_P2_COMBINE) return;
+    const bool in = (m >> lane) & 1u;
+    if (lane == ld) atomicAdd((unsigned long long*)&ptab[k0], (unsigned long long)c);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      int64_t* sec = ptab + (size_t)(1 + s) * K;
+      if (op[s] == PGPU_RED_SUM_I64) {
+        const int64_t t = wave_sum_i64(in ? (int64_t)(int32_t)val : 0);
+        if (lane == ld) atomicAdd((unsigned long long*)&sec[k0], (unsigned long long)t);
+      } else if (op[s] == PGPU_RED_SUM_F64) {
+        const double t = wave_sum_f64(in ? (double)__uint_as_float(val) : 0.0);
+        if (lane == ld) atomicAdd((double*)&sec[k0], t);
+      } else {
+        const int64_t x = idbits ? (int64_t)raw : raw_to_cell(raw, vt, op[s]);
+        if (op[s] == PGPU_RED_MIN_I64) {
+          const int64_t t = wave_min_i64(in ? x : INT64_MAX);
+          if (lane == ld) atomicMin((long long*)&sec[k0], (long long)t);
+        } else {
+          const int64_t t = wave_max_i64(in ? x : INT64_MIN);
+          if (lane == ld) atomicMax((long long*)&sec[k0], (long long)t);
+        }
+      }
+    }
+    ok = ok && !in;
+  }
+}
+// the same for the compact LDS table beside the frame-of-reference dictionary (LDM 2: u32 counts, int64 sums of the
+// ids' values, u32 MIN / MAX ids)
+template <int NS>
+FI void part_combine_for(unsigned char* base, const uint32_t (&soff)[NS > 0 ? NS : 1],
+                         const int32_t (&op)[NS > 0 ? NS : 1], const uint32_t* fimg, int fnblk, int fbits, uint32_t k,
+                         uint32_t id, bool& ok) {
+  const int lane = lane_id();
+  uint32_t* cnt = (uint32_t*)base;
+#pragma unroll 1
+  for (int it = 0; it < 2; ++it) {
+    const uint64_t live = __ballot(ok);
+    if (!live) return;
+    const int ld = __builtin_ctzll(live);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k, ld);
+    const uint64_t m = __ballot(ok && k == k0);
+    const int c = __popcll(m);
+    if (c < PGPU_P2_COMBINE) return;
+    const bool in = (m >> lane) & 1u;
+    if (lane == ld) atomicAdd(&cnt[k0], (uint32_t)c);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
+        const int64_t t = wave_sum_i64(in ? (int64_t)(int32_t)for_value(fimg, fnblk, fbits, id) : 0);
+        if (lane == ld) atomicAdd(&((unsigned long long*)(base + soff[s]))[k0], (unsigned long long)t);
+      } else if (op[s] == PGPU_RED_MIN_I64) {
+        const int64_t t = wave_min_i64(in ? (int64_t)id : (int64_t)0xFFFFFFFFu);
+        if (lane == ld) atomicMin(&((uint32_t*)(base + soff[s]))[k0], (uint32_t)t);
+      } else {
+        const int64_t t = wave_max_i64(in ? (int64_t)id : 0);
+        if (lane == ld) atomicMax(&((uint32_t*)(base + soff[s]))[k0], (uint32_t)t);
+      }
+    }
+    ok = ok && !in;
+  }
+}
+
 template <int NS, int R>
 FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS : 1], int32_t vt, int idbits,
                           const uint32_t (&k)[R], const uint32_t (&raw)[R], const uint32_t (&val)[R],
@@ -3275,15 +3402,6 @@ FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 
       }
     }
   }
-}
-
-// A value of the frame-of-reference dictionary image in LDS: block base + the id's fbits-bit offset (it may straddle
-// two words).
-FI uint32_t for_value(const uint32_t* fimg, int fnblk, int fbits, uint32_t id) {
-  const uint32_t blk = id >> 5, bit = (id & 31u) * (uint32_t)fbits;
-  const uint32_t* wds = fimg + fnblk + (size_t)blk * fbits + (bit >> 5);
-  const uint64_t two = (uint64_t)wds[0] | ((uint64_t)wds[1] << 32);
-  return fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
 }
 
 template <int NS, bool ONE, int LDM>
@@ -3353,6 +3471,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
           const uint32_t v = gld(p.recs, rb + (ok[r] ? i : n - 1));
           k[r] = v >> idbits;
           id[r] = v & idmask;
+        }
+        if (split) {  // a hot partition (skewed keys): combine each batch's repeated keys first
+#pragma unroll
+          for (int r = 0; r < R; ++r) part_combine_for<NS>(base, soff, op, fimg, fnblk, fbits, k[r], id[r], ok[r]);
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -3459,6 +3581,10 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
             }
           }
         }
+        if (split) {  // a hot partition (skewed keys): combine each batch's repeated keys first
+#pragma unroll
+          for (int r = 0; r < R; ++r) part_combine<NS>(ptab, K, op, vt, idbits, k[r], raw[r], val[r], ok[r]);
+        }
         part_reduce_batch<NS, R>(ptab, K, op, vt, idbits, k, raw, val, ok);
       }
     }
@@ -3533,6 +3659,44 @@ __global__ __launch_bounds__(256) void prologue_kernel(const u32x4* __restrict__
     else if (i < n + nk) p.table[i] = -1;
     else p.segmask[i - n - nk] = 0u;
   }
+}
+
+// Index-only dense programs (ProgJob): one wave per tile evaluates the segment's original program (bitmap / sorted /
+// inverted leaves, AND / OR / NOT) and writes the tile's match words; the query kernel then reads one word per lane.
+__global__ __launch_bounds__(256) void progbits_kernel(DevParams p, const ProgJob* jobs, int njobs, int total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = (int)blockIdx.x * 4 + wave;
+  if (g >= total) return;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cld(&jobs[mid].tile0) <= g) lo = mid; else hi = mid - 1;
+  }
+  const ProgJob jb = cld(jobs + lo);
+  const int tile = g - jb.tile0;
+  SegState ss;
+  load_seg(p, jb.seg, ss);
+  Cons cv;
+  cv.masks = (uint32_t*)(dyn_smem + (size_t)wave * p.mask_rows * 256);
+  cv.queue = nullptr;
+  cv.klist = cv.vlist = nullptr;
+  cv.acc = nullptr;
+  cv.qtiles = nullptr;
+  TileCtx t;
+  t.ss = &ss;
+  t.slot = nullptr;
+  t.tile_in_seg = tile;
+  t.doc0 = tile * WT;
+  t.lane_doc0 = t.doc0 + 32 * lane;
+  {
+    const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+    t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+  }
+  int64_t scanned = 0, dense_bytes = 0;
+  Prof pf;
+  const uint32_t m = run_program(p, cv, jb.prog_begin, jb.prog_len, t, scanned, dense_bytes, pf);
+  jb.out[(size_t)tile * 64 + lane] = m & t.valid;
 }
 
 // PGPU_Q_EXACT_FILTER_STATS: the match bits of every leaf of every segment's whole filter program over all its
@@ -3932,6 +4096,58 @@ __global__ void compact_write_kernel(const int64_t* table, uint64_t G, int32_t n
       for (int s = 0; s < nsec; ++s) out_cells[(size_t)pos * nsec + s] = table[(size_t)s * G + k];
     }
     __syncthreads();
+  }
+}
+
+// ---- node-level combine of hash tables (pgpu_node.cpp) --------------------------------------------------------------
+// Compacted rows (key words, then cells) go to the device owning their key (pgpu_key_owner_of): owners counted, rows
+// grouped by owner into a send buffer, copied peer to peer, and merged on the owner into a fresh hash table of the
+// query's layout (open addressing on the key words as the hash group-by interns them), cells by the section ops.
+__global__ void node_owner_kernel(const int64_t* keys, uint64_t n, int32_t kw, int32_t world, uint8_t* owner,
+                                  uint32_t* counts) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t o = pgpu_key_owner_of(keys + i * kw, kw, world);
+    owner[i] = (uint8_t)o;
+    atomicAdd(&counts[o], 1u);
+  }
+}
+__global__ void node_scatter_kernel(const int64_t* keys, const int64_t* cells, uint64_t n, int32_t kw, int32_t nsec,
+                                    const uint8_t* owner, uint32_t* cursor, int64_t* rows) {
+  const int width = kw + nsec;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t at = atomicAdd(&cursor[owner[i]], 1u);
+    int64_t* r = rows + (size_t)at * width;
+    for (int w = 0; w < kw; ++w) r[w] = keys[i * kw + w];
+    for (int s = 0; s < nsec; ++s) r[kw + s] = cells[i * nsec + s];
+  }
+}
+__global__ void node_init_kernel(int64_t* table, uint64_t P, int32_t nsec, int32_t kw, NodeOps ops) {
+  const uint64_t n = P * (uint64_t)(nsec + (kw == 2 ? 2 : 1));
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    table[i] = i < P * nsec ? sec_identity(ops.op[i / P]) : (int64_t)PGPU_HASH_EMPTY;
+}
+__global__ void node_merge_kernel(const int64_t* rows, uint64_t n, int32_t kw, int32_t nsec, int64_t* table,
+                                  uint64_t P, NodeOps ops, int32_t* hflag) {
+  const int width = kw + nsec;
+  uint64_t* w0 = (uint64_t*)(table + (size_t)nsec * P);
+  const uint64_t mask = P - 1;
+  const uint64_t n64 = (n + 63) & ~63ull;  // whole waves: hash_insert's probes are per lane, ballots per wave
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n64; i += (uint64_t)gridDim.x * blockDim.x) {
+    const bool live = i < n;
+    const int64_t* r = rows + (size_t)(live ? i : 0) * width;
+    uint32_t slot[1];
+    if (kw == 2) {
+      const uint64_t k0[1] = {(uint64_t)r[0]};
+      uint32_t s0[1];
+      hash_insert(w0 + P, mask, k0, live ? 1u : 0u, s0, hflag);  // intern word 0
+      const uint64_t c[1] = {((uint64_t)s0[0] << 32) | (uint64_t)r[1]};
+      hash_insert(w0, mask, c, live ? 1u : 0u, slot, hflag);
+    } else {
+      const uint64_t k[1] = {(uint64_t)r[0]};
+      hash_insert(w0, mask, k, live ? 1u : 0u, slot, hflag);
+    }
+    if (!live) continue;
+    for (int s = 0; s < nsec; ++s) cell_atomic(&table[(size_t)s * P + slot[0]], ops.op[s], r[kw + s]);
   }
 }
 
@@ -4391,6 +4607,13 @@ hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hi
   return hipGetLastError();
 }
 
+hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njobs, int total, hipStream_t st) {
+  if (njobs <= 0 || total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(progbits_kernel, dim3((total + 3) / 4), dim3(256), (size_t)4 * p.mask_rows * 256, st, p, jobs,
+                     njobs, total);
+  return hipGetLastError();
+}
+
 hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st) {
   if (p.nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(segflags_kernel, dim3(std::min(64, (p.nseg + 255) / 256)), dim3(256), 0, st, p.segany, out, p.nseg);
@@ -4490,6 +4713,27 @@ __global__ void topk_pick_kernel(TopkState* ts, uint32_t* hist, int shift) {
   ts->mask |= 255ull << shift;
 }
 
+hipError_t pgpu_launch_node_route(const int64_t* keys, const int64_t* cells, uint64_t n, int32_t kw, int32_t nsec,
+                                  int32_t world, uint8_t* owner, uint32_t* counts, uint32_t* cursor, int64_t* rows,
+                                  bool scatter, hipStream_t st) {
+  const int blocks = (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (n + 255) / 256));
+  if (!scatter)
+    hipLaunchKernelGGL(node_owner_kernel, dim3(blocks), dim3(256), 0, st, keys, n, kw, world, owner, counts);
+  else
+    hipLaunchKernelGGL(node_scatter_kernel, dim3(blocks), dim3(256), 0, st, keys, cells, n, kw, nsec, owner, cursor,
+                       rows);
+  return hipGetLastError();
+}
+hipError_t pgpu_launch_node_merge(const int64_t* rows, uint64_t n, int32_t kw, int32_t nsec, int64_t* table,
+                                  uint64_t P, const NodeOps& ops, int32_t* hflag, hipStream_t st) {
+  const int ib = (int)std::min<uint64_t>(4096, (P * (uint64_t)(nsec + 2) + 255) / 256);
+  hipLaunchKernelGGL(node_init_kernel, dim3(ib), dim3(256), 0, st, table, P, nsec, kw, ops);
+  if (n) {
+    const int blocks = (int)std::min<uint64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(node_merge_kernel, dim3(blocks), dim3(256), 0, st, rows, n, kw, nsec, table, P, ops, hflag);
+  }
+  return hipGetLastError();
+}
 hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, uint64_t* okey, TopkState* ts,
                             uint32_t* hist, hipStream_t st) {
   const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(2048, (s.G + 255) / 256));

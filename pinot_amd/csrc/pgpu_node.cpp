@@ -1,14 +1,19 @@
 // Node-level combine inside libpinotgpu: one process drives several GPUs of a node (the one-JVM Pinot server),
-// and the per-GPU partial tables are merged with RCCL over xGMI inside the library -- the combine step the
-// reference runs on the host (AggregationOnlyCombineOperator.mergeResultsBlocks,
-// core/operator/combine/AggregationOnlyCombineOperator.java:47-57; GroupByOrderByCombineOperator's IndexedTable
-// upserts, core/operator/combine/GroupByOrderByCombineOperator.java:127-248).
+// and the per-GPU partial tables are merged over xGMI inside the library -- the combine step the reference runs on
+// the host (AggregationOnlyCombineOperator.mergeResultsBlocks, core/operator/combine/AggregationOnlyCombineOperator
+// .java:47-57; GroupByOrderByCombineOperator's IndexedTable upserts and trim, core/operator/combine/
+// GroupByOrderByCombineOperator.java:127-248, GroupByUtils.java:24-41).  The same collectives as the
+// one-process-per-GPU combine (pinot_amd/combine.py):
 //
-//   dense tables : every device launches its segments into its own table; one grouped ncclReduce per section
-//                  (int64 SUM for counts and integer sums, float64 SUM, int64 MIN / MAX of order-preserving keys)
-//                  lands the merged table on device 0, which compacts it.
-//   hash tables  : slot assignments differ per device, so each device compacts its table and the rows are merged
-//                  by key on the host (AggregationFunction.merge per section).
+//   dense, small (aggregation only, or < 1 MiB) : one grouped ncclReduce per run of same-op sections to device 0,
+//                  which compacts (or trims by the ORDER BY key) -- combine.py's all_reduce + rank-0 compaction;
+//   dense, large : a reduce-scatter -- grouped ncclReduce of each section's key slice [d*K, d*K + K) to its owner d
+//                  (K = ceil(G / n), uneven G allowed) -- then every device trims ITS slice (pgpu_table_topk with
+//                  key_base = d*K: every kept row is final) and the host concatenates the slices' rows;
+//   hash tables  : slot assignments differ per device, so each device compacts its rows into device memory, routes
+//                  every row to the owner of its key (pgpu_key_owner_of: combine.py's routing, bit for bit) over
+//                  peer copies, the owner merges them into a fresh hash table (node_merge_kernel) and trims it --
+//                  combine.py's all_to_all + merge_rows + per-rank top-K.
 //
 // RCCL is loaded with dlopen on the first pgpu_node_init, so processes that never build a node (one process per
 // GPU, torch.distributed) do not load it.
@@ -16,19 +21,30 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/pinot_gpu.h"
+#include "pgpu_internal.h"
 
-// pgpu_runtime.cpp: the calling thread's pgpu_last_error message; docs of a descriptor's segments
+// pgpu_runtime.cpp: the calling thread's pgpu_last_error message; docs of a descriptor's segments; device-side
+// compaction.  pgpu_kernels.hip: the hash-row routing and merge kernels.
 int pgpu_set_error(int code, const char* msg);
 int64_t pgpu_desc_docs(const pgpu_query_desc* q);
+int pgpu_compact_to_device(pgpu_context* ctx, const pgpu_table_layout* L, const void* dev_table, hipStream_t st,
+                           int64_t* dkeys, int64_t* dcells, uint64_t capacity, uint64_t* out_n);
+hipError_t pgpu_launch_node_route(const int64_t* keys, const int64_t* cells, uint64_t n, int32_t kw, int32_t nsec,
+                                  int32_t world, uint8_t* owner, uint32_t* counts, uint32_t* cursor, int64_t* rows,
+                                  bool scatter, hipStream_t st);
+hipError_t pgpu_launch_node_merge(const int64_t* rows, uint64_t n, int32_t kw, int32_t nsec, int64_t* table,
+                                  uint64_t P, const NodeOps& ops, int32_t* hflag, hipStream_t st);
 
 namespace {
 
@@ -111,52 +127,191 @@ struct pgpu_node {
   std::vector<hipStream_t> streams;
   std::vector<ncclComm_t> comms;
   std::vector<DevBuf> tables;
+  // per device scratch of the merges: the slice copy (dense) / compacted rows, routing, send and receive buffers and
+  // the merged table (hash)
+  std::vector<DevBuf> slice, rkeys, rcells, route, send, recv, merged;
   std::mutex mu;  // one node query at a time (the tables are node-owned)
 };
 
 namespace {
 
+int sync_all(pgpu_node* nd, const char* what) {
+  for (size_t i = 0; i < nd->devices.size(); ++i) {
+    (void)hipSetDevice(nd->devices[i]);
+    const hipError_t e = hipStreamSynchronize(nd->streams[i]);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "%s: %s", what, hipGetErrorString(e));
+  }
+  return PGPU_OK;
+}
+
+int nccl_type(int op) { return op == PGPU_RED_SUM_F64 ? ncclFloat64 : ncclInt64; }
+int nccl_op(int op) { return op == PGPU_RED_MIN_I64 ? ncclMin : (op == PGPU_RED_MAX_I64 ? ncclMax : ncclSum); }
+
+// Whole dense tables reduced onto device 0: one grouped ncclReduce per run of same-op sections.
 int reduce_dense(pgpu_node* nd, const pgpu_table_layout& L) {
   const size_t G = L.num_keys;
   ncclResult_t r = g_rccl.GroupStart();
   for (size_t i = 0; i < nd->devices.size() && r == 0; ++i) {
-    // contiguous runs of sections with the same op go in one call
     int s = 0;
     while (s < L.num_sections && r == 0) {
       int e = s + 1;
       while (e < L.num_sections && L.section_op[e] == L.section_op[s]) ++e;
       const int op = L.section_op[s];
-      const int type = op == PGPU_RED_SUM_F64 ? ncclFloat64 : ncclInt64;
-      const int rop = op == PGPU_RED_MIN_I64 ? ncclMin : (op == PGPU_RED_MAX_I64 ? ncclMax : ncclSum);
       const char* src = (const char*)nd->tables[i].p + 8 * G * (size_t)s;
       char* dst = (char*)nd->tables[0].p + 8 * G * (size_t)s;  // significant on the root only
-      r = g_rccl.Reduce(src, i == 0 ? dst : (void*)src, G * (size_t)(e - s), type, rop, 0, nd->comms[i],
-                        nd->streams[i]);
+      r = g_rccl.Reduce(src, i == 0 ? dst : (void*)src, G * (size_t)(e - s), nccl_type(op), nccl_op(op), 0,
+                        nd->comms[i], nd->streams[i]);
       s = e;
     }
   }
   const ncclResult_t r2 = g_rccl.GroupEnd();
   if (r != 0 || r2 != 0) return nfail(PGPU_E_HIP, "ncclReduce: %s", g_rccl.str(r ? r : r2));
-  for (size_t i = 0; i < nd->devices.size(); ++i) {
-    (void)hipSetDevice(nd->devices[i]);
-    const hipError_t e = hipStreamSynchronize(nd->streams[i]);
-    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node reduce: %s", hipGetErrorString(e));
+  return sync_all(nd, "node reduce");
+}
+
+// Reduce-scatter of dense tables: device d ends up owning the final cells of keys [first, first + count) of
+// pgpu_slice_of (in place in its own table).  One grouped ncclReduce per section and owner slice (an uneven G
+// needs no padding).
+int reduce_slices(pgpu_node* nd, const pgpu_table_layout& L) {
+  const size_t G = L.num_keys;
+  const int n = (int)nd->devices.size();
+  ncclResult_t r = g_rccl.GroupStart();
+  for (int i = 0; i < n && r == 0; ++i)
+    for (int s = 0; s < L.num_sections && r == 0; ++s)
+      for (int d = 0; d < n && r == 0; ++d) {
+        uint64_t first = 0, count = 0;
+        pgpu_slice_of(G, n, d, &first, &count);
+        if (!count) continue;
+        char* p = (char*)nd->tables[i].p + 8 * (G * (size_t)s + first);
+        r = g_rccl.Reduce(p, p, count, nccl_type(L.section_op[s]), nccl_op(L.section_op[s]), d, nd->comms[i],
+                          nd->streams[i]);
+      }
+  const ncclResult_t r2 = g_rccl.GroupEnd();
+  if (r != 0 || r2 != 0) return nfail(PGPU_E_HIP, "ncclReduce (scatter): %s", g_rccl.str(r ? r : r2));
+  return sync_all(nd, "node reduce-scatter");
+}
+
+// Rows of one device's (slice of the) result appended to the caller's buffers: compacted, or trimmed by `order`.
+struct Out {
+  int64_t* keys;
+  int64_t* cells;
+  uint64_t capacity, n = 0;
+  int okw, nsec;
+  bool overflow = false;
+};
+int append_rows(pgpu_context* ctx, const pgpu_table_layout& L, const void* table, hipStream_t st,
+                const pgpu_topk* order, int64_t key_base, Out& out) {
+  const uint64_t G = L.num_keys;
+  std::vector<int64_t> k((size_t)G * out.okw + 1), c((size_t)G * out.nsec + 1);
+  uint64_t got = 0;
+  int rc;
+  if (order) {
+    pgpu_topk o = *order;
+    o.key_base = (uint64_t)key_base;
+    rc = pgpu_table_topk(ctx, &L, table, st, &o, k.data(), c.data(), G, &got);
+  } else {
+    rc = pgpu_table_compact(ctx, &L, table, st, k.data(), c.data(), G, &got);
   }
+  if (rc) return rc;
+  if (out.n + got > out.capacity) {
+    out.overflow = true;
+    out.n += got;
+    return PGPU_OK;
+  }
+  const bool dense = L.key_kind != PGPU_KEYS_HASH;
+  for (uint64_t r = 0; r < got; ++r) {
+    for (int w = 0; w < out.okw; ++w) out.keys[(out.n + r) * out.okw + w] = k[r * out.okw + w] + (dense ? key_base : 0);
+    memcpy(out.cells + (out.n + r) * out.nsec, c.data() + r * out.nsec, 8 * (size_t)out.nsec);
+  }
+  out.n += got;
   return PGPU_OK;
 }
 
-int64_t cell_merge(int op, int64_t a, int64_t b) {
-  if (op == PGPU_RED_SUM_I64) return (int64_t)((uint64_t)a + (uint64_t)b);
-  if (op == PGPU_RED_SUM_F64) {
-    double x, y;
-    memcpy(&x, &a, 8);
-    memcpy(&y, &b, 8);
-    x += y;
-    memcpy(&a, &x, 8);
-    return a;
+// Hash tables: every device's rows to the owners of their keys, merged there, trimmed there.
+int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgpu_topk* order, Out& out) {
+  const int n = (int)nd->devices.size();
+  const int kw = L[0].key_words == 2 ? 2 : 1, nsec = L[0].num_sections, width = kw + nsec;
+  std::vector<uint64_t> rows(n, 0);
+  std::vector<std::vector<uint32_t>> cnt(n, std::vector<uint32_t>(n, 0)), off(n, std::vector<uint32_t>(n, 0));
+  for (int i = 0; i < n; ++i) {  // compact, count per owner
+    const uint64_t G = L[i].num_keys;
+    hipError_t e = hipSetDevice(nd->devices[i]);
+    if (e == hipSuccess) e = nd->rkeys[i].ensure(8 * G * kw + 16);
+    if (e == hipSuccess) e = nd->rcells[i].ensure(8 * G * nsec + 16);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node rows: %s", hipGetErrorString(e));
+    int rc = pgpu_compact_to_device(nd->ctxs[i], &L[i], nd->tables[i].p, nd->streams[i], (int64_t*)nd->rkeys[i].p,
+                                    (int64_t*)nd->rcells[i].p, G, &rows[i]);
+    if (rc) return rc;
+    // route scratch: owner byte per row, then counts and cursors (n each)
+    e = nd->route[i].ensure(rows[i] + 16 + 8 * (size_t)n + 16);
+    if (e == hipSuccess) e = nd->send[i].ensure(8 * rows[i] * width + 16);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node route: %s", hipGetErrorString(e));
+    uint8_t* owner = (uint8_t*)nd->route[i].p;
+    uint32_t* counts = (uint32_t*)((char*)nd->route[i].p + ((rows[i] + 15) & ~15ull));
+    e = hipMemsetAsync(counts, 0, 4 * (size_t)n, nd->streams[i]);
+    if (e == hipSuccess && rows[i])
+      e = pgpu_launch_node_route((const int64_t*)nd->rkeys[i].p, nullptr, rows[i], kw, nsec, n, owner, counts,
+                                 nullptr, nullptr, false, nd->streams[i]);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt[i].data(), counts, 4 * (size_t)n, hipMemcpyDeviceToHost, nd->streams[i]);
+    if (e == hipSuccess) e = hipStreamSynchronize(nd->streams[i]);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node owners: %s", hipGetErrorString(e));
   }
-  if (op == PGPU_RED_MIN_I64) return std::min(a, b);
-  return std::max(a, b);
+  for (int i = 0; i < n; ++i) {  // rows grouped by owner in the send buffer
+    if (!rows[i]) continue;
+    uint32_t run = 0;
+    for (int o = 0; o < n; ++o) {
+      off[i][o] = run;
+      run += cnt[i][o];
+    }
+    (void)hipSetDevice(nd->devices[i]);
+    uint8_t* owner = (uint8_t*)nd->route[i].p;
+    uint32_t* cursor = (uint32_t*)((char*)nd->route[i].p + ((rows[i] + 15) & ~15ull)) + n;
+    hipError_t e = hipMemcpyAsync(cursor, off[i].data(), 4 * (size_t)n, hipMemcpyHostToDevice, nd->streams[i]);
+    if (e == hipSuccess)
+      e = pgpu_launch_node_route((const int64_t*)nd->rkeys[i].p, (const int64_t*)nd->rcells[i].p, rows[i], kw, nsec,
+                                 n, owner, nullptr, cursor, (int64_t*)nd->send[i].p, true, nd->streams[i]);
+    if (e == hipSuccess) e = hipStreamSynchronize(nd->streams[i]);  // (the cursors' host copy is a stack array)
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node scatter: %s", hipGetErrorString(e));
+  }
+  std::vector<uint64_t> incoming(n, 0);
+  for (int o = 0; o < n; ++o) {  // peer copies into the owners' receive buffers
+    for (int i = 0; i < n; ++i) incoming[o] += cnt[i][o];
+    (void)hipSetDevice(nd->devices[o]);
+    hipError_t e = nd->recv[o].ensure(8 * incoming[o] * width + 16);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node receive: %s", hipGetErrorString(e));
+    uint64_t at = 0;
+    for (int i = 0; i < n; ++i) {
+      if (!cnt[i][o]) continue;
+      (void)hipSetDevice(nd->devices[i]);
+      e = hipMemcpyPeerAsync((char*)nd->recv[o].p + 8 * at * width, nd->devices[o],
+                             (const char*)nd->send[i].p + 8 * (size_t)off[i][o] * width, nd->devices[i],
+                             8 * (size_t)cnt[i][o] * width, nd->streams[i]);
+      if (e != hipSuccess) return nfail(PGPU_E_HIP, "node peer copy: %s", hipGetErrorString(e));
+      at += cnt[i][o];
+    }
+  }
+  int rc = sync_all(nd, "node exchange");
+  if (rc) return rc;
+  NodeOps ops{};
+  for (int s = 0; s < nsec; ++s) ops.op[s] = L[0].section_op[s];
+  for (int o = 0; o < n; ++o) {  // merge on the owner, trim there
+    uint64_t P = 64;
+    while (P < 2 * incoming[o]) P <<= 1;
+    (void)hipSetDevice(nd->devices[o]);
+    hipError_t e = nd->merged[o].ensure(8 * P * (size_t)(nsec + 2) + 16);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node merged table: %s", hipGetErrorString(e));
+    int32_t* hflag = (int32_t*)((char*)nd->merged[o].p + 8 * P * (size_t)(nsec + 2));
+    e = hipMemsetAsync(hflag, 0, 4, nd->streams[o]);
+    if (e == hipSuccess)
+      e = pgpu_launch_node_merge((const int64_t*)nd->recv[o].p, incoming[o], kw, nsec, (int64_t*)nd->merged[o].p, P,
+                                 ops, hflag, nd->streams[o]);
+    if (e != hipSuccess) return nfail(PGPU_E_HIP, "node merge: %s", hipGetErrorString(e));
+    pgpu_table_layout Lo = L[0];
+    Lo.num_keys = P;
+    rc = append_rows(nd->ctxs[o], Lo, nd->merged[o].p, nd->streams[o], order, 0, out);
+    if (rc) return rc;
+  }
+  return PGPU_OK;
 }
 
 }  // namespace
@@ -187,7 +342,8 @@ int pgpu_node_init(const int32_t* device_ordinals, int32_t num_devices, pgpu_nod
     nd->streams.push_back(st);
     DevBuf b;
     b.device = device_ordinals[i];
-    nd->tables.push_back(b);
+    for (auto* v : {&nd->tables, &nd->slice, &nd->rkeys, &nd->rcells, &nd->route, &nd->send, &nd->recv, &nd->merged})
+      v->push_back(b);
   }
   nd->comms.assign(num_devices, nullptr);
   const ncclResult_t r = g_rccl.CommInitAll(nd->comms.data(), num_devices, nd->devices.data());
@@ -210,10 +366,12 @@ int pgpu_node_shutdown(pgpu_node* node) {
   if (!node) return PGPU_OK;
   for (ncclComm_t c : node->comms)
     if (c) (void)g_rccl.CommDestroy(c);
-  for (size_t i = 0; i < node->tables.size(); ++i) {
-    (void)hipSetDevice(node->tables[i].device);
-    if (node->tables[i].p) (void)hipFree(node->tables[i].p);
-  }
+  for (auto* v : {&node->tables, &node->slice, &node->rkeys, &node->rcells, &node->route, &node->send, &node->recv,
+                  &node->merged})
+    for (DevBuf& b : *v) {
+      (void)hipSetDevice(b.device);
+      if (b.p) (void)hipFree(b.p);
+    }
   for (size_t i = 0; i < node->streams.size(); ++i) {
     (void)hipSetDevice(node->devices[i]);
     (void)hipStreamDestroy(node->streams[i]);
@@ -223,10 +381,30 @@ int pgpu_node_shutdown(pgpu_node* node) {
   return PGPU_OK;
 }
 
+void pgpu_slice_of(uint64_t num_keys, int32_t world, int32_t rank, uint64_t* first, uint64_t* count) {
+  const uint64_t K = world > 0 ? (num_keys + (uint64_t)world - 1) / (uint64_t)world : num_keys;
+  const uint64_t f = std::min<uint64_t>(num_keys, K * (uint64_t)std::max(rank, 0));
+  if (first) *first = f;
+  if (count) *count = std::min<uint64_t>(K, num_keys - f);
+}
+
+int32_t pgpu_key_owner(const int64_t* key_words, int32_t num_key_words, int32_t world) {
+  if (!key_words || num_key_words < 1 || world < 1) return -1;
+  return (int32_t)pgpu_key_owner_of(key_words, num_key_words, world);
+}
+
 int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_t* out_keys, int64_t* out_cells,
                     uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
                     pgpu_table_layout* out_layout) {
+  return pgpu_node_query_topk(node, descs, nullptr, out_keys, out_cells, capacity, out_num_groups, out_stats,
+                              out_layout);
+}
+
+int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_topk* order,
+                         int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups,
+                         pgpu_query_stats* out_stats, pgpu_table_layout* out_layout) {
   if (!node || !descs || !out_num_groups) return nfail(PGPU_E_INVALID, "null argument");
+  if (order && order->k == 0) order = nullptr;
   std::lock_guard<std::mutex> lk(node->mu);
   const size_t n = node->devices.size();
   // one table layout on every device: the docs of the whole node bound the integer sums, and a split or hash
@@ -240,16 +418,22 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
     node_docs += pgpu_desc_docs(&qs[i]);
   }
   uint64_t extra = 0;
+  int32_t node_exp[16];  // fixed-point exponents of the floating SUMs: the largest any device needs
+  for (int a = 0; a < 16; ++a) node_exp[a] = INT32_MIN;
   for (size_t i = 0; i < n; ++i) {
     qs[i].reduce_docs = std::max<int64_t>(qs[i].reduce_docs, node_docs);
     const int rc = pgpu_table_layout_of(&qs[i], &L[i]);  // also validates the descriptor
     if (rc) return rc;
-    for (int a = 0; a < qs[i].num_aggs; ++a)
-      if (L[i].agg_sum_parts[a] == 3) extra |= PGPU_Q_SUM_SPLIT;
+    for (int a = 0; a < qs[i].num_aggs; ++a) {
+      const int vt = L[i].agg_value_type[a];
+      if (L[i].agg_sum_parts[a] == 3 && (vt == PGPU_INT || vt == PGPU_LONG)) extra |= PGPU_Q_SUM_SPLIT;
+      node_exp[a] = std::max(node_exp[a], L[i].agg_sum_exp[a]);
+    }
     if (L[i].key_kind == PGPU_KEYS_HASH) extra |= PGPU_Q_HASH;
   }
   for (size_t i = 0; i < n; ++i) {
     qs[i].flags |= extra;
+    qs[i].sum_exp = node_exp;
     const int rc = pgpu_table_layout_of(&qs[i], &L[i]);
     if (rc) return rc;
   }
@@ -257,7 +441,8 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
   for (size_t i = 1; i < n; ++i) {
     const bool same = L[i].num_sections == L[0].num_sections && L[i].key_kind == L[0].key_kind &&
                       (hash || L[i].num_keys == L[0].num_keys) &&
-                      !memcmp(L[i].section_op, L[0].section_op, sizeof(L[0].section_op));
+                      !memcmp(L[i].section_op, L[0].section_op, sizeof(L[0].section_op)) &&
+                      !memcmp(L[i].agg_sum_exp, L[0].agg_sum_exp, sizeof(L[0].agg_sum_exp));
     if (!same) return nfail(PGPU_E_INVALID, "device %zu's table layout differs from device 0's", i);
   }
   // launch every device, then wait for all
@@ -290,43 +475,44 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
   if (rc) return rc;
   if (out_stats) *out_stats = tot;
   if (out_layout) *out_layout = L[0];
+  const int okw = L[0].key_kind == PGPU_KEYS_HASH && L[0].key_words == 2 ? 2 : 1;
+  Out out{out_keys, out_cells, capacity, 0, okw, L[0].num_sections};
   if (!hash) {
-    rc = reduce_dense(node, L[0]);
-    if (rc) return rc;
-    return pgpu_table_compact(node->ctxs[0], &L[0], node->tables[0].p, node->streams[0], out_keys, out_cells, capacity,
-                              out_num_groups);
-  }
-  // hash tables: compact per device, merge rows by key
-  const int kw = L[0].key_words == 2 ? 2 : 1;
-  const int nsec = L[0].num_sections;
-  std::map<std::vector<int64_t>, std::vector<int64_t>> merged;
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t cap = L[i].num_keys;
-    std::vector<int64_t> keys(cap * kw + 1), cells(cap * nsec + 1);
-    uint64_t got = 0;
-    rc = pgpu_table_compact(node->ctxs[i], &L[i], node->tables[i].p, node->streams[i], keys.data(), cells.data(), cap,
-                            &got);
-    if (rc) return rc;
-    for (uint64_t r = 0; r < got; ++r) {
-      std::vector<int64_t> k(keys.begin() + r * kw, keys.begin() + (r + 1) * kw);
-      auto it = merged.find(k);
-      if (it == merged.end()) {
-        merged.emplace(std::move(k), std::vector<int64_t>(cells.begin() + r * nsec, cells.begin() + (r + 1) * nsec));
-      } else {
-        for (int s = 0; s < nsec; ++s) it->second[s] = cell_merge(L[0].section_op[s], it->second[s], cells[r * nsec + s]);
+    const uint64_t G = L[0].num_keys;
+    // PGPU_NODE_SCATTER_MIN (bytes; read per query, tests lower it to run the reduce-scatter on small tables)
+    const char* sm = getenv("PGPU_NODE_SCATTER_MIN");
+    const int64_t scatter_min = sm ? atoll(sm) : (int64_t)1 << 20;
+    const bool scatter = qs[0].num_group_columns > 0 && (int64_t)(8 * G * (uint64_t)L[0].num_sections) >= scatter_min;
+    if (!scatter) {
+      rc = reduce_dense(node, L[0]);
+      if (rc) return rc;
+      rc = append_rows(node->ctxs[0], L[0], node->tables[0].p, node->streams[0], order, 0, out);
+    } else {
+      rc = reduce_slices(node, L[0]);
+      if (rc) return rc;
+      for (size_t d = 0; d < n && rc == PGPU_OK; ++d) {  // every device trims its own slice
+        uint64_t first = 0, count = 0;
+        pgpu_slice_of(G, (int32_t)n, (int32_t)d, &first, &count);
+        if (!count) continue;
+        (void)hipSetDevice(node->devices[d]);
+        hipError_t e = node->slice[d].ensure(8 * count * (size_t)L[0].num_sections + 16);
+        if (e == hipSuccess)
+          e = hipMemcpy2DAsync(node->slice[d].p, 8 * count, (const char*)node->tables[d].p + 8 * first, 8 * G, 8 * count,
+                               (size_t)L[0].num_sections, hipMemcpyDeviceToDevice, node->streams[d]);
+        if (e != hipSuccess) return nfail(PGPU_E_HIP, "node slice: %s", hipGetErrorString(e));
+        pgpu_table_layout Ls = L[0];
+        Ls.num_keys = count;
+        rc = append_rows(node->ctxs[d], Ls, node->slice[d].p, node->streams[d], order, (int64_t)first, out);
       }
     }
+  } else {
+    rc = merge_hash(node, L, order, out);
   }
-  *out_num_groups = merged.size();
-  if (merged.size() > capacity)
-    return nfail(PGPU_E_INVALID, "%zu non-empty groups exceed capacity %llu", merged.size(),
+  if (rc) return rc;
+  *out_num_groups = out.n;
+  if (out.overflow)
+    return nfail(PGPU_E_INVALID, "%llu result rows exceed capacity %llu", (unsigned long long)out.n,
                  (unsigned long long)capacity);
-  uint64_t r = 0;
-  for (const auto& kv : merged) {
-    for (int w = 0; w < kw; ++w) out_keys[r * kw + w] = kv.first[w];
-    for (int s = 0; s < nsec; ++s) out_cells[r * nsec + s] = kv.second[s];
-    ++r;
-  }
   return PGPU_OK;
 }
 

@@ -51,6 +51,7 @@ hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, 
                             uint32_t* hist, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st);
+hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njobs, int total, hipStream_t st);
 hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
@@ -94,6 +95,21 @@ inline uint32_t le32(const uint8_t* p) {
 }
 
 int type_width(int32_t t) { return (t == PGPU_INT || t == PGPU_FLOAT) ? 4 : 8; }
+// Running max |value| of a column (HostColumn::max_abs); a NaN or infinity makes it +inf (no fixed-point SUM).
+inline double abs_bound(double m, double v) { return std::isfinite(v) ? std::max(m, std::fabs(v)) : INFINITY; }
+// max |value| of n little-endian values of type t
+double abs_bound_of(const uint8_t* le, size_t n, int32_t t) {
+  double m = 0;
+  for (size_t i = 0; i < n; ++i) {
+    double v;
+    if (t == PGPU_INT) { int32_t x; memcpy(&x, le + 4 * i, 4); v = x; }
+    else if (t == PGPU_LONG) { int64_t x; memcpy(&x, le + 8 * i, 8); v = (double)x; }
+    else if (t == PGPU_FLOAT) { float x; memcpy(&x, le + 4 * i, 4); v = x; }
+    else { double x; memcpy(&x, le + 8 * i, 8); v = x; }
+    m = abs_bound(m, v);
+  }
+  return m;
+}
 
 // PGPU_PROFILE=1: the query kernel records per-wave phase cycles; pgpu_query_wait prints their averages.
 bool profile_enabled() {
@@ -675,7 +691,6 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
     }
     return k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
   };
-  double max_abs = 0;
   int64_t prev = 0;
   for (int32_t i = 0; i < cardinality; ++i) {
     const int64_t k = order_key(i);
@@ -685,13 +700,12 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
     if (w == 4) {
       uint32_t v = be32(b + 4 * i);
       memcpy(&le[4 * i], &v, 4);
-      if (data_type == PGPU_INT) max_abs = std::max(max_abs, std::fabs((double)(int32_t)v));
     } else {
       uint64_t v = be64(b + 8 * i);
       memcpy(&le[8 * (size_t)i], &v, 8);
-      if (data_type == PGPU_LONG) max_abs = std::max(max_abs, std::fabs((double)(int64_t)v));
     }
   }
+  const double max_abs = abs_bound_of(le.data(), (size_t)cardinality, data_type);
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
@@ -745,14 +759,7 @@ int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_
   std::string err;
   rc = pgpu_decode_raw_forward((const uint8_t*)bytes, num_bytes, w, seg->num_docs, &le, &err);
   if (rc) return fail(rc, "raw forward index of column %d: %s", column, err.c_str());
-  double max_abs = 0;
-  if (data_type == PGPU_INT || data_type == PGPU_LONG)
-    for (int32_t i = 0; i < seg->num_docs; ++i) {
-      int64_t v;
-      if (w == 4) { int32_t x; memcpy(&x, &le[4 * (size_t)i], 4); v = x; }
-      else memcpy(&v, &le[8 * (size_t)i], 8);
-      max_abs = std::max(max_abs, std::fabs((double)v));
-    }
+  const double max_abs = abs_bound_of(le.data(), (size_t)seg->num_docs, data_type);
   // padded to whole PGPU_TILE-doc tiles (+16 B) like a fixed-bit stream: the kernels read whole tiles of "ids"
   const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
   const uint64_t alloc = std::max<uint64_t>(1, ntiles) * PGPU_TILE * w + 16;
@@ -919,7 +926,7 @@ int pgpu_segment_add_mv_row_columns(pgpu_segment* seg, int32_t column, int32_t l
     }
     if (fp) {
       memcpy(&sums[8 * (size_t)d], &dsum, 8);
-      max_sum = std::max(max_sum, std::fabs(dsum));
+      max_sum = abs_bound(max_sum, dsum);
     } else {
       memcpy(&sums[8 * (size_t)d], &isum, 8);
       max_sum = std::max(max_sum, std::fabs((double)isum));
@@ -1110,13 +1117,7 @@ int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int
                             (uint32_t*)ids.p, (uint32_t*)fwd.p, nwords, nullptr));
   std::vector<uint8_t> le((size_t)w * card);
   HIP_TRY(hipMemcpy(le.data(), dict.p, le.size(), hipMemcpyDeviceToHost));
-  double max_abs = 0;
-  for (uint32_t i = 0; i < card && (t == PGPU_INT || t == PGPU_LONG); ++i) {
-    int64_t v;
-    if (w == 4) { int32_t x; memcpy(&x, &le[4 * (size_t)i], 4); v = x; }
-    else memcpy(&v, &le[8 * (size_t)i], 8);
-    max_abs = std::max(max_abs, std::fabs((double)v));
-  }
+  const double max_abs = abs_bound_of(le.data(), (size_t)card, t);
   c.dict = std::move(dict);
   c.fwd = std::move(fwd);
   c.dict_type = t;
@@ -1228,6 +1229,45 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
   for (int s = 0; s < q->num_segments; ++s)
     if (q->segments[s].segment) docs += q->segments[s].segment->num_docs;
   docs = std::max<int64_t>(docs, q->reduce_docs);
+  // FLOAT / DOUBLE SUM / AVG in fixed point (three part sections each) when every such column is finite and the
+  // sections fit; otherwise all of them keep a float64 section.  PGPU_NO_FIXED_SUM=1 forces float64.
+  static const bool no_fixed = getenv("PGPU_NO_FIXED_SUM") && atoi(getenv("PGPU_NO_FIXED_SUM")) != 0;
+  int32_t fx_exp[16];
+  bool fixed = !no_fixed;
+  {
+    int with_fixed = 1, without = 1;  // sections of either choice
+    for (int a = 0; a < q->num_aggs; ++a) {
+      const pgpu_agg& ag = q->aggs[a];
+      fx_exp[a] = 0;
+      if (ag.fn == PGPU_AGG_COUNT) continue;
+      int32_t vt = -1;
+      double max_abs = 0;
+      if (ag.column >= 0 && ag.column < q->num_columns)
+        for (int s = 0; s < q->num_segments; ++s) {
+          const pgpu_segment* sg = q->segments[s].segment;
+          const int32_t sl = q->segments[s].column_map ? q->segments[s].column_map[ag.column] : -1;
+          if (!sg || sl < 0 || sl >= (int32_t)sg->cols.size()) continue;  // reported below
+          if (vt < 0) vt = sg->cols[sl].dict_type;
+          max_abs = abs_bound(max_abs, sg->cols[sl].max_abs);
+        }
+      const bool sum = ag.fn == PGPU_AGG_SUM || ag.fn == PGPU_AGG_AVG;
+      if (sum && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE)) {
+        int32_t e = max_abs > 0 ? (int32_t)std::ilogb(max_abs) + 1 - 62 : -1100;  // |v| * 2^-e < 2^62
+        if (!std::isfinite(max_abs)) e = PGPU_SUM_EXP_F64;
+        if (q->sum_exp) e = std::max(e, q->sum_exp[a]);
+        if (e >= PGPU_SUM_EXP_F64) fixed = false;
+        fx_exp[a] = e;
+        with_fixed += 3;
+        without += 1;
+      } else {
+        const int k = sum && ((q->flags & PGPU_Q_SUM_SPLIT) || max_abs * (double)docs >= 4.611686018427388e18) ? 3 : 1;
+        with_fixed += k;
+        without += k;
+      }
+    }
+    // the float64 sections when the part sections would not fit (and the integer ones would)
+    if (with_fixed > PGPU_MAX_SECTIONS && without <= PGPU_MAX_SECTIONS) fixed = false;
+  }
   for (int a = 0; a < q->num_aggs; ++a) {
     const pgpu_agg& ag = q->aggs[a];
     if (ag.fn < PGPU_AGG_COUNT || ag.fn > PGPU_AGG_AVG) return fail(PGPU_E_UNSUPPORTED, "aggregation fn %d", ag.fn);
@@ -1245,10 +1285,17 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
     int op;
     if (ag.fn == PGPU_AGG_MIN) op = PGPU_RED_MIN_I64;
     else if (ag.fn == PGPU_AGG_MAX) op = PGPU_RED_MAX_I64;
-    else op = (vt == PGPU_INT || vt == PGPU_LONG) ? PGPU_RED_SUM_I64 : PGPU_RED_SUM_F64;
-    // integer SUM: one int64 cell while max|value| x docs stays below 2^62, else three exact part sums
+    else op = (vt == PGPU_INT || vt == PGPU_LONG || fixed) ? PGPU_RED_SUM_I64 : PGPU_RED_SUM_F64;
+    // integer SUM: one int64 cell while max|value| x docs stays below 2^62, else three exact part sums; fixed-point
+    // floating SUM: always three part sums
     int parts = 1;
-    if (op == PGPU_RED_SUM_I64) {
+    out->agg_sum_exp[a] = 0;
+    if (op == PGPU_RED_SUM_F64) {
+      out->agg_sum_exp[a] = PGPU_SUM_EXP_F64;
+    } else if (op == PGPU_RED_SUM_I64 && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE)) {
+      out->agg_sum_exp[a] = fx_exp[a];
+      parts = 3;
+    } else if (op == PGPU_RED_SUM_I64) {
       double max_abs = 0;
       for (int s = 0; s < q->num_segments; ++s) {
         const pgpu_segment* sg = q->segments[s].segment;
@@ -1316,6 +1363,8 @@ struct Packer {
   // inverted-index leaves expanded before the query kernel (invexp_kernel): InvLeafX::out = word offset in rawbits,
   // InvLeafX::ids = offset in invids until launch
   std::vector<InvLeafX> invx;
+  std::vector<ProgJob> jobs;     // index-only dense programs precomputed per query (progbits_kernel)
+  int32_t job_tiles = 0;
   std::vector<int32_t> invids;
 };
 
@@ -2176,6 +2225,53 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     ds.nreg = (int32_t)aggcols.size();
     for (size_t j = 0; j < aggcols.size(); ++j) ds.reg_col[j] = aggcols[j];
   }
+  // An index-only dense program of several leaves (bitmap / expanded-bitmap / sorted, AND / OR / NOT) is evaluated
+  // once per query for all of the segment's tiles (progbits_kernel) into a match bitmap; the query kernels then
+  // read one word per lane and tile (DevSeg::single_bits).  Config 3: the interpreter's per-tile instruction
+  // fetches and leaf loads were half of the query kernel.  PGPU_NO_PROGBITS=1 keeps the interpreter.
+  static const bool no_progbits = getenv("PGPU_NO_PROGBITS") && atoi(getenv("PGPU_NO_PROGBITS")) != 0;
+  ds.single_bits = 0;
+  if (!no_progbits && ds.fast == 0 && ds.rprog_len == 0 && ds.prog_len > 1 && ds.ntiles > 0) {
+    int leaves = 0;
+    bool ok = true;
+    for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+      const DevInstr& in = pk.instrs[i];
+      if (in.op == PGPU_I_BITS) ok = ok && in.nostat, ++leaves;
+      else if (in.op == PGPU_I_SORTED || in.op == PGPU_I_INV) ++leaves;
+      else if (in.op == PGPU_I_SCAN) ok = false;
+    }
+    if (ok && leaves >= 2 && pk.raw_words + (int64_t)ds.ntiles * 64 <= kInvExpMaxWords) {
+      for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i)
+        if (pk.instrs[i].op == PGPU_I_BITS) pk.instrs[i].n = -1;  // progbits loads each leaf's words itself
+      ProgJob jb{};
+      jb.seg = (int32_t)pk.segs.size();
+      jb.prog_begin = ds.prog_begin;
+      jb.prog_len = ds.prog_len;
+      jb.tile0 = pk.job_tiles;
+      jb.ntiles = ds.ntiles;
+      jb.out = (uint32_t*)(intptr_t)pk.raw_words;  // a word offset into the workspace bitmaps until launch
+      pk.raw_words += (int64_t)ds.ntiles * 64;
+      pk.job_tiles += ds.ntiles;
+      pk.jobs.push_back(jb);
+      DevInstr in{};
+      in.op = PGPU_I_BITS;
+      in.kind = PGPU_COL_FIXED_BIT;
+      in.col = -1;
+      in.care = -1;
+      in.stage_off = -1;
+      in.nostat = 1;
+      in.n = 0;
+      in.fwd = jb.out;
+      for (int k = 0; k < 8; ++k) in.ids[k] = 0xFFFFFFFFu;
+      pk.bits_instrs.push_back((int)pk.instrs.size());
+      ds.prog_begin = (int32_t)pk.instrs.size();
+      ds.prog_len = 1;
+      pk.instrs.push_back(in);
+      ds.nbits = 1;
+      ds.bits_w[0] = jb.out;
+      ds.single_bits = 1;
+    }
+  }
   return PGPU_OK;
 }
 
@@ -2223,6 +2319,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       d.vtype = L.agg_value_type[a];
       d.emit = 0;
       d.part = parts == 3 ? k + 1 : 0;
+      d.fxe = L.agg_sum_exp[a];
     }
   }
   // multi-value group columns (every segment's column of one schema: multi-value everywhere or nowhere)
@@ -2642,7 +2739,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_mvset = align16(o_mv + pk.mvs.size() * sizeof(MvLeaf));
   const size_t o_inv = align16(o_mvset + pk.mvsets.size() * 4);
   const size_t o_invids = align16(o_inv + pk.invx.size() * sizeof(InvLeafX));
-  const size_t total = align16(o_invids + pk.invids.size() * 4) + 16;
+  const size_t o_jobs = align16(o_invids + pk.invids.size() * 4);
+  const size_t total = align16(o_jobs + pk.jobs.size() * sizeof(ProgJob)) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total, ctx->mpool, st);
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16, ctx->mpool, st);
@@ -2787,6 +2885,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     max_inv_words = std::max<int64_t>(max_inv_words, x.words);
   }
   memcpy(h + o_inv, pk.invx.data(), pk.invx.size() * sizeof(InvLeafX));
+  for (ProgJob& jb : pk.jobs) jb.out = (uint32_t*)ws->rawbits.p + (intptr_t)jb.out;
+  memcpy(h + o_jobs, pk.jobs.data(), pk.jobs.size() * sizeof(ProgJob));
   memcpy(h + o_invids, pk.invids.data(), pk.invids.size() * 4);
   memcpy(h + o_mvset, pk.mvsets.data(), pk.mvsets.size() * 4);
   memcpy(h + o_raw, pk.raws.data(), pk.raws.size() * sizeof(RawLeaf));
@@ -2828,6 +2928,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = pgpu_launch_mvpred((const MvLeaf*)(d + o_mv), (int)pk.mvs.size(), max_mv_words, st);
   if (e == hipSuccess && !pk.invx.empty())
     e = pgpu_launch_invexp((const InvLeafX*)(d + o_inv), (int)pk.invx.size(), max_inv_words, st);
+  if (e == hipSuccess && !pk.jobs.empty())
+    e = pgpu_launch_progbits(p, (const ProgJob*)(d + o_jobs), (int)pk.jobs.size(), pk.job_tiles, st);
   if (e == hipSuccess)
     e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
@@ -3113,6 +3215,7 @@ int topk_spec(const pgpu_table_layout* L, const pgpu_topk* o, TopkDev* out) {
     const bool split = L->agg_sum_parts[a] == 3;
     const int op = L->section_op[sec];
     const int vt = L->agg_value_type[a];
+    t.fxe = split && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE) ? L->agg_sum_exp[a] : 0;
     switch (o->agg_fn) {
       case PGPU_AGG_COUNT: t.mode = PGPU_TK_COUNT; break;
       case PGPU_AGG_SUM:
@@ -3229,7 +3332,44 @@ int enqueue_compact(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L
   return PGPU_OK;
 }
 
+// compact_into's passes with the rows left in device buffers (keys [n][max(kw, 1)], cells [n][nsec])
+int compact_device(pgpu_context* ctx, Workspace* ws, const pgpu_table_layout* L, const void* dev_table,
+                   hipStream_t st, int64_t* dkeys, int64_t* dcells, uint64_t capacity, uint64_t* out_n) {
+  const uint64_t G = L->num_keys;
+  const int nsec = L->num_sections;
+  const int kw = L->key_kind == PGPU_KEYS_HASH ? L->key_words : 0;
+  const uint64_t nb = (G + 4095) / 4096;
+  HIP_TRY(ws->cmp_counts.ensure(4 * nb + 16, ctx->mpool, st));
+  HIP_TRY(ws->cmp_total.ensure(16, ctx->mpool, st));
+  HIP_TRY(ws->h_total.ensure(16));
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p,
+                              (int64_t*)ws->cmp_total.p, nullptr, nullptr, true, st, nullptr, nullptr));
+  HIP_TRY(hipMemcpyAsync(ws->h_total.p, ws->cmp_total.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint64_t n = (uint64_t)*(const int64_t*)ws->h_total.p;
+  *out_n = n;
+  if (n > capacity) return fail(PGPU_E_INVALID, "%llu rows exceed the device buffer", (unsigned long long)n);
+  if (n == 0) return PGPU_OK;
+  HIP_TRY(pgpu_launch_compact((const int64_t*)dev_table, G, nsec, kw, (int32_t*)ws->cmp_counts.p, nullptr, dkeys,
+                              dcells, false, st, nullptr, nullptr));
+  HIP_TRY(hipStreamSynchronize(st));
+  return PGPU_OK;
+}
+
 }  // namespace
+
+// pgpu_node.cpp: the non-empty rows of a (hash) table compacted into device buffers that hold `capacity` rows.
+int pgpu_compact_to_device(pgpu_context* ctx, const pgpu_table_layout* L, const void* dev_table, hipStream_t st,
+                           int64_t* dkeys, int64_t* dcells, uint64_t capacity, uint64_t* out_n) {
+  if (!ctx || !L || !dev_table || !out_n) return fail(PGPU_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = 0;
+  Workspace* ws = acquire_ws(ctx, &rc);
+  if (!ws) return rc;
+  rc = compact_device(ctx, ws, L, dev_table, st ? st : ws->stream, dkeys, dcells, capacity, out_n);
+  release_ws(ctx, ws);
+  return rc;
+}
 
 extern "C" {
 

@@ -16,7 +16,7 @@ import numpy as np
 from . import _lib
 from ._lib import QueryDesc, QueryStats, TableLayout
 from .plan import (ExecutionStats, GpuPlanMaker, GroupTable, QueryResult, check_group_columns, finish,
-                   has_mv_aggregations, key_words_out, mv_lower, mv_raise, union_sorted)
+                   has_mv_aggregations, key_words_out, mv_lower, mv_raise, table_capacity, topk_spec, union_sorted)
 from .query import QueryContext
 from .segment import GpuContext, GpuSegment
 
@@ -77,6 +77,12 @@ class GpuNode:
             descs.append(desc)
         arr = (C.POINTER(QueryDesc) * len(descs))(*[C.pointer(d) for d in descs])
         L0 = self.planners[0].layout(descs[0])
+        # the server's ORDER BY ... LIMIT trim (IndexedTable.finish): every device keeps its best rows of the
+        # groups it owns after the merge (pgpu_node_query_topk)
+        pm0 = self.planners[0]
+        order = None
+        if pm0.gpu_topk and pm0.min_server_group_trim_size > 0:
+            order = topk_spec(query, [len(g) for g in globs], table_capacity(query.limit, pm0.min_server_group_trim_size))
         cap = int(min(max(L0.num_keys * len(descs), 1), 1 << 26))
         kw = 2  # enough for either key width
         keys = np.empty(cap * kw, dtype=np.int64)
@@ -84,9 +90,10 @@ class GpuNode:
         n = C.c_uint64()
         st = QueryStats()
         L = TableLayout()
-        _lib.check(self._lib.pgpu_node_query(self.handle, arr, keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                             cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
-                                             C.byref(st), C.byref(L)))
+        _lib.check(self._lib.pgpu_node_query_topk(self.handle, arr, C.byref(order) if order is not None else None,
+                                                  keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                  cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
+                                                  C.byref(st), C.byref(L)))
         kw = key_words_out(L)
         ng = n.value
         k = keys[: ng * kw].reshape(ng, kw) if kw > 1 else keys[:ng]
@@ -95,6 +102,8 @@ class GpuNode:
                                num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
                                num_total_docs=st.num_total_docs, num_segments_processed=len(everything),
+                               num_segments_matched=st.num_segments_matched,
+                               num_groups_limit_reached=bool(st.num_groups_limit_reached),
                                kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
                                dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact))
         return finish(query, GroupTable.sorted(k, c, L), globs, stats)

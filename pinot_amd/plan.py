@@ -344,13 +344,20 @@ class QueryResult:
         return self._intermediate
 
 
-def join_parts(row_cells, sec: int, parts: int) -> int:
-    """Exact integer SUM of a cell split into 21-bit-part sections (pgpu_table_layout.agg_sum_parts == 3):
-    c[sec] + c[sec+1] * 2^21 + c[sec+2] * 2^42, as a Python int (rounded once, on conversion to double)."""
+def join_parts(row_cells, sec: int, parts: int, exp: int = 0):
+    """Exact SUM of a cell split into 21-bit-part sections (pgpu_table_layout.agg_sum_parts == 3):
+    c[sec] + c[sec+1] * 2^21 + c[sec+2] * 2^42, as a Python int (rounded once, on conversion to double); a
+    fixed-point floating SUM (agg_sum_exp = exp != 0) is that integer times 2^exp, rounded once to a double."""
     if parts != 3:
         return int(row_cells[sec])
     b = _lib.PGPU_PART_BITS
-    return int(row_cells[sec]) + (int(row_cells[sec + 1]) << b) + (int(row_cells[sec + 2]) << (2 * b))
+    total = int(row_cells[sec]) + (int(row_cells[sec + 1]) << b) + (int(row_cells[sec + 2]) << (2 * b))
+    return math.ldexp(float(total), exp) if exp else total
+
+
+def sum_exp_of(L: TableLayout, ai: int) -> int:
+    """The fixed-point exponent of aggregation ai's split SUM (0 = an integer sum)."""
+    return L.agg_sum_exp[ai] if L.agg_value_type[ai] in (PGPU_FLOAT, PGPU_DOUBLE) and L.agg_sum_parts[ai] == 3 else 0
 
 
 def final_value(fn: str, cell_count: int, cell: Optional[int], op: int, vtype: int):
@@ -622,11 +629,12 @@ class GpuPlanMaker:
         return arr, len(nodes), la
 
     def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment], plan_filters: bool = True,
-                   extra_flags: int = 0, reduce_docs: int = 0):
+                   extra_flags: int = 0, reduce_docs: int = 0, sum_exp: Optional[Sequence[int]] = None):
         """Build the pgpu_query_desc.  Returns (desc, keep, globals_): `keep` owns every buffer the descriptor
         points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array).
         plan_filters=False leaves the per-segment filter programs empty (the library plans them from
-        filter_expr)."""
+        filter_expr); sum_exp (per aggregation) is the lower bound of the floating SUMs' fixed-point exponents that
+        callers combining tables across ranks agree on (pgpu_query_desc.sum_exp)."""
         columns = list(query.columns)
         col_index = {c: i for i, c in enumerate(columns)}
         nseg = len(segments)
@@ -689,7 +697,8 @@ class GpuPlanMaker:
             *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
         gcols = (C.c_int32 * max(1, ng))(*[group_col[g] for g in query.group_by])
         gcards = (C.c_int32 * max(1, ng))(*[len(g[0]) for g in globals_])
-        keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards]
+        sexp = (C.c_int32 * max(1, len(query.aggregations)))(*(sum_exp or [])) if sum_exp is not None else None
+        keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards, sexp]
         desc = QueryDesc(num_columns=len(columns), num_segments=nseg,
                          segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
                          num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
@@ -700,7 +709,8 @@ class GpuPlanMaker:
                          # NoDictionary*GroupKeyGenerator caps every key space at numGroupsLimit: with a raw group
                          # column no segment is array-based (a segment meeting more keys goes back to the CPU)
                          array_based_threshold=0 if no_dict else self.max_init_group_holder_capacity,
-                         deadline_ms=0 if self.timeout_ms is None else int(time.time() * 1000) + int(self.timeout_ms))
+                         deadline_ms=0 if self.timeout_ms is None else int(time.time() * 1000) + int(self.timeout_ms),
+                         sum_exp=C.cast(sexp, C.POINTER(C.c_int32)) if sexp is not None else None)
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:
@@ -940,7 +950,7 @@ def finish(query: QueryContext, table: GroupTable, global_dicts: Sequence, stats
         fin, inter = [], []
         for ai, a in enumerate(aggs):
             sec = L.agg_section[ai]
-            cell = join_parts(row_cells, sec, L.agg_sum_parts[ai]) if sec > 0 else None
+            cell = join_parts(row_cells, sec, L.agg_sum_parts[ai], sum_exp_of(L, ai)) if sec > 0 else None
             op = L.section_op[sec]
             vt = L.agg_value_type[ai]
             fin.append(final_value(a.function, cnt, cell, op, vt))
@@ -1089,8 +1099,9 @@ class GroupColumns:
         if fn == "COUNT":
             f = cnt.astype(np.int64)
         elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] == 3:
-            # split integer sum: join the parts exactly (Python ints), round once to double
-            s = np.array([float(join_parts(r, sec, 3)) for r in cells], dtype=np.float64)
+            # split sum: join the parts exactly (Python ints), round once to double (fixed point: times 2^exp)
+            e = sum_exp_of(L, ai)
+            s = np.array([float(join_parts(r, sec, 3, e)) for r in cells], dtype=np.float64)
             f = s if fn == "SUM" else s / cnt
         elif fn in ("SUM", "AVG"):
             s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)

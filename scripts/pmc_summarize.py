@@ -15,17 +15,36 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("query_kernel", "query_kernel_direct", "query_kernel_rdirect")
+# the kernels inside the query's timed region (pgpu_runtime.cpp: HIP events ev0..ev1): leaf bitmaps, the query kernel
+# or the partitioned group-by's phases (its sampling and planning passes included)
+TIMED = ("rawpred_kernel", "mvpred_kernel", "invexp_kernel", "progbits_kernel", "query_kernel", "part_scan_kernel",
+         "part_plan_kernel", "part_reduce_kernel")
 
 
-def _is_query_kernel(name: str) -> bool:
-    return "query_kernel" in name
+def _base(name: str) -> str:
+    n = name.split("(")[0]
+    n = n.split("<")[0]
+    return n.split("::")[-1].strip()
+
+
+def _is_timed(name: str) -> bool:
+    b = _base(name)
+    return b in TIMED or b.startswith("query_kernel")
+
+
+def _is_main(name: str) -> bool:
+    """One launch per query: the query kernel, or phase 1 proper of the partitioned group-by."""
+    b = _base(name)
+    return b.startswith("query_kernel") or (b == "part_scan_kernel" and "<false>" in name)
 
 
 def per_launch(path):
-    rows = [r for r in csv.DictReader(open(path)) if _is_query_kernel(r["Kernel_Name"])]
-    vals = [float(r["Counter_Value"]) * 1024.0 for r in rows]
-    return sum(vals) / len(vals), len(vals)
+    """(counter bytes per query over the timed kernels, queries)."""
+    rows = list(csv.DictReader(open(path)))
+    total = sum(float(r["Counter_Value"]) * 1024.0 for r in rows if _is_timed(r["Kernel_Name"]))
+    # a kernel's counter rows: one per dispatch (per-dispatch aggregation of the counter)
+    queries = len({r.get("Dispatch_Id", i) for i, r in enumerate(rows) if _is_main(r["Kernel_Name"])})
+    return total / max(1, queries), queries
 
 
 def bench_json(log):
@@ -43,10 +62,15 @@ def main():
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"kernel_stats_{wl}.csv"))
     fetch, n1 = per_launch(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
     write, n2 = per_launch(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
-    avg_ns, kname = None, None
+    avg_ns, kname, calls, per_kernel = 0.0, None, 0, {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-        if _is_query_kernel(r["Name"]):
-            avg_ns, kname = float(r["AverageNs"]), r["Name"]
+        if _is_timed(r["Name"]):
+            per_kernel[_base(r["Name"]) + ("<false>" if "<false>" in r["Name"] else "<true>" if "<true>" in r["Name"] else "")] = {
+                "calls": int(r["Calls"]), "total_ns": float(r["TotalDurationNs"]), "avg_ns": float(r["AverageNs"])}
+            avg_ns += float(r["TotalDurationNs"])
+        if _is_main(r["Name"]):
+            kname, calls = r["Name"], calls + int(r["Calls"])
+    avg_ns = avg_ns / max(1, calls)
     factor, cal = 2.0, None
     cal_csv = os.path.join(src, "pmc_cal", "run_counter_collection.csv")
     if os.path.exists(cal_csv):
@@ -66,8 +90,8 @@ def main():
            "fetch_size_bytes_raw": fetch, "write_size_bytes": write, "launches": [n1, n2],
            "fetch_correction": factor, "calibration": cal,
            "hbm_bytes_per_launch": factor * fetch + write,
-           "rocprof_avg_kernel_ns": avg_ns,
-           "note": "fetch_correction x FETCH_SIZE + WRITE_SIZE per launch; the correction is measured on the "
+           "rocprof_avg_kernel_ns": avg_ns, "rocprof_kernels": per_kernel,
+           "note": "fetch_correction x FETCH_SIZE + WRITE_SIZE per query over the kernels of its timed region (TIMED); the correction is measured on the "
                    "workload's filter stream alone (known bytes) when a calibration pass exists, else the guide's x2 "
                    "for 16-B/lane streams; the sparse sector gathers are other widths, so their share carries the "
                    "stream's factor"}
@@ -76,6 +100,10 @@ def main():
     with open(os.path.join(dst, f"pmc_{wl}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
+    for extra in ("pmc_lds", "pmc_sq"):  # optional SQ counter passes, copied beside the summary
+        d = os.path.join(src, extra)
+        if os.path.isdir(d):
+            shutil.copy(os.path.join(d, "run_counter_collection.csv"), os.path.join(dst, f"{extra}_{wl}.csv"))
 
 
 if __name__ == "__main__":

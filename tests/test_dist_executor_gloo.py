@@ -93,8 +93,8 @@ def _plan_maker():
     return HostPlanMaker(ctx=None)
 
 
-def _layout(query, segments, flags, reduce_docs, globs):
-    """pgpu_table_layout_of restated (include/pinot_gpu.h)."""
+def _layout(query, segments, flags, reduce_docs, globs, sum_exp=None):
+    """pgpu_table_layout_of restated (include/pinot_gpu.h), floating SUMs in fixed point."""
     L = TableLayout()
     G = 1
     for g in query.group_by:
@@ -107,10 +107,15 @@ def _layout(query, segments, flags, reduce_docs, globs):
             L.agg_section[i], L.agg_value_type[i] = 0, -1
             continue
         vt = segments[0].column(a.column).data_type
-        op = {"MIN": PGPU_RED_MIN_I64, "MAX": PGPU_RED_MAX_I64}.get(
-            a.function, PGPU_RED_SUM_I64 if vt in (PGPU_INT, PGPU_LONG) else PGPU_RED_SUM_F64)
+        op = {"MIN": PGPU_RED_MIN_I64, "MAX": PGPU_RED_MAX_I64}.get(a.function, PGPU_RED_SUM_I64)
         parts = 1
-        if op == PGPU_RED_SUM_I64:
+        L.agg_sum_exp[i] = 0
+        if op == PGPU_RED_SUM_I64 and vt not in (PGPU_INT, PGPU_LONG):
+            mx = max(float(np.abs(s.dictionaries[a.column].astype(np.float64)).max()) for s in segments)
+            e = math.frexp(mx)[1] - 62 if mx > 0 else -1100
+            L.agg_sum_exp[i] = max(e, sum_exp[i]) if sum_exp is not None else e
+            parts = 3
+        elif op == PGPU_RED_SUM_I64:
             mx = max(float(np.abs(s.dictionaries[a.column].astype(np.float64)).max()) for s in segments)
             parts = 3 if (flags & PGPU_Q_SUM_SPLIT) or mx * docs >= 2.0 ** 62 else 1
         L.agg_section[i], L.agg_value_type[i], L.agg_sum_parts[i] = len(ops), vt, parts
@@ -130,10 +135,10 @@ def _numpy_executor(pm):
         """The local kernel step in numpy: the table pgpu_query_launch leaves in HBM (dense cells indexed by the
         mixed-radix key, or -- PGPU_Q_HASH -- slots whose key words follow the sections)."""
 
-        def _prepare_local(self, query, segments, flags, reduce_docs):
+        def _prepare_local(self, query, segments, flags, reduce_docs, sum_exp=None):
             flags |= self.pm.query_flags
             globs = self._globals_of(query, segments)
-            L = _layout(query, segments, flags, reduce_docs, globs)
+            L = _layout(query, segments, flags, reduce_docs, globs, sum_exp)
             ops = [L.section_op[k] for k in range(L.num_sections)]
             st = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
                   "num_segments_matched": 0, "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
@@ -180,7 +185,10 @@ def _numpy_executor(pm):
                     v = np.asarray(ds.values(a.column))[docs]
                     o = L.section_op[sec]
                     if o == PGPU_RED_SUM_I64:
-                        v = v.astype(np.int64)
+                        if L.agg_value_type[i] in (PGPU_INT, PGPU_LONG):
+                            v = v.astype(np.int64)
+                        else:  # fixed point: rint(v * 2^-exp)
+                            v = np.rint(np.ldexp(v.astype(np.float64), -L.agg_sum_exp[i])).astype(np.int64)
                         if L.agg_sum_parts[i] == 3:
                             m = (1 << PGPU_PART_BITS) - 1
                             for k, part in enumerate((v & m, (v >> PGPU_PART_BITS) & m, v >> (2 * PGPU_PART_BITS))):

@@ -115,3 +115,28 @@ def test_node_combine_one_device(qi, flags):
         finally:
             for g in gs:
                 g.release()
+
+
+@pytest.mark.parametrize("scatter", [False, True], ids=["reduce", "reduce_scatter"])
+@pytest.mark.parametrize("flags", [0, PGPU_Q_HASH], ids=["dense", "hash"])
+def test_node_topk_one_device(monkeypatch, scatter, flags):
+    """pgpu_node_query_topk: the node's ORDER BY ... LIMIT trim after the merge -- the dense reduce-scatter path
+    (forced onto a small table with PGPU_NODE_SCATTER_MIN=0: slice copy + per-slice trim with key_base) and the hash
+    ownership merge (rows routed to their owner, merged in a fresh hash table by node_merge_kernel, trimmed)."""
+    from pinot_amd.node import GpuNode
+    if scatter:
+        monkeypatch.setenv("PGPU_NODE_SCATTER_MIN", "0")
+    segs = _segments(300)
+    sql = "SELECT g, h, SUM(m), COUNT(*), MAX(m) FROM t GROUP BY g, h ORDER BY SUM(m) DESC LIMIT 7"
+    with GpuNode([0], query_flags=flags, min_server_group_trim_size=20) as node:
+        gs = [GpuSegment(node.contexts[0], s) for s in segs]
+        try:
+            q = parse_sql(sql)
+            res = node.execute(q, [gs])
+            ref = engine.execute(q, segs)
+            assert [r[2] for r in res.rows] == [r[2] for r in ref.rows]
+            assert rows_close([list(r) for r in res.rows], [list(r) for r in ref.rows])
+            assert len(res.group_rows) < len(ref.group_rows)  # the trim cut
+        finally:
+            for g in gs:
+                g.release()

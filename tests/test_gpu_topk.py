@@ -72,16 +72,11 @@ def test_topk_equals_full_ordering(gpu_ctx, order, limit, flags):
     assert len(trimmed.group_rows) <= len(full.group_rows)
     assert len(full.group_rows) > max(5 * limit, 5000)  # the trim really cut
     assert len(trimmed.group_rows) >= max(5 * limit, 5000)
-    # same groups in the same order; double sums may differ in the last bit (atomic FP64 adds run in any order)
+    # same groups in the same order (ties broken by ascending key on both paths), double sums included: they are
+    # fixed-point integer sums on the GPU (pgpu_table_layout.agg_sum_exp), the same whatever order atomics land in
     q = parse_sql(sql)
-    if order.startswith(("SUM(d)", "AVG(d)", "MIN(d)")):
-        # double aggregates: atomic FP64 adds run in any order, so near-equal values may swap places between runs;
-        # the ORDER BY values agree to the north-star tolerance position by position
-        x, y = _order_column(q, trimmed.rows), _order_column(q, full.rows)
-        assert len(x) == len(y) and all(close(u, v) for u, v in zip(x, y))
-    else:  # same groups in the same order (ties broken by ascending key on both paths)
-        assert [r[:2] for r in trimmed.rows] == [r[:2] for r in full.rows]
-        assert rows_close([list(r) for r in trimmed.rows], [list(r) for r in full.rows])
+    assert [r[:2] for r in trimmed.rows] == [r[:2] for r in full.rows]
+    assert [list(r) for r in trimmed.rows] == [list(r) for r in full.rows]
     ref = engine.execute(q, segs)
     a, b = _order_column(q, trimmed.rows), _order_column(q, ref.rows)
     assert len(a) == len(b) and all(close(x, y) for x, y in zip(a, b)), (a[:5], b[:5])
@@ -112,3 +107,32 @@ def test_topk_partitioned_group_by(gpu_ctx):
     assert [r[0] for r in trimmed.rows] == [r[0] for r in full.rows] and len(trimmed.group_rows) < len(full.group_rows)
     ref = engine.execute(parse_sql(sql), segs, num_groups_limit=1_000_000)
     assert [r[1] for r in trimmed.rows] == [r[1] for r in ref.rows]
+
+
+@pytest.mark.parametrize("flags", ["dense", "hash"])
+def test_double_sum_deterministic(gpu_ctx, flags):
+    """SUM / AVG of a DOUBLE column are bit-identical run to run (fixed-point part sums, no float atomics), equal
+    to the exactly rounded sum of the values, and the layout says so (agg_sum_exp, three part sections)."""
+    rng = np.random.default_rng(11)
+    n = 200000
+    segs = []
+    for i in range(2):
+        cols = {"a": (PGPU_INT, rng.integers(0, 50, n)),
+                "d": (PGPU_DOUBLE, rng.normal(0, 1e6, n) * rng.choice([1e-9, 1.0, 1e3], n))}
+        segs.append(build_segment(f"det{i}", cols, sorted_columns=()))
+    sql = "SELECT a, SUM(d), AVG(d), COUNT(*) FROM t GROUP BY a ORDER BY SUM(d) DESC LIMIT 50"
+    qf = _lib.PGPU_Q_HASH if flags == "hash" else 0
+    runs = [_run(gpu_ctx, segs, sql, query_flags=qf).rows for _ in range(3)]
+    assert runs[0] == runs[1] == runs[2]
+    import math
+    from oracle.engine import DecodedSegment
+    vals = {}
+    for s in segs:
+        ds = DecodedSegment(s)
+        a, d = np.asarray(ds.values("a")), np.asarray(ds.values("d"), dtype=np.float64)
+        for k in np.unique(a):
+            vals.setdefault(int(k), []).append(d[a == k])
+    for r in runs[0]:
+        exact = math.fsum(np.concatenate(vals[r[0]]))  # the exactly rounded sum
+        # each value is rounded to a multiple of 2^exp, exp = ilogb(max|d|) + 1 - 62 = -29 here
+        assert abs(r[1] - exact) <= abs(exact) * 2.0 ** -50 + len(np.concatenate(vals[r[0]])) * 2.0 ** -30
