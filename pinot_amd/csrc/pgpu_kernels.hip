@@ -3338,8 +3338,24 @@ FI void part_combine(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS 
     ok = ok && !in;
   }
 }
+// Wave totals without LDS traffic (DPP row reductions + four readlanes; __shfl_xor is ds_bpermute, which competes
+// with the LDS atomics these save): the exact sum of 64 int32 values (16-bit halves), the max of 64 u32 values.
+FI int64_t wave_sum_i32_wide(int32_t v) {
+  const int lo = wave_sum_i32(v & 0xFFFF);
+  const int hi = wave_sum_i32(v >> 16);
+  return (int64_t)hi * 65536 + lo;
+}
+FI uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)dpp<DPP_QUAD_1032>((int)v));
+  v = max(v, (uint32_t)dpp<DPP_QUAD_2301>((int)v));
+  v = max(v, (uint32_t)dpp<DPP_ROW_HALF_MIRROR>((int)v));
+  v = max(v, (uint32_t)dpp<DPP_ROW_MIRROR>((int)v));
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+  return max(max(a, b), max(c, d));
+}
 // the same for the compact LDS table beside the frame-of-reference dictionary (LDM 2: u32 counts, int64 sums of the
-// ids' values, u32 MIN / MAX ids)
+// ids' values, u32 MIN / MAX ids), its reductions VALU-only
 template <int NS>
 FI void part_combine_for(unsigned char* base, const uint32_t (&soff)[NS > 0 ? NS : 1],
                          const int32_t (&op)[NS > 0 ? NS : 1], const uint32_t* fimg, int fnblk, int fbits, uint32_t k,
@@ -3360,14 +3376,14 @@ FI void part_combine_for(unsigned char* base, const uint32_t (&soff)[NS > 0 ? NS
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
-        const int64_t t = wave_sum_i64(in ? (int64_t)(int32_t)for_value(fimg, fnblk, fbits, id) : 0);
+        const int64_t t = wave_sum_i32_wide(in ? (int32_t)for_value(fimg, fnblk, fbits, id) : 0);
         if (lane == ld) atomicAdd(&((unsigned long long*)(base + soff[s]))[k0], (unsigned long long)t);
       } else if (op[s] == PGPU_RED_MIN_I64) {
-        const int64_t t = wave_min_i64(in ? (int64_t)id : (int64_t)0xFFFFFFFFu);
-        if (lane == ld) atomicMin(&((uint32_t*)(base + soff[s]))[k0], (uint32_t)t);
+        const uint32_t t = ~wave_max_u32(in ? ~id : 0u);
+        if (lane == ld) atomicMin(&((uint32_t*)(base + soff[s]))[k0], t);
       } else {
-        const int64_t t = wave_max_i64(in ? (int64_t)id : 0);
-        if (lane == ld) atomicMax(&((uint32_t*)(base + soff[s]))[k0], (uint32_t)t);
+        const uint32_t t = wave_max_u32(in ? id : 0u);
+        if (lane == ld) atomicMax(&((uint32_t*)(base + soff[s]))[k0], t);
       }
     }
     ok = ok && !in;

@@ -5,6 +5,7 @@
   range_in     LDS-DMA direct kernel (two fast leaves) with candidate aggregation
   bitmap5      inverted leaves expanded to bitmaps (invexp) + sorted ranges, index-only program
   groupby1m    partitioned group-by (phase 1 records, phase 2 LDS tables), 1M keys
+  ring_groupby ring kernel (loader waves + consumers): 50 %-selective range, 16-key LDS table, dense aggregation
 """
 import numpy as np
 import pytest
@@ -20,12 +21,14 @@ N = 1 << 25
 # looser variants where the bench query matches (almost) nothing at one segment
 SQL = {"adanalytics": WORKLOADS["adanalytics"].sql.replace("accountId IN (123456789)", "accountId < 123456789"),
        "range_in": WORKLOADS["range_in"].sql, "bitmap5": WORKLOADS["bitmap5"].sql,
-       "groupby1m": WORKLOADS["groupby1m"].sql}
+       "groupby1m": WORKLOADS["groupby1m"].sql,
+       "ring_groupby": "SELECT i, SUM(m), COUNT(*) FROM synth WHERE r BETWEEN 114691 AND 344060 GROUP BY i"}
+WORKLOAD_OF = {"ring_groupby": "range_in"}
 
 
 @pytest.mark.parametrize("name", sorted(SQL))
 def test_full_size_segment_vs_c_port(gpu_ctx, name):
-    w = WORKLOADS[name]
+    w = WORKLOADS[WORKLOAD_OF.get(name, name)]
     q = parse_sql(SQL[name])
     opts = w.options
     _, matched, counts, sums, _ = CpuBaseline(q, [synth_segment(w, 0, N)]).run(8)
