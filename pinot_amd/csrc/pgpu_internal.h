@@ -155,6 +155,12 @@ struct DevSeg {
   int32_t pfx_col;
   int32_t pfx_nr;
   uint32_t pfx_rng[PGPU_SLICE_RANGES][2];
+  // PGPU_AM_SLICED with every aggregation from value planes (self-loading kernel): the aggregated columns' value
+  // planes are DMA'd into the slot beside the staged filter columns (query column, byte offset in the slot)
+  int32_t nvstage;
+  int32_t vstage_col[2];
+  int32_t vstage_off[2];
+  int32_t pad3_;
 };
 #define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 

@@ -801,7 +801,7 @@ FI bool cursor_advance(const DevParams& p, Cursor& c, int k) {
 // ================================================================================================================
 // The loader's copy of its current segment's staging plan, in SGPRs (fixed-size, statically indexed).
 struct StageCache {
-  int nst;
+  int nst;   // staged columns, the value-plane regions (DevSeg::nvstage) included
   int instrs;
   int lin;  // bit j: column j is bit-sliced (plain 256*b tile copy)
   const char* fwd[PGPU_MAX_STAGE];
@@ -814,6 +814,7 @@ FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
   sc.instrs = cld(&sg->stage_instrs);
   sc.lin = cld(&sg->stage_sliced);
   const DevColumn* cols = p.cols + cld(&sg->col_begin);
+  const int nv = cld(&sg->nvstage);
 #pragma unroll
   for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
     if (j < sc.nst) {
@@ -821,12 +822,19 @@ FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
       sc.fwd[j] = (sc.lin >> j) & 1 ? (const char*)cld(&cols[qc].sliced) : (const char*)cld(&cols[qc].fwd);
       sc.bits[j] = cld(&cols[qc].bits);
       sc.off[j] = cld(&sg->stage_off[j]);
+    } else if (j < sc.nst + nv) {  // value planes: a plain copy of vbits 256-B rows per tile
+      const int qc = cld(&sg->vstage_col[j - sc.nst]);
+      sc.fwd[j] = (const char*)cld(&cols[qc].vsliced);
+      sc.bits[j] = cld(&cols[qc].vbits);
+      sc.off[j] = cld(&sg->vstage_off[j - sc.nst]);
+      sc.lin |= 1 << j;
     } else {
       sc.fwd[j] = nullptr;
       sc.bits[j] = 0;
       sc.off[j] = 0;
     }
   }
+  sc.nst += nv;
 }
 
 // DMA the staged columns of one tile into `slot` (16 B per lane, 1 KiB per instruction; widths that are multiples
@@ -943,6 +951,7 @@ struct SegState {
   const DevSeg* sg;
   int32_t track;  // HASH: distinct-key bitmap row + 1 (0 = not counted)
   int32_t single_bits;  // DevSeg::single_bits
+  int32_t nvstage;      // DevSeg::nvstage
   const DevColumn* cols;
   const int32_t* const* remaps;
   int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
@@ -978,6 +987,7 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   ss.fast = cld(&sg->fast);
   ss.track = cld(&sg->track);
   ss.single_bits = cld(&sg->single_bits);
+  ss.nvstage = cld(&sg->nvstage);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
@@ -2171,17 +2181,15 @@ FI bool bsi_agg(const DevAgg& ag, const DevColumn& c) {
   return c.vsliced && c.vbits >= 1 && c.vbits <= BSI_MAXB &&
          ((ag.op == PGPU_RED_SUM_I64 && ag.part == 0) || ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64);
 }
-FI void bsi_tile(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& ag, int a, int tile, uint32_t mm) {
+template <int NB>
+FI void bsi_fold(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& ag, int a, const uint32_t (&x)[NB],
+                 uint32_t mm) {
   const int vb = c.vbits;
-  const uint32_t* src = c.vsliced + (size_t)tile * 64 * vb + lane_id();
-  uint32_t x[BSI_MAXB];
-#pragma unroll
-  for (int k = 0; k < BSI_MAXB; ++k) x[k] = k < vb ? __builtin_nontemporal_load(src + 64 * k) : 0u;
   int64_t part;
   if (ag.op == PGPU_RED_SUM_I64) {
     uint64_t u = 0;
 #pragma unroll
-    for (int k = 0; k < BSI_MAXB; ++k)
+    for (int k = 0; k < NB; ++k)
       if (k < vb) u += (uint64_t)__popc(x[k] & mm) << k;
     part = (int64_t)u + (int64_t)__popc(mm) * c.vmin;
   } else {
@@ -2189,7 +2197,7 @@ FI void bsi_tile(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& 
     const bool mx = ag.op == PGPU_RED_MAX_I64;
     uint32_t cand = mm, u = 0;
 #pragma unroll
-    for (int k = BSI_MAXB - 1; k >= 0; --k) {
+    for (int k = NB - 1; k >= 0; --k) {
       if (k >= vb) continue;
       const uint32_t t = cand & (mx ? x[k] : ~x[k]);
       if (t) cand = t;
@@ -2198,6 +2206,49 @@ FI void bsi_tile(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& 
     part = mm ? c.vmin + (int64_t)u : sec_identity(ag.op);
   }
   lacc_add(la, cv, a, ag.op, part);
+}
+template <int NB>
+FI void bsi_load(const DevColumn& c, int tile, uint32_t (&x)[NB]) {
+  const int vb = c.vbits;
+  const uint32_t* src = c.vsliced + (size_t)tile * 64 * vb + lane_id();
+#pragma unroll
+  for (int k = 0; k < NB; ++k) x[k] = k < vb ? __builtin_nontemporal_load(src + 64 * k) : 0u;
+}
+FI void bsi_tile(const Cons& cv, LaneAcc& la, const DevColumn& c, const DevAgg& ag, int a, int tile, uint32_t mm) {
+  uint32_t x[BSI_MAXB];
+  bsi_load<BSI_MAXB>(c, tile, x);
+  bsi_fold<BSI_MAXB>(cv, la, c, ag, a, x, mm);
+}
+// Value planes staged in the slot (DevSeg::nvstage: the self-loading kernel DMAs them with the tile's filter planes,
+// so one counted vmcnt wait covers both -- a plain load issued behind the DMAs and used at once would wait for all of
+// them, vmcnt retiring in order)
+FI void bsi_tile_staged(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, const unsigned char* slot,
+                        uint32_t mm) {
+  for (int a = 0; a < p.nagg; ++a) {
+    if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+    const DevAgg ag = p.aggs[a];
+    const int j = cld(&ss.sg->vstage_col[0]) == ag.col ? 0 : 1;
+    const uint32_t* pl = (const uint32_t*)(slot + cld(&ss.sg->vstage_off[j])) + lane_id();
+    const DevColumn c = col_of(ss, ag.col);
+    const int vb = c.vbits;
+    int64_t part;
+    if (ag.op == PGPU_RED_SUM_I64) {  // planes read as they are folded (no 24-register plane array)
+      uint64_t u = 0;
+      for (int k = 0; k < vb; ++k) u += (uint64_t)__popc(pl[64 * k] & mm) << k;
+      part = (int64_t)u + (int64_t)__popc(mm) * c.vmin;
+    } else {
+      const bool mx = ag.op == PGPU_RED_MAX_I64;
+      uint32_t cand = mm, u = 0;
+      for (int k = vb - 1; k >= 0; --k) {
+        const uint32_t x = pl[64 * k];
+        const uint32_t t = cand & (mx ? x : ~x);
+        if (t) cand = t;
+        if ((t != 0) == mx) u |= 1u << k;
+      }
+      part = mm ? c.vmin + (int64_t)u : sec_identity(ag.op);
+    }
+    lacc_add(la, cv, a, ag.op, part);
+  }
 }
 
 FI void sliced_tile(const DevParams& p, const Cons& cv, LaneAcc& la, const SegState& ss, int tile, uint32_t mm,
@@ -2251,7 +2302,7 @@ template <int MODE, int NW>
 FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, LaneAcc& la, const SegState& ss,
                           int tile_in_seg, uint32_t mm, int& qn, int& qt, uint32_t& lane_matched, int64_t& matched,
                           int64_t& scanned, int64_t& sector_bytes, int64_t& dense_bytes, Prof& pf,
-                          int* sn = nullptr) {
+                          int* sn = nullptr, const unsigned char* slot = nullptr) {
   const int lane = lane_id();
   if (ss.rprog_len == 0 && ss.agg_mode == PGPU_AM_COUNT) {
     lane_matched += __popc(mm);
@@ -2260,7 +2311,8 @@ FI void direct_candidates(const DevParams& p, const Lds& L, const Cons& cv, Lane
     lane_matched += __popc(mm);
     const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
     mark_seg(p, ss, any);
-    if (any && sn) sliced_tile(p, cv, la, ss, tile_in_seg, mm, *sn);
+    if (any && slot && ss.nvstage > 0) bsi_tile_staged(p, cv, la, ss, slot, mm);  // planes DMA'd with the tile
+    else if (any && sn) sliced_tile(p, cv, la, ss, tile_in_seg, mm, *sn);
     if (any && (p.flags & PGPU_FLAG_STATS) && lane == 0)  // the aggregated columns' planes of this tile
       for (int a = 0; a < p.nagg; ++a)
         if (p.aggs[a].fn != PGPU_AGG_COUNT) {
@@ -2338,13 +2390,16 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
     asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(voff16) : "v"(opaque_lane()));  // lane * 16, kept live
     uint32_t bw_next = 0;
     bool bw_have = false;
-    for (int k = 0; k < own; ++k) {
-      while (issued < own && issued < k + D) {
+    auto issue_upto = [&](int upto) {
+      while (issued < own && issued < upto) {
         if (issued > 0 && cursor_advance(p, ci, NW)) load_stage(p, ci.seg, sc);
         issue_tile_direct(sc, ci.tile_in_seg, slots + (size_t)islot * S, voff16, (p.flags & PGPU_FLAG_NT) != 0);
         ++issued;
         if (++islot == D) islot = 0;
       }
+    };
+    for (int k = 0; k < own; ++k) {
+      issue_upto(k + D);
       if (--poll == 0) {
         poll = p.cancel_poll;
         if (query_cancelled(p)) break;  // in-flight DMAs drain below
@@ -2366,7 +2421,8 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
         load_seg(p, cseg, ss);
       }
       const int64_t tw = now(pf);
-      if (ss.nstage > 0) wait_vmcnt(next_instrs);  // this tile's DMAs have landed (later tiles' may be in flight)
+      // this tile's DMAs have landed (later tiles' may be in flight)
+      if (ss.nstage + ss.nvstage > 0) wait_vmcnt(next_instrs);
       PROF_ADD(pf, PGPU_P_C_FULL, tw);
       const int64_t tf = now(pf);
 #ifdef PGPU_PROFILE_BUILD
@@ -2416,7 +2472,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
       PROF_ADD(pf, PGPU_P_C_FILTER, tf);
       const int64_t ta = now(pf);
       direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, mm, qn, qt, lane_matched, matched, scanned,
-                                  sector_bytes, dense_bytes, pf, &sn);
+                                  sector_bytes, dense_bytes, pf, &sn, t.slot);
       PROF_ADD(pf, PGPU_P_C_AGG, ta);
     }
     if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);

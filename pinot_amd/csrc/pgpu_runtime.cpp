@@ -2212,10 +2212,37 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
     const int j = stage_index(in.col);
     if (j >= 0) in.stage_off = stage_offs[j];
   }
-  pk.slot_bytes = std::max(pk.slot_bytes, off);
-  pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
   int64_t tb = 0;
   for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
+  // value planes of sliced aggregation DMA'd with the tile (DevSeg::nvstage): the self-loading kernel's counted
+  // vmcnt then covers them too, where a plain load behind the DMAs would wait for every DMA in flight.
+  // PGPU_NO_VSTAGE=1 loads them per tile instead.
+  static const bool no_vstage = getenv("PGPU_NO_VSTAGE") && atoi(getenv("PGPU_NO_VSTAGE")) != 0;
+  ds.nvstage = 0;
+  if (agg_mode == PGPU_AM_SLICED && all_bsi && !no_vstage) {
+    std::vector<int> vcols;
+    for (int a = 0; a < q->num_aggs; ++a)
+      if (q->aggs[a].fn != PGPU_AGG_COUNT &&
+          std::find(vcols.begin(), vcols.end(), q->aggs[a].column) == vcols.end())
+        vcols.push_back(q->aggs[a].column);
+    int vinstrs = 0, vbytes = 0;
+    for (int qc : vcols) {
+      vinstrs += (v.dev(qc)->vbits + 3) / 4;
+      vbytes += 256 * v.dev(qc)->vbits;
+    }
+    if (vcols.size() <= 2 && staged.size() + vcols.size() <= PGPU_MAX_STAGE &&
+        ds.stage_instrs + vinstrs <= PGPU_MAX_STAGE_INSTRS && off + vbytes <= kMaxSlotBytes) {
+      for (int qc : vcols) {
+        ds.vstage_col[ds.nvstage] = qc;
+        ds.vstage_off[ds.nvstage++] = off;
+        off += 256 * v.dev(qc)->vbits;
+        tb += 256ll * v.dev(qc)->vbits;
+      }
+      ds.stage_instrs += vinstrs;
+    }
+  }
+  pk.slot_bytes = std::max(pk.slot_bytes, off);
+  pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
   pk.tile_bytes = std::max(pk.tile_bytes, tb);
   pk.est_matched += rho * seg->num_docs;
   ds.agg_mode = agg_mode;
@@ -2600,8 +2627,12 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   // sliced aggregation runs in query_kernel_direct only: elsewhere its segments gather per candidate (their staged
   // aggregation planes are then only extra DMA, never read)
   if (p.direct != 1)
-    for (DevSeg& ds : pk.segs)
+    for (DevSeg& ds : pk.segs) {
       if (ds.agg_mode == PGPU_AM_SLICED) ds.agg_mode = PGPU_AM_SPARSE;
+      for (int j = 0; j < ds.nvstage; ++j)  // (the ring loaders stage filter columns only)
+        ds.stage_instrs -= (pk.cols[ds.col_begin + ds.vstage_col[j]].vbits + 3) / 4;
+      ds.nvstage = 0;
+    }
   // one-word PART records (in-partition key, dict id) when every segment holds the same dictionary for the
   // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
   int part_idbits = 0;

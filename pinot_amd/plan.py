@@ -792,7 +792,8 @@ class GpuPlanMaker:
         if query.has_filtered_aggregations:
             parts = split_filtered_aggregations(query)
             pending = [self.submit(sq, segments) for sq, _ in parts]  # all in flight, then collected in order
-            return merge_filtered(query, parts, [self.collect(pq) for pq in pending])
+            return merge_filtered(query, parts, [self._collect_or_first_seen(pq, sq, segments)
+                                                 for pq, (sq, _) in zip(pending, parts)])
         non_scan = self.non_scan_segments(query, segments)
         if any(non_scan):
             rest = [s for s, ns in zip(segments, non_scan) if not ns]
@@ -800,6 +801,13 @@ class GpuPlanMaker:
             return merge_non_scan(query, res, [s for s, ns in zip(segments, non_scan) if ns])
         try:
             return self.collect(self.submit(query, segments))
+        except _lib.GroupsLimitError:
+            return self.first_seen_groups(query, segments)
+
+    def _collect_or_first_seen(self, pending, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:
+        """collect(), answering a numGroupsLimit overflow by the first-seen path (a filtered aggregation's part)."""
+        try:
+            return self.collect(pending)
         except _lib.GroupsLimitError:
             return self.first_seen_groups(query, segments)
 

@@ -233,7 +233,9 @@ def _rank_segments(rank, nseg=2, n=2500):
                 "x": (PGPU_INT, rng.integers(0, 100, n).astype(np.int32)),
                 "m": (PGPU_INT, rng.integers(-1000, 100000, n).astype(np.int32)),
                 "big": (PGPU_LONG, rng.integers(9 * 10 ** 15, 10 ** 16, n).astype(np.int64)),
-                "d": (PGPU_DOUBLE, np.round(rng.normal(50.0, 20.0, n), 3))}
+                "d": (PGPU_DOUBLE, np.round(rng.normal(50.0, 20.0, n), 3)),
+                # rank-dependent magnitude: the ranks' fixed-point exponents differ until they agree on the max
+                "e": (PGPU_DOUBLE, rng.normal(0.0, 10.0 ** (4 * rank), n))}
         segs.append(build_segment(f"r{rank}s{k}", cols))
     return segs
 
@@ -262,6 +264,7 @@ QUERIES = [
     "SELECT SUM(big), AVG(big), COUNT(*) FROM t WHERE x < 70",     # bound >= 2^62: split layout on every rank
     "SELECT COUNT(*), MIN(m), MAX(d) FROM t",                      # every segment answered without a scan
     "SELECT h, SUM(big), COUNT(*) FROM t GROUP BY h ORDER BY h LIMIT 20",
+    "SELECT g, SUM(e), AVG(e), COUNT(*) FROM t GROUP BY g ORDER BY SUM(e) DESC LIMIT 9",  # agreed sum_exp
 ]
 
 
