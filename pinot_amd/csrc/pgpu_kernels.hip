@@ -3907,14 +3907,42 @@ FI uint32_t fsm_sliced(const uint32_t* sl, int bits, int tile, const DevInstr& i
 }
 
 __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t* fn) {
+  // each wave walks a contiguous run of tiles (XCD-aware workgroup order), so the segment's state and leaf
+  // instructions are loaded once per segment rather than once per tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = (int)blockIdx.x * 4 + wave;
-  if (tile >= p.total_tiles) return;
-  const Cursor c = cursor_at(p, tile);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int64_t nw = (int64_t)nb * 4, gw = (int64_t)lb * 4 + wave;
+  const int tb = (int)((int64_t)p.total_tiles * gw / nw), te = (int)((int64_t)p.total_tiles * (gw + 1) / nw);
+  if (tb >= te) return;
+  Cursor c = cursor_at(p, tb);
+  int cseg = -1;
   SegState ss;
-  load_seg(p, c.seg, ss);
-  const int k = cld(&ss.sg->leaf_len);
-  const int leaf_begin = cld(&ss.sg->leaf_begin);
+  int k = 0, leaf_begin = 0;
+  DevInstr in0, in1;  // the first two leaves, and whether they are evaluated on bit planes
+  bool sl0 = false, sl1 = false;
+  const uint32_t *sp0 = nullptr, *sp1 = nullptr;
+  for (int tile = tb; tile < te; ++tile) {
+  if (tile > tb) cursor_advance(p, c, 1);
+  if (c.seg != cseg) {
+    cseg = c.seg;
+    load_seg(p, cseg, ss);
+    k = cld(&ss.sg->leaf_len);
+    leaf_begin = cld(&ss.sg->leaf_begin);
+    sl0 = sl1 = false;
+    if (k > 0) {
+      in0 = cld(p.instrs + cld(p.pool, leaf_begin));
+      const DevColumn c0 = col_of(ss, in0.col);
+      sl0 = fsm_sliced_ok(in0, c0);
+      sp0 = c0.sliced;
+    }
+    if (k > 1) {
+      in1 = cld(p.instrs + cld(p.pool, leaf_begin + 1));
+      const DevColumn c1 = col_of(ss, in1.col);
+      sl1 = fsm_sliced_ok(in1, c1);
+      sp1 = c1.sliced;
+    }
+  }
   TileCtx t;
   t.ss = &ss;
   t.slot = nullptr;
@@ -3930,20 +3958,8 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
   // the first two leaves, when bit-sliced: every plane of both is loaded before either is evaluated (one round trip
   // per tile instead of one per leaf)
   uint32_t x0[FSM_MAXB], x1[FSM_MAXB];
-  bool sl0 = false, sl1 = false;
-  DevInstr in0, in1;
-  if (k > 0) {
-    in0 = cld(p.instrs + cld(p.pool, leaf_begin));
-    const DevColumn c0 = col_of(ss, in0.col);
-    sl0 = fsm_sliced_ok(in0, c0);
-    if (sl0) fsm_load_planes(c0.sliced, in0.bits, t.tile_in_seg, x0);
-  }
-  if (k > 1) {
-    in1 = cld(p.instrs + cld(p.pool, leaf_begin + 1));
-    const DevColumn c1 = col_of(ss, in1.col);
-    sl1 = fsm_sliced_ok(in1, c1);
-    if (sl1) fsm_load_planes(c1.sliced, in1.bits, t.tile_in_seg, x1);
-  }
+  if (sl0) fsm_load_planes(sp0, in0.bits, t.tile_in_seg, x0);
+  if (sl1) fsm_load_planes(sp1, in1.bits, t.tile_in_seg, x1);
   if (sl0) m[0] = fsm_eval_planes(x0, in0) & t.valid;
   if (sl1) m[1] = fsm_eval_planes(x1, in1) & t.valid;
 #pragma unroll
@@ -4008,6 +4024,7 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
 #pragma unroll
     for (int s = 0; s < 4; ++s) o[1 + s] = h[s];
   }
+  }  // tiles
 }
 
 // One workgroup per segment: compose its tiles' maps in order and write numDocs + H (from state 0) -- the
@@ -4674,7 +4691,8 @@ hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
 
 hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st) {
   if (p.nseg <= 0) return hipSuccess;
-  if (p.total_tiles > 0) hipLaunchKernelGGL(andfsm_tile_kernel, dim3((p.total_tiles + 3) / 4), dim3(256), 0, st, p, fn);
+  if (p.total_tiles > 0)  // ~8 workgroups per CU, each wave over a contiguous run of tiles
+    hipLaunchKernelGGL(andfsm_tile_kernel, dim3(std::min(2048, (p.total_tiles + 3) / 4)), dim3(256), 0, st, p, fn);
   hipLaunchKernelGGL(andfsm_segment_kernel, dim3(p.nseg), dim3(256), 0, st, p, (const uint32_t*)fn, out);
   return hipGetLastError();
 }
