@@ -3149,14 +3149,7 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
             }
           } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              // the first live lane's partition when >= 4 lanes share it (skewed keys spread their hot partitions),
-              // else the sampled hottest one
-              const uint64_t lv = __ballot(lane_bit(mm, 8 * g8 + j));
-              const uint32_t cq = lv ? (uint32_t)__builtin_amdgcn_readlane((int)qq[j], __builtin_ctzll(lv)) : hq;
-              hm[j] = __ballot(qq[j] == cq);
-              if (cq != hq && __popcll(hm[j]) < 4) hm[j] = __ballot(qq[j] == hq);
-            }
+            for (int j = 0; j < 8; ++j) hm[j] = __ballot(qq[j] == hq);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const bool hot = (hm[j] >> lane) & 1u;
@@ -3351,101 +3344,6 @@ FI uint32_t for_value(const uint32_t* fimg, int fnblk, int fbits, uint32_t id) {
   return fimg[blk] + (uint32_t)((two >> (bit & 31u)) & ((1ull << fbits) - 1ull));
 }
 
-// Skewed keys (Zipf): the records of one hot key arriving together would serialize on one LDS address per wave
-// instruction.  Before the per-lane atomics, the key of the first live lane is matched across the wave; when >= 4
-// lanes hold it, their cells are reduced in registers (wave reductions) and that lane applies the totals -- up to two
-// keys per record batch.  For even keys the match is nearly always one lane and the check costs two ballots.
-#define PGPU_P2_COMBINE 4
-template <int NS>
-FI void part_combine(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS : 1], int32_t vt, int idbits,
-                     uint32_t k, uint32_t raw, uint32_t val, bool& ok) {
-  const int lane = lane_id();
-#pragma unroll 1
-  for (int it = 0; it < 2; ++it) {
-    const uint64_t live = __ballot(ok);
-    if (!live) return;
-    const int ld = __builtin_ctzll(live);
-    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k, ld);
-    const uint64_t m = __ballot(ok && k == k0);
-    const int c = __popcll(m);
-    if (c < PGPU_P2_COMBINE) return;
-    const bool in = (m >> lane) & 1u;
-    if (lane == ld) atomicAdd((unsigned long long*)&ptab[k0], (unsigned long long)c);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      int64_t* sec = ptab + (size_t)(1 + s) * K;
-      if (op[s] == PGPU_RED_SUM_I64) {
-        const int64_t t = wave_sum_i64(in ? (int64_t)(int32_t)val : 0);
-        if (lane == ld) atomicAdd((unsigned long long*)&sec[k0], (unsigned long long)t);
-      } else if (op[s] == PGPU_RED_SUM_F64) {
-        const double t = wave_sum_f64(in ? (double)__uint_as_float(val) : 0.0);
-        if (lane == ld) atomicAdd((double*)&sec[k0], t);
-      } else {
-        const int64_t x = idbits ? (int64_t)raw : raw_to_cell(raw, vt, op[s]);
-        if (op[s] == PGPU_RED_MIN_I64) {
-          const int64_t t = wave_min_i64(in ? x : INT64_MAX);
-          if (lane == ld) atomicMin((long long*)&sec[k0], (long long)t);
-        } else {
-          const int64_t t = wave_max_i64(in ? x : INT64_MIN);
-          if (lane == ld) atomicMax((long long*)&sec[k0], (long long)t);
-        }
-      }
-    }
-    ok = ok && !in;
-  }
-}
-// Wave totals without LDS traffic (DPP row reductions + four readlanes; __shfl_xor is ds_bpermute, which competes
-// with the LDS atomics these save): the exact sum of 64 int32 values (16-bit halves), the max of 64 u32 values.
-FI int64_t wave_sum_i32_wide(int32_t v) {
-  const int lo = wave_sum_i32(v & 0xFFFF);
-  const int hi = wave_sum_i32(v >> 16);
-  return (int64_t)hi * 65536 + lo;
-}
-FI uint32_t wave_max_u32(uint32_t v) {
-  v = max(v, (uint32_t)dpp<DPP_QUAD_1032>((int)v));
-  v = max(v, (uint32_t)dpp<DPP_QUAD_2301>((int)v));
-  v = max(v, (uint32_t)dpp<DPP_ROW_HALF_MIRROR>((int)v));
-  v = max(v, (uint32_t)dpp<DPP_ROW_MIRROR>((int)v));
-  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
-  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-  return max(max(a, b), max(c, d));
-}
-// the same for the compact LDS table beside the frame-of-reference dictionary (LDM 2: u32 counts, int64 sums of the
-// ids' values, u32 MIN / MAX ids), its reductions VALU-only
-template <int NS>
-FI void part_combine_for(unsigned char* base, const uint32_t (&soff)[NS > 0 ? NS : 1],
-                         const int32_t (&op)[NS > 0 ? NS : 1], const uint32_t* fimg, int fnblk, int fbits, uint32_t k,
-                         uint32_t id, bool& ok) {
-  const int lane = lane_id();
-  uint32_t* cnt = (uint32_t*)base;
-#pragma unroll 1
-  for (int it = 0; it < 2; ++it) {
-    const uint64_t live = __ballot(ok);
-    if (!live) return;
-    const int ld = __builtin_ctzll(live);
-    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)k, ld);
-    const uint64_t m = __ballot(ok && k == k0);
-    const int c = __popcll(m);
-    if (c < PGPU_P2_COMBINE) return;
-    const bool in = (m >> lane) & 1u;
-    if (lane == ld) atomicAdd(&cnt[k0], (uint32_t)c);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
-        const int64_t t = wave_sum_i32_wide(in ? (int32_t)for_value(fimg, fnblk, fbits, id) : 0);
-        if (lane == ld) atomicAdd(&((unsigned long long*)(base + soff[s]))[k0], (unsigned long long)t);
-      } else if (op[s] == PGPU_RED_MIN_I64) {
-        const uint32_t t = ~wave_max_u32(in ? ~id : 0u);
-        if (lane == ld) atomicMin(&((uint32_t*)(base + soff[s]))[k0], t);
-      } else {
-        const uint32_t t = wave_max_u32(in ? id : 0u);
-        if (lane == ld) atomicMax(&((uint32_t*)(base + soff[s]))[k0], t);
-      }
-    }
-    ok = ok && !in;
-  }
-}
-
 template <int NS, int R>
 FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 ? NS : 1], int32_t vt, int idbits,
                           const uint32_t (&k)[R], const uint32_t (&raw)[R], const uint32_t (&val)[R],
@@ -3543,10 +3441,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
           const uint32_t v = gld(p.recs, rb + (ok[r] ? i : n - 1));
           k[r] = v >> idbits;
           id[r] = v & idmask;
-        }
-        if (split) {  // a hot partition (skewed keys): combine each batch's repeated keys first
-#pragma unroll
-          for (int r = 0; r < R; ++r) part_combine_for<NS>(base, soff, op, fimg, fnblk, fbits, k[r], id[r], ok[r]);
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -3653,10 +3547,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
             }
           }
         }
-        if (split) {  // a hot partition (skewed keys): combine each batch's repeated keys first
-#pragma unroll
-          for (int r = 0; r < R; ++r) part_combine<NS>(ptab, K, op, vt, idbits, k[r], raw[r], val[r], ok[r]);
-        }
         part_reduce_batch<NS, R>(ptab, K, op, vt, idbits, k, raw, val, ok);
       }
     }
@@ -3737,38 +3627,49 @@ __global__ __launch_bounds__(256) void prologue_kernel(const u32x4* __restrict__
 // inverted leaves, AND / OR / NOT) and writes the tile's match words; the query kernel then reads one word per lane.
 __global__ __launch_bounds__(256) void progbits_kernel(DevParams p, const ProgJob* jobs, int njobs, int total) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  // each wave walks a contiguous run of the jobs' tiles (XCD-aware workgroup order): the job and its segment state
+  // are looked up once per run and per job change, not per tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int g = (int)blockIdx.x * 4 + wave;
-  if (g >= total) return;
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int64_t nw = (int64_t)nb * 4, gw = (int64_t)lb * 4 + wave;
+  const int gb = (int)((int64_t)total * gw / nw), ge = (int)((int64_t)total * (gw + 1) / nw);
+  if (gb >= ge) return;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (cld(&jobs[mid].tile0) <= g) lo = mid; else hi = mid - 1;
+    if (cld(&jobs[mid].tile0) <= gb) lo = mid; else hi = mid - 1;
   }
-  const ProgJob jb = cld(jobs + lo);
-  const int tile = g - jb.tile0;
-  SegState ss;
-  load_seg(p, jb.seg, ss);
   Cons cv;
   cv.masks = (uint32_t*)(dyn_smem + (size_t)wave * p.mask_rows * 256);
   cv.queue = nullptr;
   cv.klist = cv.vlist = nullptr;
   cv.acc = nullptr;
   cv.qtiles = nullptr;
-  TileCtx t;
-  t.ss = &ss;
-  t.slot = nullptr;
-  t.tile_in_seg = tile;
-  t.doc0 = tile * WT;
-  t.lane_doc0 = t.doc0 + 32 * lane;
-  {
-    const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
-    t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+  SegState ss;
+  ProgJob jb = cld(jobs + lo);
+  load_seg(p, jb.seg, ss);
+  for (int g = gb; g < ge; ++g) {
+    while (g >= jb.tile0 + jb.ntiles && lo + 1 < njobs) {
+      jb = cld(jobs + ++lo);
+      load_seg(p, jb.seg, ss);
+    }
+    const int tile = g - jb.tile0;
+    TileCtx t;
+    t.ss = &ss;
+    t.slot = nullptr;
+    t.tile_in_seg = tile;
+    t.doc0 = tile * WT;
+    t.lane_doc0 = t.doc0 + 32 * lane;
+    {
+      const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+      t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+    }
+    int64_t scanned = 0, dense_bytes = 0;
+    Prof pf;
+    const uint32_t m = run_program(p, cv, jb.prog_begin, jb.prog_len, t, scanned, dense_bytes, pf);
+    jb.out[(size_t)tile * 64 + lane] = m & t.valid;
   }
-  int64_t scanned = 0, dense_bytes = 0;
-  Prof pf;
-  const uint32_t m = run_program(p, cv, jb.prog_begin, jb.prog_len, t, scanned, dense_bytes, pf);
-  jb.out[(size_t)tile * 64 + lane] = m & t.valid;
 }
 
 // PGPU_Q_EXACT_FILTER_STATS: the match bits of every leaf of every segment's whole filter program over all its
@@ -4699,7 +4600,7 @@ hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hi
 
 hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njobs, int total, hipStream_t st) {
   if (njobs <= 0 || total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(progbits_kernel, dim3((total + 3) / 4), dim3(256), (size_t)4 * p.mask_rows * 256, st, p, jobs,
+  hipLaunchKernelGGL(progbits_kernel, dim3(std::min(2048, (total + 3) / 4)), dim3(256), (size_t)4 * p.mask_rows * 256, st, p, jobs,
                      njobs, total);
   return hipGetLastError();
 }

@@ -2038,7 +2038,8 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
                      ((whole_sum && (dc->dict_type == PGPU_INT || dc->dict_type == PGPU_LONG) && !split) ||
                       q->aggs[a].fn == PGPU_AGG_MIN || q->aggs[a].fn == PGPU_AGG_MAX);
     all_bsi = all_bsi && bsi;
-    sliced = sliced && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced &&
+    // (a split SUM is three device aggregations: the id path's two LDS sub-queues hold one per query aggregation)
+    sliced = sliced && !split && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced &&
              line_touch(rho, bsi ? dc->vbits : dc->bits) >= sliced_touch;
   }
   if (sliced && !all_bsi) {
@@ -2214,12 +2215,13 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   }
   int64_t tb = 0;
   for (int qc : staged) tb += 256ll * v.dev(qc)->bits;
-  // value planes of sliced aggregation DMA'd with the tile (DevSeg::nvstage): the self-loading kernel's counted
-  // vmcnt then covers them too, where a plain load behind the DMAs would wait for every DMA in flight.
-  // PGPU_NO_VSTAGE=1 loads them per tile instead.
-  static const bool no_vstage = getenv("PGPU_NO_VSTAGE") && atoi(getenv("PGPU_NO_VSTAGE")) != 0;
+  // value planes of sliced aggregation DMA'd with the tile (DevSeg::nvstage, PGPU_VSTAGE=1): the self-loading
+  // kernel's counted vmcnt then covers them too, where a plain load behind the DMAs waits for every DMA in flight.
+  // Measured slower (config 2: 2.52 against 1.14 ms; config 3's query kernel 2.44 against 0.93 ms): the wider
+  // slots cut the resident workgroups and the DMA depth more than the in-order waits cost, so it is opt-in.
+  static const bool vstage = getenv("PGPU_VSTAGE") && atoi(getenv("PGPU_VSTAGE")) != 0;
   ds.nvstage = 0;
-  if (agg_mode == PGPU_AM_SLICED && all_bsi && !no_vstage) {
+  if (agg_mode == PGPU_AM_SLICED && all_bsi && vstage) {
     std::vector<int> vcols;
     for (int a = 0; a < q->num_aggs; ++a)
       if (q->aggs[a].fn != PGPU_AGG_COUNT &&

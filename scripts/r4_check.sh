@@ -8,7 +8,10 @@ OUT=$R/gpurun_out/$TAG; mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_parity.py tests/test_mv_columns.py tests/test_gpu_full_size.py tests/test_gpu_segment_stats.py} \
   -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
-echo "tests rc=$?"; tail -3 "$OUT/gpu_tests.log"
+rc=$?
+echo "tests rc=$rc"; tail -3 "$OUT/gpu_tests.log"
+# a failed or faulted test run ends the GPU work of this call (rc 5: no tests selected is fine)
+if [ $rc -ne 0 ] && [ $rc -ne 5 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
 BENCH="$R/bench.py --no-cpu-baseline --no-check --no-secondary"
 for wl in ${WLS:-range_in bitmap5 adanalytics_exact}; do
