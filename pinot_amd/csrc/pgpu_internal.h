@@ -246,11 +246,12 @@ struct MvLeaf {
 // the query kernel's critical path.
 struct ProgJob {
   int32_t seg;                // query segment
-  int32_t prog_begin, prog_len;  // the original program (its BITS leaves load their words directly: n = -1)
+  int32_t prog_begin, prog_len;  // the original program
   int32_t tile0;              // first tile of this job in the progbits grid
   int32_t ntiles;
-  int32_t pad_;
+  int32_t nbits;              // its BITS leaves' bitmaps (instruction n = slot), loaded together per tile
   uint32_t* out;              // ntiles * 64 words (a workspace bitmap)
+  const uint32_t* bits_w[PGPU_PREBITS];
 };
 
 struct InvLeafX {

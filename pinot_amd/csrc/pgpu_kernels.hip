@@ -1141,6 +1141,13 @@ FI void prebits_load(const TileCtx& t, int begin, int ss_prog_begin, PreBits& pb
   for (int j = 0; j < PGPU_PREBITS; ++j) pb.w[j] = j < nb ? gld((const uint32_t*)cld(&sg->bits_w[j]), wi) : 0u;
 }
 FI void prebits_load(const DocCtx&, int, int, PreBits&) {}
+FI void prebits_load_job(const TileCtx& t, const ProgJob* job, PreBits& pb) {
+  const int nb = job->nbits;
+  const size_t wi = (size_t)(t.doc0 >> 5) + lane_id();
+#pragma unroll
+  for (int j = 0; j < PGPU_PREBITS; ++j) pb.w[j] = j < nb ? gld(job->bits_w[j], wi) : 0u;
+}
+FI void prebits_load_job(const DocCtx&, const ProgJob*, PreBits&) {}
 FI uint32_t bits_leaf(const TileCtx& t, const DevInstr& in, const PreBits& pb) {
   return in.n >= 0 ? pb.get(in.n) : leaf_bits(t, in);
 }
@@ -1148,10 +1155,11 @@ FI uint32_t bits_leaf(const DocCtx& t, const DevInstr& in, const PreBits&) { ret
 
 template <class Ctx>
 FI uint32_t run_program(const DevParams& p, const Cons& cv, int begin, int len, const Ctx& t, int64_t& scanned,
-                        int64_t& dense_bytes, Prof& pf) {
+                        int64_t& dense_bytes, Prof& pf, const ProgJob* job = nullptr) {
   uint32_t* scratch = cv.masks + (p.mask_rows - 1) * 64;
   PreBits pb;
-  prebits_load(t, begin, t.ss->prog_begin, pb);
+  if (job) prebits_load_job(t, job, pb);  // progbits_kernel: the job's leaf bitmaps (bits_w names its output)
+  else prebits_load(t, begin, t.ss->prog_begin, pb);
   int pc = 0;
   while (pc < len) {
     const int64_t tfe = now(pf);
@@ -3667,7 +3675,7 @@ __global__ __launch_bounds__(256) void progbits_kernel(DevParams p, const ProgJo
     }
     int64_t scanned = 0, dense_bytes = 0;
     Prof pf;
-    const uint32_t m = run_program(p, cv, jb.prog_begin, jb.prog_len, t, scanned, dense_bytes, pf);
+    const uint32_t m = run_program(p, cv, jb.prog_begin, jb.prog_len, t, scanned, dense_bytes, pf, &jb);
     jb.out[(size_t)tile * 64 + lane] = m & t.valid;
   }
 }

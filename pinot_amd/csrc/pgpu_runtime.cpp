@@ -2270,9 +2270,9 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       else if (in.op == PGPU_I_SCAN) ok = false;
     }
     if (ok && leaves >= 2 && pk.raw_words + (int64_t)ds.ntiles * 64 <= kInvExpMaxWords) {
-      for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i)
-        if (pk.instrs[i].op == PGPU_I_BITS) pk.instrs[i].n = -1;  // progbits loads each leaf's words itself
       ProgJob jb{};
+      jb.nbits = ds.nbits;  // the leaves keep their slots: progbits loads their words together per tile
+      for (int k = 0; k < ds.nbits; ++k) jb.bits_w[k] = ds.bits_w[k];
       jb.seg = (int32_t)pk.segs.size();
       jb.prog_begin = ds.prog_begin;
       jb.prog_len = ds.prog_len;
@@ -2918,7 +2918,10 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     max_inv_words = std::max<int64_t>(max_inv_words, x.words);
   }
   memcpy(h + o_inv, pk.invx.data(), pk.invx.size() * sizeof(InvLeafX));
-  for (ProgJob& jb : pk.jobs) jb.out = (uint32_t*)ws->rawbits.p + (intptr_t)jb.out;
+  for (ProgJob& jb : pk.jobs) {
+    jb.out = (uint32_t*)ws->rawbits.p + (intptr_t)jb.out;
+    for (int k = 0; k < jb.nbits; ++k) jb.bits_w[k] = (const uint32_t*)ws->rawbits.p + (intptr_t)jb.bits_w[k];
+  }
   memcpy(h + o_jobs, pk.jobs.data(), pk.jobs.size() * sizeof(ProgJob));
   memcpy(h + o_invids, pk.invids.data(), pk.invids.size() * 4);
   memcpy(h + o_mvset, pk.mvsets.data(), pk.mvsets.size() * 4);
