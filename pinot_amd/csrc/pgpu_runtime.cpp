@@ -2257,10 +2257,14 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   // An index-only dense program of several leaves (bitmap / expanded-bitmap / sorted, AND / OR / NOT) is evaluated
   // once per query for all of the segment's tiles (progbits_kernel) into a match bitmap; the query kernels then
   // read one word per lane and tile (DevSeg::single_bits).  Config 3: the interpreter's per-tile instruction
-  // fetches and leaf loads were half of the query kernel.  PGPU_NO_PROGBITS=1 keeps the interpreter.
-  static const bool no_progbits = getenv("PGPU_NO_PROGBITS") && atoi(getenv("PGPU_NO_PROGBITS")) != 0;
+  // fetches and leaf loads were half of the query kernel.
+  // Opt-in (PGPU_PROGBITS=1): measured slower on config 3 -- progbits_kernel 1.78 ms plus the query kernel's 0.92 ms
+  // against 1.60 ms for the query kernel interpreting the program itself (the per-tile interpreter, not the leaf
+  // loads, is the cost, and it moves with the program).
+  const char* pbe = getenv("PGPU_PROGBITS");  // read per plan: tests switch it within one process
+  const bool progbits = pbe && atoi(pbe) != 0;
   ds.single_bits = 0;
-  if (!no_progbits && ds.fast == 0 && ds.rprog_len == 0 && ds.prog_len > 1 && ds.ntiles > 0) {
+  if (progbits && ds.fast == 0 && ds.rprog_len == 0 && ds.prog_len > 1 && ds.ntiles > 0) {
     int leaves = 0;
     bool ok = true;
     for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {

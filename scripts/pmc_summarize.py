@@ -8,6 +8,7 @@ its known byte count (the kernel's own dense-byte count, bench.py bytes_breakdow
   python scripts/pmc_summarize.py <tag> [workload]
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -22,9 +23,12 @@ TIMED = ("rawpred_kernel", "mvpred_kernel", "invexp_kernel", "progbits_kernel", 
 
 
 def _base(name: str) -> str:
-    n = name.split("(")[0]
-    n = n.split("<")[0]
-    return n.split("::")[-1].strip()
+    """The kernel's own identifier in a demangled name ("void (anonymous namespace)::part_scan_kernel<false>(DevParams)"
+    -> "part_scan_kernel")."""
+    for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_]*)(?:<[^()]*>)?\(", name):
+        if m.group(1) not in ("anonymous", "void"):
+            return m.group(1)
+    return name
 
 
 def _is_timed(name: str) -> bool:
@@ -76,7 +80,10 @@ def main():
     if os.path.exists(cal_csv):
         cal_fetch, _ = per_launch(cal_csv)
         b = bench_json(os.path.join(src, "pmc_cal.log"))
-        known = b["roofline"]["bytes_breakdown"]["dense_stream"] if b else None
+        # the filter stream's known bytes: the kernel's read model (the byte model's full first-leaf stream)
+        rl = b["roofline"] if b else {}
+        known = (rl.get("bytes_read_breakdown") or {}).get("dense_stream") or \
+            (rl.get("bytes_breakdown") or {}).get("forward_full")
         if known:
             factor = known / cal_fetch
             cal = {"workload": "adanalytics_count", "known_stream_bytes": known, "fetch_size_bytes_raw": cal_fetch,

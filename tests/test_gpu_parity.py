@@ -304,9 +304,14 @@ def test_value_types_vs_oracle(gpu_ctx, types, qi):
             g.release()
 
 
+@pytest.mark.parametrize("progbits", [False, True], ids=["interp", "progbits"])
 @pytest.mark.parametrize("qi", [1, 3, 4, 9])
-def test_inverted_leaves_vs_oracle(gpu_ctx, qi):
-    """The same queries with inverted indexes loaded: EQ/IN/NOT IN/NEQ leaves become Roaring bitmap ORs."""
+def test_inverted_leaves_vs_oracle(gpu_ctx, monkeypatch, qi, progbits):
+    """The same queries with inverted indexes loaded: EQ/IN/NOT IN/NEQ leaves become Roaring bitmap ORs -- the
+    index-only programs interpreted per tile, or precomputed per query into one match bitmap (PGPU_PROGBITS=1,
+    progbits_kernel)."""
+    if progbits:
+        monkeypatch.setenv("PGPU_PROGBITS", "1")
     rng = np.random.default_rng(5)
     segs = [_random_segment(rng, 150_001, f"i{i}", inverted=["a", "b", "d", "e", "g"]) for i in range(2)]
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
