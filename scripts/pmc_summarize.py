@@ -110,7 +110,13 @@ def main():
     for extra in ("pmc_lds", "pmc_sq"):  # optional SQ counter passes, copied beside the summary
         d = os.path.join(src, extra)
         if os.path.isdir(d):
-            shutil.copy(os.path.join(d, "run_counter_collection.csv"), os.path.join(dst, f"{extra}_{wl}.csv"))
+            rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
+            keep = [r for r in rows if _is_timed(r["Kernel_Name"])]  # the query's kernels only
+            if keep:
+                with open(os.path.join(dst, f"{extra}_{wl}.csv"), "w", newline="") as o:
+                    wr = csv.DictWriter(o, fieldnames=list(keep[0].keys()))
+                    wr.writeheader()
+                    wr.writerows(keep)
 
 
 if __name__ == "__main__":
