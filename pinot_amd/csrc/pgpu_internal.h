@@ -377,8 +377,6 @@ struct DevParams {
   int32_t ldict;                  // 1: pdict copied whole; 2: its frame-of-reference image pfor (PGPU_FOR_*)
   uint32_t pdict_n;               // pdict entries
   const uint32_t* pfor;           // ldict 2: int32 base per 32-id block, then for_bits-bit offsets packed LSB-first
-  int64_t p2vmax;                 // ldict 2: the largest dictionary value when none is negative, else 0 (packed
-                                  // count + SUM cells in phase 2, part_reduce_kernel)
   int32_t for_bits;
   int32_t for_nblk;
   uint32_t cancel_gen;            // this launch's generation (see cancel)

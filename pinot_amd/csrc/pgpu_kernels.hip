@@ -3431,27 +3431,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       }
     }
     for (uint32_t i = threadIdx.x; i < (uint32_t)(fnblk * (1 + fbits) + 1); i += blockDim.x) fimg[i] = gld(p.pfor, i);
-    // packed cells: the first SUM section holds count << 42 | sum, one LDS atomic per record instead of two, when
-    // this workgroup's records n and the values bound both fields (n < 2^22, n * vmax < 2^42)
-    int spk = -1;
-#pragma unroll
-    for (int s = NS - 1; s >= 0; --s)
-      if (op[s] == PGPU_RED_SUM_I64) spk = s;
-    // (this workgroup's record count is summed in the packed section's first cell, zeroed above, then reset)
     __syncthreads();
-    unsigned long long nrec = 1ull << 62;
-    if (p.p2vmax > 0 && spk >= 0) {
-      unsigned long long* c0 = (unsigned long long*)(base + soff[spk]);
-      unsigned long long mine = 0;
-      for (int w = w0 + (int)threadIdx.x; w < w1; w += blockDim.x) mine += p.rcount[(size_t)q * nwg + w];
-      if (mine) atomicAdd(c0, mine);
-      __syncthreads();
-      nrec = *c0;
-      __syncthreads();
-      if (threadIdx.x == 0) *c0 = 0ull;
-    }
-    __syncthreads();
-    const bool pack = nrec < (1ull << 22) && (unsigned long long)p.p2vmax * nrec < (1ull << 42);
     const int idbits = p.rec_idbits;
     const uint32_t idmask = (1u << idbits) - 1u;
     constexpr int R = 16;
@@ -3470,20 +3450,17 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
           k[r] = v >> idbits;
           id[r] = v & idmask;
         }
-        if (!pack) {
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (ok[r]) atomicAdd(&cnt[k[r]], 1u);
-        }
+        for (int r = 0; r < R; ++r)
+          if (ok[r]) atomicAdd(&cnt[k[r]], 1u);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
             unsigned long long* sec = (unsigned long long*)(base + soff[s]);
-            const unsigned long long one = pack && s == spk ? (1ull << 42) : 0ull;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               if (!ok[r]) continue;
-              atomicAdd(&sec[k[r]], one + (unsigned long long)(int64_t)(int32_t)for_value(fimg, fnblk, fbits, id[r]));
+              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)for_value(fimg, fnblk, fbits, id[r]));
             }
           } else {
             uint32_t* sec = (uint32_t*)(base + soff[s]);
@@ -3499,15 +3476,11 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
     }
     __syncthreads();
     for (uint32_t kk = threadIdx.x; kk < nk; kk += blockDim.x) {
-      const uint64_t pk = pack ? ((const uint64_t*)(base + soff[spk]))[kk] : 0ull;
-      const uint32_t nkey = pack ? (uint32_t)(pk >> 42) : cnt[kk];
-      if (nkey == 0u) continue;
+      if (cnt[kk] == 0u) continue;
       for (int s = 0; s <= NS; ++s) {
         int64_t v;
         if (s == 0) {
-          v = (int64_t)nkey;
-        } else if (pack && s - 1 == spk) {
-          v = (int64_t)(pk & ((1ull << 42) - 1ull));
+          v = (int64_t)cnt[kk];
         } else if (op[s - 1] == PGPU_RED_SUM_I64 || op[s - 1] == PGPU_RED_SUM_F64) {
           v = ((const int64_t*)(base + soff[s - 1]))[kk];
         } else {  // id -> cell key of its value

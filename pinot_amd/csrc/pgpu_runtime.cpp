@@ -2811,16 +2811,6 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.pfor = for_h ? (const uint32_t*)for_h->for_dev.p : nullptr;
     p.for_bits = for_h ? for_h->for_bits : 0;
     p.for_nblk = for_h ? for_h->for_nblk : 0;
-    // phase 2 packs each key's count and SUM into one 64-bit LDS cell when the values are non-negative (the sorted
-    // dictionary's first value) and small enough; PGPU_NO_P2PACK=1 keeps separate cells
-    static const bool no_p2pack = getenv("PGPU_NO_P2PACK") && atoi(getenv("PGPU_NO_P2PACK")) != 0;
-    p.p2vmax = 0;
-    if (for_h && !no_p2pack && for_h->hdict.size() >= 4 && for_h->dict_card > 0) {
-      int32_t lo, hi;
-      memcpy(&lo, for_h->hdict.data(), 4);
-      memcpy(&hi, for_h->hdict.data() + 4 * (size_t)(for_h->dict_card - 1), 4);
-      if (lo >= 0) p.p2vmax = std::max<int64_t>(1, hi);
-    }
     p.pcol = pcol;
     p.rw = part_rw;
     p.rec_idbits = part_idbits;
