@@ -160,11 +160,7 @@ struct DevSeg {
   int32_t nvstage;
   int32_t vstage_col[2];
   int32_t vstage_off[2];
-  // the dense program's BITS-leaf bitmaps (bits_w[0, nbstage)) DMA'd with the tile like a 1-bit plane (a bitmap's
-  // words of tile t are its 256 bytes at t * 256), so the self-loading kernel reads them from the slot
-  int32_t nbstage;
-  int32_t bstage_off[PGPU_PREBITS];
-  int32_t pad4_;
+  int32_t pad3_;
 };
 #define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 

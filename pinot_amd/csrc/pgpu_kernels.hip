@@ -814,7 +814,7 @@ FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
   sc.instrs = cld(&sg->stage_instrs);
   sc.lin = cld(&sg->stage_sliced);
   const DevColumn* cols = p.cols + cld(&sg->col_begin);
-  const int nv = cld(&sg->nvstage), nbs = cld(&sg->nbstage);
+  const int nv = cld(&sg->nvstage);
 #pragma unroll
   for (int j = 0; j < PGPU_MAX_STAGE; ++j) {
     if (j < sc.nst) {
@@ -828,18 +828,13 @@ FI void load_stage(const DevParams& p, int seg, StageCache& sc) {
       sc.bits[j] = cld(&cols[qc].vbits);
       sc.off[j] = cld(&sg->vstage_off[j - sc.nst]);
       sc.lin |= 1 << j;
-    } else if (j < sc.nst + nv + nbs) {  // BITS-leaf bitmaps: one 256-B row per tile
-      sc.fwd[j] = (const char*)cld(&sg->bits_w[j - sc.nst - nv]);
-      sc.bits[j] = 1;
-      sc.off[j] = cld(&sg->bstage_off[j - sc.nst - nv]);
-      sc.lin |= 1 << j;
     } else {
       sc.fwd[j] = nullptr;
       sc.bits[j] = 0;
       sc.off[j] = 0;
     }
   }
-  sc.nst += nv + nbs;
+  sc.nst += nv;
 }
 
 // DMA the staged columns of one tile into `slot` (16 B per lane, 1 KiB per instruction; widths that are multiples
@@ -957,7 +952,6 @@ struct SegState {
   int32_t track;  // HASH: distinct-key bitmap row + 1 (0 = not counted)
   int32_t single_bits;  // DevSeg::single_bits
   int32_t nvstage;      // DevSeg::nvstage
-  int32_t nbstage;      // DevSeg::nbstage
   const DevColumn* cols;
   const int32_t* const* remaps;
   int32_t num_docs, nstage, prog_begin, prog_len, rprog_begin, rprog_len, agg_mode, nreg, reg_col0, reg_col1;
@@ -994,7 +988,6 @@ FI void load_seg(const DevParams& p, int seg, SegState& ss) {
   ss.track = cld(&sg->track);
   ss.single_bits = cld(&sg->single_bits);
   ss.nvstage = cld(&sg->nvstage);
-  ss.nbstage = cld(&sg->nbstage);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     ss.f_bits[j] = ss.f_off[j] = ss.f_kind[j] = ss.f_neg[j] = 0;
@@ -1142,13 +1135,6 @@ struct PreBits {
 };
 FI void prebits_load(const TileCtx& t, int begin, int ss_prog_begin, PreBits& pb) {
   const DevSeg* sg = t.ss->sg;
-  if (t.slot && t.ss->nbstage > 0 && begin == ss_prog_begin) {  // DMA'd with the tile (DevSeg::nbstage)
-    const int nbs = t.ss->nbstage;
-#pragma unroll
-    for (int j = 0; j < PGPU_PREBITS; ++j)
-      pb.w[j] = j < nbs ? ((const uint32_t*)(t.slot + cld(&sg->bstage_off[j])))[lane_id()] : 0u;
-    return;
-  }
   const int nb = begin == ss_prog_begin ? cld(&sg->nbits) : 0;
   const size_t wi = (size_t)(t.doc0 >> 5) + lane_id();
 #pragma unroll
@@ -2444,7 +2430,7 @@ FI Stats direct_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int
       }
       const int64_t tw = now(pf);
       // this tile's DMAs have landed (later tiles' may be in flight)
-      if (ss.nstage + ss.nvstage + ss.nbstage > 0) wait_vmcnt(next_instrs);
+      if (ss.nstage + ss.nvstage > 0) wait_vmcnt(next_instrs);
       PROF_ADD(pf, PGPU_P_C_FULL, tw);
       const int64_t tf = now(pf);
 #ifdef PGPU_PROFILE_BUILD

@@ -2243,21 +2243,6 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       ds.stage_instrs += vinstrs;
     }
   }
-  // BITS-leaf bitmaps of the dense program DMA'd with the tile (DevSeg::nbstage): an index-only program then starts
-  // from the slot instead of waiting one load round trip per tile.  PGPU_NO_BSTAGE=1 loads them per tile.
-  static const bool no_bstage = getenv("PGPU_NO_BSTAGE") && atoi(getenv("PGPU_NO_BSTAGE")) != 0;
-  ds.nbstage = 0;
-  if (!no_bstage && ds.fast == 0 && ds.prog_len > 0 && ds.nbits > 0 &&
-      (int)staged.size() + ds.nvstage + ds.nbits <= PGPU_MAX_STAGE && ds.stage_instrs + ds.nbits <= PGPU_MAX_STAGE_INSTRS &&
-      off + 256 * ds.nbits <= kMaxSlotBytes) {
-    for (int j = 0; j < ds.nbits; ++j) {
-      ds.bstage_off[j] = off;
-      off += 256;
-      tb += 256;
-    }
-    ds.nbstage = ds.nbits;
-    ds.stage_instrs += ds.nbits;  // one 256-B DMA (16 lanes x 16 B) per bitmap
-  }
   pk.slot_bytes = std::max(pk.slot_bytes, off);
   pk.max_instrs = std::max(pk.max_instrs, ds.stage_instrs);
   pk.tile_bytes = std::max(pk.tile_bytes, tb);
@@ -2318,8 +2303,6 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
       ds.nbits = 1;
       ds.bits_w[0] = jb.out;
       ds.single_bits = 1;
-      ds.stage_instrs -= ds.nbstage;  // (the staged bitmaps were the original leaves')
-      ds.nbstage = 0;
     }
   }
   return PGPU_OK;
@@ -2655,8 +2638,6 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       for (int j = 0; j < ds.nvstage; ++j)  // (the ring loaders stage filter columns only)
         ds.stage_instrs -= (pk.cols[ds.col_begin + ds.vstage_col[j]].vbits + 3) / 4;
       ds.nvstage = 0;
-      ds.stage_instrs -= ds.nbstage;
-      ds.nbstage = 0;
     }
   // one-word PART records (in-partition key, dict id) when every segment holds the same dictionary for the
   // aggregated column (the common case of one table's segments sharing value sets): half the record traffic
