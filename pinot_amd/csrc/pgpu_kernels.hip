@@ -3815,7 +3815,11 @@ FI uint32_t fsm_sliced(const uint32_t* sl, int bits, int tile, const DevInstr& i
   return m;
 }
 
-__global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t* fn) {
+// S2: every segment's filter is an AND of exactly two bit-sliced leaves (the runtime checks fsm_sliced_ok on each),
+// so the generic leaf path is compiled out and the kernel fits four waves per SIMD; the general build needs ~226
+// VGPRs (two waves).
+template <bool S2>
+__global__ __launch_bounds__(256, S2 ? 4 : 1) void andfsm_tile_kernel(DevParams p, uint32_t* fn) {
   // each wave walks a contiguous run of tiles (XCD-aware workgroup order), so the segment's state and leaf
   // instructions are loaded once per segment rather than once per tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3836,7 +3840,7 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
   if (c.seg != cseg) {
     cseg = c.seg;
     load_seg(p, cseg, ss);
-    k = cld(&ss.sg->leaf_len);
+    k = S2 ? 2 : cld(&ss.sg->leaf_len);
     leaf_begin = cld(&ss.sg->leaf_begin);
     sl0 = sl1 = false;
     if (k > 0) {
@@ -3872,7 +3876,7 @@ __global__ __launch_bounds__(256) void andfsm_tile_kernel(DevParams p, uint32_t*
   if (sl0) m[0] = fsm_eval_planes(x0, in0) & t.valid;
   if (sl1) m[1] = fsm_eval_planes(x1, in1) & t.valid;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < (S2 ? 0 : 4); ++j) {
     if (j >= k) break;
     if ((j == 0 && sl0) || (j == 1 && sl1)) continue;
     const DevInstr in = cld(p.instrs + cld(p.pool, leaf_begin + j));
@@ -4598,10 +4602,13 @@ hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st) {
+hipError_t pgpu_launch_andfsm(const DevParams& p, bool s2, uint32_t* fn, int64_t* out, hipStream_t st) {
   if (p.nseg <= 0) return hipSuccess;
-  if (p.total_tiles > 0)  // ~8 workgroups per CU, each wave over a contiguous run of tiles
-    hipLaunchKernelGGL(andfsm_tile_kernel, dim3(std::min(2048, (p.total_tiles + 3) / 4)), dim3(256), 0, st, p, fn);
+  if (p.total_tiles > 0) {  // ~8 workgroups per CU, each wave over a contiguous run of tiles
+    const dim3 g(std::min(2048, (p.total_tiles + 3) / 4));
+    if (s2) hipLaunchKernelGGL(andfsm_tile_kernel<true>, g, dim3(256), 0, st, p, fn);
+    else hipLaunchKernelGGL(andfsm_tile_kernel<false>, g, dim3(256), 0, st, p, fn);
+  }
   hipLaunchKernelGGL(andfsm_segment_kernel, dim3(p.nseg), dim3(256), 0, st, p, (const uint32_t*)fn, out);
   return hipGetLastError();
 }

@@ -52,7 +52,7 @@ hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, 
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st);
 hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njobs, int total, hipStream_t st);
-hipError_t pgpu_launch_andfsm(const DevParams& p, uint32_t* fn, int64_t* out, hipStream_t st);
+hipError_t pgpu_launch_andfsm(const DevParams& p, bool s2, uint32_t* fn, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
@@ -1349,6 +1349,7 @@ struct Packer {
   std::vector<int32_t> tracked;  // HASH: query segments whose distinct keys are counted (bitmap row order)
   int64_t leaf_words = 0;        // PGPU_Q_EXACT_FILTER_STATS: 32-bit words of all leaf bitmaps
   bool fsm = false;              // ... computed on the GPU by the andfsm kernels (every segment fsm_filter)
+  bool fsm_s2 = false;           // ... by its two-sliced-leaf build
   // raw-value leaves: until launch, RawLeaf::out holds the bitmap's word offset in Workspace::rawbits and
   // RawLeaf::vals its set's offset in rawvals; PGPU_I_BITS instructions (bits_instrs) hold the word offset in fwd
   std::vector<RawLeaf> raws;
@@ -2450,6 +2451,19 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
     if (fsm) {
       pk.fsm = true;
       pk.leaf_words = 0;  // no leaf bitmaps, no host replay
+      // the lean andfsm build: every segment an AND of two leaves, both read from bit planes (fsm_sliced_ok)
+      pk.fsm_s2 = true;
+      for (int s = 0; s < q->num_segments && pk.fsm_s2; ++s) {
+        const DevSeg& ds = pk.segs[s];
+        pk.fsm_s2 = ds.leaf_len == 2;
+        for (int j = 0; j < 2 && pk.fsm_s2; ++j) {
+          const DevInstr& in = pk.instrs[pk.pool[ds.leaf_begin + j]];
+          const DevColumn& c = pk.cols[ds.col_begin + in.col];
+          pk.fsm_s2 = in.op == PGPU_I_SCAN && in.kind == PGPU_COL_FIXED_BIT && c.sliced && in.bits >= 1 &&
+                      in.bits <= 24 &&
+                      (in.pred == 0 || in.pred == 3 || (in.pred == 2 && in.n >= 1 && in.n <= 4));  // RANGE MASK LIST
+        }
+      }
     }
   }
   return PGPU_OK;
@@ -2994,7 +3008,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess && pk.fsm) {
     void* h_ent_dev = nullptr;
     e = hipHostGetDevicePointer(&h_ent_dev, ws->h_fsment.p, 0);
-    if (e == hipSuccess) e = pgpu_launch_andfsm(p, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
+    if (e == hipSuccess) e = pgpu_launch_andfsm(p, pk.fsm_s2, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
   }
   if (e == hipSuccess && pk.leaf_words > 0) {
     e = pgpu_launch_leafbits(p, st);

@@ -84,3 +84,14 @@ def test_direct_kernels_fit_their_occupancy(res):
     for k, v in ks.items():
         assert v["private_segment_fixed_size"] == 0, (k, v)
         assert v["vgpr_count"] <= (96 if _mode(k) in (2, 4) else 128), (k, v)
+
+
+def test_andfsm_kernels_do_not_spill(res):
+    """The exact-filter-statistics transducer: no scratch in either build, and the two-sliced-leaf build (ILb1E) keeps
+    four waves per SIMD."""
+    ks = {k: v for k, v in res.items() if "andfsm_tile_kernel" in k}
+    assert len(ks) == 2
+    for k, v in ks.items():
+        assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (k, v)
+        if "ILb1E" in k:
+            assert v["vgpr_count"] <= 128, (k, v)
