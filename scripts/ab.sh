@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing of bench workloads under env knobs (kernel HIP-event ms and ms/step), plus the phase counters of the
-# profiling build.  Usage: r4_ab.sh <tag> "<workloads>" "<knob-set-1>" "<knob-set-2>" ...   (a knob set: "A=1 B=2"
+# profiling build.  Usage: ab.sh <tag> "<workloads>" "<knob-set-1>" "<knob-set-2>" ...   (a knob set: "A=1 B=2"
 # or "-" for none)
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"

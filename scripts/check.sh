@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU check: the parity suites touched this round, then rocprof kernel stats of the bench workloads named in
-# $WLS (default: the sliced-aggregation ones).  Usage: r4_check.sh <tag>
+# GPU check: the parity suites touched this round, then rocprof kernel stats of the bench workloads named in
+# $WLS (default: the sliced-aggregation ones).  Usage: check.sh <tag>
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 closing check on the GPU box: the whole -m gpu suite, then the default bench run (N = 1, headline +
+# Closing check on the GPU box: the whole -m gpu suite, then the default bench run (N = 1, headline +
 # secondary workloads with CPU baselines and full-size parity).  Stops after a failed test run.
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"

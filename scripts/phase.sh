@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-wave phase counters (libpinotgpu_prof.so, PGPU_PROFILE=1) of bench workloads, each with and without an env
-# knob.  Usage: r4_phase.sh <tag> "<workloads>" "<KNOB=value>"
+# knob.  Usage: phase.sh <tag> "<workloads>" "<KNOB=value>"
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1; WLS=$2; KNOB=${3:-}

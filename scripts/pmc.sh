@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-4 HBM-traffic profile of bench workloads: kernel-trace stats, FETCH_SIZE and WRITE_SIZE passes (one TCC
+# HBM-traffic profile of bench workloads: kernel-trace stats, FETCH_SIZE and WRITE_SIZE passes (one TCC
 # counter per pass), the FETCH_SIZE calibration pass on config 5's filter stream when adanalytics is listed, and
 # with LDS=1 an SQ pass of LDS counters.  Summaries: python scripts/pmc_summarize.py <tag>_<wl> <wl>.
-# Usage: r4_pmc.sh <tag> "<workloads>"
+# Usage: pmc.sh <tag> "<workloads>"
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1; WLS=$2

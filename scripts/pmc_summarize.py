@@ -1,4 +1,4 @@
-"""Summarise a profile_round.sh run into profiles/<tag>/ and profiles/pmc_<workload>.json.
+"""Summarise a scripts/pmc.sh run (its gpurun_out/<tag>_<workload>) into profiles/<tag>/ and profiles/pmc_<workload>.json.
 
 HBM bytes per query-kernel launch = c x FETCH_SIZE + WRITE_SIZE (KiB counters).  MI355X_MICROARCH.md "HBM": FETCH_SIZE
 reads exactly half the bytes of a 16-B/lane streaming read (c = 2 there) and other access widths are uncalibrated --
