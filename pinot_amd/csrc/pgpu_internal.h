@@ -407,6 +407,7 @@ struct DevParams {
   int32_t rd_planes;              // register-direct: planes per tile held in VGPRs (>= every leaf's width; 8/10/12/16)
   int32_t mv_gmask;               // bit g: group column g is multi-value (sparse_agg_mv expands each doc's values)
   int32_t rd_pfx;                 // register-direct: prefix planes of every segment's residual leaf (0 or PGPU_PFX_PLANES)
+  int32_t rs_vplanes;             // register streaming (direct == 3): value planes held per tile (16 or 24)
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

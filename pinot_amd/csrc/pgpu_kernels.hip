@@ -2810,6 +2810,230 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevP
   direct_epilogue<MODE>(p, L, st, wave, lane, pf);
 }
 
+// ================================================================================================================
+// REGISTER STREAMING (p.direct == 3, aggregation-only mode): every segment's filter is an AND of two bit-sliced fast
+// leaves -- one of <= 16 bits ("wide"), one of <= PN bits ("narrow") -- and every aggregation is answered from one
+// column's value planes (PGPU_AM_SLICED, no residual program).  All three plane sets of a tile stream into VGPRs
+// RD tiles ahead, so the aggregation reads registers that were loaded with the filter planes: no LDS slot, no
+// candidate queue, and no plain load issued behind a later one (vmcnt retires in order) -- one coalesced read of
+// (wide + narrow + value) planes per tile, the shape tools/stream_bench.hip reads at 5.6-6.0 TB/s.  The value
+// planes of a tile without a match are read too: the planner chose SLICED because nearly every line holds one.
+// ================================================================================================================
+struct RsIssue {
+  const uint32_t* sw;  // the wide leaf's planes (bw per tile), the narrow leaf's, the value column's
+  const uint32_t* sn;
+  const uint32_t* sv;
+  int bw, bn, vb;
+};
+// Leaf j of the segment's fast program (its instruction's query column).
+FI int rs_leaf_col(const DevParams& p, const DevSeg* sg, int j) {
+  return cld(&p.instrs[cld(&sg->prog_begin) + cld(&sg->fast_ins[j])].col);
+}
+FI void rs_load_issue(const DevParams& p, int seg, int vcol, RsIssue& is) {
+  const DevSeg* sg = p.segs + seg;
+  const DevColumn* cols = p.cols + cld(&sg->col_begin);
+  const int c0 = rs_leaf_col(p, sg, 0), c1 = rs_leaf_col(p, sg, 1);
+  const int b0 = cld(&cols[c0].bits), b1 = cld(&cols[c1].bits);
+  const bool w0 = b0 >= b1;  // (rstream_consumer makes the same choice)
+  is.sw = (const uint32_t*)cld(&cols[w0 ? c0 : c1].sliced);
+  is.sn = (const uint32_t*)cld(&cols[w0 ? c1 : c0].sliced);
+  is.bw = w0 ? b0 : b1;
+  is.bn = w0 ? b1 : b0;
+  is.sv = (const uint32_t*)cld(&cols[vcol].vsliced);
+  is.vb = cld(&cols[vcol].vbits);
+}
+template <int PL>
+FI void rs_load_planes(const uint32_t* sl, int bits, int tile_in_seg, uint32_t (&x)[PL]) {
+  const uint32_t* src = sl + (size_t)tile_in_seg * bits * 64 + lane_id();
+#pragma unroll
+  for (int k = 0; k < PL; ++k) x[k] = k < bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;
+}
+// Fast leaf j on register planes: OR of its dict-id ranges, then its negation (fast_filter's sliced branch).
+template <int PL>
+FI uint32_t rs_leaf(const SegState& ss, int j, const uint32_t (&x)[PL]) {
+  uint32_t m = rd_lt(x, j ? ss.f_r0hi[1] : ss.f_r0hi[0]) & ~rd_lt(x, j ? ss.f_r0lo[1] : ss.f_r0lo[0]);
+  const int nr = j ? ss.f_nr[1] : ss.f_nr[0];
+  for (int r = 1; r < nr; ++r) {
+    const uint32_t lo = cld(&ss.sg->f_rng[j][r][0]), hi = cld(&ss.sg->f_rng[j][r][1]);
+    m |= rd_lt(x, hi) & ~rd_lt(x, lo);
+  }
+  return (j ? ss.f_sneg[1] : ss.f_sneg[0]) ? ~m : m;
+}
+// The matched docs' aggregations from the value planes (bsi_fold with the segment's width and offset cached).
+template <int NV>
+FI void rs_fold(const DevParams& p, const Cons& cv, LaneAcc& la, const uint32_t (&x)[NV], uint32_t mm, int vb,
+                int64_t vmin) {
+  for (int a = 0; a < p.nagg; ++a) {
+    if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+    const int32_t op = p.aggs[a].op;
+    int64_t part;
+    if (op == PGPU_RED_SUM_I64) {
+      uint32_t u = 0;  // < 32 * 2^24
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        if (k < vb) u += (uint32_t)__popc(x[k] & mm) << k;
+      part = (int64_t)u + (int64_t)__popc(mm) * vmin;
+    } else {
+      const bool mx = op == PGPU_RED_MAX_I64;
+      uint32_t cand = mm, u = 0;
+#pragma unroll
+      for (int k = NV - 1; k >= 0; --k) {
+        if (k >= vb) continue;
+        const uint32_t t = cand & (mx ? x[k] : ~x[k]);
+        if (t) cand = t;
+        if ((t != 0) == mx) u |= 1u << k;
+      }
+      part = mm ? vmin + (int64_t)u : sec_identity(op);
+    }
+    lacc_add(la, cv, a, op, part);
+  }
+}
+
+template <int PN, int NV>
+FI Stats rstream_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH, PW = 16;
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  if (lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, scanned = 0, dense_bytes = 0;
+  uint32_t lane_scanned = 0, lane_matched = 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int vcol = 0;  // the one value column (runtime: every non-COUNT aggregation reads it)
+  for (int a = 0; a < p.nagg; ++a)
+    if (p.aggs[a].fn != PGPU_AGG_COUNT) vcol = p.aggs[a].col;
+  SegState ss;
+  int cseg = -1, jw = 0, vb = 0;
+  int64_t vmin = 0, vbytes = 0;
+  if (cidx < ntiles) {
+    const int own = (ntiles - cidx + NW - 1) / NW;  // this wave's tiles: cidx, cidx + NW, ...
+    Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
+    RsIssue is;
+    rs_load_issue(p, ci.seg, vcol, is);
+    uint32_t xw[RD][PW], xn[RD][PN], xv[RD][NV];
+#pragma unroll
+    for (int s = 0; s < RD; ++s) {
+      if (s < own) {
+        if (s > 0 && cursor_advance(p, ci, NW)) rs_load_issue(p, ci.seg, vcol, is);
+        rs_load_planes(is.sw, is.bw, ci.tile_in_seg, xw[s]);
+        rs_load_planes(is.sn, is.bn, ci.tile_in_seg, xn[s]);
+        rs_load_planes(is.sv, is.vb, ci.tile_in_seg, xv[s]);
+      }
+    }
+    int poll = p.cancel_poll;
+    bool stop = false;
+    for (int k0 = 0; k0 < own && !stop; k0 += RD) {
+#pragma unroll
+      for (int s = 0; s < RD; ++s) {
+        const int k = k0 + s;
+        if (k >= own || stop) break;
+        if (--poll == 0) {
+          poll = p.cancel_poll;
+          if (query_cancelled(p)) {
+            stop = true;
+            break;
+          }
+        }
+        if (k > 0) cursor_advance(p, cur, NW);
+        if (cur.seg != cseg) {
+          cseg = cur.seg;
+          load_seg(p, cseg, ss);
+          jw = cld(&ss.cols[rs_leaf_col(p, ss.sg, 0)].bits) >= cld(&ss.cols[rs_leaf_col(p, ss.sg, 1)].bits) ? 0 : 1;
+          vb = cld(&ss.cols[vcol].vbits);
+          vmin = cld(&ss.cols[vcol].vmin);
+          vbytes = 0;  // the aggregated columns' planes per matched tile (direct_candidates' dense-bytes model)
+          for (int a = 0; a < p.nagg; ++a)
+            if (p.aggs[a].fn != PGPU_AGG_COUNT) vbytes += (int64_t)WT * vb / 8;
+        }
+        const int64_t tf = now(pf);
+#ifdef PGPU_PROFILE_BUILD
+        if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+#endif
+        const int doc0 = cur.tile_in_seg * WT;
+        uint32_t valid;
+        {
+          const int ndocs = min(WT, ss.num_docs - doc0);
+          const int rem = ndocs - 32 * lane;
+          valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * (ss.f_bits[0] + ss.f_bits[1]) + 7) / 8;
+        }
+        // the AND in program order for the scanned-entries count: leaf 0 reads every doc, leaf 1 leaf 0's matches
+        const uint32_t mw = rs_leaf(ss, jw, xw[s]), mn = rs_leaf(ss, 1 - jw, xn[s]);
+        const uint32_t m0 = valid & (jw == 0 ? mw : mn);
+        if (!(ss.f_kind[0] >> 8)) lane_scanned += __popc(valid);
+        if (!(ss.f_kind[1] >> 8)) lane_scanned += __popc(m0);
+        const uint32_t mm = m0 & mw & mn;
+        PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+        const int64_t ta = now(pf);
+        lane_matched += __popc(mm);
+        const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
+        mark_seg(p, ss, any);
+        if (any) {
+          rs_fold<NV>(p, cv, la, xv[s], mm, vb, vmin);
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += vbytes;
+        }
+        PROF_ADD(pf, PGPU_P_C_AGG, ta);
+        // refill this register slot with the tile RD ahead (its loads overlap the next tile's work)
+        if (k + RD < own) {
+          if (cursor_advance(p, ci, NW)) rs_load_issue(p, ci.seg, vcol, is);
+          rs_load_planes(is.sw, is.bw, ci.tile_in_seg, xw[s]);
+          rs_load_planes(is.sn, is.bn, ci.tile_in_seg, xn[s]);
+          rs_load_planes(is.sv, is.vb, ci.tile_in_seg, xv[s]);
+        }
+      }
+    }
+  }
+  {
+    const int64_t ls = wave_sum_i64((int64_t)lane_scanned), lm = wave_sum_i64((int64_t)lane_matched);
+    if (lane == 0) {
+      scanned += ls;
+      matched += lm;
+    }
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+#pragma unroll
+  for (int a = 0; a < NREG_ACC; ++a)
+    if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  Stats st;
+  st.matched = matched;
+  st.scanned = scanned;
+  st.sector_bytes = 0;
+  st.dense_bytes = dense_bytes;
+  return st;
+}
+
+template <int PN, int NV>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rstream(DevParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  __syncthreads();
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const Stats st = rstream_consumer<PN, NV>(p, L, wave, t0, t1 - t0, pf);
+  direct_epilogue<PGPU_MODE_AGG>(p, L, st, wave, lane, pf);
+}
+
 // ---- the query kernel ----------------------------------------------------------------------------------------------
 template <int MODE, int DENSE>
 __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams p) {
@@ -4184,6 +4408,26 @@ static hipError_t rd_attrs(size_t lds_bytes) {
   if (e == hipSuccess && PK == 0) e = rd_attr<M, 16, 0>(lds_bytes);
   return e;
 }
+// register streaming: narrow-leaf planes 4 / 8, value planes 16 / 24
+template <int PN, int NV>
+static hipError_t rs_attr(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void*)query_kernel_rstream<PN, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
+[[maybe_unused]] static hipError_t rs_attrs(size_t lds_bytes) {
+  hipError_t e = rs_attr<4, 16>(lds_bytes);
+  if (e == hipSuccess) e = rs_attr<4, 24>(lds_bytes);
+  if (e == hipSuccess) e = rs_attr<8, 16>(lds_bytes);
+  if (e == hipSuccess) e = rs_attr<8, 24>(lds_bytes);
+  return e;
+}
+[[maybe_unused]] static void rs_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+  const dim3 g(grid), b(PGPU_DIRECT_THREADS);
+  if (p.rd_planes <= 4 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rstream<4, 16>), g, b, dyn_smem, st, p);
+  else if (p.rd_planes <= 4) hipLaunchKernelGGL((query_kernel_rstream<4, 24>), g, b, dyn_smem, st, p);
+  else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rstream<8, 16>), g, b, dyn_smem, st, p);
+  else hipLaunchKernelGGL((query_kernel_rstream<8, 24>), g, b, dyn_smem, st, p);
+}
 // Per aggregation mode (one translation unit each): launch the ring or direct query kernel, set its LDS attribute.
 #define PGPU_MODE_FUNCS(M, NAME)                                                                                  \
   hipError_t pgpu_launch_query_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {          \
@@ -4192,7 +4436,10 @@ static hipError_t rd_attrs(size_t lds_bytes) {
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    if (p.direct == 2) {                                                                                        \
+    if (p.direct == 3) {                                                                                        \
+      if constexpr (M == PGPU_MODE_AGG) rs_launch(p, grid, dyn_smem, st);                                       \
+      else return hipErrorInvalidValue;                                                                         \
+    } else if (p.direct == 2) {                                                                                 \
       if (p.rd_pfx) rd_launch<M, PGPU_PFX_PLANES>(p, grid, dyn_smem, st);                                       \
       else rd_launch<M, 0>(p, grid, dyn_smem, st);                                                              \
     } else                                                                                                      \
@@ -4210,6 +4457,8 @@ static hipError_t rd_attrs(size_t lds_bytes) {
                               (int)lds_bytes);                                                                  \
     if (e == hipSuccess) e = rd_attrs<M, 0>(lds_bytes);                                                         \
     if (e == hipSuccess) e = rd_attrs<M, PGPU_PFX_PLANES>(lds_bytes);                                           \
+    if constexpr (M == PGPU_MODE_AGG)                                                                           \
+      if (e == hipSuccess) e = rs_attrs(lds_bytes);                                                             \
     return e;                                                                                                   \
   }
 #define PGPU_MODE_DECLS(NAME)                                                                   \

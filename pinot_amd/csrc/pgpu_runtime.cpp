@@ -2643,12 +2643,51 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       grid = std::max(1, g);
       dyn = rdyn;
     }
+    // register streaming (query_kernel_rstream): aggregation-only, every segment an AND of two bit-sliced fast
+    // leaves (<= 16 and <= 8 bits) with its aggregations all answered from one column's value planes (<= 24)
+    const bool no_rstream = getenv("PGPU_NO_RSTREAM") && atoi(getenv("PGPU_NO_RSTREAM")) != 0;  // per plan (tests)
+    bool rs = ok && !no_rstream && p.mode == PGPU_MODE_AGG && rdyn <= PGPU_LDS_LIMIT;
+    int vcol = -1, rs_narrow = 1, rs_vb = 1;
+    for (int a = 0; a < p.nagg && rs; ++a) {
+      const DevAgg& ag = p.aggs[a];
+      if (ag.fn == PGPU_AGG_COUNT) continue;
+      rs = (vcol < 0 || vcol == ag.col) && ((ag.op == PGPU_RED_SUM_I64 && ag.part == 0) ||
+                                            ag.op == PGPU_RED_MIN_I64 || ag.op == PGPU_RED_MAX_I64);
+      vcol = ag.col;
+    }
+    rs = rs && vcol >= 0;
+    for (const DevSeg& ds : pk.segs) {
+      if (!rs || !ds.ntiles) continue;
+      rs = ds.nstage == 2 && ds.fast == 2 && ds.stage_sliced == 3 && ds.agg_mode == PGPU_AM_SLICED &&
+           ds.rprog_len == 0 && ds.f_nr[0] > 0 && ds.f_nr[1] > 0;
+      if (!rs) break;
+      const DevColumn& vc = pk.cols[ds.col_begin + vcol];
+      int b[2];
+      for (int j = 0; j < 2; ++j) b[j] = pk.cols[ds.col_begin + pk.instrs[ds.prog_begin + ds.fast_ins[j]].col].bits;
+      rs = vc.vsliced && vc.vbits >= 1 && vc.vbits <= 24 && std::max(b[0], b[1]) <= 16 && std::min(b[0], b[1]) >= 1 &&
+           std::min(b[0], b[1]) <= 8;
+      rs_narrow = std::max(rs_narrow, std::min(b[0], b[1]));
+      rs_vb = std::max(rs_vb, (int)vc.vbits);
+    }
+    if (rs) {
+      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : 3, PGPU_LDS_LIMIT / rdyn);
+      int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
+      if (g >= 8) g &= ~7;
+      p.direct = 3;
+      p.rd_planes = rs_narrow <= 4 ? 4 : 8;
+      p.rs_vplanes = rs_vb <= 16 ? 16 : 24;
+      p.rd_pfx = 0;
+      p.dslots = 0;
+      grid = std::max(1, g);
+      dyn = rdyn;
+    }
   }
-  // sliced aggregation runs in query_kernel_direct only: elsewhere its segments gather per candidate (their staged
-  // aggregation planes are then only extra DMA, never read)
+  // sliced aggregation runs in the self-loading kernels only (query_kernel_direct, and query_kernel_rstream with the
+  // value planes in VGPRs): elsewhere its segments gather per candidate (their staged aggregation planes are then
+  // only extra DMA, never read)
   if (p.direct != 1)
     for (DevSeg& ds : pk.segs) {
-      if (ds.agg_mode == PGPU_AM_SLICED) ds.agg_mode = PGPU_AM_SPARSE;
+      if (ds.agg_mode == PGPU_AM_SLICED && p.direct != 3) ds.agg_mode = PGPU_AM_SPARSE;
       for (int j = 0; j < ds.nvstage; ++j)  // (the ring loaders stage filter columns only)
         ds.stage_instrs -= (pk.cols[ds.col_begin + ds.vstage_col[j]].vbits + 3) / 4;
       ds.nvstage = 0;

@@ -268,6 +268,35 @@ def test_sliced_aggregation_vs_oracle(gpu_ctx, qi, n, types):
             g.release()
 
 
+# config 2's shape: an AND of two bit-sliced leaves (<= 16 and <= 8 bits) with every aggregation over one column's
+# value planes -- query_kernel_rstream streams all three plane sets into VGPRs (PGPU_NO_RSTREAM=1: the LDS-DMA
+# direct kernel); entries scanned in program order (leaf 0 every doc, leaf 1 leaf 0's matches)
+RSTREAM_QUERIES = [
+    "SELECT COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t WHERE c < 2000 AND b IN (3, 9, 30, 42)",
+    "SELECT SUM(m) FROM t WHERE b > 3 AND c BETWEEN 100 AND 2500",
+    "SELECT COUNT(*), MAX(m), MIN(m) FROM t WHERE g <> 9 AND c >= 300",
+    "SELECT SUM(c), COUNT(*) FROM t WHERE c NOT IN (5, 600, 1200) AND b < 40",
+]
+
+
+@pytest.mark.parametrize("rstream", [True, False], ids=["rstream", "lds_dma"])
+@pytest.mark.parametrize("n", [1, 4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(RSTREAM_QUERIES)))
+def test_two_sliced_leaves_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, rstream):
+    if not rstream:
+        monkeypatch.setenv("PGPU_NO_RSTREAM", "1")
+    rng = np.random.default_rng(900 + qi + n)
+    segs = [_random_segment(rng, n + 2048 * i, f"rs{i}") for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(RSTREAM_QUERIES[qi])
+        res = _gpu(gpu_ctx, q, gs)
+    finally:
+        for g in gs:
+            g.release()
+    _assert_same(res, _oracle(q, segs))
+
+
 @pytest.mark.parametrize("n", [2048, 70_001])
 def test_value_planes_negative_and_long(gpu_ctx, n):
     """Bit-sliced value planes (DevColumn::vsliced: value - vmin) over negative INT and LONG dictionaries of <= 24

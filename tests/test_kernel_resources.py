@@ -47,7 +47,7 @@ def kernel_resources(path: str) -> dict:
         shutil.rmtree(d, ignore_errors=True)
     out, cur = {}, None
     for line in notes.splitlines():
-        m = re.match(r"\s+\.(name|vgpr_count|sgpr_count|private_segment_fixed_size|vgpr_spill_count):\s+(\S+)", line)
+        m = re.match(r"\s+\.(name|vgpr_count|sgpr_count|private_segment_fixed_size|vgpr_spill_count|sgpr_spill_count):\s+(\S+)", line)
         if not m:
             continue
         k, v = m.groups()
@@ -95,3 +95,11 @@ def test_andfsm_kernels_do_not_spill(res):
         assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (k, v)
         if "ILb1E" in k:
             assert v["vgpr_count"] <= 128, (k, v)
+
+
+def test_register_streaming_kernels_do_not_spill(res):
+    """query_kernel_rstream holds RD tiles of (16 + narrow + value) planes in VGPRs: no scratch in any variant."""
+    ks = {k: v for k, v in res.items() if "query_kernel_rstream" in k}
+    assert len(ks) == 4
+    for k, v in ks.items():
+        assert v["private_segment_fixed_size"] == 0 and v["vgpr_spill_count"] == 0, (k, v)
