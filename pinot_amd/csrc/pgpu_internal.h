@@ -160,7 +160,13 @@ struct DevSeg {
   int32_t nvstage;
   int32_t vstage_col[2];
   int32_t vstage_off[2];
-  int32_t pad3_;
+  // index-only dense program as a truth table (register streaming, DevParams::direct == 4): bit t = the program's
+  // result when leaf i has the value of bit i of t; leaves 0 .. nbits - 1 are the BITS slots, then the SORTED leaves
+  // at instruction indexes psorted[0 .. pnsorted) (absolute, into DevParams::instrs)
+  uint32_t ptt;
+  int32_t pnsorted;
+  int32_t psorted[2];
+  int32_t pad4_;
 };
 #define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 

@@ -2862,9 +2862,9 @@ FI uint32_t rs_leaf(const SegState& ss, int j, const uint32_t (&x)[PL]) {
 // The matched docs' aggregations from the value planes (bsi_fold with the segment's width and offset cached).
 template <int NV>
 FI void rs_fold(const DevParams& p, const Cons& cv, LaneAcc& la, const uint32_t (&x)[NV], uint32_t mm, int vb,
-                int64_t vmin) {
+                int64_t vmin, int vcol) {
   for (int a = 0; a < p.nagg; ++a) {
-    if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+    if (p.aggs[a].fn == PGPU_AGG_COUNT || p.aggs[a].col != vcol) continue;
     const int32_t op = p.aggs[a].op;
     int64_t part;
     if (op == PGPU_RED_SUM_I64) {
@@ -2981,7 +2981,7 @@ FI Stats rstream_consumer(const DevParams& p, const Lds& L, int cidx, int t0, in
         const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
         mark_seg(p, ss, any);
         if (any) {
-          rs_fold<NV>(p, cv, la, xv[s], mm, vb, vmin);
+          rs_fold<NV>(p, cv, la, xv[s], mm, vb, vmin, vcol);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += vbytes;
         }
         PROF_ADD(pf, PGPU_P_C_AGG, ta);
@@ -3031,6 +3031,207 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rstream(DevP
   for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
 #endif
   const Stats st = rstream_consumer<PN, NV>(p, L, wave, t0, t1 - t0, pf);
+  direct_epilogue<PGPU_MODE_AGG>(p, L, st, wave, lane, pf);
+}
+
+// ================================================================================================================
+// REGISTER STREAMING OF INDEX-ONLY PROGRAMS (p.direct == 4, aggregation-only mode): every segment's dense program
+// reads only precomputed bitmaps (BITS leaves: inverted-index leaves expanded by invexp_kernel, raw-value leaves)
+// and sorted-column doc ranges, <= 5 leaves, none counted as scanned entries; its aggregations come from <= 2
+// columns' value planes.  The runtime turns the program into a truth table over its leaves (DevSeg::ptt), so a
+// tile's match word is a 31-deep v_bfi mux tree over the leaf words -- no instruction fetch, no LDS mask rows -- and
+// the leaves' bitmap words ride in the register ring with the value planes (as in query_kernel_rstream).
+// ================================================================================================================
+#define PGPU_RPROG_LEAVES 5
+struct RpIssue {
+  const uint32_t* bw[PGPU_PREBITS];
+  const uint32_t* sv[2];
+  int nb, vb[2];
+};
+FI void rp_load_issue(const DevParams& p, int seg, int vc0, int vc1, RpIssue& is) {
+  const DevSeg* sg = p.segs + seg;
+  const DevColumn* cols = p.cols + cld(&sg->col_begin);
+  is.nb = cld(&sg->nbits);
+#pragma unroll
+  for (int j = 0; j < PGPU_PREBITS; ++j) is.bw[j] = (const uint32_t*)cld(&sg->bits_w[j]);
+  is.sv[0] = (const uint32_t*)cld(&cols[vc0].vsliced);
+  is.vb[0] = cld(&cols[vc0].vbits);
+  is.sv[1] = vc1 >= 0 ? (const uint32_t*)cld(&cols[vc1].vsliced) : nullptr;
+  is.vb[1] = vc1 >= 0 ? cld(&cols[vc1].vbits) : 0;
+}
+template <int NA, int NV>
+FI void rp_load(const RpIssue& is, int tile_in_seg, uint32_t (&w)[PGPU_PREBITS], uint32_t (&x)[NA][NV]) {
+  const size_t wi = (size_t)tile_in_seg * (WT / 32) + lane_id();  // the lane's 32 docs: one word of each bitmap
+#pragma unroll
+  for (int j = 0; j < PGPU_PREBITS; ++j) w[j] = j < is.nb ? __builtin_nontemporal_load(is.bw[j] + wi) : 0u;
+#pragma unroll
+  for (int c = 0; c < NA; ++c) rs_load_planes(is.sv[c], is.vb[c], tile_in_seg, x[c]);
+}
+// f(w) for the 5-input truth table T (bit t = f at leaf values t): a mux tree, leaf 0 first.
+FI uint32_t tt_eval(uint32_t T, const uint32_t (&w)[PGPU_RPROG_LEAVES]) {
+  uint32_t g[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t one = 0u - ((T >> (2 * j + 1)) & 1u), zero = 0u - ((T >> (2 * j)) & 1u);
+    g[j] = (w[0] & one) | (~w[0] & zero);
+  }
+#pragma unroll
+  for (int lv = 1; lv < PGPU_RPROG_LEAVES; ++lv) {
+#pragma unroll
+    for (int j = 0; j < (16 >> lv); ++j) g[j] = (w[lv] & g[2 * j + 1]) | (~w[lv] & g[2 * j]);
+  }
+  return g[0];
+}
+
+template <int NA, int NV>
+FI Stats rprog_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH;
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  if (lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, dense_bytes = 0;
+  uint32_t lane_matched = 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int vc0 = -1, vc1 = -1;  // the value columns, in first-use order (runtime: at most NA)
+  for (int a = 0; a < p.nagg; ++a) {
+    const int c = p.aggs[a].col;
+    if (p.aggs[a].fn == PGPU_AGG_COUNT || c == vc0) continue;
+    if (vc0 < 0) vc0 = c;
+    else vc1 = c;
+  }
+  SegState ss;
+  int cseg = -1, nb = 0, nsorted = 0, ps0 = 0, ps1 = 0, vb0 = 0, vb1 = 0;
+  uint32_t T = 0;
+  int64_t vmin0 = 0, vmin1 = 0, vbytes = 0;
+  if (cidx < ntiles) {
+    const int own = (ntiles - cidx + NW - 1) / NW;  // this wave's tiles: cidx, cidx + NW, ...
+    Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
+    RpIssue is;
+    rp_load_issue(p, ci.seg, vc0, vc1, is);
+    uint32_t pw[RD][PGPU_PREBITS], xv[RD][NA][NV];
+#pragma unroll
+    for (int s = 0; s < RD; ++s) {
+      if (s < own) {
+        if (s > 0 && cursor_advance(p, ci, NW)) rp_load_issue(p, ci.seg, vc0, vc1, is);
+        rp_load<NA, NV>(is, ci.tile_in_seg, pw[s], xv[s]);
+      }
+    }
+    int poll = p.cancel_poll;
+    bool stop = false;
+    for (int k0 = 0; k0 < own && !stop; k0 += RD) {
+#pragma unroll
+      for (int s = 0; s < RD; ++s) {
+        const int k = k0 + s;
+        if (k >= own || stop) break;
+        if (--poll == 0) {
+          poll = p.cancel_poll;
+          if (query_cancelled(p)) {
+            stop = true;
+            break;
+          }
+        }
+        if (k > 0) cursor_advance(p, cur, NW);
+        if (cur.seg != cseg) {
+          cseg = cur.seg;
+          load_seg(p, cseg, ss);
+          T = cld(&ss.sg->ptt);
+          nb = cld(&ss.sg->nbits);
+          nsorted = cld(&ss.sg->pnsorted);
+          ps0 = cld(&ss.sg->psorted[0]);
+          ps1 = cld(&ss.sg->psorted[1]);
+          vb0 = cld(&ss.cols[vc0].vbits);
+          vmin0 = cld(&ss.cols[vc0].vmin);
+          vb1 = vc1 >= 0 ? cld(&ss.cols[vc1].vbits) : 0;
+          vmin1 = vc1 >= 0 ? cld(&ss.cols[vc1].vmin) : 0;
+          vbytes = 0;  // the aggregated columns' planes per matched tile (direct_candidates' dense-bytes model)
+          for (int a = 0; a < p.nagg; ++a)
+            if (p.aggs[a].fn != PGPU_AGG_COUNT) vbytes += (int64_t)WT * (p.aggs[a].col == vc0 ? vb0 : vb1) / 8;
+        }
+        const int64_t tf = now(pf);
+#ifdef PGPU_PROFILE_BUILD
+        if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
+#endif
+        TileCtx t;
+        t.ss = &ss;
+        t.slot = nullptr;
+        t.tile_in_seg = cur.tile_in_seg;
+        t.doc0 = cur.tile_in_seg * WT;
+        t.lane_doc0 = t.doc0 + 32 * lane;
+        {
+          const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+          t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+        }
+        const uint32_t sw0 = nsorted > 0 ? leaf_sorted(p, t, cld(p.instrs + ps0)) : 0u;
+        const uint32_t sw1 = nsorted > 1 ? leaf_sorted(p, t, cld(p.instrs + ps1)) : 0u;
+        uint32_t w[PGPU_RPROG_LEAVES];
+#pragma unroll
+        for (int i = 0; i < PGPU_RPROG_LEAVES; ++i)
+          w[i] = (i < PGPU_PREBITS && i < nb) ? pw[s][i < PGPU_PREBITS ? i : 0] : (i == nb ? sw0 : (i == nb + 1 ? sw1 : 0u));
+        const uint32_t mm = tt_eval(T, w) & t.valid;
+        PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+        const int64_t ta = now(pf);
+        lane_matched += __popc(mm);
+        const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
+        mark_seg(p, ss, any);
+        if (any) {
+          rs_fold<NV>(p, cv, la, xv[s][0], mm, vb0, vmin0, vc0);
+          if constexpr (NA > 1) rs_fold<NV>(p, cv, la, xv[s][NA - 1], mm, vb1, vmin1, vc1);
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += vbytes;
+        }
+        PROF_ADD(pf, PGPU_P_C_AGG, ta);
+        if (k + RD < own) {  // refill this register slot with the tile RD ahead
+          if (cursor_advance(p, ci, NW)) rp_load_issue(p, ci.seg, vc0, vc1, is);
+          rp_load<NA, NV>(is, ci.tile_in_seg, pw[s], xv[s]);
+        }
+      }
+    }
+  }
+  {
+    const int64_t lm = wave_sum_i64((int64_t)lane_matched);
+    if (lane == 0) matched += lm;
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+#pragma unroll
+  for (int a = 0; a < NREG_ACC; ++a)
+    if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  Stats st;
+  st.matched = matched;
+  st.scanned = 0;  // (the runtime admits only leaves that count no scanned entries)
+  st.sector_bytes = 0;
+  st.dense_bytes = dense_bytes;
+  return st;
+}
+
+template <int NA, int NV>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rprog(DevParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  __syncthreads();
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const Stats st = rprog_consumer<NA, NV>(p, L, wave, t0, t1 - t0, pf);
   direct_epilogue<PGPU_MODE_AGG>(p, L, st, wave, lane, pf);
 }
 
@@ -4421,6 +4622,26 @@ static hipError_t rs_attr(size_t lds_bytes) {
   if (e == hipSuccess) e = rs_attr<8, 24>(lds_bytes);
   return e;
 }
+template <int NA, int NV>
+static hipError_t rp_attr(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void*)query_kernel_rprog<NA, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
+[[maybe_unused]] static hipError_t rp_attrs(size_t lds_bytes) {
+  hipError_t e = rp_attr<1, 16>(lds_bytes);
+  if (e == hipSuccess) e = rp_attr<1, 24>(lds_bytes);
+  if (e == hipSuccess) e = rp_attr<2, 16>(lds_bytes);
+  if (e == hipSuccess) e = rp_attr<2, 24>(lds_bytes);
+  return e;
+}
+// (index-only register streaming: rd_planes = value columns 1 / 2, rs_vplanes = value planes 16 / 24)
+[[maybe_unused]] static void rp_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+  const dim3 g(grid), b(PGPU_DIRECT_THREADS);
+  if (p.rd_planes <= 1 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<1, 16>), g, b, dyn_smem, st, p);
+  else if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rprog<1, 24>), g, b, dyn_smem, st, p);
+  else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<2, 16>), g, b, dyn_smem, st, p);
+  else hipLaunchKernelGGL((query_kernel_rprog<2, 24>), g, b, dyn_smem, st, p);
+}
 [[maybe_unused]] static void rs_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
   if (p.rd_planes <= 4 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rstream<4, 16>), g, b, dyn_smem, st, p);
@@ -4436,9 +4657,12 @@ static hipError_t rs_attr(size_t lds_bytes) {
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    if (p.direct == 3) {                                                                                        \
-      if constexpr (M == PGPU_MODE_AGG) rs_launch(p, grid, dyn_smem, st);                                       \
-      else return hipErrorInvalidValue;                                                                         \
+    if (p.direct == 3 || p.direct == 4) {                                                                       \
+      if constexpr (M == PGPU_MODE_AGG) {                                                                       \
+        if (p.direct == 3) rs_launch(p, grid, dyn_smem, st);                                                    \
+        else rp_launch(p, grid, dyn_smem, st);                                                                  \
+      } else                                                                                                    \
+        return hipErrorInvalidValue;                                                                            \
     } else if (p.direct == 2) {                                                                                 \
       if (p.rd_pfx) rd_launch<M, PGPU_PFX_PLANES>(p, grid, dyn_smem, st);                                       \
       else rd_launch<M, 0>(p, grid, dyn_smem, st);                                                              \
@@ -4459,6 +4683,8 @@ static hipError_t rs_attr(size_t lds_bytes) {
     if (e == hipSuccess) e = rd_attrs<M, PGPU_PFX_PLANES>(lds_bytes);                                           \
     if constexpr (M == PGPU_MODE_AGG)                                                                           \
       if (e == hipSuccess) e = rs_attrs(lds_bytes);                                                             \
+    if constexpr (M == PGPU_MODE_AGG)                                                                           \
+      if (e == hipSuccess) e = rp_attrs(lds_bytes);                                                             \
     return e;                                                                                                   \
   }
 #define PGPU_MODE_DECLS(NAME)                                                                   \

@@ -2309,6 +2309,65 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
   return PGPU_OK;
 }
 
+// The index-only dense program of `ds` as a truth table over its leaves (DevSeg::ptt, query_kernel_rprog): leaves
+// 0 .. nbits - 1 are its BITS slots, then up to two SORTED leaves with inline doc ranges.  False when the program
+// reads anything else (SCAN / INV leaves load per tile) or counts scanned entries.  An AND's short-circuit only skips
+// children whose rows nobody reads afterwards, so evaluating every instruction gives the interpreter's result.
+bool program_truth_table(const Packer& pk, DevSeg& ds) {
+  std::vector<int> sorted;
+  int maxrow = 0;
+  for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+    const DevInstr& in = pk.instrs[i];
+    switch (in.op) {
+      case PGPU_I_BITS:
+        if (in.n < 0 || in.n >= ds.nbits || !in.nostat) return false;
+        break;
+      case PGPU_I_SORTED:
+        if (in.n > 4) return false;
+        sorted.push_back(i);
+        break;
+      case PGPU_I_ALL: case PGPU_I_EMPTY: case PGPU_I_AND_BEGIN: case PGPU_I_AND_CHILD: case PGPU_I_AND_END:
+      case PGPU_I_OR_BEGIN: case PGPU_I_OR_CHILD: case PGPU_I_OR_END: case PGPU_I_NOT:
+        break;
+      default:
+        return false;
+    }
+    maxrow = std::max({maxrow, in.dst, in.src, in.care});
+  }
+  if (ds.prog_len <= 0 || sorted.size() > 2 || ds.nbits + (int)sorted.size() > 5) return false;
+  uint32_t tt = 0;
+  std::vector<uint8_t> row((size_t)maxrow + 1);
+  for (int t = 0; t < 32; ++t) {
+    std::fill(row.begin(), row.end(), 0);
+    for (int i = ds.prog_begin; i < ds.prog_begin + ds.prog_len; ++i) {
+      const DevInstr& in = pk.instrs[i];
+      const uint8_t care = in.care < 0 ? 1 : row[in.care];
+      uint8_t* d = in.dst >= 0 ? &row[in.dst] : nullptr;
+      switch (in.op) {
+        case PGPU_I_ALL: *d = 1; break;
+        case PGPU_I_EMPTY: *d = 0; break;
+        case PGPU_I_BITS: *d = ((t >> in.n) & 1) & care; break;
+        case PGPU_I_SORTED: {
+          const int leaf = ds.nbits + (int)(std::find(sorted.begin(), sorted.end(), i) - sorted.begin());
+          *d = (t >> leaf) & 1;
+          break;
+        }
+        case PGPU_I_AND_BEGIN: *d = care; break;
+        case PGPU_I_AND_CHILD: *d &= row[in.src]; break;
+        case PGPU_I_OR_BEGIN: *d = 0; break;
+        case PGPU_I_OR_CHILD: *d |= row[in.src]; break;
+        case PGPU_I_NOT: *d = !row[in.src] & care; break;
+        default: break;
+      }
+    }
+    if (row[0]) tt |= 1u << t;
+  }
+  ds.ptt = tt;
+  ds.pnsorted = (int32_t)sorted.size();
+  for (size_t j = 0; j < 2; ++j) ds.psorted[j] = j < sorted.size() ? sorted[j] : 0;
+  return true;
+}
+
 int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_layout& L, Packer& pk, DevParams& p) {
   memset(&p, 0, sizeof(p));
   p.ncols = q->num_columns;
@@ -2682,12 +2741,56 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       dyn = rdyn;
     }
   }
+  // register streaming of index-only programs (query_kernel_rprog): aggregation-only, every segment's dense program
+  // a truth table over <= 5 bitmap / sorted leaves, its aggregations from <= 2 columns' value planes (<= 24)
+  if (p.direct == 1 && p.mode == PGPU_MODE_AGG) {
+    const bool no_rprog = getenv("PGPU_NO_RPROG") && atoi(getenv("PGPU_NO_RPROG")) != 0;  // per plan (tests)
+    bool rp = !no_rprog;
+    int vcols[2] = {-1, -1}, nv = 0, vbmax = 1;
+    for (int a = 0; a < p.nagg && rp; ++a) {
+      const DevAgg& ag = p.aggs[a];
+      if (ag.fn == PGPU_AGG_COUNT || ag.col == vcols[0] || ag.col == vcols[1]) continue;
+      rp = nv < 2 && ((ag.op == PGPU_RED_SUM_I64 && ag.part == 0) || ag.op == PGPU_RED_MIN_I64 ||
+                      ag.op == PGPU_RED_MAX_I64);
+      if (rp) vcols[nv++] = ag.col;
+    }
+    for (int a = 0; a < p.nagg && rp; ++a)  // (every aggregation over a value column must be a value-plane one)
+      if (p.aggs[a].fn != PGPU_AGG_COUNT)
+        rp = (p.aggs[a].op == PGPU_RED_SUM_I64 && p.aggs[a].part == 0) || p.aggs[a].op == PGPU_RED_MIN_I64 ||
+             p.aggs[a].op == PGPU_RED_MAX_I64;
+    rp = rp && nv >= 1;
+    for (DevSeg& ds : pk.segs) {
+      if (!rp || !ds.ntiles) continue;
+      rp = ds.nstage == 0 && ds.fast == 0 && ds.agg_mode == PGPU_AM_SLICED && ds.rprog_len == 0 && ds.nvstage == 0 &&
+           program_truth_table(pk, ds);
+      for (int c = 0; c < nv && rp; ++c) {
+        const DevColumn& vc = pk.cols[ds.col_begin + vcols[c]];
+        rp = vc.vsliced && vc.vbits >= 1 && vc.vbits <= 24;
+        vbmax = std::max(vbmax, (int)vc.vbits);
+      }
+    }
+    const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;
+    if (rp && rdyn <= PGPU_LDS_LIMIT) {
+      static const int env_wgs = getenv("PGPU_DIRECT_WGS") ? atoi(getenv("PGPU_DIRECT_WGS")) : 0;  // per CU
+      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : (nv > 1 && vbmax > 16 ? 2 : 3),
+                                               PGPU_LDS_LIMIT / rdyn);
+      int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
+      if (g >= 8) g &= ~7;
+      p.direct = 4;
+      p.rd_planes = nv;
+      p.rs_vplanes = vbmax <= 16 ? 16 : 24;
+      p.rd_pfx = 0;
+      p.dslots = 0;
+      grid = std::max(1, g);
+      dyn = rdyn;
+    }
+  }
   // sliced aggregation runs in the self-loading kernels only (query_kernel_direct, and query_kernel_rstream with the
   // value planes in VGPRs): elsewhere its segments gather per candidate (their staged aggregation planes are then
   // only extra DMA, never read)
   if (p.direct != 1)
     for (DevSeg& ds : pk.segs) {
-      if (ds.agg_mode == PGPU_AM_SLICED && p.direct != 3) ds.agg_mode = PGPU_AM_SPARSE;
+      if (ds.agg_mode == PGPU_AM_SLICED && p.direct != 3 && p.direct != 4) ds.agg_mode = PGPU_AM_SPARSE;
       for (int j = 0; j < ds.nvstage; ++j)  // (the ring loaders stage filter columns only)
         ds.stage_instrs -= (pk.cols[ds.col_begin + ds.vstage_col[j]].vbits + 3) / 4;
       ds.nvstage = 0;

@@ -297,6 +297,49 @@ def test_two_sliced_leaves_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, r
     _assert_same(res, _oracle(q, segs))
 
 
+# config 3's shape: index-only programs (inverted leaves expanded to bitmaps, sorted-column doc ranges) with value-plane
+# aggregations over <= 2 columns -- query_kernel_rprog evaluates the program as a truth table over the leaf words
+# (PGPU_NO_RPROG=1: the LDS-DMA direct kernel's interpreter); the last query has five bitmap leaves (no rprog)
+RPROG_QUERIES = [
+    "SELECT SUM(m), MAX(m), COUNT(*) FROM t WHERE a = 1 OR b IN (0, 9, 18)",
+    "SELECT SUM(m), SUM(d), MIN(d) FROM t WHERE (a = 2 AND b IN (3, 30)) OR (c = 50 AND g <> 9 AND s BETWEEN 200 AND 700)",
+    "SELECT COUNT(*), MIN(f), MAX(f) FROM t WHERE NOT (a = 3 AND e = 0) AND b NOT IN (3, 6)",
+    "SELECT SUM(m), AVG(m) FROM t WHERE s < 300 OR e = 1",
+    "SELECT SUM(f) FROM t WHERE a IN (1, 2) AND b <> 0 AND c = 7 AND e = 1 AND g IN (1, 2, 3)",
+]
+
+
+def _index_segment(rng, n, name):
+    cols = {"a": (PGPU_INT, rng.integers(0, 4, n).astype(np.int32)),
+            "b": (PGPU_INT, (rng.integers(0, 16, n) * 3).astype(np.int32)),
+            "c": (PGPU_INT, rng.integers(0, 64, n).astype(np.int32)),
+            "e": (PGPU_INT, rng.integers(0, 2, n).astype(np.int32)),
+            "g": (PGPU_INT, rng.integers(0, 40, n).astype(np.int32)),
+            "s": (PGPU_INT, np.sort(rng.integers(0, 1000, n)).astype(np.int32)),
+            "m": (PGPU_INT, rng.integers(-500, 60_000, n).astype(np.int32)),
+            "d": (PGPU_INT, rng.integers(0, 3_000_000, n).astype(np.int32)),
+            "f": (PGPU_INT, rng.integers(0, 300, n).astype(np.int32))}
+    return build_segment(name, cols, inverted=["a", "b", "c", "e", "g"])
+
+
+@pytest.mark.parametrize("rprog", [True, False], ids=["rprog", "interp"])
+@pytest.mark.parametrize("n", [1, 4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(RPROG_QUERIES)))
+def test_index_only_programs_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, rprog):
+    if not rprog:
+        monkeypatch.setenv("PGPU_NO_RPROG", "1")
+    rng = np.random.default_rng(1300 + qi + n)
+    segs = [_index_segment(rng, n + 2048 * i, f"ip{i}") for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(RPROG_QUERIES[qi])
+        res = _gpu(gpu_ctx, q, gs)
+    finally:
+        for g in gs:
+            g.release()
+    _assert_same(res, _oracle(q, segs))
+
+
 @pytest.mark.parametrize("n", [2048, 70_001])
 def test_value_planes_negative_and_long(gpu_ctx, n):
     """Bit-sliced value planes (DevColumn::vsliced: value - vmin) over negative INT and LONG dictionaries of <= 24
