@@ -4631,15 +4631,18 @@ static hipError_t rp_attr(size_t lds_bytes) {
   hipError_t e = rp_attr<1, 16>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<1, 24>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 16>(lds_bytes);
+  if (e == hipSuccess) e = rp_attr<2, 20>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 24>(lds_bytes);
   return e;
 }
-// (index-only register streaming: rd_planes = value columns 1 / 2, rs_vplanes = value planes 16 / 24)
+// (index-only register streaming: rd_planes = value columns 1 / 2, rs_vplanes = value planes 16 / 20 / 24; two
+// columns of <= 20 planes keep three waves per SIMD, of 24 two)
 [[maybe_unused]] static void rp_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
   if (p.rd_planes <= 1 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<1, 16>), g, b, dyn_smem, st, p);
   else if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rprog<1, 24>), g, b, dyn_smem, st, p);
   else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<2, 16>), g, b, dyn_smem, st, p);
+  else if (p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rprog<2, 20>), g, b, dyn_smem, st, p);
   else hipLaunchKernelGGL((query_kernel_rprog<2, 24>), g, b, dyn_smem, st, p);
 }
 [[maybe_unused]] static void rs_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {

@@ -2772,13 +2772,13 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;
     if (rp && rdyn <= PGPU_LDS_LIMIT) {
       static const int env_wgs = getenv("PGPU_DIRECT_WGS") ? atoi(getenv("PGPU_DIRECT_WGS")) : 0;  // per CU
-      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : (nv > 1 && vbmax > 16 ? 2 : 3),
+      const int per_cu = (int)std::min<size_t>(env_wgs >= 1 ? env_wgs : (nv > 1 && vbmax > 20 ? 2 : 3),
                                                PGPU_LDS_LIMIT / rdyn);
       int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
       if (g >= 8) g &= ~7;
       p.direct = 4;
       p.rd_planes = nv;
-      p.rs_vplanes = vbmax <= 16 ? 16 : 24;
+      p.rs_vplanes = vbmax <= 16 ? 16 : (vbmax <= 20 && nv > 1) ? 20 : 24;
       p.rd_pfx = 0;
       p.dslots = 0;
       grid = std::max(1, g);
