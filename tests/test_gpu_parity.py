@@ -159,11 +159,11 @@ def test_baseball_quickstart_gpu(gpu_ctx):
 
 
 # ---- randomized parity against the oracle ------------------------------------------------------------------------
-def _random_segment(rng, n, name="rand", inverted=(), types=None):
+def _random_segment(rng, n, name="rand", inverted=(), types=None, offsets=None):
     cols = {}
     cards = {"a": 3, "b": 16, "c": 1000, "d": 70_000, "e": 2, "m": 5000, "f": 300, "g": 40}
     for c, card in cards.items():
-        base = rng.choice(np.arange(card * 3, dtype=np.int64), size=card, replace=False)
+        base = rng.choice(np.arange(card * 3, dtype=np.int64), size=card, replace=False) - (offsets or {}).get(c, 0)
         vals = base[rng.integers(0, card, n)]
         dt = (types or {}).get(c, PGPU_INT)
         if dt == PGPU_DOUBLE:
@@ -279,14 +279,16 @@ RSTREAM_QUERIES = [
 ]
 
 
+@pytest.mark.parametrize("neg", [False, True], ids=["pos", "neg"])
 @pytest.mark.parametrize("rstream", [True, False], ids=["rstream", "lds_dma"])
 @pytest.mark.parametrize("n", [1, 4097, 200_003])
 @pytest.mark.parametrize("qi", range(len(RSTREAM_QUERIES)))
-def test_two_sliced_leaves_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, rstream):
+def test_two_sliced_leaves_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, rstream, neg):
+    """neg: the aggregated column's values straddle zero (value planes of value - vmin with vmin < 0)."""
     if not rstream:
         monkeypatch.setenv("PGPU_NO_RSTREAM", "1")
     rng = np.random.default_rng(900 + qi + n)
-    segs = [_random_segment(rng, n + 2048 * i, f"rs{i}") for i in range(3)]
+    segs = [_random_segment(rng, n + 2048 * i, f"rs{i}", offsets={"m": 7000} if neg else None) for i in range(3)]
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         q = parse_sql(RSTREAM_QUERIES[qi])
