@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 9
+#define PGPU_ABI_VERSION 10
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -288,11 +288,14 @@ typedef struct {
    * at launch), the query is cancelled and pgpu_query_wait / _collect / _execute / pgpu_node_query return
    * PGPU_E_TIMEOUT. */
   int64_t deadline_ms;
-  /* Per aggregation (num_aggs entries), or NULL: a lower bound of the fixed-point exponent of each FLOAT / DOUBLE
-   * SUM / AVG (pgpu_table_layout.agg_sum_exp).  The layout takes the larger of it and the launch's own, so callers
-   * that combine tables across launches (ranks, devices) pass the max of their launches' agg_sum_exp and get one
-   * layout everywhere; PGPU_SUM_EXP_F64 forces the float64 section. */
+  /* Per aggregation (num_aggs entries), or both NULL: the fixed-point layout (exponent, part count) of each FLOAT /
+   * DOUBLE SUM / AVG agreed across the launches whose tables are combined (ranks, devices), as
+   * pgpu_sum_layout_agree returns it from their own layouts (pgpu_table_layout.agg_sum_exp / agg_sum_parts).  The
+   * launch takes it verbatim (PGPU_SUM_EXP_F64, or more than PGPU_MAX_FIXED_PARTS parts: a float64 section), so every
+   * table has one layout; it fails with PGPU_E_INVALID when the agreed window does not cover its own values at its
+   * own precision.  Entries of other aggregations are ignored. */
   const int32_t* sum_exp;
+  const int32_t* sum_parts;
 } pgpu_query_desc;
 
 #define PGPU_Q_STATS 1ull /* count touched 32-B sectors of sparse column reads (roofline accounting) */
@@ -327,15 +330,21 @@ typedef struct {
  *                                  SUM = c[s] + c[s+1] * 2^21 + c[s+2] * 2^42, exact for < 2^42 docs
  *                                  (SumAggregationFunction.java:55-92 adds doubles in doc order and never
  *                                  wraps; an int64 cell would)
- *                              SUM of FLOAT/DOUBLE      -> three 21-bit-part int64 SUM sections of the
-                                                          values in fixed point: v -> rint(v * 2^-e) with
-                                                          e = ilogb(max|value|) + 1 - 62 (agg_sum_exp), so that
-                                                          integer adds make the sum independent of the order
-                                                          the GPU adds in (a float64 SUM of atomics is not);
-                                                          value = round(exact part sum) * 2^e, within 2^-61 of
-                                                          max|value| per value of the exact sum.  A NaN or
-                                                          infinity in the column (or no section budget) keeps
-                                                          one float64 SUM section (agg_sum_exp = PGPU_SUM_EXP_F64)
+ *                              SUM of FLOAT/DOUBLE      -> P = agg_sum_parts (3..PGPU_MAX_FIXED_PARTS) int64 SUM
+ *                                                          sections of the values in fixed point: |v| -> the
+ *                                                          integer I = rint(|v| * 2^-e) (e = agg_sum_exp), section
+ *                                                          s+k sums sign(v) * (bits [21k, 21k+21) of I), so that
+ *                                                          integer adds make the sum independent of the order the
+ *                                                          GPU adds in (a float64 SUM of atomics is not).  SUM =
+ *                                                          round(sum_k c[s+k] * 2^(21k)) * 2^e.  e and P come from
+ *                                                          the column's values (pgpu_fixed_sum_layout): each value
+ *                                                          is exact, or rounded by at most 2^-41 of itself, so the
+ *                                                          result is within 2^-41 * sum|v| of the exact sum (the
+ *                                                          reference's doc-order double adds: (n-1) * 2^-53 *
+ *                                                          sum|v|).  A NaN or infinity in the column, a value range
+ *                                                          needing more than PGPU_MAX_FIXED_PARTS parts, or no
+ *                                                          section budget keeps one float64 SUM section
+ *                                                          (agg_sum_exp = PGPU_SUM_EXP_F64)
  *                              MIN / MAX                -> int64 MIN / MAX of an order-preserving key
  *                              AVG                      -> as SUM (count comes from section 0)
  *                              COUNT                    -> no section (section 0)
@@ -347,6 +356,9 @@ typedef struct {
 #define PGPU_RED_MIN_I64 2
 #define PGPU_RED_MAX_I64 3
 #define PGPU_SUM_EXP_F64 32767 /* agg_sum_exp of a float64 SUM section */
+#define PGPU_SUM_EXP_ZERO (-32767) /* agg_sum_exp of a fixed-point SUM over a column holding no nonzero value */
+#define PGPU_MAX_FIXED_PARTS 6  /* 126-bit fixed-point window of a floating SUM */
+#define PGPU_FIXED_TOL_BITS 40  /* a value may be rounded by at most 2^-(TOL+1) of itself */
 
 /* key_kind of a table layout */
 #define PGPU_KEYS_DENSE 0 /* cell index = global raw key: sum_j gid_j * prod_{k<j} card_k (< 2^31) */
@@ -358,9 +370,12 @@ typedef struct {
   int32_t section_op[PGPU_MAX_SECTIONS]; /* PGPU_RED_* per section (section 0 = count) */
   int32_t agg_section[16]; /* section of agg i, or 0 for COUNT */
   int32_t agg_value_type[16]; /* stored type of the agg column (PGPU_INT..), -1 for COUNT */
-  int32_t agg_sum_parts[16];  /* SUM / AVG: 1 = one int64 (or float64) section, 3 = 21-bit-part sections */
-  int32_t agg_sum_exp[16];    /* SUM / AVG of FLOAT / DOUBLE in fixed point: value = (exact part sum) * 2^exp;
-                                 PGPU_SUM_EXP_F64 = a float64 section; 0 for integer columns */
+  int32_t agg_sum_parts[16];  /* SUM / AVG: 1 = one int64 (or float64) section, > 1 = that many 21-bit-part sections
+                                 (3 for a split integer SUM, 3..PGPU_MAX_FIXED_PARTS for a fixed-point floating SUM) */
+  int32_t agg_sum_exp[16];    /* SUM / AVG of FLOAT / DOUBLE in fixed point: value = (exact part sum) * 2^exp
+                                 (PGPU_SUM_EXP_ZERO: the column holds only zeros); PGPU_SUM_EXP_F64 = a float64
+                                 section; 0 for integer columns (whether a SUM is fixed point is decided by
+                                 agg_value_type and agg_sum_parts, never by this exponent) */
   /* Group keys.  Dense: the cell index is the key.  Hash: key_words int64 words per slot follow the sections
    * (word w of slot i at int64 index (num_sections + w) * num_keys + i; an empty slot holds -1).  Word 0 is the
    * mixed-radix key of group columns [0, key_split), word 1 (when key_words == 2, key spaces above 2^63, the
@@ -375,6 +390,16 @@ typedef struct {
 uint64_t pgpu_table_bytes(const pgpu_table_layout* layout);
 
 int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out);
+/* The fixed-point window of a FLOAT / DOUBLE SUM over values with max |v| = max_abs, smallest nonzero |v| of binary
+ * exponent min_exp and lowest significand bit 2^min_lsb (the layout's own choice, exposed for callers and tests):
+ * *out_parts 21-bit parts at exponent *out_exp, or PGPU_SUM_EXP_F64 / PGPU_SUM_EXP_ZERO. */
+void pgpu_fixed_sum_layout(double max_abs, int32_t min_exp, int32_t min_lsb, int32_t* out_exp, int32_t* out_parts);
+/* One fixed-point layout for tables combined across launches: from each launch's own layout (pgpu_table_layout_of
+ * without sum_exp) the window spanning all of them at the finest exponent any needs, per aggregation (out_exp /
+ * out_parts: num_aggs entries, passed back as pgpu_query_desc.sum_exp / sum_parts).  A float64 layout anywhere stays
+ * float64 everywhere; a window wider than PGPU_MAX_FIXED_PARTS parts makes every launch take float64. */
+int pgpu_sum_layout_agree(const pgpu_table_layout* layouts, int32_t num_layouts, int32_t num_aggs, int32_t* out_exp,
+                          int32_t* out_parts);
 
 typedef struct {
   int64_t num_docs_scanned;              /* docs matching the filter (AggregationOperator.java:82-87) */

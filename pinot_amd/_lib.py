@@ -39,7 +39,10 @@ PGPU_Q_EXACT_FILTER_STATS = 32
 PGPU_KEYS_DENSE, PGPU_KEYS_HASH = 0, 1
 PGPU_PART_BITS = 21  # split integer SUM: three sections of 21-bit parts (include/pinot_gpu.h)
 PGPU_SUM_EXP_F64 = 32767  # pgpu_table_layout.agg_sum_exp of a float64 SUM section
-ABI_VERSION = 9
+PGPU_SUM_EXP_ZERO = -32767  # ... of a fixed-point SUM over a column holding only zeros
+PGPU_MAX_FIXED_PARTS = 6  # widest fixed-point window (21-bit parts) of a floating SUM
+PGPU_FIXED_TOL_BITS = 40
+ABI_VERSION = 10
 
 
 class PinotGpuError(RuntimeError):
@@ -91,7 +94,7 @@ class QueryDesc(C.Structure):
                 ("group_columns", C.POINTER(C.c_int32)), ("group_cardinalities", C.POINTER(C.c_int32)),
                 ("flags", C.c_uint64), ("reduce_docs", C.c_int64), ("num_groups_limit", C.c_int32),
                 ("array_based_threshold", C.c_int32), ("deadline_ms", C.c_int64),
-                ("sum_exp", C.POINTER(C.c_int32))]
+                ("sum_exp", C.POINTER(C.c_int32)), ("sum_parts", C.POINTER(C.c_int32))]
 
 
 class TableLayout(C.Structure):
@@ -158,6 +161,9 @@ SIGNATURES = [
     ("pgpu_remap_upload", C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),
     ("pgpu_buffer_release", C.c_int, [_P]),
     ("pgpu_table_layout_of", C.c_int, [C.POINTER(QueryDesc), C.POINTER(TableLayout)]),
+    ("pgpu_fixed_sum_layout", None, [C.c_double, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("pgpu_sum_layout_agree", C.c_int, [C.POINTER(TableLayout), C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32)]),
     ("pgpu_table_bytes", C.c_uint64, [C.POINTER(TableLayout)]),
     ("pgpu_query_launch", C.c_int, [_P, C.POINTER(QueryDesc), _P, _P, C.c_uint64, C.POINTER(_P)]),
     ("pgpu_query_wait", C.c_int, [_P, C.POINTER(QueryStats)]),

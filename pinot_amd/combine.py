@@ -31,7 +31,7 @@ import numpy as np
 from . import _lib
 from ._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64,
                    PGPU_RED_SUM_F64, PGPU_RED_SUM_I64, PGPU_STRING, QueryStats, TableLayout)
-from .plan import (ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
+from .plan import (fixed_window, ExecutionStats, GpuPlanMaker, GroupColumns, GroupTable, QueryResult, check_group_columns, finish,
                    has_mv_aggregations, key_words_out, merge_filtered, mv_lower, mv_raise, table_capacity,
                    topk_spec, union_sorted)
 from .query import QueryContext, split_filtered_aggregations
@@ -315,10 +315,11 @@ class DistributedExecutor:
         return hit[0]
 
     def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int):
-        """(flags, sum_exp) that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's
+        """(flags, sum_layout) that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's
         integer-SUM bound needs the split sections, PGPU_Q_HASH when any rank's key space takes the hash group-by,
-        and per aggregation the largest fixed-point exponent any rank's floating SUM needs
-        (pgpu_table_layout.agg_sum_exp; PGPU_SUM_EXP_F64 anywhere makes every rank keep float64 sections)."""
+        and per aggregation the fixed-point window of a floating SUM spanning every rank's own (pgpu_sum_layout_agree
+        over the ranks: the highest top, the finest exponent; PGPU_SUM_EXP_F64 anywhere makes every rank keep
+        float64 sections)."""
         key = (tuple((a.function, a.column) for a in query.aggregations), tuple(query.group_by),
                self._seg_key(segments))
         hit = self._split.get(key)
@@ -330,27 +331,49 @@ class DistributedExecutor:
             split = any(L.agg_sum_parts[i] == 3 and L.agg_value_type[i] in (_lib.PGPU_INT, _lib.PGPU_LONG)
                         for i in range(na))
             hashed = L.key_kind == _lib.PGPU_KEYS_HASH
-            s_any, h_any, *exps = self._allreduce_i64([int(split), int(hashed)] + [L.agg_sum_exp[i] for i in range(na)],
-                                                      "max")
-            hit = (((_lib.PGPU_Q_SUM_SPLIT if s_any else 0) | (_lib.PGPU_Q_HASH if h_any else 0), tuple(exps)),
-                   tuple(segments))
+            none = -(1 << 40)
+            per = []
+            for i in range(na):
+                e, p = L.agg_sum_exp[i], L.agg_sum_parts[i]
+                fp = L.agg_value_type[i] in (_lib.PGPU_FLOAT, _lib.PGPU_DOUBLE)
+                f64 = fp and e == _lib.PGPU_SUM_EXP_F64
+                live = fp and p > 1 and e not in (_lib.PGPU_SUM_EXP_F64, _lib.PGPU_SUM_EXP_ZERO)
+                per += [int(f64), e + _lib.PGPU_PART_BITS * p if live else none, -e if live else none]
+            red = self._allreduce_i64([int(split), int(hashed)] + per, "max")
+            s_any, h_any = red[0], red[1]
+            exps, parts = [], []
+            for i in range(na):
+                f64, top, negb = red[2 + 3 * i: 5 + 3 * i]
+                if f64:
+                    exps.append(_lib.PGPU_SUM_EXP_F64)
+                    parts.append(1)
+                elif top == none:
+                    exps.append(_lib.PGPU_SUM_EXP_ZERO if L.agg_value_type[i] in (_lib.PGPU_FLOAT, _lib.PGPU_DOUBLE)
+                                else 0)
+                    parts.append(3 if L.agg_value_type[i] in (_lib.PGPU_FLOAT, _lib.PGPU_DOUBLE) else 0)
+                else:
+                    e, p = fixed_window(top, -negb)
+                    exps.append(e)
+                    parts.append(p)
+            hit = (((_lib.PGPU_Q_SUM_SPLIT if s_any else 0) | (_lib.PGPU_Q_HASH if h_any else 0),
+                    (tuple(exps), tuple(parts))), tuple(segments))
             self._split[key] = hit
         return hit[0]
 
     # ---- local kernel step (libpinotgpu) -------------------------------------------------------------------------
-    def _local_layout(self, query, segments, flags, reduce_docs, sum_exp=None) -> TableLayout:
-        return self._prepare_local(query, segments, flags, reduce_docs, sum_exp)[0]
+    def _local_layout(self, query, segments, flags, reduce_docs, sum_layout=None) -> TableLayout:
+        return self._prepare_local(query, segments, flags, reduce_docs, sum_layout)[0]
 
     def _alloc_table(self, n: int):
         import torch
         pool = self._tables.setdefault(n, [])
         return pool.pop() if pool else torch.empty(n, dtype=torch.int64, device=self.device)
 
-    def _prepare_local(self, query, segments, flags, reduce_docs, sum_exp=None):
+    def _prepare_local(self, query, segments, flags, reduce_docs, sum_layout=None):
         """(table layout, launch(table) -> handle) for this rank's scanned segments."""
         expr = self.pm.filter_expr(query, segments)
         desc, keep, _ = self.pm.build_desc(query, segments, plan_filters=expr is None, extra_flags=flags,
-                                           reduce_docs=reduce_docs, sum_exp=sum_exp)
+                                           reduce_docs=reduce_docs, sum_layout=sum_layout)
         L = self.pm.layout(desc)
 
         def launch(table):
@@ -418,12 +441,12 @@ class DistributedExecutor:
             raise ValueError("every rank needs at least one segment")
         globals_ = self._global_dicts(query, segments) if query.group_by else []
         reduce_docs = self._reduce_docs(segments)
-        flags, sum_exp = self._layout_flags(query, segments, reduce_docs)
+        flags, sum_layout = self._layout_flags(query, segments, reduce_docs)
         non_scan = self.pm.non_scan_segments(query, segments)
         scan = [s for s, ns in zip(segments, non_scan) if not ns]
         # the layout is the same on every rank: group cardinalities are global, the split-SUM choice and the
         # fixed-point exponents agreed
-        L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs, sum_exp)
+        L, launch = self._prepare_local(query, scan if scan else segments, flags, reduce_docs, sum_layout)
         n = _lib.table_bytes(L) // 8 if L.key_kind == _lib.PGPU_KEYS_HASH else int(L.num_sections * L.num_keys)
         table = self._alloc_table(n)
         handle = None

@@ -467,7 +467,7 @@ inline int pgpu_stage_instrs(int bits, bool sliced = false) {
 // group ids.  Every function compiles for both sides (this header is only included by hipcc-built files).
 #define PGPU_TK_COUNT 0
 #define PGPU_TK_SUM_I64 1
-#define PGPU_TK_SUM_SPLIT 2   // three 21-bit-part sections, exact as a 128-bit integer
+#define PGPU_TK_SUM_SPLIT 2   // TopkDev::parts 21-bit-part sections, exact as a 256-bit integer
 #define PGPU_TK_SUM_F64 3
 #define PGPU_TK_MINMAX_INT 4  // order-preserving cell = the integer value
 #define PGPU_TK_MINMAX_FP 5   // order-preserving cell = key of the double
@@ -487,7 +487,7 @@ struct TopkDev {
   int32_t kw;        // 0 dense (cell index = key), 1 one hash key word, 2 two-level hash key
   uint64_t key_base; // dense: key of cell 0
   int32_t fxe;       // SUM / AVG split of a fixed-point floating SUM: value = part sum * 2^fxe (0: integer)
-  int32_t pad_;
+  int32_t parts;     // SUM / AVG split: part sections
 };
 struct TopkState {  // radix-select state: the best-k threshold's high bits found so far
   uint64_t prefix, mask, kleft;
@@ -500,42 +500,54 @@ __host__ __device__ inline uint64_t pgpu_tk_double(double d) {
   const int64_t k = b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
   return (uint64_t)k ^ 0x8000000000000000ull;
 }
-// (hi:lo) two's-complement 128-bit integer -> nearest double (ties to even), via a 64-bit window with a sticky bit.
-__host__ __device__ inline double pgpu_i128_to_double(int64_t hi, uint64_t lo) {
-  const bool neg = hi < 0;
-  uint64_t h = (uint64_t)hi, l = lo;
+// sum_p c[p] * 2^(21 p) over `parts` signed int64 part sums (a split integer SUM, a fixed-point floating SUM) as a
+// 256-bit two's-complement integer, rounded once to the nearest double (ties to even): a 64-bit window below the
+// leading bit with a sticky bit for everything under it (> 11 guard bits remain below the 53-bit mantissa).
+__host__ __device__ inline double pgpu_parts_to_double(const int64_t* c, int parts) {
+  uint64_t w[4] = {0, 0, 0, 0};
+  for (int p = 0; p < parts; ++p) {
+    const uint64_t src[4] = {(uint64_t)c[p], c[p] < 0 ? ~0ull : 0ull, c[p] < 0 ? ~0ull : 0ull, c[p] < 0 ? ~0ull : 0ull};
+    const int sh = PGPU_PART_BITS * p, limb = sh / 64, bit = sh % 64;
+    uint64_t carry = 0;
+    for (int i = 0; i < 4; ++i) {
+      uint64_t a = 0;
+      if (i >= limb) {
+        a = bit ? (src[i - limb] << bit) : src[i - limb];
+        if (bit && i - limb - 1 >= 0) a |= src[i - limb - 1] >> (64 - bit);
+      }
+      const uint64_t s1 = w[i] + a;
+      const uint64_t c1 = s1 < a ? 1u : 0u;
+      w[i] = s1 + carry;
+      carry = c1 + (w[i] < s1 ? 1u : 0u);
+    }
+  }
+  const bool neg = (int64_t)w[3] < 0;
   if (neg) {  // negate
-    l = ~l + 1;
-    h = ~h + (l == 0 ? 1 : 0);
+    uint64_t carry = 1;
+    for (int i = 0; i < 4; ++i) {
+      w[i] = ~w[i] + carry;
+      carry = (carry && w[i] == 0) ? 1u : 0u;
+    }
   }
-  if (h == 0) return neg ? -(double)l : (double)l;
-  const int lz = __builtin_clzll(h);    // h != 0
-  const int shift = 64 - lz;            // bits of l below the 64-bit window (1..64)
-  uint64_t m;
-  if (shift == 64) {
-    m = h | (l != 0 ? 1u : 0u);
+  int k = 3;
+  while (k > 0 && w[k] == 0) --k;
+  double d;
+  if (k == 0) {
+    d = (double)w[0];
   } else {
-    m = (h << lz) | (l >> shift);
-    if (l & ((1ull << shift) - 1)) m |= 1;  // sticky: > 11 guard bits remain below the 53-bit mantissa
+    const int lz = __builtin_clzll(w[k]);
+    uint64_t m = lz ? ((w[k] << lz) | (w[k - 1] >> (64 - lz))) : w[k];
+    bool sticky = lz ? (w[k - 1] << lz) != 0 : w[k - 1] != 0;
+    for (int i = 0; i < k - 1; ++i) sticky = sticky || w[i] != 0;
+    if (sticky) m |= 1;
+    d = ldexp((double)m, 64 * (k - 1) + (64 - lz));
   }
-  double d = (double)m;
-  for (int i = 0; i < shift; ++i) d *= 2.0;  // exact scaling by 2^shift
   return neg ? -d : d;
 }
-__host__ __device__ inline double pgpu_tk_split_sum(const int64_t* t, uint64_t G, int sec, uint64_t row) {
-  // c0 + c1 * 2^21 + c2 * 2^42 with 128-bit arithmetic (each part sum is a signed int64)
-  const int64_t c[3] = {t[(uint64_t)sec * G + row], t[(uint64_t)(sec + 1) * G + row], t[(uint64_t)(sec + 2) * G + row]};
-  int64_t hi = 0;
-  uint64_t lo = 0;
-  for (int p = 0; p < 3; ++p) {
-    const int sh = 21 * p;
-    const uint64_t vlo = sh ? ((uint64_t)c[p] << sh) : (uint64_t)c[p];
-    const int64_t vhi = sh ? (c[p] >> (64 - sh)) : (c[p] < 0 ? -1 : 0);
-    const uint64_t nlo = lo + vlo;
-    hi += vhi + (nlo < lo ? 1 : 0);
-    lo = nlo;
-  }
-  return pgpu_i128_to_double(hi, lo);
+__host__ __device__ inline double pgpu_tk_split_sum(const int64_t* t, uint64_t G, int sec, int parts, uint64_t row) {
+  int64_t c[PGPU_MAX_FIXED_PARTS];
+  for (int p = 0; p < parts && p < PGPU_MAX_FIXED_PARTS; ++p) c[p] = t[(uint64_t)(sec + p) * G + row];
+  return pgpu_parts_to_double(c, parts < PGPU_MAX_FIXED_PARTS ? parts : PGPU_MAX_FIXED_PARTS);
 }
 __host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDev& s, uint64_t row) {
   const uint64_t G = s.G;
@@ -544,7 +556,7 @@ __host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDe
   switch (s.mode) {
     case PGPU_TK_COUNT: u = (uint64_t)cnt ^ 0x8000000000000000ull; break;
     case PGPU_TK_SUM_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row]); break;
-    case PGPU_TK_SUM_SPLIT: u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, row), s.fxe)); break;
+    case PGPU_TK_SUM_SPLIT: u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, s.parts, row), s.fxe)); break;
     case PGPU_TK_SUM_F64: {
       double d;
       __builtin_memcpy(&d, &t[(uint64_t)s.sec * G + row], 8);
@@ -562,7 +574,7 @@ __host__ __device__ inline uint64_t pgpu_topk_key(const int64_t* t, const TopkDe
     }
     case PGPU_TK_AVG_I64: u = pgpu_tk_double((double)t[(uint64_t)s.sec * G + row] / (double)cnt); break;
     case PGPU_TK_AVG_SPLIT:
-      u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, row), s.fxe) / (double)cnt);
+      u = pgpu_tk_double(ldexp(pgpu_tk_split_sum(t, G, s.sec, s.parts, row), s.fxe) / (double)cnt);
       break;
     case PGPU_TK_AVG_F64: {
       double d;

@@ -270,17 +270,35 @@ FI int64_t part_of(int64_t v, int32_t part) {
   if (part == 3) return v >> (2 * PGPU_PART_BITS);
   return v;
 }
-// Fixed-point floating SUM (DevAgg::fxe, pgpu_table_layout.agg_sum_exp): the double v as the integer
-// rint(v * 2^-fxe), |.| < 2^62 by the layout's choice of fxe; integer adds make the sums order-independent.
-FI int64_t fixed_of(int64_t bits, int32_t fxe) {
-  return (int64_t)__builtin_rint(__builtin_ldexp(__longlong_as_double(bits), -fxe));
+// Fixed-point floating SUM (DevAgg::fxe / part, pgpu_table_layout.agg_sum_exp / agg_sum_parts): the double v as
+// the integer I = rint(|v| * 2^-fxe) (< 2^(21 * parts) by the layout's choice), and this section's share of it:
+// sign(v) * bits [21 (part-1), 21 part) of I.  Integer adds make the sums order-independent.  Bits of I above the
+// double's own significand come from shifting it (exact); only a value finer than 2^fxe is rounded.
+FI int64_t fixed_part(int64_t bits, int32_t fxe, int32_t part) {
+  const uint64_t mag = (uint64_t)bits & 0x7FFFFFFFFFFFFFFFull;
+  if (mag == 0) return 0;
+  const int be = (int)(mag >> 52);
+  const uint64_t m = be ? ((mag & 0xFFFFFFFFFFFFFull) | (1ull << 52)) : mag;  // |v| = m * 2^((be ? be : 1) - 1075)
+  const int s = (be ? be : 1) - 1075 - fxe;                                  // I = m * 2^s
+  const int lo = PGPU_PART_BITS * (part - 1);
+  uint64_t d;
+  if (s < 0) {  // below the window's last bit: round (I < 2^53)
+    const uint64_t i = (uint64_t)__builtin_rint(__builtin_ldexp(__longlong_as_double((int64_t)mag), -fxe));
+    d = lo < 64 ? (i >> lo) : 0;
+  } else {
+    const int t = lo - s;  // bits [lo, lo + 21) of m << s = bits [t, t + 21) of m
+    d = t >= 0 ? (t < 64 ? (m >> t) : 0) : (-t < PGPU_PART_BITS ? (m << -t) : 0);
+  }
+  d &= (1ull << PGPU_PART_BITS) - 1;
+  return bits < 0 ? -(int64_t)d : (int64_t)d;
 }
-// gather_cells' SUM values -> the agg's cells: the fixed-point integer of a floating value, then its part section
+// gather_cells' SUM values -> the agg's cells: a floating value's fixed-point part, or an integer's part section
 template <int N>
 FI void apply_part(int64_t (&v)[N], const DevAgg& ag) {
   if (ag.op == PGPU_RED_SUM_I64 && (ag.vtype == PGPU_FLOAT || ag.vtype == PGPU_DOUBLE)) {
 #pragma unroll
-    for (int r = 0; r < N; ++r) v[r] = fixed_of(v[r], ag.fxe);
+    for (int r = 0; r < N; ++r) v[r] = fixed_part(v[r], ag.fxe, ag.part);
+    return;
   }
   if (ag.part == 0) return;
 #pragma unroll

@@ -418,8 +418,7 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
     node_docs += pgpu_desc_docs(&qs[i]);
   }
   uint64_t extra = 0;
-  int32_t node_exp[16];  // fixed-point exponents of the floating SUMs: the largest any device needs
-  for (int a = 0; a < 16; ++a) node_exp[a] = INT32_MIN;
+  int32_t node_exp[16], node_parts[16];  // fixed-point layouts of the floating SUMs, agreed across the devices
   for (size_t i = 0; i < n; ++i) {
     qs[i].reduce_docs = std::max<int64_t>(qs[i].reduce_docs, node_docs);
     const int rc = pgpu_table_layout_of(&qs[i], &L[i]);  // also validates the descriptor
@@ -427,13 +426,17 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
     for (int a = 0; a < qs[i].num_aggs; ++a) {
       const int vt = L[i].agg_value_type[a];
       if (L[i].agg_sum_parts[a] == 3 && (vt == PGPU_INT || vt == PGPU_LONG)) extra |= PGPU_Q_SUM_SPLIT;
-      node_exp[a] = std::max(node_exp[a], L[i].agg_sum_exp[a]);
     }
     if (L[i].key_kind == PGPU_KEYS_HASH) extra |= PGPU_Q_HASH;
+  }
+  {
+    const int rc = pgpu_sum_layout_agree(L.data(), (int32_t)n, qs[0].num_aggs, node_exp, node_parts);
+    if (rc) return rc;
   }
   for (size_t i = 0; i < n; ++i) {
     qs[i].flags |= extra;
     qs[i].sum_exp = node_exp;
+    qs[i].sum_parts = node_parts;
     const int rc = pgpu_table_layout_of(&qs[i], &L[i]);
     if (rc) return rc;
   }
@@ -442,7 +445,8 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
     const bool same = L[i].num_sections == L[0].num_sections && L[i].key_kind == L[0].key_kind &&
                       (hash || L[i].num_keys == L[0].num_keys) &&
                       !memcmp(L[i].section_op, L[0].section_op, sizeof(L[0].section_op)) &&
-                      !memcmp(L[i].agg_sum_exp, L[0].agg_sum_exp, sizeof(L[0].agg_sum_exp));
+                      !memcmp(L[i].agg_sum_exp, L[0].agg_sum_exp, sizeof(L[0].agg_sum_exp)) &&
+                      !memcmp(L[i].agg_sum_parts, L[0].agg_sum_parts, sizeof(L[0].agg_sum_parts));
     if (!same) return nfail(PGPU_E_INVALID, "device %zu's table layout differs from device 0's", i);
   }
   // launch every device, then wait for all

@@ -97,18 +97,39 @@ inline uint32_t le32(const uint8_t* p) {
 int type_width(int32_t t) { return (t == PGPU_INT || t == PGPU_FLOAT) ? 4 : 8; }
 // Running max |value| of a column (HostColumn::max_abs); a NaN or infinity makes it +inf (no fixed-point SUM).
 inline double abs_bound(double m, double v) { return std::isfinite(v) ? std::max(m, std::fabs(v)) : INFINITY; }
-// max |value| of n little-endian values of type t
-double abs_bound_of(const uint8_t* le, size_t n, int32_t t) {
-  double m = 0;
-  for (size_t i = 0; i < n; ++i) {
-    double v;
-    if (t == PGPU_INT) { int32_t x; memcpy(&x, le + 4 * i, 4); v = x; }
-    else if (t == PGPU_LONG) { int64_t x; memcpy(&x, le + 8 * i, 8); v = (double)x; }
-    else if (t == PGPU_FLOAT) { float x; memcpy(&x, le + 4 * i, 4); v = x; }
-    else { double x; memcpy(&x, le + 8 * i, 8); v = x; }
-    m = abs_bound(m, v);
+// Magnitudes of a column's values: max |value| (integer SUM bound, fixed-point top), and for FLOAT / DOUBLE the
+// smallest nonzero |value|'s binary exponent and the lowest set mantissa bit's exponent over all nonzero values --
+// what the fixed-point floating SUM needs to be exact or within its per-value tolerance (pgpu_table_layout_of).
+struct ValueRange {
+  double max_abs = 0;
+  int32_t min_exp = INT32_MAX;  // min ilogb(|v|) over nonzero values
+  int32_t min_lsb = INT32_MAX;  // min exponent of the lowest set bit of v's significand over nonzero values
+  void add_fp(double v) {
+    max_abs = abs_bound(max_abs, v);
+    if (v == 0 || !std::isfinite(v)) return;
+    uint64_t b;
+    memcpy(&b, &v, 8);
+    const int be = (int)((b >> 52) & 0x7ff);
+    const uint64_t m = be ? ((b & ((1ull << 52) - 1)) | (1ull << 52)) : (b & ((1ull << 52) - 1));
+    min_exp = std::min(min_exp, (int32_t)std::ilogb(v));
+    min_lsb = std::min(min_lsb, (int32_t)((be ? be : 1) - 1075 + __builtin_ctzll(m)));
   }
-  return m;
+  void merge(const ValueRange& o) {
+    max_abs = abs_bound(max_abs, o.max_abs);
+    min_exp = std::min(min_exp, o.min_exp);
+    min_lsb = std::min(min_lsb, o.min_lsb);
+  }
+};
+// ValueRange of n little-endian values of type t
+ValueRange value_range_of(const uint8_t* le, size_t n, int32_t t) {
+  ValueRange r;
+  for (size_t i = 0; i < n; ++i) {
+    if (t == PGPU_INT) { int32_t x; memcpy(&x, le + 4 * i, 4); r.max_abs = std::max(r.max_abs, std::fabs((double)x)); }
+    else if (t == PGPU_LONG) { int64_t x; memcpy(&x, le + 8 * i, 8); r.max_abs = std::max(r.max_abs, std::fabs((double)x)); }
+    else if (t == PGPU_FLOAT) { float x; memcpy(&x, le + 4 * i, 4); r.add_fp(x); }
+    else { double x; memcpy(&x, le + 8 * i, 8); r.add_fp(x); }
+  }
+  return r;
 }
 
 // PGPU_PROFILE=1: the query kernel records per-wave phase cycles; pgpu_query_wait prints their averages.
@@ -288,6 +309,13 @@ struct HostColumn {
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
   double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
+  int32_t min_exp = INT32_MAX;         // FLOAT / DOUBLE: ValueRange::min_exp / min_lsb (fixed-point SUM layout)
+  int32_t min_lsb = INT32_MAX;
+  void set_range(const ValueRange& r) {
+    max_abs = r.max_abs;
+    min_exp = r.min_exp;
+    min_lsb = r.min_lsb;
+  }
   int32_t range_index = 0;             // range index version (2 = exact bit-sliced, 1 = legacy), 0 = none
   uint64_t dict_hash[2] = {0, 0};      // two independent 64-bit hashes of the dictionary bytes (shared-dict checks)
   // INT dictionary in frame-of-reference form (phase 2 of the partitioned group-by keeps it in LDS): per block of
@@ -705,7 +733,7 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
       memcpy(&le[8 * (size_t)i], &v, 8);
     }
   }
-  const double max_abs = abs_bound_of(le.data(), (size_t)cardinality, data_type);
+  const ValueRange vr = value_range_of(le.data(), (size_t)cardinality, data_type);
   HIP_TRY(hipSetDevice(seg->ctx->device));
   HIP_TRY(upload(c.dict, le.data(), le.size(), le.size(), PGPU_MEM_HOST));
   c.dict_bytes = num_bytes;
@@ -740,7 +768,7 @@ int pgpu_segment_add_dictionary(pgpu_segment* seg, int32_t column, int32_t data_
   }
   dictionary_hash(le, c.dict_hash);
   c.hdict = std::move(le);
-  c.max_abs = max_abs;
+  c.set_range(vr);
   return PGPU_OK;
 }
 
@@ -759,7 +787,7 @@ int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_
   std::string err;
   rc = pgpu_decode_raw_forward((const uint8_t*)bytes, num_bytes, w, seg->num_docs, &le, &err);
   if (rc) return fail(rc, "raw forward index of column %d: %s", column, err.c_str());
-  const double max_abs = abs_bound_of(le.data(), (size_t)seg->num_docs, data_type);
+  const ValueRange vr = value_range_of(le.data(), (size_t)seg->num_docs, data_type);
   // padded to whole PGPU_TILE-doc tiles (+16 B) like a fixed-bit stream: the kernels read whole tiles of "ids"
   const uint64_t ntiles = ((uint64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE;
   const uint64_t alloc = std::max<uint64_t>(1, ntiles) * PGPU_TILE * w + 16;
@@ -770,7 +798,7 @@ int pgpu_segment_add_raw_forward_index(pgpu_segment* seg, int32_t column, int32_
   c.fwd_card = seg->num_docs;
   c.fwd_bytes = num_bytes;
   c.dict_bytes = le.size();
-  c.max_abs = max_abs;
+  c.set_range(vr);
   return PGPU_OK;
 }
 
@@ -861,7 +889,7 @@ int pgpu_segment_mv_row(pgpu_segment* seg, int32_t column, int32_t doc, int32_t*
 
 namespace {
 // Install host little-endian values as a raw column in `slot` (padded like a decoded raw forward index).
-int install_raw(pgpu_segment* seg, int32_t slot, int32_t data_type, std::vector<uint8_t>& le, double max_abs) {
+int install_raw(pgpu_segment* seg, int32_t slot, int32_t data_type, std::vector<uint8_t>& le, const ValueRange& vr) {
   int rc = check_column(seg, slot);
   if (rc) return rc;
   HostColumn& c = seg->cols[slot];
@@ -874,7 +902,7 @@ int install_raw(pgpu_segment* seg, int32_t slot, int32_t data_type, std::vector<
   c.dict_type = data_type;
   c.fwd_card = seg->num_docs;
   c.dict_bytes = le.size();
-  c.max_abs = max_abs;
+  c.set_range(vr);
   return PGPU_OK;
 }
 }  // namespace
@@ -936,10 +964,17 @@ int pgpu_segment_add_mv_row_columns(pgpu_segment* seg, int32_t column, int32_t l
     memcpy(&maxs[w * (size_t)d], &c.hdict[w * (size_t)hi_id], w);
   }
   HIP_TRY(hipSetDevice(seg->ctx->device));
-  if (len_column >= 0 && (rc = install_raw(seg, len_column, PGPU_INT, lens, max_len))) return rc;
-  if (sum_column >= 0 && (rc = install_raw(seg, sum_column, fp ? PGPU_DOUBLE : PGPU_LONG, sums, max_sum))) return rc;
-  if (min_column >= 0 && (rc = install_raw(seg, min_column, t, mins, max_val))) return rc;
-  if (max_column >= 0 && (rc = install_raw(seg, max_column, t, maxs, max_val))) return rc;
+  ValueRange r_len, r_sum, r_val;
+  r_len.max_abs = max_len;
+  if (fp) r_sum = value_range_of(sums.data(), (size_t)n, PGPU_DOUBLE);  // row sums: their own fixed-point range
+  r_sum.max_abs = max_sum;
+  r_val.max_abs = max_val;
+  r_val.min_exp = c.min_exp;  // row min / max values are dictionary values
+  r_val.min_lsb = c.min_lsb;
+  if (len_column >= 0 && (rc = install_raw(seg, len_column, PGPU_INT, lens, r_len))) return rc;
+  if (sum_column >= 0 && (rc = install_raw(seg, sum_column, fp ? PGPU_DOUBLE : PGPU_LONG, sums, r_sum))) return rc;
+  if (min_column >= 0 && (rc = install_raw(seg, min_column, t, mins, r_val))) return rc;
+  if (max_column >= 0 && (rc = install_raw(seg, max_column, t, maxs, r_val))) return rc;
   return PGPU_OK;
 }
 
@@ -1117,7 +1152,7 @@ int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int
                             (uint32_t*)ids.p, (uint32_t*)fwd.p, nwords, nullptr));
   std::vector<uint8_t> le((size_t)w * card);
   HIP_TRY(hipMemcpy(le.data(), dict.p, le.size(), hipMemcpyDeviceToHost));
-  const double max_abs = abs_bound_of(le.data(), (size_t)card, t);
+  const ValueRange vr = value_range_of(le.data(), (size_t)card, t);
   c.dict = std::move(dict);
   c.fwd = std::move(fwd);
   c.dict_type = t;
@@ -1127,7 +1162,7 @@ int pgpu_segment_add_group_dictionary(pgpu_segment* seg, int32_t raw_column, int
   c.bits = bits;
   c.fwd_card = (int32_t)card;
   c.fwd_bytes = need;
-  c.max_abs = max_abs;
+  c.set_range(vr);
   dictionary_hash(le, c.dict_hash);
   c.hdict = std::move(le);
   if (seg->sealed) {
@@ -1213,6 +1248,63 @@ int pgpu_buffer_release(pgpu_buffer* buf) {
   return PGPU_OK;
 }
 
+void pgpu_fixed_sum_layout(double max_abs, int32_t min_exp, int32_t min_lsb, int32_t* out_exp, int32_t* out_parts) {
+  if (!(max_abs > 0)) {  // no nonzero value: any window holds the zero sums
+    *out_exp = PGPU_SUM_EXP_ZERO;
+    *out_parts = 3;
+    return;
+  }
+  // every |v| < 2^top, and rint(|v| * 2^-e) <= 2^(top - 1) < 2^(21 * parts) even where rounding carries up
+  const int32_t top = (int32_t)std::ilogb(max_abs) + 2;
+  // the exponent each value needs: its own last bit (exact), or 41 bits below its leading bit (rounding error
+  // <= 2^-41 |v|), whichever is coarser
+  const int64_t need = std::max<int64_t>(min_lsb, (int64_t)min_exp - PGPU_FIXED_TOL_BITS);
+  const int64_t span = (int64_t)top - need;
+  const int64_t parts = std::max<int64_t>(3, (span + PGPU_PART_BITS - 1) / PGPU_PART_BITS);
+  if (parts > PGPU_MAX_FIXED_PARTS) {
+    *out_exp = PGPU_SUM_EXP_F64;
+    *out_parts = 1;
+    return;
+  }
+  *out_exp = top - PGPU_PART_BITS * (int32_t)parts;
+  *out_parts = (int32_t)parts;
+}
+
+int pgpu_sum_layout_agree(const pgpu_table_layout* layouts, int32_t num_layouts, int32_t num_aggs, int32_t* out_exp,
+                          int32_t* out_parts) {
+  if (!layouts || num_layouts < 1 || num_aggs < 0 || num_aggs > 16 || !out_exp || !out_parts)
+    return fail(PGPU_E_INVALID, "bad sum layout arguments");
+  for (int a = 0; a < num_aggs; ++a) {
+    int64_t top = INT64_MIN, bottom = INT64_MAX;
+    bool f64 = false, any = false;
+    for (int i = 0; i < num_layouts; ++i) {
+      const pgpu_table_layout& L = layouts[i];
+      const int vt = L.agg_value_type[a];
+      if (vt != PGPU_FLOAT && vt != PGPU_DOUBLE) continue;
+      const int32_t e = L.agg_sum_exp[a];
+      if (e == PGPU_SUM_EXP_F64) f64 = true;
+      if (e == PGPU_SUM_EXP_F64 || e == PGPU_SUM_EXP_ZERO || L.agg_sum_parts[a] < 1) continue;
+      any = true;
+      top = std::max<int64_t>(top, (int64_t)e + PGPU_PART_BITS * L.agg_sum_parts[a]);
+      bottom = std::min<int64_t>(bottom, e);
+    }
+    out_exp[a] = 0;
+    out_parts[a] = 0;
+    if (f64) {
+      out_exp[a] = PGPU_SUM_EXP_F64;
+      out_parts[a] = 1;
+    } else if (!any) {
+      out_exp[a] = PGPU_SUM_EXP_ZERO;
+      out_parts[a] = 3;
+    } else {
+      const int64_t parts = std::max<int64_t>(3, (top - bottom + PGPU_PART_BITS - 1) / PGPU_PART_BITS);
+      out_parts[a] = (int32_t)std::min<int64_t>(parts, PGPU_MAX_FIXED_PARTS + 1);  // > MAX: every layout takes f64
+      out_exp[a] = (int32_t)(top - PGPU_PART_BITS * parts);
+    }
+  }
+  return PGPU_OK;
+}
+
 int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
   if (!q || !out) return fail(PGPU_E_INVALID, "null argument");
   if (q->num_aggs < 0 || q->num_aggs > PGPU_MAX_AGGS) return fail(PGPU_E_UNSUPPORTED, "%d aggregations", q->num_aggs);
@@ -1229,44 +1321,70 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
   for (int s = 0; s < q->num_segments; ++s)
     if (q->segments[s].segment) docs += q->segments[s].segment->num_docs;
   docs = std::max<int64_t>(docs, q->reduce_docs);
-  // FLOAT / DOUBLE SUM / AVG in fixed point (three part sections each) when every such column is finite and the
-  // sections fit; otherwise all of them keep a float64 section.  PGPU_NO_FIXED_SUM=1 forces float64.
+  // FLOAT / DOUBLE SUM / AVG in fixed point (fx_parts[a] 21-bit part sections each, pgpu_fixed_sum_layout) when the
+  // column is finite and the part count fits; otherwise that aggregation keeps a float64 section (and all of them do
+  // when the part sections would not fit the table).  PGPU_NO_FIXED_SUM=1 forces float64.
   static const bool no_fixed = getenv("PGPU_NO_FIXED_SUM") && atoi(getenv("PGPU_NO_FIXED_SUM")) != 0;
-  int32_t fx_exp[16];
-  bool fixed = !no_fixed;
+  if (q->sum_exp && !q->sum_parts) return fail(PGPU_E_INVALID, "sum_exp without sum_parts");
+  int32_t fx_exp[16], fx_parts[16];
+  bool fixed_all = !no_fixed;
   {
     int with_fixed = 1, without = 1;  // sections of either choice
     for (int a = 0; a < q->num_aggs; ++a) {
       const pgpu_agg& ag = q->aggs[a];
       fx_exp[a] = 0;
+      fx_parts[a] = 0;
       if (ag.fn == PGPU_AGG_COUNT) continue;
       int32_t vt = -1;
-      double max_abs = 0;
+      ValueRange vr;
       if (ag.column >= 0 && ag.column < q->num_columns)
         for (int s = 0; s < q->num_segments; ++s) {
           const pgpu_segment* sg = q->segments[s].segment;
           const int32_t sl = q->segments[s].column_map ? q->segments[s].column_map[ag.column] : -1;
           if (!sg || sl < 0 || sl >= (int32_t)sg->cols.size()) continue;  // reported below
           if (vt < 0) vt = sg->cols[sl].dict_type;
-          max_abs = abs_bound(max_abs, sg->cols[sl].max_abs);
+          ValueRange c;
+          c.max_abs = sg->cols[sl].max_abs;
+          c.min_exp = sg->cols[sl].min_exp;
+          c.min_lsb = sg->cols[sl].min_lsb;
+          vr.merge(c);
         }
       const bool sum = ag.fn == PGPU_AGG_SUM || ag.fn == PGPU_AGG_AVG;
       if (sum && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE)) {
-        int32_t e = max_abs > 0 ? (int32_t)std::ilogb(max_abs) + 1 - 62 : -1100;  // |v| * 2^-e < 2^62
-        if (!std::isfinite(max_abs)) e = PGPU_SUM_EXP_F64;
-        if (q->sum_exp) e = std::max(e, q->sum_exp[a]);
-        if (e >= PGPU_SUM_EXP_F64) fixed = false;
+        int32_t e = PGPU_SUM_EXP_F64, parts = 1;
+        if (std::isfinite(vr.max_abs)) pgpu_fixed_sum_layout(vr.max_abs, vr.min_exp, vr.min_lsb, &e, &parts);
+        if (q->sum_exp && e != PGPU_SUM_EXP_F64) {  // the layout agreed across launches (pgpu_sum_layout_agree)
+          const int32_t ge = q->sum_exp[a], gp = q->sum_parts[a];
+          if (ge == PGPU_SUM_EXP_F64) {
+            e = PGPU_SUM_EXP_F64;
+          } else if (ge == PGPU_SUM_EXP_ZERO) {
+            if (e != PGPU_SUM_EXP_ZERO) return fail(PGPU_E_INVALID, "agg %d: agreed fixed-point layout is empty", a);
+          } else if (gp > PGPU_MAX_FIXED_PARTS) {
+            e = PGPU_SUM_EXP_F64;
+          } else {
+            // the agreed window must hold this launch's values at no less precision than its own choice
+            if (gp < 3 || (e != PGPU_SUM_EXP_ZERO && (ge > e || ge + 21 * gp < e + 21 * parts)))
+              return fail(PGPU_E_INVALID, "agg %d: agreed fixed-point layout (2^%d, %d parts) does not cover the launch",
+                          a, ge, gp);
+            e = ge;
+            parts = gp;
+          }
+        } else if (q->sum_exp && q->sum_exp[a] != PGPU_SUM_EXP_F64) {
+          return fail(PGPU_E_INVALID, "agg %d: agreed fixed-point layout for a column with NaN / infinity", a);
+        }
+        if (e == PGPU_SUM_EXP_F64) parts = 1;
         fx_exp[a] = e;
-        with_fixed += 3;
+        fx_parts[a] = parts;
+        with_fixed += parts;
         without += 1;
       } else {
-        const int k = sum && ((q->flags & PGPU_Q_SUM_SPLIT) || max_abs * (double)docs >= 4.611686018427388e18) ? 3 : 1;
+        const int k = sum && ((q->flags & PGPU_Q_SUM_SPLIT) || vr.max_abs * (double)docs >= 4.611686018427388e18) ? 3 : 1;
         with_fixed += k;
         without += k;
       }
     }
     // the float64 sections when the part sections would not fit (and the integer ones would)
-    if (with_fixed > PGPU_MAX_SECTIONS && without <= PGPU_MAX_SECTIONS) fixed = false;
+    if (with_fixed > PGPU_MAX_SECTIONS && without <= PGPU_MAX_SECTIONS) fixed_all = false;
   }
   for (int a = 0; a < q->num_aggs; ++a) {
     const pgpu_agg& ag = q->aggs[a];
@@ -1285,16 +1403,17 @@ int pgpu_table_layout_of(const pgpu_query_desc* q, pgpu_table_layout* out) {
     int op;
     if (ag.fn == PGPU_AGG_MIN) op = PGPU_RED_MIN_I64;
     else if (ag.fn == PGPU_AGG_MAX) op = PGPU_RED_MAX_I64;
-    else op = (vt == PGPU_INT || vt == PGPU_LONG || fixed) ? PGPU_RED_SUM_I64 : PGPU_RED_SUM_F64;
+    else op = (vt == PGPU_INT || vt == PGPU_LONG || (fixed_all && fx_exp[a] != PGPU_SUM_EXP_F64)) ? PGPU_RED_SUM_I64
+                                                                                                  : PGPU_RED_SUM_F64;
     // integer SUM: one int64 cell while max|value| x docs stays below 2^62, else three exact part sums; fixed-point
-    // floating SUM: always three part sums
+    // floating SUM: fx_parts[a] part sums
     int parts = 1;
     out->agg_sum_exp[a] = 0;
     if (op == PGPU_RED_SUM_F64) {
       out->agg_sum_exp[a] = PGPU_SUM_EXP_F64;
     } else if (op == PGPU_RED_SUM_I64 && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE)) {
       out->agg_sum_exp[a] = fx_exp[a];
-      parts = 3;
+      parts = fx_parts[a];
     } else if (op == PGPU_RED_SUM_I64) {
       double max_abs = 0;
       for (int s = 0; s < q->num_segments; ++s) {
@@ -2411,7 +2530,7 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
       d.op = L.section_op[d.sec];
       d.vtype = L.agg_value_type[a];
       d.emit = 0;
-      d.part = parts == 3 ? k + 1 : 0;
+      d.part = parts > 1 ? k + 1 : 0;
       d.fxe = L.agg_sum_exp[a];
     }
   }
@@ -3408,10 +3527,11 @@ int topk_spec(const pgpu_table_layout* L, const pgpu_topk* o, TopkDev* out) {
     if (a < 0 || a >= 16) return fail(PGPU_E_INVALID, "top-k aggregation index %d", a);
     const int sec = L->agg_section[a];
     t.sec = sec;
-    const bool split = L->agg_sum_parts[a] == 3;
+    const bool split = L->agg_sum_parts[a] > 1;
     const int op = L->section_op[sec];
     const int vt = L->agg_value_type[a];
     t.fxe = split && (vt == PGPU_FLOAT || vt == PGPU_DOUBLE) ? L->agg_sum_exp[a] : 0;
+    t.parts = split ? L->agg_sum_parts[a] : 1;
     switch (o->agg_fn) {
       case PGPU_AGG_COUNT: t.mode = PGPU_TK_COUNT; break;
       case PGPU_AGG_SUM:

@@ -344,20 +344,39 @@ class QueryResult:
         return self._intermediate
 
 
-def join_parts(row_cells, sec: int, parts: int, exp: int = 0):
-    """Exact SUM of a cell split into 21-bit-part sections (pgpu_table_layout.agg_sum_parts == 3):
-    c[sec] + c[sec+1] * 2^21 + c[sec+2] * 2^42, as a Python int (rounded once, on conversion to double); a
-    fixed-point floating SUM (agg_sum_exp = exp != 0) is that integer times 2^exp, rounded once to a double."""
-    if parts != 3:
+def join_parts(row_cells, sec: int, parts: int, exp: Optional[int] = None):
+    """Exact SUM of a cell split into 21-bit-part sections (pgpu_table_layout.agg_sum_parts > 1):
+    sum_k c[sec+k] * 2^(21k), as a Python int (rounded once, on conversion to double).  A fixed-point floating SUM
+    (exp = its agg_sum_exp, see sum_exp_of) is that integer times 2^exp, rounded once to a double -- +-infinity past
+    DBL_MAX, as the reference's double adds overflow."""
+    if parts <= 1:
         return int(row_cells[sec])
     b = _lib.PGPU_PART_BITS
-    total = int(row_cells[sec]) + (int(row_cells[sec + 1]) << b) + (int(row_cells[sec + 2]) << (2 * b))
-    return math.ldexp(float(total), exp) if exp else total
+    total = sum(int(row_cells[sec + k]) << (b * k) for k in range(parts))
+    if exp is None:
+        return total
+    if total == 0 or exp == _lib.PGPU_SUM_EXP_ZERO:
+        return 0.0
+    try:
+        return math.ldexp(float(total), exp)
+    except OverflowError:
+        return math.inf if total > 0 else -math.inf
 
 
-def sum_exp_of(L: TableLayout, ai: int) -> int:
-    """The fixed-point exponent of aggregation ai's split SUM (0 = an integer sum)."""
-    return L.agg_sum_exp[ai] if L.agg_value_type[ai] in (PGPU_FLOAT, PGPU_DOUBLE) and L.agg_sum_parts[ai] == 3 else 0
+def sum_exp_of(L: TableLayout, ai: int) -> Optional[int]:
+    """The fixed-point exponent of aggregation ai's split SUM, or None for an integer (or float64) sum: fixed point is
+    a FLOAT / DOUBLE SUM carried in part sections, whatever its exponent (0 is a valid one)."""
+    if L.agg_value_type[ai] in (PGPU_FLOAT, PGPU_DOUBLE) and L.agg_sum_parts[ai] > 1:
+        return L.agg_sum_exp[ai]
+    return None
+
+
+def fixed_window(top: int, bottom: int) -> Tuple[int, int]:
+    """(exp, parts) of the fixed-point window covering [2^bottom, 2^top) in 21-bit parts (at least 3), as
+    pgpu_sum_layout_agree chooses it; parts > PGPU_MAX_FIXED_PARTS means every launch keeps a float64 section."""
+    b = _lib.PGPU_PART_BITS
+    p = max(3, -(-(top - bottom) // b))
+    return top - b * p, min(p, _lib.PGPU_MAX_FIXED_PARTS + 1)
 
 
 def final_value(fn: str, cell_count: int, cell: Optional[int], op: int, vtype: int):
@@ -629,12 +648,13 @@ class GpuPlanMaker:
         return arr, len(nodes), la
 
     def build_desc(self, query: QueryContext, segments: Sequence[GpuSegment], plan_filters: bool = True,
-                   extra_flags: int = 0, reduce_docs: int = 0, sum_exp: Optional[Sequence[int]] = None):
+                   extra_flags: int = 0, reduce_docs: int = 0,
+                   sum_layout: Optional[Tuple[Sequence[int], Sequence[int]]] = None):
         """Build the pgpu_query_desc.  Returns (desc, keep, globals_): `keep` owns every buffer the descriptor
         points to (one node array, one id pool, one column-map array, one remap-handle array, one plan array).
         plan_filters=False leaves the per-segment filter programs empty (the library plans them from
-        filter_expr); sum_exp (per aggregation) is the lower bound of the floating SUMs' fixed-point exponents that
-        callers combining tables across ranks agree on (pgpu_query_desc.sum_exp)."""
+        filter_expr); sum_layout = (exps, parts) per aggregation is the floating SUMs' fixed-point layout that callers
+        combining tables across ranks agree on (fixed_window; pgpu_query_desc.sum_exp / sum_parts)."""
         columns = list(query.columns)
         col_index = {c: i for i, c in enumerate(columns)}
         nseg = len(segments)
@@ -697,8 +717,10 @@ class GpuPlanMaker:
             *[Agg(AGG_FN[a.function], -1 if a.column is None else col_index[a.column]) for a in query.aggregations])
         gcols = (C.c_int32 * max(1, ng))(*[group_col[g] for g in query.group_by])
         gcards = (C.c_int32 * max(1, ng))(*[len(g[0]) for g in globals_])
-        sexp = (C.c_int32 * max(1, len(query.aggregations)))(*(sum_exp or [])) if sum_exp is not None else None
-        keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards, sexp]
+        na = max(1, len(query.aggregations))
+        sexp = (C.c_int32 * na)(*sum_layout[0]) if sum_layout is not None else None
+        sparts = (C.c_int32 * na)(*sum_layout[1]) if sum_layout is not None else None
+        keep = [cmap, pool, vpool, narr, remap, plans, aggs, gcols, gcards, sexp, sparts]
         desc = QueryDesc(num_columns=len(columns), num_segments=nseg,
                          segments=C.cast(C.c_void_p(plans.ctypes.data), C.POINTER(SegmentPlan)),
                          num_aggs=len(query.aggregations), num_group_columns=ng, aggs=aggs,
@@ -710,7 +732,8 @@ class GpuPlanMaker:
                          # column no segment is array-based (a segment meeting more keys goes back to the CPU)
                          array_based_threshold=0 if no_dict else self.max_init_group_holder_capacity,
                          deadline_ms=0 if self.timeout_ms is None else int(time.time() * 1000) + int(self.timeout_ms),
-                         sum_exp=C.cast(sexp, C.POINTER(C.c_int32)) if sexp is not None else None)
+                         sum_exp=C.cast(sexp, C.POINTER(C.c_int32)) if sexp is not None else None,
+                         sum_parts=C.cast(sparts, C.POINTER(C.c_int32)) if sparts is not None else None)
         return desc, keep, globals_
 
     def layout(self, desc: QueryDesc) -> TableLayout:
@@ -1106,10 +1129,10 @@ class GroupColumns:
         s = None
         if fn == "COUNT":
             f = cnt.astype(np.int64)
-        elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] == 3:
+        elif fn in ("SUM", "AVG") and L.agg_sum_parts[ai] > 1:
             # split sum: join the parts exactly (Python ints), round once to double (fixed point: times 2^exp)
-            e = sum_exp_of(L, ai)
-            s = np.array([float(join_parts(r, sec, 3, e)) for r in cells], dtype=np.float64)
+            e, parts = sum_exp_of(L, ai), L.agg_sum_parts[ai]
+            s = np.array([float(join_parts(r, sec, parts, e)) for r in cells], dtype=np.float64)
             f = s if fn == "SUM" else s / cnt
         elif fn in ("SUM", "AVG"):
             s = cell.astype(np.float64) if op == PGPU_RED_SUM_I64 else cell.view(np.float64)

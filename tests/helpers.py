@@ -109,3 +109,41 @@ def check_groups(res, ref, rel=1e-9):
         assert set(g) == set(o), (len(g), len(o))
     for k in g:
         assert rows_close([g[k]], [o[k]], rel), (k, g[k], o[k])
+
+
+# ---- fixed-point floating SUM restated (include/pinot_gpu.h, pgpu_fixed_sum_layout / the kernels' fixed_part) ----
+def fixed_sum_layout(values):
+    """(exp, parts) pgpu_fixed_sum_layout picks for these FLOAT / DOUBLE values (as doubles)."""
+    from pinot_amd import _lib
+    v = np.asarray(values, dtype=np.float64)
+    if not np.all(np.isfinite(v)):
+        return _lib.PGPU_SUM_EXP_F64, 1
+    nz = np.abs(v[v != 0])
+    if len(nz) == 0:
+        return _lib.PGPU_SUM_EXP_ZERO, 3
+    top = math.frexp(float(nz.max()))[1] + 1  # ilogb(max) + 2
+    min_exp = math.frexp(float(nz.min()))[1] - 1
+    min_lsb = min(_lsb_exp(float(x)) for x in np.unique(nz))
+    need = max(min_lsb, min_exp - _lib.PGPU_FIXED_TOL_BITS)
+    parts = max(3, -(-(top - need) // _lib.PGPU_PART_BITS))
+    if parts > _lib.PGPU_MAX_FIXED_PARTS:
+        return _lib.PGPU_SUM_EXP_F64, 1
+    return top - _lib.PGPU_PART_BITS * parts, parts
+
+
+def _lsb_exp(x: float) -> int:
+    m, e = math.frexp(abs(x))
+    M = int(m * (1 << 53))  # exact: x = M * 2^(e - 53)
+    return e - 53 + ((M & -M).bit_length() - 1)
+
+
+def fixed_digits(x: float, exp: int, parts: int):
+    """The part sections' shares of x: sign(x) * 21-bit digits of rint(|x| * 2^-exp) (half to even)."""
+    from fractions import Fraction
+    from pinot_amd import _lib
+    if x == 0:
+        return [0] * parts
+    i = round(Fraction(abs(x)) / Fraction(2) ** exp)
+    b, m = _lib.PGPU_PART_BITS, (1 << _lib.PGPU_PART_BITS) - 1
+    sg = -1 if x < 0 else 1
+    return [sg * ((i >> (b * k)) & m) for k in range(parts)]

@@ -90,3 +90,49 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
         assert int(out[cname]) == C.sizeof(ct), cname
         for fname, _ in ct._fields_:
             assert int(out[f"{cname}.{fname}"]) == getattr(ct, fname).offset, (cname, fname)
+
+
+def test_fixed_sum_layout_matches_restatement():
+    """pgpu_fixed_sum_layout (the layout's fixed-point window) against tests/helpers.fixed_sum_layout."""
+    import math
+    import numpy as np
+    from tests.helpers import _lsb_exp, fixed_sum_layout
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    cases = [np.array([0.0]), np.array([1.0, 2.0, 3.0]), np.array([0.5, 0.25]), np.array([1e-3, 1e12]),
+             np.array([1e-20, 1.0]), np.array([1e-200, 1e200]), rng.normal(0, 1, 1000), np.array([-7.5, 3e9]),
+             np.round(rng.normal(0, 100, 500), 2), np.array([5e-324, 1.0]), np.array([2.0 ** 61, 1.0]),
+             rng.uniform(1, 2, 100).astype(np.float32).astype(np.float64)]
+    for v in cases:
+        nz = np.abs(v[v != 0])
+        mx = float(np.abs(v).max())
+        mn_exp = math.frexp(float(nz.min()))[1] - 1 if len(nz) else 2 ** 31 - 1
+        mn_lsb = min(_lsb_exp(float(x)) for x in nz) if len(nz) else 2 ** 31 - 1
+        e, p = C.c_int32(), C.c_int32()
+        lib.pgpu_fixed_sum_layout(mx, mn_exp, mn_lsb, C.byref(e), C.byref(p))
+        assert (e.value, p.value) == fixed_sum_layout(v), (v[:4], e.value, p.value, fixed_sum_layout(v))
+
+
+def test_sum_layout_agree_matches_combine():
+    """pgpu_sum_layout_agree (the node combine) and plan.fixed_window (combine.py over RCCL) choose one window."""
+    from pinot_amd.plan import fixed_window
+    lib = _lib.load()
+    cases = [[(-40, 3)], [(-40, 3), (-20, 3)], [(-90, 5), (-10, 3)], [(-120, 6), (10, 3)],
+             [(_lib.PGPU_SUM_EXP_ZERO, 3), (-50, 4)], [(_lib.PGPU_SUM_EXP_F64, 1), (-50, 4)],
+             [(_lib.PGPU_SUM_EXP_ZERO, 3)]]
+    for case in cases:
+        arr = (_lib.TableLayout * len(case))()
+        for i, (e, p) in enumerate(case):
+            arr[i].agg_value_type[0] = _lib.PGPU_DOUBLE
+            arr[i].agg_sum_exp[0] = e
+            arr[i].agg_sum_parts[0] = p
+        oe, op = (C.c_int32 * 1)(), (C.c_int32 * 1)()
+        assert lib.pgpu_sum_layout_agree(arr, len(case), 1, oe, op) == 0
+        live = [(e, p) for e, p in case if e not in (_lib.PGPU_SUM_EXP_F64, _lib.PGPU_SUM_EXP_ZERO)]
+        if any(e == _lib.PGPU_SUM_EXP_F64 for e, _ in case):
+            want = (_lib.PGPU_SUM_EXP_F64, 1)
+        elif not live:
+            want = (_lib.PGPU_SUM_EXP_ZERO, 3)
+        else:
+            want = fixed_window(max(e + 21 * p for e, p in live), min(e for e, _ in live))
+        assert (oe[0], op[0]) == want, (case, oe[0], op[0], want)

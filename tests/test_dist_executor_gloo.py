@@ -23,9 +23,11 @@ torch = pytest.importorskip("torch")
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-from pinot_amd._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_PART_BITS,  # noqa: E402
-                            PGPU_Q_SUM_SPLIT, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64,
+from pinot_amd._lib import (PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_MAX_FIXED_PARTS,  # noqa: E402
+                            PGPU_PART_BITS, PGPU_Q_SUM_SPLIT, PGPU_SUM_EXP_F64, PGPU_RED_MAX_I64, PGPU_RED_MIN_I64, PGPU_RED_SUM_F64,
                             PGPU_RED_SUM_I64, PGPU_STRING, TableLayout)
+
+from tests.helpers import fixed_digits, fixed_sum_layout  # noqa: E402
 
 WORLD = 2
 
@@ -93,8 +95,9 @@ def _plan_maker():
     return HostPlanMaker(ctx=None)
 
 
-def _layout(query, segments, flags, reduce_docs, globs, sum_exp=None):
-    """pgpu_table_layout_of restated (include/pinot_gpu.h), floating SUMs in fixed point."""
+def _layout(query, segments, flags, reduce_docs, globs, sum_layout=None):
+    """pgpu_table_layout_of restated (include/pinot_gpu.h), floating SUMs in fixed point (helpers.fixed_sum_layout;
+    an agreed sum_layout = (exps, parts) taken verbatim)."""
     L = TableLayout()
     G = 1
     for g in query.group_by:
@@ -111,10 +114,13 @@ def _layout(query, segments, flags, reduce_docs, globs, sum_exp=None):
         parts = 1
         L.agg_sum_exp[i] = 0
         if op == PGPU_RED_SUM_I64 and vt not in (PGPU_INT, PGPU_LONG):
-            mx = max(float(np.abs(s.dictionaries[a.column].astype(np.float64)).max()) for s in segments)
-            e = math.frexp(mx)[1] - 62 if mx > 0 else -1100
-            L.agg_sum_exp[i] = max(e, sum_exp[i]) if sum_exp is not None else e
-            parts = 3
+            vals = np.concatenate([np.asarray(s.dictionaries[a.column], dtype=np.float64) for s in segments])
+            e, parts = fixed_sum_layout(vals)
+            if sum_layout is not None:
+                e, parts = sum_layout[0][i], sum_layout[1][i]
+            if e == PGPU_SUM_EXP_F64 or parts > PGPU_MAX_FIXED_PARTS:
+                op, e, parts = PGPU_RED_SUM_F64, PGPU_SUM_EXP_F64, 1
+            L.agg_sum_exp[i] = e
         elif op == PGPU_RED_SUM_I64:
             mx = max(float(np.abs(s.dictionaries[a.column].astype(np.float64)).max()) for s in segments)
             parts = 3 if (flags & PGPU_Q_SUM_SPLIT) or mx * docs >= 2.0 ** 62 else 1
@@ -135,10 +141,10 @@ def _numpy_executor(pm):
         """The local kernel step in numpy: the table pgpu_query_launch leaves in HBM (dense cells indexed by the
         mixed-radix key, or -- PGPU_Q_HASH -- slots whose key words follow the sections)."""
 
-        def _prepare_local(self, query, segments, flags, reduce_docs, sum_exp=None):
+        def _prepare_local(self, query, segments, flags, reduce_docs, sum_layout=None):
             flags |= self.pm.query_flags
             globs = self._globals_of(query, segments)
-            L = _layout(query, segments, flags, reduce_docs, globs, sum_exp)
+            L = _layout(query, segments, flags, reduce_docs, globs, sum_layout)
             ops = [L.section_op[k] for k in range(L.num_sections)]
             st = {"num_docs_scanned": 0, "num_entries_scanned_in_filter": 0, "num_total_docs": 0,
                   "num_segments_matched": 0, "sparse_sector_bytes": 0, "dense_bytes": 0, "kernel_ms": 0.0}
@@ -185,10 +191,14 @@ def _numpy_executor(pm):
                     v = np.asarray(ds.values(a.column))[docs]
                     o = L.section_op[sec]
                     if o == PGPU_RED_SUM_I64:
-                        if L.agg_value_type[i] in (PGPU_INT, PGPU_LONG):
-                            v = v.astype(np.int64)
-                        else:  # fixed point: rint(v * 2^-exp)
-                            v = np.rint(np.ldexp(v.astype(np.float64), -L.agg_sum_exp[i])).astype(np.int64)
+                        if L.agg_value_type[i] not in (PGPU_INT, PGPU_LONG):  # fixed point: signed digits of |I|
+                            P = L.agg_sum_parts[i]
+                            digits = np.array([fixed_digits(float(x), L.agg_sum_exp[i], P) for x in v],
+                                              dtype=np.int64).reshape(len(v), P)
+                            for k in range(P):
+                                np.add.at(t[sec + k], cell, digits[:, k])
+                            continue
+                        v = v.astype(np.int64)
                         if L.agg_sum_parts[i] == 3:
                             m = (1 << PGPU_PART_BITS) - 1
                             for k, part in enumerate((v & m, (v >> PGPU_PART_BITS) & m, v >> (2 * PGPU_PART_BITS))):
