@@ -552,14 +552,30 @@ class DistributedExecutor:
 
         from .datatable import _merge
         from .plan import result_from_intermediate
-        r = self.pm.first_seen_groups(p.query, p.segments)
-        mine = (r.intermediate, {f: getattr(r.stats, f) for f in STAT_FIELDS},
-                bool(r.stats.num_groups_limit_reached), bool(r.stats.filter_stats_exact), r.stats.kernel_ms)
-        every = [None] * self.world
-        dist.all_gather_object(every, mine, group=self.group)
-        tot = {f: sum(e[1][f] for e in every) for f in STAT_FIELDS}
-        st = ExecutionStats(kernel_ms=r.stats.kernel_ms, num_groups_limit_reached=any(e[2] for e in every),
-                            filter_stats_exact=all(e[3] for e in every), **tot)
+        # a failure on one rank must not leave the others waiting in the collective: every rank sends its outcome
+        # (an error travels as its message) and all of them raise together
+        try:
+            r = self.pm.first_seen_groups(p.query, p.segments)
+            mine = (r.intermediate, {f: getattr(r.stats, f) for f in STAT_FIELDS},
+                    bool(r.stats.num_groups_limit_reached), bool(r.stats.filter_stats_exact), r.stats.kernel_ms, None)
+        except Exception as exc:  # noqa: BLE001 -- re-raised below on every rank
+            r, mine = None, (None, None, False, False, 0.0, f"rank {self.rank}: {type(exc).__name__}: {exc}")
+        failed = self._allreduce_i64([0 if mine[5] is None else 1], "max")[0]
+        if failed:
+            msg = [None] * self.world
+            dist.all_gather_object(msg, mine[5], group=self.group)
+            raise _lib.PinotGpuError(_lib.PGPU_E_INVALID, "first-seen group path failed: " +
+                                     "; ".join(m for m in msg if m))
+        # only rank 0 merges: gather the ranks' groups there
+        every = [None] * self.world if self.rank == 0 else None
+        dist.gather_object(mine, every, dst=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                           group=self.group)
+        stat_vec = self._allreduce_i64([getattr(r.stats, f) for f in STAT_FIELDS] +
+                                       [int(bool(r.stats.num_groups_limit_reached)),
+                                        0 if r.stats.filter_stats_exact else 1])
+        tot = dict(zip(STAT_FIELDS, stat_vec[:len(STAT_FIELDS)]))
+        st = ExecutionStats(kernel_ms=r.stats.kernel_ms, num_groups_limit_reached=stat_vec[-2] > 0,
+                            filter_stats_exact=stat_vec[-1] == 0, **tot)
         self.last_stats = st
         if self.rank != 0:
             return None

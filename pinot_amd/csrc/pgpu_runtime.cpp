@@ -3020,7 +3020,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
 
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
+  hipStream_t bail_stream = nullptr;
   auto bail = [&](int code) {
+    // a bail after the query kernel was enqueued but before segflags_kernel: the matched-segment words it may
+    // have set must not count towards the workspace's next query (they are zero between queries)
+    if (bail_stream && ws->segany.p) (void)hipMemsetAsync(ws->segany.p, 0, ws->segany.n, bail_stream);
     release_ws(ctx, ws);
     return code;
   };
@@ -3038,6 +3042,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     }
   }
   hipStream_t st = stream ? (hipStream_t)stream : ctx->qstream;
+  bail_stream = st;
 
   // arena: segs | instrs | cols | pool | remaps
   const size_t o_segs = 0;
