@@ -124,6 +124,20 @@ def algorithmic_bytes(ex, pm, q, segs, w, seg_ids, num_docs):
     return algo, st, parts, read, read_parts
 
 
+def resident_bytes(ctx, segs, rows):
+    """HBM held by the workload's segments on this GPU (pgpu_segment_device_bytes_ex): the reference's own indexes
+    and the derived copies the table's policy builds (Workload.sliced_columns / value_planes_columns)."""
+    kinds = {}
+    for s in segs:
+        for k, v in s.device_bytes_by_kind().items():
+            kinds[k] = kinds.get(k, 0) + v
+    derived = kinds["sliced"] + kinds["value_planes"]
+    used, budget = ctx.derived_bytes()
+    return {"resident_bytes_per_gpu": kinds["total"], "bytes_per_row": kinds["total"] / rows,
+            "forward_index_bytes_per_row": kinds["forward"] / rows, "derived_bytes_per_row": derived / rows,
+            "by_kind": kinds, "derived_budget_bytes": budget, "context_derived_bytes": used}
+
+
 def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier):
     """Generate the workload's segments in HBM, measure it, time the CPU baseline beside it; returns the fields
     of one result (the headline line or an entry of `workloads`)."""
@@ -141,6 +155,9 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
     torch.cuda.synchronize()
     gen_s = time.time() - t0
     log(f"{name}: generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
+    hbm = resident_bytes(ctx, segs, nseg * args.docs)
+    log(f"{name}: resident {hbm['resident_bytes_per_gpu'] / 1e9:.2f} GB per GPU, {hbm['bytes_per_row']:.2f} B/row "
+        f"({hbm['forward_index_bytes_per_row']:.2f} forward index, {hbm['derived_bytes_per_row']:.2f} derived)")
     opts = dict(w.options)
     q = parse_sql(w.sql)
     pm = GpuPlanMaker(ctx, **plan_options(opts))
@@ -177,6 +194,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
                        "groups": (len(result.group_rows) if result and result.group_rows is not None else None),
                        "rows": [list(r) for r in (result.rows[:3] if result else [])]},
             "parity_check": check,
+            "hbm": hbm,
             "setup_s": round(gen_s, 1),
         }
     finally:
@@ -187,7 +205,8 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
 # Secondary workloads measured after the headline in the default run (BASELINE.json configs 2-4 and the SURVEY 8(d)
 # variants): (name, steps, warmup, segments per GPU or 0 = the workload's own, CPU sample seconds)
 SECONDARY = [("range_in", 10, 2, 0, 3.0), ("groupby1m", 5, 1, 0, 3.0), ("bitmap5", 10, 2, 0, 3.0),
-             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 0, 3.0), ("adanalytics_exact", 10, 2, 0, 2.0)]
+             ("groupby1m_zipf", 5, 1, 0, 3.0), ("adanalytics_inv", 10, 2, 0, 3.0), ("adanalytics_exact", 10, 2, 0, 2.0),
+             ("adanalytics_8b", 5, 1, 0, 2.0)]
 
 
 def main():
@@ -247,6 +266,7 @@ def main():
             "cpu_baseline": head["cpu_baseline"],
             "result": head["result"],
             "parity_check": head["parity_check"],
+            "hbm": head["hbm"],
             "setup_s": head["setup_s"],
         }
         if workloads:
@@ -296,6 +316,7 @@ def inverted_bytes_read(q, segs):
 
 # Looser variants of the bench queries (same plan shapes) so the parity sample matches rows, not only zero.
 PARITY_VARIANTS = {"adanalytics": ("accountId IN (123456789)", "accountId < 123456789"),
+                   "adanalytics_8b": ("accountId IN (123456789)", "accountId < 123456789"),
                    "adanalytics_exact": ("accountId IN (123456789)", "accountId < 123456789")}
 
 

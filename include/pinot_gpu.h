@@ -170,6 +170,29 @@ int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void
 int pgpu_segment_add_docid_column(pgpu_segment* seg, int32_t column);
 /* HBM bytes held by the segment (all columns, including padding and container directories). */
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes);
+/* The same, by kind: the reference's own indexes (forward incl. raw values, dictionary, sorted, inverted,
+ * multi-value) and the derived copies seal builds (bit-sliced forward indexes, value planes). */
+typedef struct {
+  uint64_t forward, dictionary, sorted, inverted, multi_value, sliced, value_planes, total;
+} pgpu_segment_bytes;
+int pgpu_segment_device_bytes_ex(const pgpu_segment* seg, pgpu_segment_bytes* out);
+/* ---- HBM residency of derived copies (IndexLoadingConfig seam) -------------------------------------------------
+ * pgpu_segment_seal derives two copies of a column's forward index that only this path reads: a bit-sliced copy
+ * (PGPU_DERIVE_SLICED, same bytes as the forward index; scan-filter leaves streamed as bit planes) and, for INT /
+ * LONG dictionaries of <= 32 value bits, value planes (PGPU_DERIVE_VALUE_PLANES, vbits bits per doc; aggregation of
+ * densely matched metrics without dictionary gathers).  As the reference loads only the indexes a table's
+ * IndexLoadingConfig names (seglocal/segment/index/column/PhysicalColumnIndexContainer.java:80,151-156), a server
+ * names per column which copies to build -- its GPU filter columns and metric columns
+ * (pinot.server.query.executor.gpu.sliced.columns / .value.planes.columns) -- before seal; the default is both.
+ * Every copy is also built only while the context's derived bytes stay within its budget (default half of the
+ * device's memory; 0 = none).  Queries plan around a missing copy (packed streams, dictionary gathers): results are
+ * the same, only the kernel chosen differs. */
+#define PGPU_DERIVE_SLICED 1
+#define PGPU_DERIVE_VALUE_PLANES 2
+#define PGPU_DERIVE_ALL 3
+int pgpu_segment_set_derived(pgpu_segment* seg, int32_t column, int32_t flags);
+int pgpu_context_set_derived_budget(pgpu_context* ctx, uint64_t bytes);
+int pgpu_context_derived_bytes(pgpu_context* ctx, uint64_t* out_used, uint64_t* out_budget);
 int pgpu_segment_release(pgpu_segment* seg);
 
 /* ---- group-key remap tables ------------------------------------------------------------------------------

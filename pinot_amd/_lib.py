@@ -105,6 +105,16 @@ class TableLayout(C.Structure):
                 ("key_split", C.c_int32), ("reserved", C.c_int32)]
 
 
+class SegmentBytes(C.Structure):
+    """pgpu_segment_bytes: HBM bytes of a segment by kind (pgpu_segment_device_bytes_ex)."""
+    _fields_ = [(n, C.c_uint64) for n in ("forward", "dictionary", "sorted", "inverted", "multi_value", "sliced",
+                                           "value_planes", "total")]
+
+
+# derived copies seal may build per column (pgpu_segment_set_derived)
+PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES, PGPU_DERIVE_ALL = 1, 2, 3
+
+
 class QueryStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_total_docs", C.c_int64), ("num_segments_matched", C.c_int64),
@@ -157,6 +167,10 @@ SIGNATURES = [
     ("pgpu_segment_add_docid_column", C.c_int, [_P, C.c_int32]),
     ("pgpu_segment_dictionary_values", C.c_int, [_P, C.c_int32, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pgpu_segment_device_bytes", C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    ("pgpu_segment_device_bytes_ex", C.c_int, [_P, C.POINTER(SegmentBytes)]),
+    ("pgpu_segment_set_derived", C.c_int, [_P, C.c_int32, C.c_int32]),
+    ("pgpu_context_set_derived_budget", C.c_int, [_P, C.c_uint64]),
+    ("pgpu_context_derived_bytes", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("pgpu_segment_release", C.c_int, [_P]),
     ("pgpu_remap_upload", C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32, C.POINTER(_P)]),
     ("pgpu_buffer_release", C.c_int, [_P]),

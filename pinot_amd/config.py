@@ -19,14 +19,18 @@ GPU keys:
   than the scan);
 * ``…gpu.exact.filter.stats`` (false): numEntriesScannedInFilter as the reference's iterators count it where
   they leap-frog (one more pass, PGPU_Q_EXACT_FILTER_STATS);
-* ``…gpu.topk`` (true): select the ORDER BY trim on the GPU (pgpu_query_collect_topk).
+* ``…gpu.topk`` (true): select the ORDER BY trim on the GPU (pgpu_query_collect_topk);
+* ``…gpu.sliced.columns`` / ``…gpu.value.planes.columns`` ("*"): the columns whose bit-sliced copy (filter columns)
+  / value planes (metric columns) seal builds -- the GPU's IndexLoadingConfig (PhysicalColumnIndexContainer loads
+  only the indexes a table names); a comma list, ``*`` = every column, empty = none;
+* ``…gpu.derived.budget.bytes`` (-1 = half of the device's memory): HBM those copies may take per GPU.
 
 INTEGRATION.md §3.3 shows the Java side reading the same keys from the server's PinotConfiguration.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Mapping, Optional, Sequence, Tuple
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 EXECUTOR_PREFIX = "pinot.server.query.executor."
 GPU_PREFIX = EXECUTOR_PREFIX + "gpu."
@@ -72,6 +76,9 @@ class GpuExecutorConfig:
     min_query_docs: int = 0
     exact_filter_stats: bool = False
     topk: bool = True
+    sliced_columns: str = "*"
+    value_planes_columns: str = "*"
+    derived_budget_bytes: int = -1
 
     @classmethod
     def from_properties(cls, props: Mapping[str, str]) -> "GpuExecutorConfig":
@@ -95,6 +102,9 @@ class GpuExecutorConfig:
         get(GPU_PREFIX + "min.query.docs", int, "min_query_docs")
         get(GPU_PREFIX + "exact.filter.stats", _bool, "exact_filter_stats")
         get(GPU_PREFIX + "topk", _bool, "topk")
+        get(GPU_PREFIX + "sliced.columns", str, "sliced_columns")
+        get(GPU_PREFIX + "value.planes.columns", str, "value_planes_columns")
+        get(GPU_PREFIX + "derived.budget.bytes", int, "derived_budget_bytes")
         unknown = [k for k in props if k.startswith(GPU_PREFIX) and k[len(GPU_PREFIX):] not in _GPU_KEYS]
         if unknown:
             raise ValueError(f"unknown GPU executor key(s): {unknown}")
@@ -116,6 +126,23 @@ class GpuExecutorConfig:
                     continue
                 props[s[:sep].strip()] = s[sep + 1:].strip()
         return cls.from_properties(props)
+
+    def derived_flags(self, columns: Sequence[str]) -> Dict[str, int]:
+        """Column -> PGPU_DERIVE_* flags of the copies seal builds (GpuSegment(derived=...))."""
+        from ._lib import PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES
+
+        def named(spec: str):
+            s = spec.strip()
+            return None if s == "*" else {c.strip() for c in s.split(",") if c.strip()}
+
+        sl, vp = named(self.sliced_columns), named(self.value_planes_columns)
+        return {c: (PGPU_DERIVE_SLICED if sl is None or c in sl else 0) |
+                   (PGPU_DERIVE_VALUE_PLANES if vp is None or c in vp else 0) for c in columns}
+
+    def apply_budget(self, ctx) -> None:
+        """Set the context's derived-copy budget when the server names one."""
+        if self.derived_budget_bytes >= 0:
+            ctx.set_derived_budget(self.derived_budget_bytes)
 
     def device_ids(self, num_visible: int) -> List[int]:
         return parse_devices(self.devices, num_visible)
@@ -146,4 +173,5 @@ class GpuExecutorConfig:
                             gpu_topk=self.topk, min_server_group_trim_size=self.min_server_group_trim_size)
 
 
-_GPU_KEYS = ("enabled", "devices", "min.segment.docs", "min.query.docs", "exact.filter.stats", "topk")
+_GPU_KEYS = ("enabled", "devices", "min.segment.docs", "min.query.docs", "exact.filter.stats", "topk",
+             "sliced.columns", "value.planes.columns", "derived.budget.bytes")

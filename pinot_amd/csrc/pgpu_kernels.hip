@@ -3755,16 +3755,15 @@ __global__ __launch_bounds__(1024) void part_plan_kernel(DevParams p, int grid1)
   __syncthreads();
   for (int k = 0; k < 2; ++k) {
     if (ns[k] > 1 && extra > (uint32_t)spare) ns[k] = 1 + (uint32_t)((uint64_t)(ns[k] - 1) * spare / extra);
-    if (ns[k] > (uint32_t)grid1) ns[k] = (uint32_t)grid1;  // at least one phase-1 region per phase-2 workgroup
   }
   const uint32_t w0 = block_excl_scan(ns[0] + ns[1], scratch);
   for (int k = 0; k < 2; ++k) {
     const uint32_t first = w0 + (k ? ns[0] : 0u);
-    for (uint32_t j = 0; j < ns[k]; ++j) {
+    for (uint32_t j = 0; j < ns[k]; ++j) {  // share j of ns of the partition's records (RegionWalk)
       int32_t* wk = p.p2work + 4 * (first + j);
       wk[0] = 2 * t + k;
-      wk[1] = (int32_t)((uint64_t)j * grid1 / ns[k]);
-      wk[2] = (int32_t)((uint64_t)(j + 1) * grid1 / ns[k]);
+      wk[1] = (int32_t)j;
+      wk[2] = (int32_t)ns[k];
       wk[3] = ns[k] > 1;
     }
   }
@@ -3825,6 +3824,64 @@ FI void part_reduce_batch(int64_t* ptab, uint32_t K, const int32_t (&op)[NS > 0 
   }
 }
 
+// Phase 2 of a partition split over several workgroups (part_plan_kernel): workgroup j of ns takes the records
+// [j * T / ns, (j + 1) * T / ns) of the partition's T records, counted across the phase-1 regions in region order,
+// so a heavy partition's share does not depend on how its records fell into regions.  Each wave walks the regions
+// round-robin (region w to wave w % nwaves) and gets (region base + first record, record count) per region it
+// holds a non-empty piece of.
+struct RegionWalk {
+  const DevParams* p;
+  uint32_t q;
+  int nwg, wave, nwaves;
+  uint64_t r0, r1;     // this workgroup's record range in the partition
+  uint64_t run;        // records of the regions before the current chunk of 64
+  int wb;              // current chunk's first region
+  uint64_t todo;       // lanes (regions) of the chunk left for this wave
+  uint64_t excl;       // lane's region: first record (partition-wide)
+  uint32_t cnt;        // lane's region: records
+  size_t base;         // out: first record's index in p.recs
+  uint32_t n;          // out: records
+  int visited;
+  FI RegionWalk(const DevParams& pp, uint32_t qq, int j, int ns, int nw, int wv, int nwv)
+      : p(&pp), q(qq), nwg(nw), wave(wv), nwaves(nwv), run(0), wb(-64), todo(0), excl(0), cnt(0), base(0), n(0),
+        visited(0) {
+    r0 = 0;
+    r1 = ~0ull;
+    if (ns > 1) {
+      uint64_t t = 0;
+      for (int w = lane_id(); w < nwg; w += 64) t += pp.rcount[(size_t)qq * nwg + w];
+      t = (uint64_t)wave_sum_i64((int64_t)t);
+      r0 = t * (uint64_t)j / (uint64_t)ns;
+      r1 = t * (uint64_t)(j + 1) / (uint64_t)ns;
+    }
+  }
+  FI bool next() {
+    while (!todo) {
+      wb += 64;
+      if (wb >= nwg) return false;
+      const int w = wb + lane_id();
+      const uint32_t c = w < nwg ? p->rcount[(size_t)q * nwg + w] : 0u;
+      // 64-bit prefix of 32-bit counts: the high and low halves scanned apart (each sum < 2^22)
+      excl = run + ((uint64_t)(uint32_t)wave_excl_scan((int)(c >> 16)) << 16) +
+             (uint64_t)(uint32_t)wave_excl_scan((int)(c & 0xFFFFu));
+      run += (uint64_t)wave_sum_i64((int64_t)c);
+      cnt = c;
+      const bool mine = w < nwg && w % nwaves == wave && excl < r1 && excl + c > r0;
+      todo = __ballot(mine);
+    }
+    const int l = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const uint64_t e = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(excl >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)excl, l);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, l);
+    const uint64_t a = e > r0 ? e : r0, b2 = e + c < r1 ? e + c : r1;
+    base = part_base(*p, q, (uint32_t)(wb + l)) + (size_t)(a - e);
+    n = (uint32_t)(b2 - a);
+    ++visited;
+    return true;
+  }
+};
+
 template <int NS, bool ONE, int LDM>
 __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg) {
   extern __shared__ __attribute__((aligned(16))) int64_t ptab[];
@@ -3832,14 +3889,14 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   const uint32_t K = 1u << p.pshift;
   // this workgroup's partition and run of phase-1 regions [w0, w1) (part_plan_kernel), or all of partition blockIdx.x
   uint32_t q = blockIdx.x;
-  int w0 = 0, w1 = nwg;
+  int pj = 0, pns = 1;  // this workgroup's share j of ns of the partition's records
   bool split = false;
   if (p.p2work) {
     const int32_t* wk = p.p2work + 4 * blockIdx.x;
     if (wk[0] < 0) return;
     q = (uint32_t)wk[0];
-    w0 = wk[1];
-    w1 = wk[2];
+    pj = wk[1];
+    pns = wk[2];
     split = wk[3] != 0;
   }
   const uint64_t key0 = (uint64_t)q * K;
@@ -3878,10 +3935,11 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
     const int idbits = p.rec_idbits;
     const uint32_t idmask = (1u << idbits) - 1u;
     constexpr int R = 16;
-    for (int w = w0 + wave; w < w1; w += nwaves) {
-      if (((w - w0 - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
-      const uint32_t n = p.rcount[(size_t)q * nwg + w];
-      const size_t rb = part_base(p, q, w);
+    RegionWalk rwk(p, q, pj, pns, nwg, wave, nwaves);
+    while (rwk.next()) {
+      if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
+      const uint32_t n = rwk.n;
+      const size_t rb = rwk.base;
       for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
         uint32_t k[R], id[R];
         bool ok[R];
@@ -3958,10 +4016,11 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
   for (int s = 0; s < NS; ++s) need_val |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
   {
     constexpr int R = 16;
-    for (int w = w0 + wave; w < w1; w += nwaves) {
-      if (((w - w0 - wave) / nwaves) % 8 == 7 && query_cancelled(p)) break;
-      const uint32_t n = p.rcount[(size_t)q * nwg + w];
-      const size_t base = part_base(p, q, w);
+    RegionWalk rwk(p, q, pj, pns, nwg, wave, nwaves);
+    while (rwk.next()) {
+      if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
+      const uint32_t n = rwk.n;
+      const size_t base = rwk.base;
       for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
         uint32_t k[R], raw[R], val[R];
         bool ok[R];
@@ -4745,6 +4804,7 @@ hipError_t pgpu_prepare_part_reduce() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)part_scan_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             PGPU_LDS_LIMIT);
+
   return e;
 }
 

@@ -271,6 +271,10 @@ struct pgpu_context {
   // memory to the device on its own (release threshold = max), so no query-path allocation reaches the driver
   // twice.  nullptr when the device has no memory pools: growth then falls back to hipMalloc / hipFree.
   hipMemPool_t mpool = nullptr;
+  // HBM held by derived copies (bit-sliced forward indexes, value planes) of this context's segments, and the budget
+  // they are built under (pgpu_context_set_derived_budget; default half of the device's memory)
+  std::atomic<uint64_t> derived_bytes{0};
+  uint64_t derived_budget = UINT64_MAX;
   ~pgpu_context() {
     pool.clear();
     if (qstream) (void)hipStreamDestroy(qstream);
@@ -309,6 +313,7 @@ struct HostColumn {
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
   double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
+  int32_t derive = PGPU_DERIVE_ALL;    // derived copies seal may build (pgpu_segment_set_derived)
   int32_t min_exp = INT32_MAX;         // FLOAT / DOUBLE: ValueRange::min_exp / min_lsb (fixed-point SUM layout)
   int32_t min_lsb = INT32_MAX;
   void set_range(const ValueRange& r) {
@@ -593,6 +598,10 @@ int pgpu_init(int device_ordinal, pgpu_context** out_ctx) {
   auto* ctx = new pgpu_context();
   ctx->device = device_ordinal;
   ctx->num_cus = prop.multiProcessorCount;
+  {  // derived copies may take up to half of the device's memory unless the server says otherwise
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) ctx->derived_budget = tot / 2;
+  }
   int pools = 0;
   if (hipDeviceGetAttribute(&pools, hipDeviceAttributeMemoryPoolsSupported, device_ordinal) == hipSuccess && pools) {
     hipMemPoolProps props{};
@@ -1032,13 +1041,29 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
 
 namespace {
 // The kernels' view of column i (DevColumn), with its bit-sliced copy built first (fixed-bit columns).
+// Reserve `bytes` of the context's derived-copy budget (false: over budget, the copy is not built).
+bool reserve_derived(pgpu_context* ctx, uint64_t bytes) {
+  uint64_t cur = ctx->derived_bytes.load();
+  do {
+    if (cur + bytes > ctx->derived_budget) return false;
+  } while (!ctx->derived_bytes.compare_exchange_weak(cur, cur + bytes));
+  return true;
+}
+
 int seal_column(pgpu_segment* seg, size_t i) {
   static const bool no_slice = getenv("PGPU_NO_SLICE") && atoi(getenv("PGPU_NO_SLICE")) != 0;
   HostColumn& c = seg->cols[i];
-  if (c.kind == PGPU_COL_FIXED_BIT && !no_slice && !c.sliced.p) {
+  // derived copies (PhysicalColumnIndexContainer.java:80,151-156 loads only the indexes IndexLoadingConfig names):
+  // the column's pgpu_segment_set_derived flags, within the context's budget; the kernels plan without them
+  if (c.kind == PGPU_COL_FIXED_BIT && !no_slice && !c.sliced.p && (c.derive & PGPU_DERIVE_SLICED) &&
+      reserve_derived(seg->ctx, c.fwd.n)) {
     // bit planes of every 2048-doc tile of the padded stream (same byte count as the packed copy)
     const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
-    HIP_TRY(c.sliced.alloc(c.fwd.n));
+    const hipError_t ae = c.sliced.alloc(c.fwd.n);
+    if (ae != hipSuccess) {
+      seg->ctx->derived_bytes -= c.fwd.n;
+      return fail(PGPU_E_HIP, "bit-sliced copy of column %zu: %s", i, hipGetErrorString(ae));
+    }
     HIP_TRY(hipMemset(c.sliced.p, 0, c.sliced.n));
     HIP_TRY(pgpu_launch_bitslice((const uint32_t*)c.fwd.p, (uint32_t*)c.sliced.p, c.bits, ntiles, nullptr));
   }
@@ -1061,9 +1086,14 @@ int seal_column(pgpu_segment* seg, size_t i) {
     const uint64_t range = (uint64_t)hi - (uint64_t)lo;  // ascending dictionary (checked at upload)
     int vb = 0;
     while (vb < 64 && (range >> vb)) ++vb;
-    if (hi >= lo && vb >= 1 && vb <= 32) {
-      const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
-      HIP_TRY(c.vsliced.alloc((size_t)ntiles * 256 * vb));
+    const int64_t ntiles = ((int64_t)seg->num_docs + PGPU_TILE - 1) / PGPU_TILE * (PGPU_TILE / PGPU_WT);
+    if (hi >= lo && vb >= 1 && vb <= 32 && (c.derive & PGPU_DERIVE_VALUE_PLANES) &&
+        reserve_derived(seg->ctx, (uint64_t)ntiles * 256 * vb)) {
+      const hipError_t ae = c.vsliced.alloc((size_t)ntiles * 256 * vb);
+      if (ae != hipSuccess) {
+        seg->ctx->derived_bytes -= (uint64_t)ntiles * 256 * vb;
+        return fail(PGPU_E_HIP, "value planes of column %zu: %s", i, hipGetErrorString(ae));
+      }
       HIP_TRY(pgpu_launch_vslice((const uint32_t*)c.fwd.p, c.dict.p, c.dict_type, lo, c.bits, vb,
                                  (uint32_t*)c.vsliced.p, ntiles, nullptr));
       c.vmin = lo;
@@ -1213,17 +1243,61 @@ int pgpu_segment_dictionary_values(const pgpu_segment* seg, int32_t column, void
 }
 
 int pgpu_segment_device_bytes(const pgpu_segment* seg, uint64_t* out_bytes) {
-  if (!seg || !out_bytes) return fail(PGPU_E_INVALID, "null argument");
-  uint64_t t = 0;
-  for (const HostColumn& c : seg->cols)
-    t += c.fwd.n + c.sliced.n + c.vsliced.n + c.sorted.n + c.dict.n + c.inv_dir.n + c.inv_ct.n + c.inv_data.n + c.mv_off.n;
-  *out_bytes = t;
+  pgpu_segment_bytes b;
+  const int rc = pgpu_segment_device_bytes_ex(seg, &b);
+  if (rc) return rc;
+  if (!out_bytes) return fail(PGPU_E_INVALID, "null argument");
+  *out_bytes = b.total;
+  return PGPU_OK;
+}
+
+int pgpu_segment_device_bytes_ex(const pgpu_segment* seg, pgpu_segment_bytes* out) {
+  if (!seg || !out) return fail(PGPU_E_INVALID, "null argument");
+  memset(out, 0, sizeof(*out));
+  for (const HostColumn& c : seg->cols) {
+    if (c.kind == PGPU_COL_MV) out->multi_value += c.fwd.n + c.mv_off.n;
+    else out->forward += c.fwd.n;
+    // a raw column's values sit in the dictionary's slot (they are its forward index)
+    if (c.kind == PGPU_COL_RAW) out->forward += c.dict.n;
+    else out->dictionary += c.dict.n + c.for_dev.n;
+    out->sorted += c.sorted.n;
+    out->inverted += c.inv_dir.n + c.inv_ct.n + c.inv_data.n;
+    out->sliced += c.sliced.n;
+    out->value_planes += c.vsliced.n;
+  }
+  out->total = out->forward + out->dictionary + out->sorted + out->inverted + out->multi_value + out->sliced +
+               out->value_planes;
+  return PGPU_OK;
+}
+
+int pgpu_segment_set_derived(pgpu_segment* seg, int32_t column, int32_t flags) {
+  const int rc = check_column(seg, column);
+  if (rc) return rc;
+  if (flags < 0 || flags > PGPU_DERIVE_ALL) return fail(PGPU_E_INVALID, "derived-copy flags %d", flags);
+  if (seg->sealed) return fail(PGPU_E_INVALID, "segment already sealed");
+  seg->cols[column].derive = flags;
+  return PGPU_OK;
+}
+
+int pgpu_context_set_derived_budget(pgpu_context* ctx, uint64_t bytes) {
+  if (!ctx) return fail(PGPU_E_INVALID, "null context");
+  ctx->derived_budget = bytes;
+  return PGPU_OK;
+}
+
+int pgpu_context_derived_bytes(pgpu_context* ctx, uint64_t* out_used, uint64_t* out_budget) {
+  if (!ctx || !out_used || !out_budget) return fail(PGPU_E_INVALID, "null argument");
+  *out_used = ctx->derived_bytes.load();
+  *out_budget = ctx->derived_budget;
   return PGPU_OK;
 }
 
 int pgpu_segment_release(pgpu_segment* seg) {
   if (!seg) return PGPU_OK;
   (void)hipSetDevice(seg->ctx->device);
+  uint64_t derived = 0;
+  for (const HostColumn& c : seg->cols) derived += c.sliced.n + c.vsliced.n;
+  seg->ctx->derived_bytes -= derived;
   delete seg;
   return PGPU_OK;
 }

@@ -130,6 +130,16 @@ class GpuContext:
     def add_listener(self, obj) -> None:
         self._listeners.add(obj)
 
+    def set_derived_budget(self, nbytes: int) -> None:
+        """HBM the derived copies of this context's segments may take (pgpu_context_set_derived_budget)."""
+        _lib.check(self._lib.pgpu_context_set_derived_budget(self.handle, int(nbytes)))
+
+    def derived_bytes(self):
+        """(bytes held by derived copies, budget)."""
+        used, budget = C.c_uint64(), C.c_uint64()
+        _lib.check(self._lib.pgpu_context_derived_bytes(self.handle, C.byref(used), C.byref(budget)))
+        return used.value, budget.value
+
     def segment_released(self, uid: int) -> None:
         """A segment left HBM: drop its remap tables and every cache entry naming it (bounded host / HBM state
         in a server whose pruning yields a different segment set per query)."""
@@ -240,7 +250,9 @@ class GpuSegment:
     per-segment state (global group dictionaries, remap tables) key on it."""
 
     def __init__(self, ctx: GpuContext, data: SegmentData, columns: Optional[Sequence[str]] = None,
-                 _incremental: bool = False):
+                 _incremental: bool = False, derived: Optional[Dict[str, int]] = None):
+        """``derived``: column -> PGPU_DERIVE_* flags of the copies seal builds for it (the table's GPU filter /
+        metric columns, GpuExecutorConfig.derived_flags); columns it does not name get both (the default)."""
         self.ctx = ctx
         self.uid = next(_UIDS)
         self.data = data
@@ -263,6 +275,7 @@ class GpuSegment:
         self._capacity = nslots
         self._gdict_free = list(range(nslots - nraw - 1, nslots - 1))  # spare slots (after every column's own)
         self._docid_slot = None if _incremental else nslots - 1
+        self._derived_flags = dict(derived or {})
         if _incremental:
             return
         try:
@@ -274,10 +287,11 @@ class GpuSegment:
             raise
 
     @classmethod
-    def begin(cls, ctx: GpuContext, name: str, num_docs: int, num_columns: int) -> "GpuSegment":
+    def begin(cls, ctx: GpuContext, name: str, num_docs: int, num_columns: int,
+              derived: Optional[Dict[str, int]] = None) -> "GpuSegment":
         """Incremental upload: add_column() per column, then seal()."""
         data = SegmentData(name, num_docs)
-        return cls(ctx, data, columns=[f"_{i}" for i in range(num_columns)], _incremental=True)
+        return cls(ctx, data, columns=[f"_{i}" for i in range(num_columns)], _incremental=True, derived=derived)
 
     def add_column(self, col: ColumnIndexes) -> None:
         need = 1 + (len(MV_ROW_COLUMNS) if col.is_mv else 0)
@@ -285,6 +299,8 @@ class GpuSegment:
             raise ValueError("segment column capacity exceeded")
         slot = len(self.slots)
         self._upload_column(slot, col)
+        if col.name in self._derived_flags:
+            _lib.check(self.ctx._lib.pgpu_segment_set_derived(self.handle, slot, int(self._derived_flags[col.name])))
         self.slots[col.name] = slot
         self.dictionaries[col.name] = col.dictionary_values()
         self.data.columns[col.name] = col
@@ -448,6 +464,12 @@ class GpuSegment:
         n = C.c_uint64()
         _lib.check(self.ctx._lib.pgpu_segment_device_bytes(self.handle, C.byref(n)))
         return n.value
+
+    def device_bytes_by_kind(self) -> Dict[str, int]:
+        """HBM bytes by kind: the reference's indexes and the derived copies (pgpu_segment_device_bytes_ex)."""
+        b = _lib.SegmentBytes()
+        _lib.check(self.ctx._lib.pgpu_segment_device_bytes_ex(self.handle, C.byref(b)))
+        return {n: int(getattr(b, n)) for n, _ in _lib.SegmentBytes._fields_}
 
     def release(self) -> None:
         if self.handle:

@@ -16,8 +16,9 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import dataclasses
 from dataclasses import dataclass
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -97,6 +98,18 @@ class Workload:
     seed: int
     description: str
     segments: int = 30      # segments per GPU in bench.py (2^25 docs each): BASELINE.json configs' row counts
+    # the table's GPU IndexLoadingConfig (pinot.server.query.executor.gpu.sliced.columns / .value.planes.columns):
+    # its scan-filter columns get a bit-sliced copy, its dense metric columns value planes; None = every column
+    sliced_columns: Optional[Tuple[str, ...]] = None
+    value_planes_columns: Optional[Tuple[str, ...]] = None
+
+    def derived_flags(self) -> Dict[str, int]:
+        """Column -> PGPU_DERIVE_* flags of the copies seal builds (GpuSegment(derived=...))."""
+        from ._lib import PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES
+        return {c.name: (PGPU_DERIVE_SLICED if self.sliced_columns is None or c.name in self.sliced_columns else 0) |
+                        (PGPU_DERIVE_VALUE_PLANES if self.value_planes_columns is None or
+                         c.name in self.value_planes_columns else 0)
+                for c in self.columns}
 
 
 def _days():
@@ -118,20 +131,23 @@ WORKLOADS: Dict[str, Workload] = {
         "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
         "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
         "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
-        {}, 5, "config 5: AdAnalytics filtered GROUP BY SUM (README example query)"),
+        {}, 5, "config 5: AdAnalytics filtered GROUP BY SUM (README example query)",
+        sliced_columns=("daysSinceEpoch", "accountId"), value_planes_columns=()),
     "range_in": Workload(
         "range_in", "synth",
         [SynthColumn("r", 1 << 16, lambda: (np.arange(1 << 16, dtype=np.int32) * 7 + 3)),
          SynthColumn("i", 16, lambda: np.arange(16, dtype=np.int32) * 100),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 13))],
         "SELECT COUNT(*), SUM(m) FROM synth WHERE r BETWEEN 114691 AND 344060 AND i IN (100, 500, 900)",
-        {}, 1, "config 2: COUNT(*)+SUM(metric) WHERE range AND IN"),
+        {}, 1, "config 2: COUNT(*)+SUM(metric) WHERE range AND IN",
+        sliced_columns=("r", "i"), value_planes_columns=("m",)),
     "groupby1m": Workload(
         "groupby1m", "synth",
         [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
-        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4: 1M-key GROUP BY SUM/MAX/COUNT",
+        segments=60, sliced_columns=(), value_planes_columns=()),
     "bitmap5": Workload(
         "bitmap5", "bitmap5",
         [SynthColumn("a", 4, lambda: np.arange(4, dtype=np.int32) * 10, index="inv"),
@@ -143,14 +159,16 @@ WORKLOADS: Dict[str, Workload] = {
          SynthColumn("m2", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 16))],
         "SELECT SUM(m1), SUM(m2) FROM bitmap5 "
         "WHERE (a = 10 AND b IN (30, 70)) OR (c = 50 AND d <> 90 AND e BETWEEN 640 AND 1910)",
-        {}, 3, "config 3: inverted-index (Roaring) AND/OR/NOT filter + sorted range, SUM on 2 metric columns"),
+        {}, 3, "config 3: inverted-index (Roaring) AND/OR/NOT filter + sorted range, SUM on 2 metric columns",
+        sliced_columns=(), value_planes_columns=("m1", "m2")),
     # SURVEY.md 8(d) variants: config 4 with Zipf(1.1)-skewed keys, config 5 with accountId inverted-indexed
     "groupby1m_zipf": Workload(
         "groupby1m_zipf", "synth",
         [SynthColumn("k", 1 << 20, lambda: np.arange(1 << 20, dtype=np.int32) * 3, dist="zipf", zipf_s=1.1),
          SynthColumn("m", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 14))],
         "SELECT k, SUM(m), MAX(m), COUNT(*) FROM synth GROUP BY k ORDER BY SUM(m) DESC LIMIT 100",
-        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT", segments=60),
+        {"num_groups_limit": 2_000_000, "min_server_group_trim_size": -1}, 4, "config 4, Zipf(1.1) keys: 1M-key GROUP BY SUM/MAX/COUNT",
+        segments=60, sliced_columns=(), value_planes_columns=()),
     # PMC calibration (not a bench line): config 5's filter stream alone, a known byte count for FETCH_SIZE
     "adanalytics_count": Workload(
         "adanalytics_count", "adAnalytics",
@@ -159,7 +177,8 @@ WORKLOADS: Dict[str, Workload] = {
          SynthColumn("clicks", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 11)),
          SynthColumn("impressions", 1 << 16, lambda: sorted_distinct_in(1 << 16, 1 << 20, 12))],
         "SELECT COUNT(*) FROM adAnalytics WHERE daysSinceEpoch BETWEEN 17849 AND 17856",
-        {}, 5, "config 5's filter stream alone (FETCH_SIZE calibration of the register-direct stream)"),
+        {}, 5, "config 5's filter stream alone (FETCH_SIZE calibration of the register-direct stream)",
+        sliced_columns=("daysSinceEpoch", "accountId"), value_planes_columns=()),
     # config 5 with the reference's numEntriesScannedInFilter (PGPU_Q_EXACT_FILTER_STATS: one more pass over every
     # filter leaf and the host iterator replay): the cost of pinot.server.query.executor.gpu.exact.filter.stats
     "adanalytics_exact": Workload(
@@ -171,7 +190,8 @@ WORKLOADS: Dict[str, Workload] = {
         "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
         "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
         "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
-        {"exact_filter_stats": True}, 5, "config 5 with the reference's exact numEntriesScannedInFilter"),
+        {"exact_filter_stats": True}, 5, "config 5 with the reference's exact numEntriesScannedInFilter",
+        sliced_columns=("daysSinceEpoch", "accountId"), value_planes_columns=()),
     "adanalytics_inv": Workload(
         "adanalytics_inv", "adAnalytics",
         [SynthColumn("daysSinceEpoch", 1024, _days),
@@ -181,8 +201,14 @@ WORKLOADS: Dict[str, Workload] = {
         "SELECT daysSinceEpoch, SUM(clicks), SUM(impressions) FROM adAnalytics "
         "WHERE daysSinceEpoch BETWEEN 17849 AND 17856 AND accountId IN (123456789) "
         "GROUP BY daysSinceEpoch ORDER BY SUM(impressions) DESC LIMIT 100",
-        {}, 5, "config 5, accountId inverted-indexed: the IN leaf is a Roaring bitmap"),
+        {}, 5, "config 5, accountId inverted-indexed: the IN leaf is a Roaring bitmap",
+        sliced_columns=("daysSinceEpoch",), value_planes_columns=()),
 }
+# config 5 at its literal size on ONE GPU: 8B rows (240 segments of 2^25 docs) -- HBM residency bounded by the
+# table's derived-copy policy (forward indexes 62 bits/row + the two filter columns' bit-sliced copies 30 bits/row)
+WORKLOADS["adanalytics_8b"] = dataclasses.replace(
+    WORKLOADS["adanalytics"], name="adanalytics_8b", segments=240,
+    description="config 5 at 8B rows on one GPU (240 x 2^25 docs): HBM residency under the derived-copy policy")
 
 
 def sorted_index_bytes(num_docs: int, card: int) -> bytes:
@@ -288,7 +314,7 @@ def build_segments_gpu(ctx: GpuContext, w: Workload, segment_ids: List[int], num
                 _h2d(sl, p, table)
                 cdfs[c.name] = p
         for s in segment_ids:
-            gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns))
+            gs = GpuSegment.begin(ctx, f"{w.name}_{s}", num_docs, len(w.columns), derived=w.derived_flags())
             for c in w.columns:
                 if c.index == "sorted":
                     gs.add_column(ColumnIndexes(c.name, PGPU_INT, c.cardinality, dictionary=dicts[c.name],

@@ -83,3 +83,20 @@ def test_table_capacity_min_trim():
     assert table_capacity(2000) == 10000
     assert table_capacity(10, 100) == 100
     assert table_capacity(10, 0) >= 1 << 62
+
+
+def test_derived_copy_columns():
+    """…gpu.sliced.columns / …gpu.value.planes.columns: the GPU's IndexLoadingConfig (per-column derived copies)."""
+    from pinot_amd._lib import PGPU_DERIVE_ALL, PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES
+    c = GpuExecutorConfig.from_properties({})
+    assert c.derived_flags(["a", "b"]) == {"a": PGPU_DERIVE_ALL, "b": PGPU_DERIVE_ALL}
+    c = GpuExecutorConfig.from_properties({
+        "pinot.server.query.executor.gpu.sliced.columns": "daysSinceEpoch, accountId",
+        "pinot.server.query.executor.gpu.value.planes.columns": "",
+        "pinot.server.query.executor.gpu.derived.budget.bytes": "1000000"})
+    f = c.derived_flags(["daysSinceEpoch", "accountId", "clicks"])
+    assert f == {"daysSinceEpoch": PGPU_DERIVE_SLICED, "accountId": PGPU_DERIVE_SLICED, "clicks": 0}
+    assert c.derived_budget_bytes == 1_000_000
+    c = GpuExecutorConfig.from_properties({"pinot.server.query.executor.gpu.value.planes.columns": "m"})
+    assert c.derived_flags(["m", "r"]) == {"m": PGPU_DERIVE_ALL, "r": PGPU_DERIVE_SLICED}
+    assert PGPU_DERIVE_VALUE_PLANES | PGPU_DERIVE_SLICED == PGPU_DERIVE_ALL

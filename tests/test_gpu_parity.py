@@ -703,3 +703,38 @@ def test_partitioned_groupby_shared_dictionary_vs_oracle(gpu_ctx):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.parametrize("dist", ["uniform", "skewed", "filtered"])
+def test_partitioned_groupby_shared_dictionary(gpu_ctx, dist):
+    """One-word records (every segment shares the aggregated column's dictionary) over >= 65,536 keys, phase 1 by
+    part_scan_kernel: the same groups and values as the oracle -- with skewed keys the hot partition is split over
+    several phase-2 workgroups by record ranges (RegionWalk), whatever regions its records fell into."""
+    rng = np.random.default_rng(4242)
+    mvals = np.unique(rng.integers(-(1 << 30), 1 << 30, 5000)).astype(np.int32)  # one dictionary for every segment
+    segs = []
+    for i in range(3):
+        n = 400_003 + 4096 * i
+        if dist == "skewed":  # most records in the first key partition, a few keys very hot
+            k = np.where(rng.random(n) < 0.8, rng.zipf(1.3, n) % 4096, rng.integers(0, 200_000, n))
+        else:
+            k = rng.integers(0, 200_000, n)
+        m = mvals[rng.integers(0, len(mvals), n)]
+        f = rng.integers(0, 100, n)
+        cols = {"k": (PGPU_INT, k.astype(np.int32)), "m": (PGPU_INT, m), "f": (PGPU_INT, f.astype(np.int32))}
+        segs.append(build_segment(f"sd{dist}{i}", cols, sorted_columns=()))
+    where = " WHERE f < 37" if dist == "filtered" else ""
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        for sql in (f"SELECT k, SUM(m), MAX(m), COUNT(*) FROM t{where} GROUP BY k ORDER BY SUM(m) DESC LIMIT 50",
+                    f"SELECT k, COUNT(*) FROM t{where} GROUP BY k ORDER BY COUNT(*) DESC, k LIMIT 50",
+                    f"SELECT k, MIN(m), AVG(m) FROM t{where} GROUP BY k ORDER BY AVG(m) LIMIT 20"):
+            q = parse_sql(sql)
+            res = _gpu(gpu_ctx, q, gs, num_groups_limit=1_000_000, min_server_group_trim_size=-1)
+            ref = engine.execute(q, segs, num_groups_limit=1_000_000)
+            _assert_same(res, ref)
+            if "AVG" not in sql:
+                assert res.rows == ref.rows
+    finally:
+        for g in gs:
+            g.release()

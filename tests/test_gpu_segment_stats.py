@@ -102,3 +102,62 @@ def test_num_groups_limit_reached_at_the_limit(gpu_ctx, limit, reached):
     assert ref.num_groups_limit_reached == reached
     assert res.stats.num_groups_limit_reached == reached
     assert res.rows == ref.rows
+
+
+def test_derived_copies_follow_the_residency_policy(gpu_ctx):
+    """pgpu_segment_set_derived / the context budget: the copies seal builds, the bytes reported by kind, and the
+    same results with or without them (PhysicalColumnIndexContainer.java:80,151-156 -- only named indexes load)."""
+    import numpy as np
+    from oracle import engine
+    from oracle.segment_writer import build_segment
+    from pinot_amd import _lib
+    from pinot_amd.plan import GpuPlanMaker
+    from pinot_amd.query import parse_sql
+    from pinot_amd.segment import GpuSegment
+    from tests.helpers import close
+    rng = np.random.default_rng(17)
+    n = 300_000
+    data = build_segment("res", {"f": (_lib.PGPU_INT, rng.integers(0, 1000, n).astype(np.int32)),
+                                 "g": (_lib.PGPU_INT, rng.integers(0, 50, n).astype(np.int32)),
+                                 "m": (_lib.PGPU_INT, rng.integers(0, 1 << 16, n).astype(np.int32))},
+                         sorted_columns=())
+    sqls = ["SELECT COUNT(*), SUM(m), MAX(m) FROM t WHERE f BETWEEN 100 AND 700 AND g IN (3, 7, 11)",
+            "SELECT g, SUM(m) FROM t WHERE f < 500 GROUP BY g ORDER BY g LIMIT 100"]
+    used0, budget0 = gpu_ctx.derived_bytes()
+    assert budget0 > 0
+    variants = {"all": None, "none": {"f": 0, "g": 0, "m": 0},
+                "policy": {"f": _lib.PGPU_DERIVE_SLICED, "g": _lib.PGPU_DERIVE_SLICED, "m": _lib.PGPU_DERIVE_VALUE_PLANES}}
+    for name, derived in variants.items():
+        seg = GpuSegment(gpu_ctx, data, derived=derived)
+        try:
+            b = seg.device_bytes_by_kind()
+            assert b["total"] == seg.device_bytes() == sum(v for k, v in b.items() if k != "total")
+            if name == "none":
+                assert b["sliced"] == 0 and b["value_planes"] == 0
+            elif name == "all":
+                assert b["sliced"] == b["forward"] and b["value_planes"] > 0
+            else:
+                assert 0 < b["sliced"] < b["forward"] and b["value_planes"] > 0
+            assert gpu_ctx.derived_bytes()[0] == used0 + b["sliced"] + b["value_planes"]
+            for sql in sqls:
+                q = parse_sql(sql)
+                res = GpuPlanMaker(gpu_ctx).execute(q, [seg])
+                ref = engine.execute(q, [data])
+                if res.aggregation_result is not None:
+                    assert all(close(x, y) for x, y in zip(res.aggregation_result, ref.aggregation_result))
+                else:
+                    assert res.rows == ref.rows
+        finally:
+            seg.release()
+        assert gpu_ctx.derived_bytes()[0] == used0
+    # a zero budget: no derived copy at all, whatever the flags say
+    gpu_ctx.set_derived_budget(0)
+    try:
+        seg = GpuSegment(gpu_ctx, data)
+        try:
+            b = seg.device_bytes_by_kind()
+            assert b["sliced"] == 0 and b["value_planes"] == 0
+        finally:
+            seg.release()
+    finally:
+        gpu_ctx.set_derived_budget(budget0)
