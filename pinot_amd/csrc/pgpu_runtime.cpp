@@ -2233,11 +2233,12 @@ int plan_segment(const pgpu_query_desc* q, const pgpu_segment_plan& sp, const pg
                       q->aggs[a].fn == PGPU_AGG_MIN || q->aggs[a].fn == PGPU_AGG_MAX);
     all_bsi = all_bsi && bsi;
     // (a split SUM is three device aggregations: the id path's two LDS sub-queues hold one per query aggregation)
-    sliced = sliced && !split && dc->kind == PGPU_COL_FIXED_BIT && dc->sliced &&
+    // value planes alone serve a value-plane aggregation; the id planes (bit-sliced copy) the others
+    sliced = sliced && !split && dc->kind == PGPU_COL_FIXED_BIT && (dc->sliced || bsi) &&
              line_touch(rho, bsi ? dc->vbits : dc->bits) >= sliced_touch;
   }
-  if (sliced && !all_bsi) {
-    for (int qc : aggcols) sliced = sliced && v.dev(qc)->bits >= 1 && v.dev(qc)->bits <= 16;
+  if (sliced && !all_bsi) {  // the id-plane path reads every aggregated column's bit-sliced copy
+    for (int qc : aggcols) sliced = sliced && v.dev(qc)->sliced && v.dev(qc)->bits >= 1 && v.dev(qc)->bits <= 16;
     sliced = sliced && nvalue <= 2;
   }
   if (aggcols.empty()) {
