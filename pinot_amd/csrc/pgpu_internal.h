@@ -166,7 +166,11 @@ struct DevSeg {
   uint32_t ptt;
   int32_t pnsorted;
   int32_t psorted[2];
-  int32_t pad4_;
+  // query_kernel_rkey (DevParams::direct == 5): the segment's first (segment, container key) unit, and for each BITS
+  // slot the inverted leaf it stands for (index into DevParams::invx)
+  int32_t unit_begin;
+  int32_t inv_leaf[PGPU_PREBITS];
+  int32_t pad5_[3];
 };
 #define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 
@@ -270,7 +274,10 @@ struct InvLeafX {
   int32_t negate;
   int32_t num_docs;
   int32_t words;
+  int32_t nkeys;           // 65,536-doc container keys of the segment
+  int32_t ctab_off;        // query_kernel_rkey: its (id, key) records in DevParams::rk_ctab, id-major
 };
+#define PGPU_RKEY_PAIRS 64  // query_kernel_rkey: (leaf, id) pairs of one segment's program at most
 
 #define PGPU_RAW_RANGE_LO_INCL 1
 #define PGPU_RAW_RANGE_HI_INCL 2
@@ -414,6 +421,10 @@ struct DevParams {
   int32_t mv_gmask;               // bit g: group column g is multi-value (sparse_agg_mv expands each doc's values)
   int32_t rd_pfx;                 // register-direct: prefix planes of every segment's residual leaf (0 or PGPU_PFX_PLANES)
   int32_t rs_vplanes;             // register streaming (direct == 3): value planes held per tile (16 or 24)
+  int32_t total_units;            // query_kernel_rkey: (segment, 65,536-doc container key) units
+  int32_t rk_leaves;              // query_kernel_rkey: leaf images per LDS buffer (max BITS slots of a segment)
+  const struct InvLeafX* invx;    // query_kernel_rkey: the inverted leaves (containers read per unit)
+  const struct DevContainer* rk_ctab;  // query_kernel_rkey: container record per (leaf, id, key) (rkey_ctab_kernel)
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

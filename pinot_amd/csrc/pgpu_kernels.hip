@@ -3253,6 +3253,257 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rprog(DevPar
   direct_epilogue<PGPU_MODE_AGG>(p, L, st, wave, lane, pf);
 }
 
+// ================================================================================================================
+// INDEX-ONLY PROGRAMS OVER ROARING CONTAINERS IN LDS (p.direct == 5): query_kernel_rprog's shape when every BITS
+// leaf of every segment is an inverted-index leaf.  Instead of expanding those leaves into HBM bitmaps first
+// (invexp_kernel: one write and one read of a doc bitmap per leaf), a workgroup takes one (segment, 65,536-doc
+// container key) unit at a time, ORs the key's container of each leaf's ids into an 8 KiB LDS image per leaf
+// (BitmapBasedFilterOperator.java:66-110: bitmap containers copied, array values and runs set with LDS atomics,
+// NOT IN / <> complemented within the segment), then its four waves evaluate the unit's 32 tiles from those
+// images -- the truth table over the leaf words and sorted ranges, the value planes in a register ring that runs
+// ahead across units, so the next unit's planes are in flight while its containers are read.
+// ================================================================================================================
+FI int unit_segment(const DevParams& p, int u) {
+  int lo = 0, hi = p.nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cld(&p.segs[mid].unit_begin) <= u) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+// A wave's tile sequence over the units [u, u1): unit u's tiles wave, wave + NW, ... of its <= 32.
+struct UnitCursor {
+  int u, u1, seg, key, k, nt;  // unit, end, its segment, container key, next tile index in unit, tiles in unit
+  int ntiles_seg, unit0;
+};
+FI void unit_enter(const DevParams& p, UnitCursor& c) {
+  c.seg = unit_segment(p, c.u);
+  c.unit0 = cld(&p.segs[c.seg].unit_begin);
+  c.ntiles_seg = cld(&p.segs[c.seg].ntiles);
+  c.key = c.u - c.unit0;
+  c.nt = min(32, c.ntiles_seg - 32 * c.key);
+}
+// advance to this wave's next tile (true: *tile_in_seg / *seg set); false past the end
+FI bool unit_next(const DevParams& p, UnitCursor& c, int wave, int* seg, int* tile_in_seg) {
+  while (c.u < c.u1) {
+    if (c.k < c.nt) {
+      *seg = c.seg;
+      *tile_in_seg = 32 * c.key + c.k;
+      c.k += PGPU_DIRECT_WAVES;
+      return true;
+    }
+    if (++c.u >= c.u1) break;
+    unit_enter(p, c);
+    c.k = wave;
+  }
+  return false;
+}
+template <int NA, int NV>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevParams p) {
+  constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH, NT = PGPU_DIRECT_THREADS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  int& rk_stop = *(int*)L.ring;  // the query was cancelled: every wave leaves at the same unit
+  DevContainer* recs = (DevContainer*)(L.ring + 16);  // [PGPU_RKEY_PAIRS] the unit's container per (leaf, id)
+  uint32_t* img = (uint32_t*)(L.ring + 16 + 16 * PGPU_RKEY_PAIRS);  // [nbits][2048]: the unit's leaf images
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const int64_t t_start = now(pf);
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)wave * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  if (lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int vc0 = -1, vc1 = -1;  // the value columns, in first-use order (runtime: at most NA)
+  for (int a = 0; a < p.nagg; ++a) {
+    const int c = p.aggs[a].col;
+    if (p.aggs[a].fn == PGPU_AGG_COUNT || c == vc0) continue;
+    if (vc0 < 0) vc0 = c;
+    else vc1 = c;
+  }
+  // this workgroup's contiguous run of units (XCD-aware order, as the tile ranges of the other kernels)
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int u0 = (int)(((int64_t)p.total_units * lb) / nb);
+  const int u1 = (int)(((int64_t)p.total_units * (lb + 1)) / nb);
+  int64_t dense_bytes = 0;
+  uint32_t lane_matched = 0;
+  // the value-plane ring: issue cursor `ci` runs RD tiles ahead of the consumed sequence
+  uint32_t xv[RD][NA][NV];
+  UnitCursor ci{u0, u1, 0, 0, wave, 0, 0, 0};
+  if (u0 < u1) unit_enter(p, ci);
+  int have = 0;  // tiles issued into the ring and not yet consumed
+#define RK_ISSUE(S)                                                                                          \
+  do {                                                                                                       \
+    int sseg, stile;                                                                                         \
+    if (unit_next(p, ci, wave, &sseg, &stile)) {                                                             \
+      const DevColumn* pc = p.cols + cld(&p.segs[sseg].col_begin);                                           \
+      rs_load_planes(cld(&pc[vc0].vsliced), cld(&pc[vc0].vbits), stile, xv[S][0]);                          \
+      if constexpr (NA > 1) rs_load_planes(cld(&pc[vc1].vsliced), cld(&pc[vc1].vbits), stile, xv[S][NA - 1]); \
+      ++have;                                                                                                \
+    }                                                                                                        \
+  } while (0)
+#pragma unroll
+  for (int s = 0; s < RD; ++s) RK_ISSUE(s);
+  SegState ss;
+  int cseg = -1, nbits = 0, nsorted = 0, ps0 = 0, ps1 = 0, vb0 = 0, vb1 = 0;
+  uint32_t T = 0, negm = 0;
+  int64_t vmin0 = 0, vmin1 = 0, vbytes = 0;
+  int nid[PGPU_PREBITS] = {0, 0, 0, 0}, npairs = 0;  // ids per leaf, (leaf, id) pairs of the segment
+  int slot = 0;
+  for (int u = u0; u < u1; ++u) {
+    const int seg = unit_segment(p, u);
+    if (seg != cseg) {
+      cseg = seg;
+      load_seg(p, cseg, ss);
+      T = cld(&ss.sg->ptt);
+      nbits = cld(&ss.sg->nbits);
+      nsorted = cld(&ss.sg->pnsorted);
+      ps0 = cld(&ss.sg->psorted[0]);
+      ps1 = cld(&ss.sg->psorted[1]);
+      vb0 = cld(&ss.cols[vc0].vbits);
+      vmin0 = cld(&ss.cols[vc0].vmin);
+      vb1 = vc1 >= 0 ? cld(&ss.cols[vc1].vbits) : 0;
+      vmin1 = vc1 >= 0 ? cld(&ss.cols[vc1].vmin) : 0;
+      vbytes = 0;
+      for (int a = 0; a < p.nagg; ++a)
+        if (p.aggs[a].fn != PGPU_AGG_COUNT) vbytes += (int64_t)WT * (p.aggs[a].col == vc0 ? vb0 : vb1) / 8;
+      negm = 0;  // leaves of NOT IN / <> predicates: complemented within the segment
+      npairs = 0;
+      for (int j = 0; j < nbits; ++j) {
+        negm |= (cld(&p.invx[cld(&ss.sg->inv_leaf[j])].negate) ? 1u : 0u) << j;
+        nid[j] = cld(&p.invx[cld(&ss.sg->inv_leaf[j])].nids);
+        npairs += nid[j];
+      }
+    }
+    const int key = u - cld(&ss.sg->unit_begin);
+    const int nt = min(32, cld(&ss.sg->ntiles) - 32 * key);
+    // the unit's leaf images: every earlier reader is done, clear; the unit's container record of every (leaf, id)
+    // from the query's container table (rkey_ctab_kernel: no container search here), then OR the containers in
+    const int64_t tf = now(pf);
+    __syncthreads();
+    if (threadIdx.x == 0) rk_stop = query_cancelled(p) ? 1 : 0;
+    for (int i = threadIdx.x; i < nbits * 2048; i += NT) img[i] = 0u;
+    if (threadIdx.x < npairs) {
+      int j = 0, k = threadIdx.x;
+      while (j + 1 < nbits && k >= nid[j]) k -= nid[j++];
+      const InvLeafX X = p.invx[cld(&ss.sg->inv_leaf[j])];
+      recs[threadIdx.x] = p.rk_ctab[(size_t)X.ctab_off + (size_t)k * X.nkeys + key];
+    }
+    __syncthreads();
+    if (rk_stop) break;
+    for (int t2 = 0, j = 0, left = nbits > 0 ? nid[0] : 0; t2 < npairs; ++t2) {
+      while (left == 0) left = nid[++j];
+      --left;
+      const DevContainer rc = recs[t2];
+      const uint32_t type = sgpr(rc.type), card = sgpr(rc.card), offset = sgpr(rc.offset);
+      if (card == 0) continue;  // no container of this id under this key
+      uint32_t* w = img + j * 2048;
+      const uint8_t* data = (const uint8_t*)cld(&p.invx[cld(&ss.sg->inv_leaf[j])].data);
+      if (type == PGPU_CT_BITMAP) {
+        const uint32_t* bm = (const uint32_t*)(data + offset);
+        for (int i = threadIdx.x; i < 2048; i += NT) atomicOr(&w[i], gld(bm, i));
+      } else if (type == PGPU_CT_RUN) {
+        const uint16_t* r = (const uint16_t*)(data + offset);
+        for (uint32_t q = threadIdx.x; q < card; q += NT) {
+          const uint32_t s0 = gld(r, 2 * q), e0 = s0 + gld(r, 2 * q + 1);  // inclusive
+          const uint32_t a = s0 >> 5, z = e0 >> 5;
+          for (uint32_t x = a; x <= z; ++x) {
+            const uint32_t lo = x == a ? (s0 & 31) : 0u, hi = x == z ? (e0 & 31) : 31u;
+            atomicOr(&w[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+          }
+        }
+      } else {
+        const uint16_t* v = (const uint16_t*)(data + offset);
+        for (uint32_t q = threadIdx.x; q < card; q += NT) {
+          const uint32_t x = gld(v, q);
+          atomicOr(&w[x >> 5], 1u << (x & 31));
+        }
+      }
+    }
+    __syncthreads();
+    PROF_ADD(pf, PGPU_P_C_FETCH, tf);
+    for (int k = wave; k < nt; k += NW) {
+      if (have == 0) break;  // (never: the ring was issued over the same sequence)
+      const int64_t tt = now(pf);
+      TileCtx t;
+      t.ss = &ss;
+      t.slot = nullptr;
+      t.tile_in_seg = 32 * key + k;
+      t.doc0 = t.tile_in_seg * WT;
+      t.lane_doc0 = t.doc0 + 32 * lane;
+      {
+        const int rem = min(WT, ss.num_docs - t.doc0) - 32 * lane;
+        t.valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+      }
+      const uint32_t sw0 = nsorted > 0 ? leaf_sorted(p, t, cld(p.instrs + ps0)) : 0u;
+      const uint32_t sw1 = nsorted > 1 ? leaf_sorted(p, t, cld(p.instrs + ps1)) : 0u;
+      uint32_t w[PGPU_RPROG_LEAVES];
+#pragma unroll
+      for (int i = 0; i < PGPU_RPROG_LEAVES; ++i) {
+        uint32_t x = 0u;
+        if (i < PGPU_PREBITS && i < nbits) {
+          x = img[i * 2048 + k * 64 + lane];
+          if ((negm >> i) & 1u) x = ~x & t.valid;
+        } else if (i == nbits) {
+          x = sw0;
+        } else if (i == nbits + 1) {
+          x = sw1;
+        }
+        w[i] = x;
+      }
+      const uint32_t mm = tt_eval(T, w) & t.valid;
+      PROF_ADD(pf, PGPU_P_C_FILTER, tt);
+      const int64_t ta = now(pf);
+      lane_matched += __popc(mm);
+      const bool any = __builtin_amdgcn_ballot_w64(mm != 0) != 0;
+      mark_seg(p, ss, any);
+      // the ring slot holding this tile (issued in the same per-wave order)
+#pragma unroll
+      for (int s = 0; s < RD; ++s) {
+        if (s != slot) continue;
+        if (any) {
+          rs_fold<NV>(p, cv, la, xv[s][0], mm, vb0, vmin0, vc0);
+          if constexpr (NA > 1) rs_fold<NV>(p, cv, la, xv[s][NA - 1], mm, vb1, vmin1, vc1);
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += vbytes;
+        }
+        --have;
+        RK_ISSUE(s);
+      }
+      slot = slot + 1 == RD ? 0 : slot + 1;
+      PROF_ADD(pf, PGPU_P_C_AGG, ta);
+    }
+  }
+#undef RK_ISSUE
+  {
+    const int64_t lm = wave_sum_i64((int64_t)lane_matched);
+    PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+    Stats st;
+    st.matched = lane == 0 ? lm : 0;
+    st.scanned = 0;
+    st.sector_bytes = 0;
+    st.dense_bytes = dense_bytes;
+    direct_epilogue<PGPU_MODE_AGG>(p, L, st, wave, lane, pf);
+  }
+}
+
 // ---- the query kernel ----------------------------------------------------------------------------------------------
 template <int MODE, int DENSE>
 __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams p) {
@@ -4704,8 +4955,18 @@ static hipError_t rp_attr(size_t lds_bytes) {
   return hipFuncSetAttribute((const void*)query_kernel_rprog<NA, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds_bytes);
 }
+template <int NA, int NV>
+static hipError_t rk_attr(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void*)query_kernel_rkey<NA, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
 [[maybe_unused]] static hipError_t rp_attrs(size_t lds_bytes) {
   hipError_t e = rp_attr<1, 16>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<1, 16>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<1, 24>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<2, 16>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<2, 20>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<2, 24>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<1, 24>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 16>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 20>(lds_bytes);
@@ -4716,6 +4977,15 @@ static hipError_t rp_attr(size_t lds_bytes) {
 // columns of <= 20 planes keep three waves per SIMD, of 24 two)
 [[maybe_unused]] static void rp_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
+  if (p.direct == 5) {  // the inverted leaves' containers read into LDS per unit (query_kernel_rkey)
+    const dim3 kb(PGPU_DIRECT_THREADS);
+    if (p.rd_planes <= 1 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rkey<1, 16>), g, kb, dyn_smem, st, p);
+    else if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rkey<1, 24>), g, kb, dyn_smem, st, p);
+    else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rkey<2, 16>), g, kb, dyn_smem, st, p);
+    else if (p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rkey<2, 20>), g, kb, dyn_smem, st, p);
+    else hipLaunchKernelGGL((query_kernel_rkey<2, 24>), g, kb, dyn_smem, st, p);
+    return;
+  }
   if (p.rd_planes <= 1 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<1, 16>), g, b, dyn_smem, st, p);
   else if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rprog<1, 24>), g, b, dyn_smem, st, p);
   else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rprog<2, 16>), g, b, dyn_smem, st, p);
@@ -4737,7 +5007,7 @@ static hipError_t rp_attr(size_t lds_bytes) {
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    if (p.direct == 3 || p.direct == 4) {                                                                       \
+    if (p.direct >= 3) {                                                                                        \
       if constexpr (M == PGPU_MODE_AGG) {                                                                       \
         if (p.direct == 3) rs_launch(p, grid, dyn_smem, st);                                                    \
         else rp_launch(p, grid, dyn_smem, st);                                                                  \
@@ -5077,6 +5347,38 @@ __global__ __launch_bounds__(256) void invexp_kernel(const InvLeafX* leaves) {
     }
     L.out[word0 + i] = x;
   }
+}
+
+// query_kernel_rkey's container table: for every inverted leaf, id and 65,536-doc container key, the id's container
+// of that key (card 0: none) -- the container searches done once per query, all in parallel, so the query kernel's
+// units read one record per (leaf, id) instead of a chain of dependent directory loads.
+__global__ __launch_bounds__(256) void rkey_ctab_kernel(const InvLeafX* leaves, DevContainer* out) {
+  const InvLeafX L = cld(leaves + blockIdx.y);
+  const int64_t n = (int64_t)L.nids * L.nkeys;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint32_t k = (uint32_t)(i / L.nkeys), key = (uint32_t)(i % L.nkeys);
+    const uint32_t id = (uint32_t)gld(L.ids, k);
+    int32_t a = (int32_t)gld(L.dir, id), z = (int32_t)gld(L.dir, id + 1) - 1;
+    DevContainer r{key, 0u, 0u, 0u};
+    while (a <= z) {
+      const int32_t mid = (a + z) >> 1;
+      const DevContainer c = L.ct[mid];
+      if (c.key == key) {
+        r = c;
+        break;
+      }
+      if (c.key < key) a = mid + 1; else z = mid - 1;
+    }
+    out[(size_t)L.ctab_off + (size_t)i] = r;
+  }
+}
+
+hipError_t pgpu_launch_rkey_ctab(const InvLeafX* dev_leaves, int nleaves, int64_t max_pairs, DevContainer* out,
+                                 hipStream_t st) {
+  if (nleaves <= 0) return hipSuccess;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(256, (max_pairs + 255) / 256));
+  hipLaunchKernelGGL(rkey_ctab_kernel, dim3((unsigned)blocks, (unsigned)nleaves), dim3(256), 0, st, dev_leaves, out);
+  return hipGetLastError();
 }
 
 hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st) {

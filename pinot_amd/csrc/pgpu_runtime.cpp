@@ -58,6 +58,8 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
 hipError_t pgpu_launch_rawpred(const RawLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_mvpred(const MvLeaf* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
 hipError_t pgpu_launch_invexp(const InvLeafX* dev_leaves, int nleaves, int64_t max_words, hipStream_t st);
+hipError_t pgpu_launch_rkey_ctab(const InvLeafX* dev_leaves, int nleaves, int64_t max_pairs, DevContainer* out,
+                                 hipStream_t st);
 // on-the-fly group dictionaries of raw columns (pgpu_gdict.hip)
 size_t pgpu_gdict_temp_bytes(int64_t n);
 hipError_t pgpu_gdict_sort_unique(const void* vals, int32_t dtype, int64_t n, uint64_t* keys, uint64_t* sorted,
@@ -241,6 +243,7 @@ struct Workspace {
   DevMem segany;                       // per-segment matched words (DevParams::segany), zero between queries
   DevMem fsmfn;                        // exact filter stats on the GPU: per-tile transducer maps (andfsm kernels)
   DevMem rawbits;                      // match bitmaps of the raw-value leaves (rawpred_kernel)
+  DevMem rkctab;                       // query_kernel_rkey: container record per (leaf, id, key)
   DevMem tk_keys, tk_state;            // pgpu_table_topk: per-row order keys, radix-select state + histogram
   PinnedMem h_arena, h_stats, h_total, h_table, h_segcnt, h_leafbits, h_segany, h_fsment;
   DevMem d_cancel;                     // cancel word (DevParams::cancel): = the query's generation -> stop
@@ -1560,6 +1563,7 @@ struct Packer {
   std::vector<ProgJob> jobs;     // index-only dense programs precomputed per query (progbits_kernel)
   int32_t job_tiles = 0;
   std::vector<int32_t> invids;
+  int64_t rk_ctab_records = 0;   // query_kernel_rkey: container records of every inverted leaf (id, key)
 };
 
 // Inverted leaves are expanded into doc bitmaps while their words stay within this budget (per query); the rest
@@ -1575,6 +1579,7 @@ int64_t inv_leaf(Packer& pk, const pgpu_segment* seg, const DevColumn& dc, const
   L.negate = nd.negate ? 1 : 0;
   L.num_docs = seg->num_docs;
   L.words = (int32_t)(((int64_t)seg->num_docs + PGPU_WT - 1) / PGPU_WT * 64);
+  L.nkeys = (L.words + 2047) / 2048;
   for (const InvLeafX& o : pk.invx) {
     if (o.dir != L.dir || o.nids != L.nids || o.negate != L.negate) continue;
     if (!std::equal(nd.ids, nd.ids + nd.num_ids, pk.invids.begin() + (intptr_t)o.ids)) continue;
@@ -2977,6 +2982,45 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       p.dslots = 0;
       grid = std::max(1, g);
       dyn = rdyn;
+      // every BITS leaf an inverted one: read the containers per (segment, container key) unit into LDS instead of
+      // expanding them into HBM bitmaps first (query_kernel_rkey)
+      const bool no_rkey = getenv("PGPU_NO_RKEY") && atoi(getenv("PGPU_NO_RKEY")) != 0;  // per plan (tests)
+      bool rk = !no_rkey && !pk.invx.empty();
+      int maxbits = 0, units = 0;
+      for (DevSeg& ds : pk.segs) {
+        ds.unit_begin = units;
+        units += (ds.ntiles + 31) / 32;
+        maxbits = std::max(maxbits, (int)ds.nbits);
+        int pairs = 0;
+        for (int k = 0; k < ds.nbits && rk; ++k) {
+          int found = -1;
+          for (size_t i = 0; i < pk.invx.size() && found < 0; ++i)
+            if (pk.invx[i].out == ds.bits_w[k]) found = (int)i;  // (word offsets until launch)
+          rk = found >= 0;
+          ds.inv_leaf[k] = found;
+          if (found >= 0) pairs += pk.invx[found].nids;
+        }
+        rk = rk && pairs <= PGPU_RKEY_PAIRS;
+      }
+      // the container table (every leaf's (id, key) records) and the unit's records and leaf images in LDS
+      int64_t ctab = 0;
+      for (InvLeafX& x : pk.invx) {
+        x.ctab_off = (int32_t)ctab;
+        ctab += (int64_t)x.nids * x.nkeys;
+      }
+      rk = rk && ctab <= INT32_MAX;
+      pk.rk_ctab_records = rk ? ctab : 0;
+      const size_t kdyn = rdyn + 16 * PGPU_RKEY_PAIRS + (size_t)std::max(1, maxbits) * 8192;
+      if (rk && kdyn <= PGPU_LDS_LIMIT) {
+        p.direct = 5;
+        p.total_units = units;
+        p.rk_leaves = std::max(1, maxbits);
+        const int per_cu = (int)std::min<size_t>(nv > 1 && vbmax > 20 ? 2 : 3, PGPU_LDS_LIMIT / kdyn);
+        int gk = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, units / 2));
+        if (gk >= 8) gk &= ~7;
+        grid = std::max(1, gk);
+        dyn = kdyn;
+      }
     }
   }
   // sliced aggregation runs in the self-loading kernels only (query_kernel_direct, and query_kernel_rstream with the
@@ -3214,9 +3258,15 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.recs = (uint32_t*)ws->recs.p;
     p.rcount = (uint32_t*)ws->rcount.p;
   }
-  if (pk.raw_words > 0) {
+  if (pk.raw_words > 0 && p.direct != 5) {  // (query_kernel_rkey builds its leaf images in LDS)
     e = ws->rawbits.ensure(4ull * pk.raw_words, ctx->mpool, st);
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "raw-value leaf bitmaps: %s", hipGetErrorString(e)));
+  }
+  p.rk_ctab = nullptr;
+  if (p.direct == 5) {
+    e = ws->rkctab.ensure(sizeof(DevContainer) * (size_t)std::max<int64_t>(1, pk.rk_ctab_records), ctx->mpool, st);
+    if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "container table: %s", hipGetErrorString(e)));
+    p.rk_ctab = (const DevContainer*)ws->rkctab.p;
   }
   if (pk.fsm) {
     e = ws->fsmfn.ensure(32ull * std::max(1, p.total_tiles), ctx->mpool, st);
@@ -3321,8 +3371,15 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = pgpu_launch_rawpred((const RawLeaf*)(d + o_raw), (int)pk.raws.size(), max_raw_words, st);
   if (e == hipSuccess && !pk.mvs.empty())
     e = pgpu_launch_mvpred((const MvLeaf*)(d + o_mv), (int)pk.mvs.size(), max_mv_words, st);
-  if (e == hipSuccess && !pk.invx.empty())
+  p.invx = (const InvLeafX*)(d + o_inv);
+  if (e == hipSuccess && !pk.invx.empty() && p.direct != 5)  // (query_kernel_rkey reads the containers itself)
     e = pgpu_launch_invexp((const InvLeafX*)(d + o_inv), (int)pk.invx.size(), max_inv_words, st);
+  if (e == hipSuccess && p.direct == 5) {
+    int64_t max_pairs = 0;
+    for (const InvLeafX& x : pk.invx) max_pairs = std::max<int64_t>(max_pairs, (int64_t)x.nids * x.nkeys);
+    e = pgpu_launch_rkey_ctab((const InvLeafX*)(d + o_inv), (int)pk.invx.size(), max_pairs,
+                              (DevContainer*)ws->rkctab.p, st);
+  }
   if (e == hipSuccess && !pk.jobs.empty())
     e = pgpu_launch_progbits(p, (const ProgJob*)(d + o_jobs), (int)pk.jobs.size(), pk.job_tiles, st);
   if (e == hipSuccess)

@@ -4,7 +4,8 @@
   adanalytics  register-direct kernel (bit-sliced fast leaf + prefix pre-filter, candidate queue)
   range_in     register streaming (two bit-sliced fast leaves + the metric's value planes in VGPRs)
   range_in_lds the same query on the LDS-DMA direct kernel (PGPU_NO_RSTREAM=1), value planes per matched tile
-  bitmap5      inverted leaves expanded to bitmaps (invexp) + sorted ranges, index-only program
+  bitmap5      inverted leaves' containers read into LDS per container key (query_kernel_rkey) + sorted ranges,
+               index-only program; bitmap5_invexp the same with the leaves expanded to HBM bitmaps first (invexp)
   groupby1m    partitioned group-by (phase 1 records, phase 2 LDS tables), 1M keys
   ring_groupby ring kernel (loader waves + consumers): 50 %-selective range, 16-key LDS table, dense aggregation
 """
@@ -22,10 +23,10 @@ N = 1 << 25
 # looser variants where the bench query matches (almost) nothing at one segment
 SQL = {"adanalytics": WORKLOADS["adanalytics"].sql.replace("accountId IN (123456789)", "accountId < 123456789"),
        "range_in": WORKLOADS["range_in"].sql, "range_in_lds": WORKLOADS["range_in"].sql, "bitmap5": WORKLOADS["bitmap5"].sql,
-       "groupby1m": WORKLOADS["groupby1m"].sql,
+       "bitmap5_invexp": WORKLOADS["bitmap5"].sql, "groupby1m": WORKLOADS["groupby1m"].sql,
        "ring_groupby": "SELECT i, SUM(m), COUNT(*) FROM synth WHERE r BETWEEN 114691 AND 344060 GROUP BY i"}
-WORKLOAD_OF = {"ring_groupby": "range_in", "range_in_lds": "range_in"}
-ENV = {"range_in_lds": {"PGPU_NO_RSTREAM": "1"}}
+WORKLOAD_OF = {"ring_groupby": "range_in", "range_in_lds": "range_in", "bitmap5_invexp": "bitmap5"}
+ENV = {"range_in_lds": {"PGPU_NO_RSTREAM": "1"}, "bitmap5_invexp": {"PGPU_NO_RKEY": "1"}}
 
 
 @pytest.mark.parametrize("name", sorted(SQL))

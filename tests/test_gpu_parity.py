@@ -324,12 +324,16 @@ def _index_segment(rng, n, name):
     return build_segment(name, cols, inverted=["a", "b", "c", "e", "g"])
 
 
-@pytest.mark.parametrize("rprog", [True, False], ids=["rprog", "interp"])
+@pytest.mark.parametrize("rprog", ["rkey", "rprog", "interp"])
 @pytest.mark.parametrize("n", [1, 4097, 200_003])
 @pytest.mark.parametrize("qi", range(len(RPROG_QUERIES)))
 def test_index_only_programs_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n, rprog):
-    if not rprog:
+    """Index-only programs: the containers read into LDS per container key (query_kernel_rkey), the expanded
+    bitmaps streamed (query_kernel_rprog, PGPU_NO_RKEY=1) and the interpreter (PGPU_NO_RPROG=1)."""
+    if rprog == "interp":
         monkeypatch.setenv("PGPU_NO_RPROG", "1")
+    elif rprog == "rprog":
+        monkeypatch.setenv("PGPU_NO_RKEY", "1")
     rng = np.random.default_rng(1300 + qi + n)
     segs = [_index_segment(rng, n + 2048 * i, f"ip{i}") for i in range(3)]
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
