@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 10
+#define PGPU_ABI_VERSION 11
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -435,7 +435,16 @@ typedef struct {
   int64_t filter_stats_exact;            /* 1: num_entries_scanned_in_filter is the reference's figure */
   int64_t num_groups_limit_reached;      /* 1: a segment met >= num_groups_limit distinct group keys
                                             (AggregationGroupByOrderByOperator.java:111) */
+  int64_t kernel_variant;                /* PGPU_KV_*: the query kernel the runtime chose (diagnostic) */
 } pgpu_query_stats;
+#define PGPU_KV_RING 0       /* loader + consumer waves through an LDS ring */
+#define PGPU_KV_DIRECT 1     /* self-loading waves, LDS-DMA slots */
+#define PGPU_KV_RDIRECT 2    /* one bit-sliced fast leaf in VGPRs */
+#define PGPU_KV_RSTREAM 3    /* two fast leaves and value planes in VGPRs */
+#define PGPU_KV_RPROG 4      /* index-only program as a truth table over expanded leaf bitmaps */
+#define PGPU_KV_RKEY 5       /* index-only program over Roaring containers read into LDS per container key */
+#define PGPU_KV_CAND 6       /* candidates from a sparse leading inverted leaf's containers */
+#define PGPU_KV_PSCAN 7      /* partitioned group-by, phase-1 scan + phase-2 reduce */
 
 /* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the partial table in
  * caller-provided device memory `dev_table` (table_bytes >= pgpu_table_bytes(layout)).  Does not synchronize.

@@ -42,7 +42,7 @@ PGPU_SUM_EXP_F64 = 32767  # pgpu_table_layout.agg_sum_exp of a float64 SUM secti
 PGPU_SUM_EXP_ZERO = -32767  # ... of a fixed-point SUM over a column holding only zeros
 PGPU_MAX_FIXED_PARTS = 6  # widest fixed-point window (21-bit parts) of a floating SUM
 PGPU_FIXED_TOL_BITS = 40
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class PinotGpuError(RuntimeError):
@@ -111,6 +111,10 @@ class SegmentBytes(C.Structure):
                                            "value_planes", "total")]
 
 
+# pgpu_query_stats.kernel_variant
+PGPU_KV_RING, PGPU_KV_DIRECT, PGPU_KV_RDIRECT, PGPU_KV_RSTREAM, PGPU_KV_RPROG, PGPU_KV_RKEY, PGPU_KV_CAND, PGPU_KV_PSCAN = \
+    range(8)
+
 # derived copies seal may build per column (pgpu_segment_set_derived)
 PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES, PGPU_DERIVE_ALL = 1, 2, 3
 
@@ -119,7 +123,8 @@ class QueryStats(C.Structure):
     _fields_ = [("num_docs_scanned", C.c_int64), ("num_entries_scanned_in_filter", C.c_int64),
                 ("num_total_docs", C.c_int64), ("num_segments_matched", C.c_int64),
                 ("sparse_sector_bytes", C.c_int64), ("dense_bytes", C.c_int64), ("kernel_ms", C.c_double),
-                ("filter_stats_exact", C.c_int64), ("num_groups_limit_reached", C.c_int64)]
+                ("filter_stats_exact", C.c_int64), ("num_groups_limit_reached", C.c_int64),
+                ("kernel_variant", C.c_int64)]
 
 
 PGPU_TOPK_AGG, PGPU_TOPK_GROUP = 0, 1

@@ -168,9 +168,12 @@ struct DevSeg {
   int32_t psorted[2];
   // query_kernel_rkey (DevParams::direct == 5): the segment's first (segment, container key) unit, and for each BITS
   // slot the inverted leaf it stands for (index into DevParams::invx)
+  // query_kernel_cand (direct == 6) units are the containers of the leading inverted leaf instead: unit_begin is the
+  // segment's first, cand_leaf that leaf (index into DevParams::invx)
   int32_t unit_begin;
   int32_t inv_leaf[PGPU_PREBITS];
-  int32_t pad5_[3];
+  int32_t cand_leaf;
+  int32_t pad5_[2];
 };
 #define PGPU_PFX_PLANES 3  // top bit planes of the residual column streamed beside the fast leaf (DevParams::rd_pfx)
 
@@ -276,6 +279,8 @@ struct InvLeafX {
   int32_t words;
   int32_t nkeys;           // 65,536-doc container keys of the segment
   int32_t ctab_off;        // query_kernel_rkey: its (id, key) records in DevParams::rk_ctab, id-major
+  int32_t skip;            // not expanded (query_kernel_cand iterates its containers and nothing reads `out`)
+  int32_t pad_;
 };
 #define PGPU_RKEY_PAIRS 64  // query_kernel_rkey: (leaf, id) pairs of one segment's program at most
 
@@ -421,10 +426,12 @@ struct DevParams {
   int32_t mv_gmask;               // bit g: group column g is multi-value (sparse_agg_mv expands each doc's values)
   int32_t rd_pfx;                 // register-direct: prefix planes of every segment's residual leaf (0 or PGPU_PFX_PLANES)
   int32_t rs_vplanes;             // register streaming (direct == 3): value planes held per tile (16 or 24)
-  int32_t total_units;            // query_kernel_rkey: (segment, 65,536-doc container key) units
+  int32_t total_units;            // query_kernel_rkey: (segment, 65,536-doc container key) units; query_kernel_cand:
+                                  // (segment, container) units
   int32_t rk_leaves;              // query_kernel_rkey: leaf images per LDS buffer (max BITS slots of a segment)
   const struct InvLeafX* invx;    // query_kernel_rkey: the inverted leaves (containers read per unit)
   const struct DevContainer* rk_ctab;  // query_kernel_rkey: container record per (leaf, id, key) (rkey_ctab_kernel)
+  const uint32_t* cand_ct;        // query_kernel_cand: per unit {segment, its container's index in InvLeafX::ct}
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

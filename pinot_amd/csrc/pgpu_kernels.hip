@@ -3504,6 +3504,138 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
   }
 }
 
+// ================================================================================================================
+// CANDIDATE ITERATION from a sparse leading inverted leaf (p.direct == 6).  AndDocIdSet.iterator iterates the index
+// child's bitmap and applies the scan children to those docs only (AndDocIdSet.java:87-140, SVScanDocIdIterator
+// .applyAnd :79-94).  When every segment's dense program is one inclusive inverted leaf whose ids hold few docs, the
+// launch runs over that leaf's Roaring containers -- one unit per (segment, container) -- instead of over tiles: a
+// wave turns its container's docs into candidate-queue entries (array values as they are, bitmap and run containers
+// through a private 8 KiB LDS image), and flush_queue applies the residual program and the sparse aggregation to
+// them.  Tiles holding no doc of the leaf are never visited.  A single-value column's ids have disjoint doc sets, so
+// no doc is queued twice (the runtime takes a multi-value column here with one id only).
+// ================================================================================================================
+template <int MODE>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_cand(DevParams p) {
+  constexpr int NT = PGPU_DIRECT_THREADS, NW = PGPU_DIRECT_WAVES;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  if (MODE == PGPU_MODE_LDS) {
+    const int n = p.nsec * (int)p.G;
+    for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+  }
+  __syncthreads();
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const int64_t t_start = now(pf);
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)wave * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  uint32_t* img = (uint32_t*)(L.ring + (size_t)wave * 8192);  // [2048] this wave's container image
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  SegState ss;
+  int cseg = -1;
+  const DevContainer* ct = nullptr;
+  const uint8_t* data = nullptr;
+  const int nwaves = gridDim.x * NW;
+  int poll = 0;
+  for (int u = blockIdx.x * NW + wave; u < p.total_units; u += nwaves) {
+    if ((poll++ & 7) == 0 && query_cancelled(p)) break;
+    const int64_t tf = now(pf);
+    const int seg = sgpr((int)cld(p.cand_ct + 2 * (size_t)u));
+    const uint32_t ci = (uint32_t)sgpr((int)cld(p.cand_ct + 2 * (size_t)u + 1));
+    if (seg != cseg) {
+      cseg = seg;
+      load_seg(p, cseg, ss);
+      const int leaf = cld(&ss.sg->cand_leaf);
+      ct = (const DevContainer*)cld(&p.invx[leaf].ct);
+      data = (const uint8_t*)cld(&p.invx[leaf].data);
+    }
+    const uint32_t key = (uint32_t)sgpr((int)cld(&ct[ci].key)), type = (uint32_t)sgpr((int)cld(&ct[ci].type));
+    const uint32_t card = (uint32_t)sgpr((int)cld(&ct[ci].card)), off = (uint32_t)sgpr((int)cld(&ct[ci].offset));
+    // the container spans 32 tiles: queue entry = tile index << 11 | doc in tile = the doc's low 16 bits
+    if (lane < PGPU_CQ_TILES) cv.qtiles[lane] = (int)key * PGPU_CQ_TILES + lane;
+    PROF_ADD(pf, PGPU_P_C_FETCH, tf);
+    const int64_t tq = now(pf);
+    if (type != PGPU_CT_BITMAP && type != PGPU_CT_RUN) {  // array: the sorted low 16 bits themselves
+      const uint16_t* v = (const uint16_t*)(data + off);
+      for (uint32_t b = 0; b < card; b += PGPU_CQ_CAP) {
+        const int n = (int)min((uint32_t)PGPU_CQ_CAP, card - b);
+        for (int i = lane; i < n; i += 64) cv.queue[i] = gld(v, b + i);
+        flush_queue<MODE, NW>(p, L, cv, la, ss, n, matched, scanned, sector_bytes, dense_bytes, pf);
+      }
+      PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+      continue;
+    }
+    if (type == PGPU_CT_BITMAP) {
+      const uint32_t* bm = (const uint32_t*)(data + off);
+      for (int i = lane; i < 2048; i += 64) img[i] = gld(bm, i);
+    } else {
+      for (int i = lane; i < 2048; i += 64) img[i] = 0u;
+      wave_sync();
+      const uint16_t* r = (const uint16_t*)(data + off);
+      for (uint32_t q = lane; q < card; q += 64) {
+        const uint32_t s0 = gld(r, 2 * q), e0 = s0 + gld(r, 2 * q + 1);  // inclusive
+        const uint32_t a = s0 >> 5, z = e0 >> 5;
+        for (uint32_t x = a; x <= z; ++x) {
+          const uint32_t lo = x == a ? (s0 & 31) : 0u, hi = x == z ? (e0 & 31) : 31u;
+          atomicOr(&img[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+        }
+      }
+    }
+    wave_sync();
+    // the image's set bits in doc order, PGPU_CQ_CAP entries per flush
+    int qn = 0;
+    for (int w0 = 0; w0 < 2048; w0 += 64) {
+      uint32_t x = img[w0 + lane];
+      const int c = __popc(x);
+      const int tot = sgpr(wave_sum_i32(c));
+      if (tot == 0) continue;
+      if (qn + tot > PGPU_CQ_CAP) {
+        flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+        qn = 0;
+      }
+      int at = qn + wave_excl_scan(c);
+      while (x) {
+        const int bit = __ffs(x) - 1;
+        x &= x - 1u;
+        cv.queue[at++] = (uint16_t)((w0 + lane) * 32 + bit);
+      }
+      qn += tot;
+    }
+    if (qn) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+    PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  if (MODE == PGPU_MODE_AGG) {
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  }
+  Stats st;
+  st.matched = matched;
+  st.scanned = scanned;
+  st.sector_bytes = sector_bytes;
+  st.dense_bytes = dense_bytes;
+  direct_epilogue<MODE>(p, L, st, wave, lane, pf);
+}
+
 // ---- the query kernel ----------------------------------------------------------------------------------------------
 template <int MODE, int DENSE>
 __global__ __launch_bounds__(PGPU_THREADS(DENSE), 1) void query_kernel(DevParams p) {
@@ -5007,7 +5139,12 @@ static hipError_t rk_attr(size_t lds_bytes) {
     return hipGetLastError();                                                                                   \
   }                                                                                                             \
   hipError_t pgpu_launch_direct_##NAME(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {         \
-    if (p.direct >= 3) {                                                                                        \
+    if (p.direct == 6) {                                                                                        \
+      if constexpr (M != PGPU_MODE_PART)                                                                        \
+        hipLaunchKernelGGL((query_kernel_cand<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);     \
+      else                                                                                                      \
+        return hipErrorInvalidValue;                                                                            \
+    } else if (p.direct >= 3) {                                                                                 \
       if constexpr (M == PGPU_MODE_AGG) {                                                                       \
         if (p.direct == 3) rs_launch(p, grid, dyn_smem, st);                                                    \
         else rp_launch(p, grid, dyn_smem, st);                                                                  \
@@ -5029,6 +5166,10 @@ static hipError_t rk_attr(size_t lds_bytes) {
     if (e == hipSuccess)                                                                                        \
       e = hipFuncSetAttribute((const void*)query_kernel_direct<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                               (int)lds_bytes);                                                                  \
+    if constexpr (M != PGPU_MODE_PART)                                                                          \
+      if (e == hipSuccess)                                                                                      \
+        e = hipFuncSetAttribute((const void*)query_kernel_cand<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                (int)lds_bytes);                                                                \
     if (e == hipSuccess) e = rd_attrs<M, 0>(lds_bytes);                                                         \
     if (e == hipSuccess) e = rd_attrs<M, PGPU_PFX_PLANES>(lds_bytes);                                           \
     if constexpr (M == PGPU_MODE_AGG)                                                                           \
@@ -5305,7 +5446,7 @@ __global__ __launch_bounds__(256) void invexp_kernel(const InvLeafX* leaves) {
   const InvLeafX L = cld(leaves + blockIdx.y);
   const uint32_t key = blockIdx.x;
   const int64_t word0 = (int64_t)key * 2048;
-  if (word0 >= L.words) return;
+  if (word0 >= L.words || L.skip) return;
   const int t = threadIdx.x;
   for (int i = t; i < 2048; i += 256) w[i] = 0u;
   __syncthreads();

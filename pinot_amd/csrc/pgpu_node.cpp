@@ -474,6 +474,7 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
     tot.sparse_sector_bytes += st.sparse_sector_bytes;
     tot.dense_bytes += st.dense_bytes;
     tot.kernel_ms = std::max(tot.kernel_ms, st.kernel_ms);
+    tot.kernel_variant = std::max(tot.kernel_variant, st.kernel_variant);
     tot.filter_stats_exact &= st.filter_stats_exact;
   }
   if (rc) return rc;

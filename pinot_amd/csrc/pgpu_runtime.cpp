@@ -313,6 +313,8 @@ struct HostColumn {
   int32_t vbits = 0;
   uint64_t fwd_bytes = 0, dict_bytes = 0, inv_bytes = 0;
   std::vector<uint32_t> inv_cards;     // docs per dict id of the inverted index (selectivity estimates)
+  std::vector<uint32_t> inv_hdir;      // its container directory (first container of each dict id, then the total):
+                                       // query_kernel_cand's unit list is built on the host
   std::vector<int32_t> sorted_pairs;   // sorted index (start, end) per dict id (selectivity estimates)
   std::vector<uint8_t> hdict;          // numeric dictionary, little-endian (per-segment predicate planning)
   double max_abs = 0;                  // numeric dictionary (or raw values): largest |value| (integer SUM bound)
@@ -1039,6 +1041,7 @@ int pgpu_segment_add_inverted_index(pgpu_segment* seg, int32_t column, const voi
   c.inv_card = cardinality;
   c.inv_bytes = num_bytes;
   c.inv_cards.swap(cards);
+  c.inv_hdir.swap(dir);
   return PGPU_OK;
 }
 
@@ -1564,11 +1567,16 @@ struct Packer {
   int32_t job_tiles = 0;
   std::vector<int32_t> invids;
   int64_t rk_ctab_records = 0;   // query_kernel_rkey: container records of every inverted leaf (id, key)
+  std::vector<uint32_t> cand;    // query_kernel_cand: {segment, container index} per unit
 };
 
 // Inverted leaves are expanded into doc bitmaps while their words stay within this budget (per query); the rest
 // are evaluated per tile (bitmap_word).  PGPU_NO_INVEXP=1 turns the expansion off.
 constexpr int64_t kInvExpMaxWords = (int64_t)1 << 29;  // 2 GiB of bitmaps
+// query_kernel_cand: the leading inverted leaf's ids hold at most this share of each segment's docs (above it the tile
+// sweep reads the expanded bitmap at stream speed), in at most this many containers per query
+constexpr double kCandDensity = 1.0 / 16;
+constexpr size_t kCandMaxUnits = (size_t)1 << 24;
 
 int64_t inv_leaf(Packer& pk, const pgpu_segment* seg, const DevColumn& dc, const pgpu_filter_node& nd) {
   InvLeafX L{};
@@ -3023,6 +3031,77 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       }
     }
   }
+  // candidate iteration from a sparse leading inverted leaf (query_kernel_cand; AndDocIdSet.java:87-140): every
+  // segment's dense program is one inclusive inverted leaf (a BITS leaf over its expansion) whose ids hold at most
+  // kCandDensity of the segment's docs; the units are that leaf's containers, so the tiles without a doc of the leaf
+  // are never visited and the leaf is not expanded.  PGPU_NO_CAND=1 / PGPU_CAND_DENSITY (read per plan: tests).
+  pk.cand.clear();
+  if (p.direct == 1 && !pk.invx.empty()) {
+    const bool no_cand = getenv("PGPU_NO_CAND") && atoi(getenv("PGPU_NO_CAND")) != 0;
+    const double cand_max = getenv("PGPU_CAND_DENSITY") ? atof(getenv("PGPU_CAND_DENSITY")) : kCandDensity;
+    bool ok = !no_cand;
+    std::vector<uint32_t> units;
+    std::vector<int> leaves;
+    for (int s = 0; s < (int)pk.segs.size() && ok; ++s) {
+      DevSeg& ds = pk.segs[s];
+      ds.unit_begin = (int32_t)(units.size() / 2);
+      ds.cand_leaf = -1;
+      if (ds.ntiles == 0) continue;
+      ok = ds.prog_len == 1 && ds.nstage == 0 && ds.fast == 0 && ds.nvstage == 0 && ds.single_bits == 0 &&
+           (ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&
+           pk.instrs[ds.prog_begin].op == PGPU_I_BITS;
+      if (!ok) break;
+      const DevInstr& in = pk.instrs[ds.prog_begin];
+      int leaf = -1;
+      for (size_t i = 0; i < pk.invx.size() && leaf < 0; ++i)
+        if (pk.invx[i].out == in.fwd) leaf = (int)i;  // (word offsets until launch)
+      ok = leaf >= 0 && !pk.invx[leaf].negate && in.col >= 0 && in.col < q->num_columns;
+      if (!ok) break;
+      const InvLeafX& x = pk.invx[leaf];
+      const pgpu_segment* sgm = q->segments[s].segment;
+      const HostColumn& h = sgm->cols[q->segments[s].column_map[in.col]];
+      const DevColumn& dc = pk.cols[ds.col_begin + in.col];
+      ok = (x.nids == 1 || dc.kind == PGPU_COL_FIXED_BIT || dc.kind == PGPU_COL_RAW) &&
+           h.inv_hdir.size() == (size_t)h.inv_card + 1 && h.inv_cards.size() == (size_t)h.inv_card;
+      const int32_t* ids = pk.invids.data() + (intptr_t)x.ids;
+      double docs = 0;
+      for (int k = 0; k < x.nids && ok; ++k) {
+        ok = ids[k] >= 0 && ids[k] < h.inv_card;
+        if (ok) docs += h.inv_cards[ids[k]];
+      }
+      ok = ok && docs <= cand_max * (double)sgm->num_docs;
+      for (int k = 0; k < x.nids && ok; ++k)
+        for (uint32_t c = h.inv_hdir[ids[k]]; c < h.inv_hdir[ids[k] + 1]; ++c) {
+          units.push_back((uint32_t)s);
+          units.push_back(c);
+        }
+      ok = ok && units.size() / 2 <= kCandMaxUnits;
+      ds.cand_leaf = leaf;
+      leaves.push_back(leaf);
+    }
+    // a wave's consumer area and 8 KiB container image; four waves per workgroup
+    const size_t cdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + (size_t)4 * 8192;
+    if (ok && cdyn <= PGPU_LDS_LIMIT) {
+      const int nu = (int)(units.size() / 2);
+      const int per_cu = (int)std::min<size_t>(4, PGPU_LDS_LIMIT / cdyn);
+      const int g = (int)std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, (nu + 3) / 4));
+      p.direct = 6;
+      p.total_units = nu;
+      grid = std::max(1, g);
+      dyn = cdyn;
+      pk.cand.swap(units);
+      // the iterated leaves need no doc bitmap unless the exact-statistics replay or a residual program reads it
+      std::vector<const uint32_t*> read;
+      for (const DevSeg& ds : pk.segs)
+        for (int i = ds.rprog_begin; i < ds.rprog_begin + ds.rprog_len; ++i)
+          if (pk.instrs[i].op == PGPU_I_BITS) read.push_back(pk.instrs[i].fwd);
+      if (pk.leaf_words == 0)
+        for (int lf : leaves)
+          if (std::find(read.begin(), read.end(), pk.invx[lf].out) == read.end()) pk.invx[lf].skip = 1;
+    } else {
+      for (DevSeg& ds : pk.segs) ds.cand_leaf = -1;
+    }
+  }
   // sliced aggregation runs in the self-loading kernels only (query_kernel_direct, and query_kernel_rstream with the
   // value planes in VGPRs): elsewhere its segments gather per candidate (their staged aggregation planes are then
   // only extra DMA, never read)
@@ -3137,6 +3216,18 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   }
   const int nwaves = grid * (p.direct || p.pscan ? 4 : PGPU_WAVES_OF(p.dense));
 
+  static const bool trace = getenv("PGPU_PLAN_TRACE") && atoi(getenv("PGPU_PLAN_TRACE")) != 0;
+  if (trace) {  // diagnostics: the plan of each segment and the kernel chosen
+    fprintf(stderr, "[pgpu plan] mode %d dense %d direct %d pscan %d grid %d dyn %zu tiles %d units %d invx %zu\n",
+            p.mode, p.dense, p.direct, p.pscan, grid, dyn, p.total_tiles, p.total_units, pk.invx.size());
+    for (size_t i = 0; i < pk.segs.size(); ++i) {
+      const DevSeg& ds = pk.segs[i];
+      fprintf(stderr, "[pgpu plan]  seg %zu tiles %d prog %d (op %d) rprog %d agg_mode %d nstage %d fast %d sliced %d "
+              "nvstage %d single_bits %d nbits %d\n", i, ds.ntiles, ds.prog_len,
+              ds.prog_len ? pk.instrs[ds.prog_begin].op : -1, ds.rprog_len, ds.agg_mode, ds.nstage, ds.fast,
+              ds.stage_sliced, ds.nvstage, ds.single_bits, ds.nbits);
+    }
+  }
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
   hipStream_t bail_stream = nullptr;
@@ -3176,7 +3267,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   const size_t o_inv = align16(o_mvset + pk.mvsets.size() * 4);
   const size_t o_invids = align16(o_inv + pk.invx.size() * sizeof(InvLeafX));
   const size_t o_jobs = align16(o_invids + pk.invids.size() * 4);
-  const size_t total = align16(o_jobs + pk.jobs.size() * sizeof(ProgJob)) + 16;
+  const size_t o_cand = align16(o_jobs + pk.jobs.size() * sizeof(ProgJob));
+  const size_t total = align16(o_cand + pk.cand.size() * 4) + 16;
   hipError_t e = ws->h_arena.ensure(total);
   if (e == hipSuccess) e = ws->arena.ensure(total, ctx->mpool, st);
   if (e == hipSuccess) e = ws->slab.ensure(8ull * nwaves * L.num_sections + 16, ctx->mpool, st);
@@ -3332,6 +3424,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     for (int k = 0; k < jb.nbits; ++k) jb.bits_w[k] = (const uint32_t*)ws->rawbits.p + (intptr_t)jb.bits_w[k];
   }
   memcpy(h + o_jobs, pk.jobs.data(), pk.jobs.size() * sizeof(ProgJob));
+  memcpy(h + o_cand, pk.cand.data(), pk.cand.size() * 4);
+  p.cand_ct = (const uint32_t*)(d + o_cand);
   memcpy(h + o_invids, pk.invids.data(), pk.invids.size() * 4);
   memcpy(h + o_mvset, pk.mvsets.data(), pk.mvsets.size() * 4);
   memcpy(h + o_raw, pk.raws.data(), pk.raws.size() * sizeof(RawLeaf));
@@ -3372,7 +3466,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess && !pk.mvs.empty())
     e = pgpu_launch_mvpred((const MvLeaf*)(d + o_mv), (int)pk.mvs.size(), max_mv_words, st);
   p.invx = (const InvLeafX*)(d + o_inv);
-  if (e == hipSuccess && !pk.invx.empty() && p.direct != 5)  // (query_kernel_rkey reads the containers itself)
+  bool expand = false;  // (query_kernel_rkey and query_kernel_cand read their leaves' containers themselves)
+  for (const InvLeafX& x : pk.invx) expand |= !x.skip;
+  if (e == hipSuccess && expand && p.direct != 5)
     e = pgpu_launch_invexp((const InvLeafX*)(d + o_inv), (int)pk.invx.size(), max_inv_words, st);
   if (e == hipSuccess && p.direct == 5) {
     int64_t max_pairs = 0;
@@ -3562,6 +3658,7 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, qq->ws->ev0, qq->ws->ev1));
   qq->stats.kernel_ms = ms;
+  qq->stats.kernel_variant = qq->params.pscan ? PGPU_KV_PSCAN : qq->params.direct;
   if (const int st = qq->stop.load()) {
     if (out_stats) *out_stats = qq->stats;
     return fail(st, st == PGPU_E_TIMEOUT ? "query passed its deadline before it finished (EXECUTION_TIMEOUT_ERROR)"

@@ -292,6 +292,7 @@ class ExecutionStats:
     num_groups_limit_reached: bool = False   # some segment met >= numGroupsLimit distinct group keys
     num_segments_matched: int = 0            # segments with numDocsScanned > 0 (CombineOperatorUtils.java:64-67)
     segment_matched: Optional[np.ndarray] = None  # per segment of the launch (uint8), for unions over passes
+    kernel_variant: int = -1                 # PGPU_KV_* of the launch (diagnostic; -1: not a single GPU launch)
 
 
 def key_words_out(L: TableLayout) -> int:
@@ -808,7 +809,8 @@ class GpuPlanMaker:
                                dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact),
                                num_groups_limit_reached=bool(st.num_groups_limit_reached),
                                num_segments_matched=st.num_segments_matched,
-                               segment_matched=pending.matched[:pending.num_segments].copy())
+                               segment_matched=pending.matched[:pending.num_segments].copy(),
+                               kernel_variant=st.kernel_variant)
         return finish(query, table, [g[0] for g in pending.globals_], stats)
 
     def execute(self, query: QueryContext, segments: Sequence[GpuSegment]) -> QueryResult:

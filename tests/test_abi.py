@@ -36,7 +36,7 @@ def test_abi_version_and_struct_sizes():
     assert lib.pgpu_abi_version() == _lib.ABI_VERSION
     assert C.sizeof(_lib.FilterNode) == 48
     assert C.sizeof(_lib.Agg) == 8
-    assert C.sizeof(_lib.QueryStats) == 72
+    assert C.sizeof(_lib.QueryStats) == 80
 
 
 def test_init_fails_loudly_without_a_gpu():
