@@ -168,8 +168,9 @@ struct DevSeg {
   int32_t psorted[2];
   // query_kernel_rkey (DevParams::direct == 5): the segment's first (segment, container key) unit, and for each BITS
   // slot the inverted leaf it stands for (index into DevParams::invx)
-  // query_kernel_cand (direct == 6) units are the containers of the leading inverted leaf instead: unit_begin is the
-  // segment's first, cand_leaf that leaf (index into DevParams::invx)
+  // query_kernel_cand (direct == 6) units are the containers of the leading inverted leaf (or the sorted leaf's
+  // ranges) instead: unit_begin is the segment's first, cand_leaf the inverted leaf (index into DevParams::invx; -1
+  // for a sorted one)
   int32_t unit_begin;
   int32_t inv_leaf[PGPU_PREBITS];
   int32_t cand_leaf;
@@ -431,7 +432,8 @@ struct DevParams {
   int32_t rk_leaves;              // query_kernel_rkey: leaf images per LDS buffer (max BITS slots of a segment)
   const struct InvLeafX* invx;    // query_kernel_rkey: the inverted leaves (containers read per unit)
   const struct DevContainer* rk_ctab;  // query_kernel_rkey: container record per (leaf, id, key) (rkey_ctab_kernel)
-  const uint32_t* cand_ct;        // query_kernel_cand: per unit {segment, its container's index in InvLeafX::ct}
+  const uint32_t* cand_ct;        // query_kernel_cand: per unit {segment, its container's index in InvLeafX::ct
+                                  // (~0u: a sorted leaf's doc range), first doc, last doc}
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];

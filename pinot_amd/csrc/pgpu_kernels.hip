@@ -3505,13 +3505,13 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
 }
 
 // ================================================================================================================
-// CANDIDATE ITERATION from a sparse leading inverted leaf (p.direct == 6).  AndDocIdSet.iterator iterates the index
+// CANDIDATE ITERATION from a sparse leading index leaf (p.direct == 6).  AndDocIdSet.iterator iterates the index
 // child's bitmap and applies the scan children to those docs only (AndDocIdSet.java:87-140, SVScanDocIdIterator
-// .applyAnd :79-94).  When every segment's dense program is one inclusive inverted leaf whose ids hold few docs, the
-// launch runs over that leaf's Roaring containers -- one unit per (segment, container) -- instead of over tiles: a
-// wave turns its container's docs into candidate-queue entries (array values as they are, bitmap and run containers
-// through a private 8 KiB LDS image), and flush_queue applies the residual program and the sparse aggregation to
-// them.  Tiles holding no doc of the leaf are never visited.  A single-value column's ids have disjoint doc sets, so
+// .applyAnd :79-94).  When every segment's dense program is one inclusive inverted or sorted leaf holding few docs,
+// the launch runs over that leaf's Roaring containers (or sorted doc ranges split at 65,536-doc keys) -- one unit
+// each -- instead of over tiles: a wave turns its unit's docs into candidate-queue entries (array values as they
+// are, bitmap and run containers through a private 8 KiB LDS image, ranges counted out), and flush_queue applies the
+// residual program and the sparse aggregation to them.  Tiles holding no doc of the leaf are never visited.  A single-value column's ids have disjoint doc sets, so
 // no doc is queued twice (the runtime takes a multi-value column here with one id only).
 // ================================================================================================================
 template <int MODE>
@@ -3558,14 +3558,30 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_cand(DevPara
   for (int u = blockIdx.x * NW + wave; u < p.total_units; u += nwaves) {
     if ((poll++ & 7) == 0 && query_cancelled(p)) break;
     const int64_t tf = now(pf);
-    const int seg = sgpr((int)cld(p.cand_ct + 2 * (size_t)u));
-    const uint32_t ci = (uint32_t)sgpr((int)cld(p.cand_ct + 2 * (size_t)u + 1));
+    const uint32_t* ur = p.cand_ct + 4 * (size_t)u;
+    const int seg = sgpr((int)cld(ur));
+    const uint32_t ci = (uint32_t)sgpr((int)cld(ur + 1));
     if (seg != cseg) {
       cseg = seg;
       load_seg(p, cseg, ss);
       const int leaf = cld(&ss.sg->cand_leaf);
-      ct = (const DevContainer*)cld(&p.invx[leaf].ct);
-      data = (const uint8_t*)cld(&p.invx[leaf].data);
+      if (leaf >= 0) {
+        ct = (const DevContainer*)cld(&p.invx[leaf].ct);
+        data = (const uint8_t*)cld(&p.invx[leaf].data);
+      }
+    }
+    if (ci == ~0u) {  // a sorted leaf's doc range [lo, hi] within one 65,536-doc key
+      const uint32_t lo = (uint32_t)sgpr((int)cld(ur + 2)), hi = (uint32_t)sgpr((int)cld(ur + 3));
+      if (lane < PGPU_CQ_TILES) cv.qtiles[lane] = (int)(lo >> 16) * PGPU_CQ_TILES + lane;
+      PROF_ADD(pf, PGPU_P_C_FETCH, tf);
+      const int64_t tq = now(pf);
+      for (uint32_t b = lo; b <= hi; b += PGPU_CQ_CAP) {
+        const int n = (int)min((uint32_t)PGPU_CQ_CAP, hi - b + 1);
+        for (int i = lane; i < n; i += 64) cv.queue[i] = (uint16_t)((b + i) & 0xFFFFu);
+        flush_queue<MODE, NW>(p, L, cv, la, ss, n, matched, scanned, sector_bytes, dense_bytes, pf);
+      }
+      PROF_ADD(pf, PGPU_P_C_FLUSH, tq);
+      continue;
     }
     const uint32_t key = (uint32_t)sgpr((int)cld(&ct[ci].key)), type = (uint32_t)sgpr((int)cld(&ct[ci].type));
     const uint32_t card = (uint32_t)sgpr((int)cld(&ct[ci].card)), off = (uint32_t)sgpr((int)cld(&ct[ci].offset));

@@ -1567,7 +1567,7 @@ struct Packer {
   int32_t job_tiles = 0;
   std::vector<int32_t> invids;
   int64_t rk_ctab_records = 0;   // query_kernel_rkey: container records of every inverted leaf (id, key)
-  std::vector<uint32_t> cand;    // query_kernel_cand: {segment, container index} per unit
+  std::vector<uint32_t> cand;    // query_kernel_cand: {segment, container index or ~0u, first doc, last doc} per unit
 };
 
 // Inverted leaves are expanded into doc bitmaps while their words stay within this budget (per query); the rest
@@ -3031,34 +3031,50 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       }
     }
   }
-  // candidate iteration from a sparse leading inverted leaf (query_kernel_cand; AndDocIdSet.java:87-140): every
-  // segment's dense program is one inclusive inverted leaf (a BITS leaf over its expansion) whose ids hold at most
-  // kCandDensity of the segment's docs; the units are that leaf's containers, so the tiles without a doc of the leaf
-  // are never visited and the leaf is not expanded.  PGPU_NO_CAND=1 / PGPU_CAND_DENSITY (read per plan: tests).
+  // candidate iteration from a sparse leading index leaf (query_kernel_cand; AndDocIdSet.java:87-140): every
+  // segment's dense program is one inclusive inverted leaf (a BITS leaf over its expansion) or sorted leaf holding at
+  // most kCandDensity of the segment's docs; the units are the inverted leaf's containers or the sorted ranges split
+  // at 65,536-doc keys, so the tiles without a doc of the leaf are never visited and the leaf is not expanded.  PGPU_NO_CAND=1 / PGPU_CAND_DENSITY (read per plan: tests).
   pk.cand.clear();
-  if (p.direct == 1 && !pk.invx.empty()) {
+  if (p.direct == 1) {
     const bool no_cand = getenv("PGPU_NO_CAND") && atoi(getenv("PGPU_NO_CAND")) != 0;
     const double cand_max = getenv("PGPU_CAND_DENSITY") ? atof(getenv("PGPU_CAND_DENSITY")) : kCandDensity;
     bool ok = !no_cand;
-    std::vector<uint32_t> units;
+    std::vector<uint32_t> units;  // {segment, container index (~0u: a sorted doc range), first doc, last doc}
     std::vector<int> leaves;
     for (int s = 0; s < (int)pk.segs.size() && ok; ++s) {
       DevSeg& ds = pk.segs[s];
-      ds.unit_begin = (int32_t)(units.size() / 2);
+      ds.unit_begin = (int32_t)(units.size() / 4);
       ds.cand_leaf = -1;
       if (ds.ntiles == 0) continue;
       ok = ds.prog_len == 1 && ds.nstage == 0 && ds.fast == 0 && ds.nvstage == 0 && ds.single_bits == 0 &&
-           (ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE) &&
-           pk.instrs[ds.prog_begin].op == PGPU_I_BITS;
+           (ds.agg_mode == PGPU_AM_COUNT || ds.agg_mode == PGPU_AM_SPARSE);
       if (!ok) break;
       const DevInstr& in = pk.instrs[ds.prog_begin];
+      const pgpu_segment* sgm = q->segments[s].segment;
+      if (in.op == PGPU_I_SORTED) {  // SortedIndexBasedFilterOperator: doc ranges, split at container keys
+        ok = !in.negate;
+        int64_t docs = 0;
+        for (int k = 0; k < in.n && ok; ++k) docs += (int64_t)pk.pool[in.pool_off + 2 * k + 1] - pk.pool[in.pool_off + 2 * k] + 1;
+        ok = ok && (double)docs <= cand_max * (double)sgm->num_docs;
+        for (int k = 0; k < in.n && ok; ++k) {
+          for (int64_t lo = pk.pool[in.pool_off + 2 * k], hi = pk.pool[in.pool_off + 2 * k + 1]; lo <= hi;) {
+            const int64_t end = std::min<int64_t>(hi, (lo | 0xFFFF));
+            units.insert(units.end(), {(uint32_t)s, ~0u, (uint32_t)lo, (uint32_t)end});
+            lo = end + 1;
+          }
+        }
+        ok = ok && units.size() / 4 <= kCandMaxUnits;
+        continue;
+      }
+      ok = in.op == PGPU_I_BITS;
+      if (!ok) break;
       int leaf = -1;
       for (size_t i = 0; i < pk.invx.size() && leaf < 0; ++i)
         if (pk.invx[i].out == in.fwd) leaf = (int)i;  // (word offsets until launch)
       ok = leaf >= 0 && !pk.invx[leaf].negate && in.col >= 0 && in.col < q->num_columns;
       if (!ok) break;
       const InvLeafX& x = pk.invx[leaf];
-      const pgpu_segment* sgm = q->segments[s].segment;
       const HostColumn& h = sgm->cols[q->segments[s].column_map[in.col]];
       const DevColumn& dc = pk.cols[ds.col_begin + in.col];
       ok = (x.nids == 1 || dc.kind == PGPU_COL_FIXED_BIT || dc.kind == PGPU_COL_RAW) &&
@@ -3071,18 +3087,15 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       }
       ok = ok && docs <= cand_max * (double)sgm->num_docs;
       for (int k = 0; k < x.nids && ok; ++k)
-        for (uint32_t c = h.inv_hdir[ids[k]]; c < h.inv_hdir[ids[k] + 1]; ++c) {
-          units.push_back((uint32_t)s);
-          units.push_back(c);
-        }
-      ok = ok && units.size() / 2 <= kCandMaxUnits;
+        for (uint32_t c = h.inv_hdir[ids[k]]; c < h.inv_hdir[ids[k] + 1]; ++c) units.insert(units.end(), {(uint32_t)s, c, 0u, 0u});
+      ok = ok && units.size() / 4 <= kCandMaxUnits;
       ds.cand_leaf = leaf;
       leaves.push_back(leaf);
     }
     // a wave's consumer area and 8 KiB container image; four waves per workgroup
     const size_t cdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + (size_t)4 * 8192;
     if (ok && cdyn <= PGPU_LDS_LIMIT) {
-      const int nu = (int)(units.size() / 2);
+      const int nu = (int)(units.size() / 4);
       const int per_cu = (int)std::min<size_t>(4, PGPU_LDS_LIMIT / cdyn);
       const int g = (int)std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, (nu + 3) / 4));
       p.direct = 6;

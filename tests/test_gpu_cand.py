@@ -154,3 +154,32 @@ def test_cand_adanalytics_inv(gpu_ctx):
     res = _run(gpu_ctx, segs, w.sql)
     assert res.stats.kernel_variant == _lib.PGPU_KV_CAND
     _check(res, engine.execute(parse_sql(w.sql), segs, iterator_stats=True))
+
+
+def _sorted_segments(seed=17, nseg=2, n=200_003):
+    """`s` sorted (SortedIndexBasedFilterOperator leaves: doc ranges), ~40 docs per value."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(nseg):
+        cols = {"s": (_lib.PGPU_INT, np.sort(rng.integers(0, 5_000, n))), "d": (_lib.PGPU_INT, rng.integers(0, 100, n)),
+                "e": (_lib.PGPU_INT, rng.integers(0, 3, n)), "g": (_lib.PGPU_INT, rng.integers(0, 50, n)),
+                "m": (_lib.PGPU_INT, rng.integers(-1000, 100_000, n))}
+        out.append(build_segment(f"sorted{i}", cols, sorted_columns=["s"]))
+    return out
+
+
+def test_cand_sorted_leading_leaf(gpu_ctx, monkeypatch):
+    """A sorted leading leaf: its doc ranges, split at 65,536-doc keys (one range crosses doc 65,536), are the units."""
+    segs = _sorted_segments()
+    sv = np.asarray(engine.DecodedSegment(segs[0]).values("s"))
+    lo, hi = int(sv[65_500]), int(sv[65_600])
+    for sql in (f"SELECT COUNT(*), SUM(m) FROM t WHERE s BETWEEN {lo} AND {hi} AND d < 50",
+                "SELECT g, COUNT(*), MAX(m) FROM t WHERE s IN (17, 2500, 4999) AND e <> 1 GROUP BY g",
+                "SELECT COUNT(*), MIN(m) FROM t WHERE s = 3000"):
+        ref = engine.execute(parse_sql(sql), segs, iterator_stats=True)
+        res = _run(gpu_ctx, segs, sql)
+        assert res.stats.kernel_variant == _lib.PGPU_KV_CAND, (sql, res.stats.kernel_variant)
+        _check(res, ref)
+        monkeypatch.setenv("PGPU_NO_CAND", "1")
+        _check(_run(gpu_ctx, segs, sql), ref)
+        monkeypatch.delenv("PGPU_NO_CAND")
