@@ -417,7 +417,7 @@ struct DevParams {
   int32_t* hflag;
   uint32_t* leaf_bits;            // PGPU_Q_EXACT_FILTER_STATS (see DevSeg::leaf_bits_off)
   uint32_t* segany;               // [nseg] set to 1 by any wave that matched a doc of the segment (numSegmentsMatched);
-                                  // zero between queries (segflags_kernel resets the words it reads)
+                                  // zero between queries (finalize_kernel resets the words it reads)
   const int32_t* cancel;          // == cancel_gen: stop (pgpu_query_cancel / deadline); HBM word, polled per tile range
   int32_t key_words;
   int32_t key_split;

@@ -4485,8 +4485,27 @@ __global__ void table_init_kernel(int64_t* table, uint64_t G, int32_t nsec, DevP
 
 // Reduce AGG-mode slabs into the G=1 table and the per-wave stats: block x reduces column x (a section, then the
 // PGPU_NSTATS stats) over all waves with a fixed-shape tree, so double sums are deterministic.
-__global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nslabs, int64_t* stats_out) {
+// The query's epilogue, one launch: blocks [0, nsec + NSTATS) reduce the AGG-mode slabs (also into the pinned host
+// table) and the per-wave statistics (finalize); the next nseg_blocks turn the numSegmentsMatched words into pinned
+// host flags and reset them; the rest copy a non-AGG table into pinned host memory (the three are independent).
+__global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nslabs, int64_t* stats_out, uint8_t* seg_out,
+                                                       int32_t nseg_blocks, int64_t* host_table, uint64_t table_words) {
   __shared__ int64_t red[256];
+  const int nfin = p.nsec + PGPU_NSTATS;
+  if ((int)blockIdx.x >= nfin) {
+    const int b = (int)blockIdx.x - nfin;
+    if (b < nseg_blocks) {
+      for (int i = b * 256 + threadIdx.x; i < p.nseg; i += nseg_blocks * 256) {
+        seg_out[i] = p.segany[i] != 0u ? 1 : 0;
+        p.segany[i] = 0u;
+      }
+    } else {
+      const int nb = (int)gridDim.x - nfin - nseg_blocks;
+      for (uint64_t i = (uint64_t)(b - nseg_blocks) * 256ull + threadIdx.x; i < table_words; i += nb * 256ull)
+        host_table[i] = p.table[i];
+    }
+    return;
+  }
   const int col = blockIdx.x;
   const bool is_stat = col >= p.nsec;
   if (!is_stat && p.mode != PGPU_MODE_AGG) return;
@@ -4502,8 +4521,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(DevParams p, int32_t nsla
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (is_stat) stats_out[col - p.nsec] = red[0];
-    else p.table[col] = red[0];
+    if (is_stat) {
+      stats_out[col - p.nsec] = red[0];
+    } else {
+      p.table[col] = red[0];
+      if (host_table) host_table[col] = red[0];
+    }
   }
 }
 
@@ -4901,16 +4924,7 @@ __global__ __launch_bounds__(256) void segcount_kernel(DevParams p, int64_t* out
 }
 // numSegmentsMatched: the per-segment match words into pinned host memory (one byte per segment), each word reset to
 // 0 for the workspace's next query.
-__global__ __launch_bounds__(256) void segflags_kernel(uint32_t* segany, uint8_t* out, int32_t n) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    out[i] = segany[i] != 0u ? 1 : 0;
-    segany[i] = 0u;
-  }
-}
 // Copy `words` int64 of a finished table into pinned host memory.
-__global__ __launch_bounds__(256) void export_kernel(const int64_t* __restrict__ src, int64_t* dst, uint64_t words) {
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) dst[i] = src[i];
-}
 
 // ---- compaction of a dense table (keys with count > 0) -------------------------------------------------------------
 #define CMP_BLOCK 256
@@ -5635,11 +5649,6 @@ hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njo
   return hipGetLastError();
 }
 
-hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st) {
-  if (p.nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(segflags_kernel, dim3(std::min(64, (p.nseg + 255) / 256)), dim3(256), 0, st, p.segany, out, p.nseg);
-  return hipGetLastError();
-}
 
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st) {
   if (!p.segmask || p.segmask_rows <= 0) return hipSuccess;
@@ -5663,14 +5672,14 @@ hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void
   return hipGetLastError();
 }
 
-hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st) {
-  const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(64, (words + 255) / 256));
-  hipLaunchKernelGGL(export_kernel, dim3(blocks), dim3(256), 0, st, src, host_dst, words);
-  return hipGetLastError();
-}
 
-hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(p.nsec + PGPU_NSTATS), dim3(256), 0, st, p, nslabs, stats_out);
+hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, uint8_t* seg_out,
+                                int64_t* host_table, uint64_t table_words, hipStream_t st) {
+  const int nseg_blocks = p.nseg > 0 ? std::min(64, (p.nseg + 255) / 256) : 0;
+  const bool copy = host_table && p.mode != PGPU_MODE_AGG;  // (AGG: finalize writes the host cells itself)
+  const int nexp = copy ? (int)std::max<uint64_t>(1, std::min<uint64_t>(64, (table_words + 255) / 256)) : 0;
+  hipLaunchKernelGGL(finalize_kernel, dim3(p.nsec + PGPU_NSTATS + nseg_blocks + nexp), dim3(256), 0, st, p, nslabs,
+                     stats_out, seg_out, nseg_blocks, host_table, copy ? table_words : (uint64_t)0);
   return hipGetLastError();
 }
 

@@ -36,21 +36,20 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
-hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, hipStream_t st);
+hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, uint8_t* seg_out,
+                                int64_t* host_table, uint64_t table_words, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
 hipError_t pgpu_launch_bitslice(const uint32_t* fwd, uint32_t* out, int bits, int64_t ntiles, hipStream_t st);
 hipError_t pgpu_launch_vslice(const uint32_t* fwd, const void* dict, int dict_type, int64_t vmin, int bits, int vbits,
                               uint32_t* out, int64_t ntiles, hipStream_t st);
 hipError_t pgpu_launch_prologue(const DevParams& p, const void* host_arena, void* dev_arena, size_t bytes,
                                 bool init_table, hipStream_t st);
-hipError_t pgpu_launch_export(const int64_t* src, int64_t* host_dst, uint64_t words, hipStream_t st);
 hipError_t pgpu_launch_compact(const int64_t* table, uint64_t G, int32_t nsec, int32_t kw, int32_t* block_counts,
                                int64_t* total, int64_t* out_keys, int64_t* out_cells, bool count_only, hipStream_t st,
                                const uint64_t* okey = nullptr, const TopkState* ts = nullptr);
 hipError_t pgpu_launch_topk(const int64_t* table, const TopkDev& s, uint64_t k, uint64_t* okey, TopkState* ts,
                             uint32_t* hist, hipStream_t st);
 hipError_t pgpu_launch_segcount(const DevParams& p, int64_t* out, hipStream_t st);
-hipError_t pgpu_launch_segflags(const DevParams& p, uint8_t* out, hipStream_t st);
 hipError_t pgpu_launch_progbits(const DevParams& p, const ProgJob* jobs, int njobs, int total, hipStream_t st);
 hipError_t pgpu_launch_andfsm(const DevParams& p, bool s2, uint32_t* fn, int64_t* out, hipStream_t st);
 hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st);
@@ -214,6 +213,7 @@ struct PinnedMem {
   void reset() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    dev = nullptr;
     n = 0;
   }
   hipError_t ensure(size_t bytes) {
@@ -225,6 +225,19 @@ struct PinnedMem {
     else p = nullptr;
     return e;
   }
+  // the buffer's device address (looked up once per allocation: a runtime call per query otherwise)
+  hipError_t device_ptr(void** out) {
+    if (!dev) {
+      const hipError_t e = hipHostGetDevicePointer(&dev, p, 0);
+      if (e != hipSuccess) {
+        dev = nullptr;
+        return e;
+      }
+    }
+    *out = dev;
+    return hipSuccess;
+  }
+  void* dev = nullptr;
 };
 
 // System.currentTimeMillis (QueryContext end times are on this clock)
@@ -3245,7 +3258,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (!ws) return rc;
   hipStream_t bail_stream = nullptr;
   auto bail = [&](int code) {
-    // a bail after the query kernel was enqueued but before segflags_kernel: the matched-segment words it may
+    // a bail after the query kernel was enqueued but before finalize_kernel: the matched-segment words it may
     // have set must not count towards the workspace's next query (they are zero between queries)
     if (bail_stream && ws->segany.p) (void)hipMemsetAsync(ws->segany.p, 0, ws->segany.n, bail_stream);
     release_ws(ctx, ws);
@@ -3385,7 +3398,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     p.leaf_bits = (uint32_t*)ws->leafbits.p;
   }
   {
-    // numSegmentsMatched words: grown in stream order and zeroed once; segflags_kernel resets them after each query
+    // numSegmentsMatched words: grown in stream order and zeroed once; finalize_kernel resets them after each query
     const size_t want = 4ull * std::max(1, p.nseg);
     if (ws->segany.n < want) {
       e = ws->segany.ensure(want, ctx->mpool, st);
@@ -3469,8 +3482,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   p.cancel_gen = ws->cancel_gen;
   const bool expired = q->deadline_ms > 0 && now_epoch_ms() >= q->deadline_ms;
   if (expired) e = hipMemsetD32Async((hipDeviceptr_t)ws->d_cancel.p, (int)ws->cancel_gen, 1, st);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(&h_arena_dev, ws->h_arena.p, 0);
-  if (e == hipSuccess) e = hipHostGetDevicePointer(&h_stats_dev, ws->h_stats.p, 0);
+  if (e == hipSuccess) e = ws->h_arena.device_ptr(&h_arena_dev);
+  if (e == hipSuccess) e = ws->h_stats.device_ptr(&h_stats_dev);
   if (e == hipSuccess) e = pgpu_launch_prologue(p, h_arena_dev, ws->arena.p, total, p.mode != PGPU_MODE_AGG, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev0, st);
   // raw-value leaves' match bitmaps (timed with the query: they are part of its filter)
@@ -3496,25 +3509,26 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
-  if (e == hipSuccess) e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, st);
+  // statistics, numSegmentsMatched flags and a small table into pinned host memory: one launch
   if (e == hipSuccess) {
     void* h_seg_dev = nullptr;
-    e = hipHostGetDevicePointer(&h_seg_dev, ws->h_segany.p, 0);
-    if (e == hipSuccess) e = pgpu_launch_segflags(p, (uint8_t*)h_seg_dev, st);
+    e = ws->h_segany.device_ptr(&h_seg_dev);
+    if (e == hipSuccess)
+      e = pgpu_launch_finalize(p, nwaves, (int64_t*)h_stats_dev, (uint8_t*)h_seg_dev, host_table,
+                               host_table ? pgpu_table_bytes(&L) / 8 : 0, st);
   }
   if (e == hipSuccess && p.mode == PGPU_MODE_HASH) {
     // probe-overflow flag and the tracked segments' distinct-key counts, into pinned host memory
     void* h_cnt_dev = nullptr;
     if (p.segmask_rows) {
-      e = hipHostGetDevicePointer(&h_cnt_dev, ws->h_segcnt.p, 0);
+      e = ws->h_segcnt.device_ptr(&h_cnt_dev);
       if (e == hipSuccess) e = pgpu_launch_segcount(p, (int64_t*)h_cnt_dev, st);
     }
     if (e == hipSuccess) e = hipMemcpyAsync((char*)ws->h_stats.p + 8 * PGPU_NSTATS, ws->hflag.p, 4, hipMemcpyDeviceToHost, st);
   }
-  if (e == hipSuccess && host_table) e = pgpu_launch_export((const int64_t*)dev_table, host_table, pgpu_table_bytes(&L) / 8, st);
   if (e == hipSuccess && pk.fsm) {
     void* h_ent_dev = nullptr;
-    e = hipHostGetDevicePointer(&h_ent_dev, ws->h_fsment.p, 0);
+    e = ws->h_fsment.device_ptr(&h_ent_dev);
     if (e == hipSuccess) e = pgpu_launch_andfsm(p, pk.fsm_s2, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
   }
   if (e == hipSuccess && pk.leaf_words > 0) {
@@ -4315,7 +4329,7 @@ static int submit_impl(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_t
   void* h_table_dev = nullptr;
   if (small) {
     e = tws->h_table.ensure(bytes);
-    if (e == hipSuccess) e = hipHostGetDevicePointer(&h_table_dev, tws->h_table.p, 0);
+    if (e == hipSuccess) e = tws->h_table.device_ptr(&h_table_dev);
     if (e != hipSuccess) {
       release_ws(ctx, tws);
       return fail(PGPU_E_HIP, "host table buffer: %s", hipGetErrorString(e));

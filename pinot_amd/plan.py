@@ -524,12 +524,37 @@ class GpuPlanMaker:
         self.max_init_group_holder_capacity = max_init_group_holder_capacity
         self.collect_stats = collect_stats
         self._global_dicts: Dict[tuple, tuple] = {}
+        self._col_kinds: Dict[tuple, tuple] = {}  # segment uids -> (raw columns, raw or range-indexed columns)
+        self._desc_static: Dict[tuple, tuple] = {}  # (segment uids, columns, views) -> (column maps, handles)
         if hasattr(ctx, "add_listener"):
             ctx.add_listener(self)  # segment_released: forget global dictionaries naming a released segment
 
     def segment_released(self, uid: int) -> None:
         for k in [k for k in self._global_dicts if uid in k[1]]:
             self._evict_global(k)
+        for k in [k for k in self._col_kinds if uid in k[:-1]]:
+            del self._col_kinds[k]
+        for k in [k for k in self._desc_static if uid in k[0]]:
+            del self._desc_static[k]
+
+    def column_kinds(self, segments: Sequence[GpuSegment]) -> tuple:
+        """(columns raw in some segment, columns raw or range-indexed in some segment) of a segment set: fixed once
+        the segments are sealed, so computed once per set instead of per query and predicate."""
+        key = tuple(s.uid for s in segments) + (sum(len(s.derived) for s in segments),)  # (columns derived later)
+        hit = self._col_kinds.get(key)
+        if hit is None:
+            raw, host = set(), set()
+            for s in segments:
+                for name in set(s.data.columns) | set(s.derived):
+                    c = s.column(name)
+                    if c.is_raw:
+                        raw.add(name)
+                    if c.is_raw or c.range_index is not None:
+                        host.add(name)
+            if len(self._col_kinds) >= 64:
+                self._col_kinds.clear()
+            hit = self._col_kinds[key] = (frozenset(raw), frozenset(host))
+        return hit
 
     def _evict_global(self, key: tuple) -> None:
         entry = self._global_dicts.pop(key)
@@ -590,6 +615,7 @@ class GpuPlanMaker:
             return None
         col_index = {c: i for i, c in enumerate(query.columns)}
         seg0 = segments[0]
+        host_cols = self.column_kinds(segments)[1]
         nodes: list = []
         lits: list = []
 
@@ -618,7 +644,7 @@ class GpuPlanMaker:
             p = fc.predicate
             if seg0.column(p.column).data_type == PGPU_STRING:
                 return False
-            if any(s.column(p.column).is_raw or s.column(p.column).range_index is not None for s in segments):
+            if p.column in host_cols:
                 return False  # raw-value leaves / range-index leaves: planned per segment here
             kind = {"EQ": _lib.PGPU_P_EQ, "NOT_EQ": _lib.PGPU_P_NOT_EQ, "IN": _lib.PGPU_P_IN,
                     "NOT_IN": _lib.PGPU_P_NOT_IN, "RANGE": _lib.PGPU_P_RANGE}[p.type]
@@ -667,8 +693,9 @@ class GpuPlanMaker:
         group_col = {}
         views: Dict[int, str] = {}
         no_dict = False
+        raw_cols = self.column_kinds(segments)[0] if segments else frozenset()
         for g in query.group_by:
-            if any(s.column(g).is_raw for s in segments):
+            if g in raw_cols:
                 no_dict = True
                 views[len(columns)] = g
                 group_col[g] = len(columns)
@@ -678,20 +705,30 @@ class GpuPlanMaker:
         nodes: list = []
         ids: list = []
         vals: list = []
-        starts = []
-        cmaps = []
         flt = query.filter if plan_filters else None
-        for seg in segments:
-            slots = seg.slots
-            cmaps.append([slots[seg.group_view(views[i])] if i in views else slots[c] for i, c in enumerate(columns)]
-                         if columns else [0])
-            starts.append(len(nodes))
-            if flt is not None:
+        # the column maps and segment handles are fixed for a segment set and column list: built once, shared
+        # read-only by every descriptor that names them
+        skey = (tuple(s.uid for s in segments), tuple(columns), tuple(sorted(views.items())))
+        static = self._desc_static.get(skey)
+        if static is None:
+            cmaps = [[slots[seg.group_view(views[i])] if i in views else slots[c] for i, c in enumerate(columns)]
+                     if columns else [0] for seg, slots in ((seg, seg.slots) for seg in segments)]
+            cmap = np.array(cmaps, dtype=np.int32).reshape(nseg, max(1, len(columns)))
+            handles = np.array([seg.handle.value for seg in segments], dtype=np.uint64)
+            if len(self._desc_static) >= 64:
+                self._desc_static.clear()
+            static = self._desc_static[skey] = (cmap, handles)
+        cmap, handles = static
+        if flt is not None:
+            starts = []
+            for seg in segments:
+                starts.append(len(nodes))
                 op = SegmentFilterPlanner(seg).build(flt)
                 if op.kind != "ALL":
                     emit_program(op, col_index, nodes, ids, vals)
-        starts.append(len(nodes))
-        cmap = np.array(cmaps, dtype=np.int32).reshape(nseg, max(1, len(columns)))
+            starts.append(len(nodes))
+        else:
+            starts = [0] * (nseg + 1)
         pool = np.array(ids if ids else [0], dtype=np.int32)
         vpool = np.array(vals if vals else [0], dtype=np.int64)
         narr = np.zeros(max(1, len(nodes)), dtype=NODE_DTYPE)
@@ -707,7 +744,7 @@ class GpuPlanMaker:
         for g, (_, rms) in enumerate(globals_):
             remap[:, g] = [(rm.handle.value or 0) if rm is not None else 0 for rm in rms]
         plans = np.zeros(nseg, dtype=PLAN_DTYPE)
-        plans["segment"] = [seg.handle.value for seg in segments]
+        plans["segment"] = handles
         plans["column_map"] = cmap.ctypes.data + cmap.strides[0] * np.arange(nseg, dtype=np.uint64)
         st = np.array(starts, dtype=np.int64)
         plans["filter"] = narr.ctypes.data + NODE_DTYPE.itemsize * st[:-1].astype(np.uint64)
