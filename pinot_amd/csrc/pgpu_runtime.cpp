@@ -240,6 +240,33 @@ struct PinnedMem {
   void* dev = nullptr;
 };
 
+// PGPU_HOST_TIMING=N: average host microseconds of the submit phases, printed to stderr every N submits
+struct HostTiming {
+  int every = 0, n = 0;
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  HostTiming() {
+    const char* e = getenv("PGPU_HOST_TIMING");
+    every = e ? atoi(e) : 0;
+  }
+  static double us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void add(int k, double t0, double t1) {
+    if (every > 0) acc[k] += t1 - t0;
+  }
+  void done() {
+    if (every <= 0 || ++n < every) return;
+    fprintf(stderr, "[pgpu host] per submit (us): expr %.1f layout %.1f pack %.1f workspace %.1f launch %.1f total %.1f\n",
+            acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n);
+    n = 0;
+    for (double& a : acc) a = 0;
+  }
+};
+HostTiming& host_timing() {
+  static HostTiming t;
+  return t;
+}
+
 // System.currentTimeMillis (QueryContext end times are on this clock)
 int64_t now_epoch_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
@@ -2775,7 +2802,9 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
                 (unsigned long long)need);
   Packer pk;
   DevParams p;
+  const double tp0 = HostTiming::us();
   rc = pack_query(ctx, q, L, pk, p);
+  host_timing().add(2, tp0, HostTiming::us());
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
 
@@ -3254,6 +3283,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
               ds.stage_sliced, ds.nvstage, ds.single_bits, ds.nbits);
     }
   }
+  const double tw0 = HostTiming::us();
   Workspace* ws = acquire_ws(ctx, &rc);
   if (!ws) return rc;
   hipStream_t bail_stream = nullptr;
@@ -3461,6 +3491,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   memcpy(h + o_cols, pk.cols.data(), pk.cols.size() * sizeof(DevColumn));
   memcpy(h + o_pool, pk.pool.data(), pk.pool.size() * 4);
   memcpy(h + o_rem, pk.remaps.data(), pk.remaps.size() * sizeof(void*));
+  const double tl0 = HostTiming::us();
+  host_timing().add(3, tw0, tl0);
   p.segs = (const DevSeg*)(d + o_segs);
   p.instrs = (const DevInstr*)(d + o_ins);
   p.cols = (const DevColumn*)(d + o_cols);
@@ -3543,6 +3575,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   if (e == hipSuccess) e = hipEventRecord(ws->done, st);
   if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "query launch: %s", hipGetErrorString(e)));
 
+  host_timing().add(4, tl0, HostTiming::us());
   auto* qq = new pgpu_query();
   qq->ctx = ctx;
   qq->ws = ws;
@@ -4306,9 +4339,11 @@ extern "C" {
 
 static int submit_impl(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_topk* order, pgpu_query** out_query) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
+  const double t0 = HostTiming::us();
   pgpu_table_layout L;
   int rc = pgpu_table_layout_of(q, &L);
   if (rc) return rc;
+  host_timing().add(1, t0, HostTiming::us());
   HIP_TRY(hipSetDevice(ctx->device));
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -4362,10 +4397,15 @@ int pgpu_query_submit_ordered(pgpu_context* ctx, const pgpu_query_desc* q, const
                               int32_t num_nodes, const pgpu_topk* order, pgpu_query** out_query) {
   if (!ctx || !q || !out_query) return fail(PGPU_E_INVALID, "null argument");
   if (!expr) return submit_impl(ctx, q, order, out_query);
+  const double t0 = HostTiming::us();
   PlannedDesc pd;
-  const int rc = plan_expr(q, expr, num_nodes, pd);
+  int rc = plan_expr(q, expr, num_nodes, pd);
   if (rc) return rc;
-  return submit_impl(ctx, &pd.q, order, out_query);  // the descriptor is copied by the submit
+  host_timing().add(0, t0, HostTiming::us());
+  rc = submit_impl(ctx, &pd.q, order, out_query);  // the descriptor is copied by the submit
+  host_timing().add(5, t0, HostTiming::us());
+  host_timing().done();
+  return rc;
 }
 
 int pgpu_query_collect(pgpu_query* qq, int64_t* out_keys, int64_t* out_cells, uint64_t capacity,
