@@ -138,6 +138,12 @@ def resident_bytes(ctx, segs, rows):
             "by_kind": kinds, "derived_budget_bytes": budget, "context_derived_bytes": used}
 
 
+# pgpu_query_stats.kernel_variant -> the query kernel the runtime chose (and the kernels timed beside it)
+KERNEL_NAMES = {0: "query_kernel (ring)", 1: "query_kernel_direct", 2: "query_kernel_rdirect", 3: "query_kernel_rstream",
+                4: "query_kernel_rprog + invexp_kernel", 5: "query_kernel_rkey + rkey_ctab_kernel",
+                6: "query_kernel_cand", 7: "part_scan_kernel + part_reduce_kernel"}
+
+
 def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier):
     """Generate the workload's segments in HBM, measure it, time the CPU baseline beside it; returns the fields
     of one result (the headline line or an entry of `workloads`)."""
@@ -185,7 +191,8 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
                        "parallelism": f"segments sharded over {world} GPU(s); partial tables merged over RCCL"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "query_kernel", "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel": KERNEL_NAMES.get(getattr(ex.last_stats, "kernel_variant", -1), "query_kernel"),
+                         "algorithmic_bytes_per_launch": algo_bytes,
                          "kernel_ms_avg": avg_kernel_ms, "bytes_breakdown": breakdown,
                          "bytes_definition": "SURVEY 8(d) workload bytes (tools/bytemodel.py), strategy-independent",
                          "bytes_read_model": read_bytes, "bytes_read_breakdown": read_breakdown},
