@@ -385,6 +385,8 @@ struct DevParams {
   int32_t pscan;                  // > 0: phase 1 by part_scan_kernel (dense filter programs) with LDS rings of
                                   // this many records per partition (a power of two, >= two 128-B lines)
   int32_t pscan_wave_bytes;       // its per-wave LDS area (filter mask rows)
+  int32_t pscan_kb, pscan_vb;     // > 0: every segment's key and carried column are fixed-bit of these widths (no
+                                  // filter, one group column): phase 1 reads the next tile's words a step ahead
   int32_t mask_rows;              // mask rows per consumer (filter slots used + 1 scratch row)
   int32_t cons_bytes;             // PGPU_CONS_BYTES(dense, mask_rows)
   int32_t direct;                 // query_kernel_direct: self-loading waves (every staged column a sliced fast leaf)

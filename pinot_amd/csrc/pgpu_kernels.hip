@@ -3848,7 +3848,17 @@ FI void pscan_flush(const DevParams& p, uint32_t* ht, const uint32_t* ring,
 
 // COUNT: the sizing pass -- every psample-th tile, matched records counted per partition into pcount, nothing
 // written.  Otherwise phase 1 proper.
-template <bool COUNT>
+// KB, VB > 0 (phase 1 proper only): every segment's group key and carried column are fixed-bit columns of KB / VB
+// bits and there is no filter -- the next step's tile words are loaded a step ahead, raw, into VGPRs (phase 1 runs
+// two waves per SIMD, bound by its LDS rings, so the registers are free), and the step's own HBM latency overlaps
+// the previous step's inserts, flush and barriers.
+template <int B>
+FI void hbm_lane_raw(const uint32_t* fwd, int tile_in_seg, uint32_t (&w)[B]) {
+  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = src[k];
+}
+template <bool COUNT, int KB = 0, int VB = 0>
 __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3913,9 +3923,30 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
   SegState ss;
   int cseg = -1;
   const int nsteps = (t1 - t0 + PGPU_PSCAN_WAVES - 1) / PGPU_PSCAN_WAVES;
+  constexpr bool PF = KB > 0 && VB > 0 && !COUNT;
+  uint32_t nkw[PF ? KB : 1], nvw[PF ? VB : 1];  // the next step's raw words (PF)
+  auto prefetch = [&](int ptile) {
+    if constexpr (PF) {
+      if (ptile < t1 && ptile < p.total_tiles) {
+        const Cursor cn = cursor_at(p, ptile);
+        const DevColumn* pc = p.cols + cld(&p.segs[cn.seg].col_begin);
+        hbm_lane_raw<KB>(cld(&pc[p.gcols[0]].fwd), cn.tile_in_seg, nkw);
+        hbm_lane_raw<VB>(cld(&pc[p.pcol].fwd), cn.tile_in_seg, nvw);
+      }
+    }
+  };
+  prefetch(t0 + wave);
   for (int step = 0; step < nsteps; ++step) {
     const int tile = (t0 + step * PGPU_PSCAN_WAVES + wave) * S;
     int64_t tp = now(pf);
+    uint32_t ckw[PF ? KB : 1], cvw[PF ? VB : 1];
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) ckw[k] = nkw[k];
+#pragma unroll
+      for (int k = 0; k < VB; ++k) cvw[k] = nvw[k];
+      prefetch(tile + PGPU_PSCAN_WAVES);
+    }
     if (tile < t1 * S && tile < p.total_tiles) {
       if (pf.on) pf.t[PGPU_P_C_TILES] += 1;
       const Cursor cu = cursor_at(p, tile);
@@ -3944,7 +3975,22 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
         uint32_t key[32], val[32];
 #pragma unroll
         for (int i = 0; i < 32; ++i) key[i] = val[i] = 0;
-        for (int g = 0; g < p.ngcols; ++g) {
+        if constexpr (PF) {  // (one group column; ngcols is 1)
+#pragma unroll
+          for (int k = 0; k < KB; ++k) ckw[k] = bswap32(ckw[k]);
+          uint32_t ids[32];
+          unpack_b<KB>(ckw, ids);
+          const int32_t* remap = cld(ss.remaps, 0);
+          if (remap) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) ids[i] = lane_bit(mm, i) ? (uint32_t)gld(remap, ids[i]) : 0u;
+          }
+          const uint32_t st = p.gstride[0];
+#pragma unroll
+          for (int i = 0; i < 32; ++i) key[i] = ids[i] * st;
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * KB + 7) / 8;
+        }
+        for (int g = 0; g < (PF ? 0 : p.ngcols); ++g) {
           const DevColumn c = col_of(ss, p.gcols[g]);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
           uint32_t ids[32];
@@ -3966,7 +4012,13 @@ __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevPar
         if (p.pcol >= 0) {
           const DevColumn c = col_of(ss, p.pcol);
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * c.bits + 7) / 8;
-          column_ids(c.kind, c.bits, nullptr, c.fwd, t.tile_in_seg, val);
+          if constexpr (PF) {
+#pragma unroll
+            for (int k = 0; k < VB; ++k) cvw[k] = bswap32(cvw[k]);
+            unpack_b<VB>(cvw, val);
+          } else {
+            column_ids(c.kind, c.bits, nullptr, c.fwd, t.tile_in_seg, val);
+          }
           if (!idbits) {
 #pragma unroll
             for (int i = 0; i < 32; ++i) val[i] = lane_bit(mm, i) ? gld((const uint32_t*)c.dict, val[i]) : 0u;
@@ -5245,7 +5297,12 @@ hipError_t pgpu_prepare_part_reduce() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)part_scan_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             PGPU_LDS_LIMIT);
-
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)part_scan_kernel<false, 20, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PGPU_LDS_LIMIT);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)part_scan_kernel<false, 16, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PGPU_LDS_LIMIT);
   return e;
 }
 
@@ -5260,9 +5317,15 @@ hipError_t pgpu_launch_part_scan(const DevParams& p, int grid, size_t dyn_smem, 
     hipLaunchKernelGGL(part_scan_kernel<true>, dim3(cg), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
     hipLaunchKernelGGL(part_plan_kernel, dim3(1), dim3(1024), 0, st, p, grid);
   }
-  hipLaunchKernelGGL(part_scan_kernel<false>, dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+  if (p.pscan_kb == 20 && p.pscan_vb == 16)
+    hipLaunchKernelGGL((part_scan_kernel<false, 20, 16>), dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+  else if (p.pscan_kb == 16 && p.pscan_vb == 16)
+    hipLaunchKernelGGL((part_scan_kernel<false, 16, 16>), dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
+  else
+    hipLaunchKernelGGL(part_scan_kernel<false>, dim3(grid), dim3(PGPU_PSCAN_THREADS), dyn_smem, st, p);
   return hipGetLastError();
 }
+bool pgpu_pscan_prefetch_ok(int kb, int vb) { return (kb == 20 || kb == 16) && vb == 16; }
 
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st) {
   size_t lds = (size_t)p.nsec * ((size_t)1 << p.pshift) * 8 + (p.ldict == 1 ? (size_t)4 << p.slice_shift : 0);

@@ -36,6 +36,7 @@ hipError_t pgpu_prepare_query_kernels(size_t lds_bytes);
 hipError_t pgpu_launch_table_init(const DevParams& p, hipStream_t st);
 hipError_t pgpu_launch_query(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
 hipError_t pgpu_launch_query_direct(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st);
+bool pgpu_pscan_prefetch_ok(int kb, int vb);
 hipError_t pgpu_launch_finalize(const DevParams& p, int nslabs, int64_t* stats_out, uint8_t* seg_out,
                                 int64_t* host_table, uint64_t table_words, hipStream_t st);
 hipError_t pgpu_launch_part_reduce(const DevParams& p, int nwg, hipStream_t st);
@@ -3249,6 +3250,26 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       if (rc < min_rc) continue;
       p.pscan = (int32_t)rc;
       p.pscan_wave_bytes = (int32_t)wave_bytes;
+      // the widths the prefetching phase 1 is compiled for (part_scan_kernel<false, KB, VB>)
+      p.pscan_kb = p.pscan_vb = 0;
+      const bool no_pfetch = getenv("PGPU_NO_PSCAN_PREFETCH") && atoi(getenv("PGPU_NO_PSCAN_PREFETCH")) != 0;
+      if (!no_pfetch && p.ngcols == 1 && pcol >= 0) {
+        int kb = -1, vb = -1;
+        bool same = true;
+        for (const DevSeg& ds : pk.segs) {
+          if (!ds.ntiles) continue;
+          const DevColumn& kc = pk.cols[ds.col_begin + p.gcols[0]];
+          const DevColumn& vc = pk.cols[ds.col_begin + pcol];
+          same = same && ds.prog_len == 0 && kc.kind == PGPU_COL_FIXED_BIT && vc.kind == PGPU_COL_FIXED_BIT &&
+                 (kb < 0 || kb == kc.bits) && (vb < 0 || vb == vc.bits);
+          kb = kc.bits;
+          vb = vc.bits;
+        }
+        if (same && pgpu_pscan_prefetch_ok(kb, vb)) {
+          p.pscan_kb = kb;
+          p.pscan_vb = vb;
+        }
+      }
       int g = (int)std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 4));
       if (g >= 8) g &= ~7;
       p.direct = 0;

@@ -688,9 +688,13 @@ def test_inverted_container_kinds_vs_oracle(gpu_ctx, force):
 
 
 @pytest.mark.gpu
-def test_partitioned_groupby_shared_dictionary_vs_oracle(gpu_ctx):
+@pytest.mark.parametrize("prefetch", [True, False], ids=["prefetch", "generic"])
+def test_partitioned_groupby_shared_dictionary_vs_oracle(gpu_ctx, monkeypatch, prefetch):
     """Config 4's shape on small segments: 1M-key GROUP BY through the partitioned path, one-word records over the
-    shared 64K-value metric dictionary, whose phase-2 lookups read its frame-of-reference image in LDS."""
+    shared 64K-value metric dictionary, whose phase-2 lookups read its frame-of-reference image in LDS; phase 1 with
+    the 20/16-bit words read a step ahead (part_scan_kernel<false, 20, 16>) and the generic phase 1."""
+    if not prefetch:
+        monkeypatch.setenv("PGPU_NO_PSCAN_PREFETCH", "1")
     from oracle.segment_writer import pack_fixed_bit
     from pinot_amd.synth import WORKLOADS, build_segment_cpu
     w = WORKLOADS["groupby1m"]
