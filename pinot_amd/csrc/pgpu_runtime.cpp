@@ -3129,6 +3129,11 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
         if (ok) docs += h.inv_cards[ids[k]];
       }
       ok = ok && docs <= cand_max * (double)sgm->num_docs;
+      // at most one container per tile of the segment: past that the tile sweep is as cheap, and a long IN list's
+      // containers would cost the host more to list than the sweep costs the GPU
+      uint64_t nct = 0;
+      for (int k = 0; k < x.nids && ok; ++k) nct += h.inv_hdir[ids[k] + 1] - h.inv_hdir[ids[k]];
+      ok = ok && nct <= (uint64_t)ds.ntiles;
       for (int k = 0; k < x.nids && ok; ++k)
         for (uint32_t c = h.inv_hdir[ids[k]]; c < h.inv_hdir[ids[k] + 1]; ++c) units.insert(units.end(), {(uint32_t)s, c, 0u, 0u});
       ok = ok && units.size() / 4 <= kCandMaxUnits;

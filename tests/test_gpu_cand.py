@@ -21,7 +21,7 @@ from tests.helpers import check_groups, close
 pytestmark = pytest.mark.gpu
 
 
-def _segments(seed=11, nseg=3, n=200_003, force=None, bitmap=False):
+def _segments(seed=11, nseg=3, n=200_003, force=None, bitmap=False, card=40_000):
     """`a`: 40,000 ids (~5 docs each per segment, inverted); `d`, `e`: scan columns; `g`: group key; `m`, `x`:
     metrics.  `force` rewrites a's inverted index with one container kind (array or run: the portable format takes
     a container of <= 4,096 values for an array, so bitmap containers come from `bitmap`: 5,000 docs of id 77 spread
@@ -29,7 +29,7 @@ def _segments(seed=11, nseg=3, n=200_003, force=None, bitmap=False):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(nseg):
-        a = rng.integers(0, 40_000, n)
+        a = rng.integers(0, card, n)
         if i == 1:  # long runs of one id (run containers in the portable format) in the second segment
             a[50_000:50_600] = 77  # (sparse enough that the scan children stay per-candidate residuals)
             a[120_000:120_500] = 1234
@@ -130,11 +130,11 @@ def test_cand_exact_filter_stats(gpu_ctx):
 
 
 def test_cand_density_threshold(gpu_ctx, monkeypatch):
-    """A leaf above the density bound (4,000 ids, ~10 % of the docs) takes the tile sweep; raising the bound to 1
-    takes the candidate kernel for it, with the same results."""
-    segs = _segments(seed=9, nseg=2)
-    ids = list(range(0, 40_000, 3))
-    sql = f"SELECT g, COUNT(*), SUM(m) FROM t WHERE a IN ({', '.join(map(str, ids[:4000]))}) GROUP BY g"
+    """A leaf above the density bound (3 of 40 ids, ~7.5 % of the docs) takes the tile sweep; raising the bound to 1
+    takes the candidate kernel for it, with the same results.  (A long IN list whose containers outnumber the
+    segment's tiles keeps the sweep whatever the bound.)"""
+    segs = _segments(seed=9, nseg=2, card=40)
+    sql = "SELECT g, COUNT(*), SUM(m) FROM t WHERE a IN (0, 1, 2) GROUP BY g"
     ref = engine.execute(parse_sql(sql), segs, iterator_stats=True)
     dense = _run(gpu_ctx, segs, sql)
     assert dense.stats.kernel_variant != _lib.PGPU_KV_CAND
@@ -143,6 +143,11 @@ def test_cand_density_threshold(gpu_ctx, monkeypatch):
     forced = _run(gpu_ctx, segs, sql)
     assert forced.stats.kernel_variant == _lib.PGPU_KV_CAND
     _check(forced, ref)
+    many = _segments(seed=9, nseg=1)
+    sql = f"SELECT COUNT(*), SUM(m) FROM t WHERE a IN ({', '.join(map(str, range(0, 6000, 3)))})"
+    res = _run(gpu_ctx, many, sql)
+    assert res.stats.kernel_variant != _lib.PGPU_KV_CAND
+    _check(res, engine.execute(parse_sql(sql), many, iterator_stats=True))
 
 
 def test_cand_adanalytics_inv(gpu_ctx):
