@@ -38,7 +38,9 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _entry(rank, fn, port, args):
+def _entry(rank, fn, port, args, world=2):
+    global WORLD
+    WORLD = world  # (the spawned process's own module copy: the helpers below read it)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     # a collective that one rank skips must fail the test, not hang it
@@ -49,8 +51,8 @@ def _entry(rank, fn, port, args):
         dist.destroy_process_group()
 
 
-def _spawn(fn, *args):
-    mp.spawn(_entry, args=(fn, _free_port(), args), nprocs=WORLD, join=True)
+def _spawn(fn, *args, world=2):
+    mp.spawn(_entry, args=(fn, _free_port(), args, world), nprocs=world, join=True)
 
 
 # ---- a host-only stand-in for GpuSegment / GpuPlanMaker ----------------------------------------------------------
@@ -315,6 +317,13 @@ def test_distributed_executor_vs_oracle(qi, scatter):
     _spawn(_query_worker, qi, scatter)
 
 
+@pytest.mark.parametrize("qi", [0, 2, 6])
+def test_distributed_executor_three_ranks(qi):
+    """World size 3: the reduce-scatter slices of ceil(G / 3) keys are uneven (the last rank's is short or empty),
+    each rank trims its own slice, rank 0 gathers the candidates."""
+    _spawn(_query_worker, qi, True, world=3)
+
+
 def _split_agree_worker(rank):
     """Only rank 1 holds large values: the split-SUM layout must still be chosen on both ranks."""
     from oracle import engine
@@ -379,6 +388,11 @@ def _hash_worker(rank, qi, force_on):
 @pytest.mark.parametrize("qi", [0, 2, 5])
 def test_hash_tables_merge_by_key_ownership(qi, force_on):
     _spawn(_hash_worker, qi, force_on)
+
+
+def test_hash_tables_merge_three_ranks():
+    """World size 3: hash rows routed to three key owners (all_to_all with uneven splits)."""
+    _spawn(_hash_worker, 2, (0, 1, 2), world=3)
 
 
 LIMIT_SQL = "SELECT g, h, COUNT(*), SUM(m) FROM t WHERE x < 90 GROUP BY g, h ORDER BY SUM(m) DESC, g, h LIMIT 15"
