@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -46,7 +46,13 @@ def parse_args():
     ap.add_argument("--no-check", action="store_true", help="skip the small GPU-vs-oracle check of this workload")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false",
                     help="measure the headline workload only (default N=1 run: also configs 2-4 and variants)")
-    return ap.parse_args()
+    ap.add_argument("--node", action="store_true",
+                    help="drive --gpus devices from this one process through libpinotgpu's node combine "
+                         "(pgpu_node_query_topk, RCCL inside the library: the one-JVM server's shape) instead of one "
+                         "process per GPU")
+    ap.add_argument("--full-out", default=os.environ.get("PGPU_BENCH_FULL", os.path.join("gpurun_out", "bench_full.json")),
+                    help="file for the full per-workload records (the stdout line carries a compact summary)")
+    return ap.parse_args(argv)
 
 
 def available_cores() -> int:
@@ -93,7 +99,7 @@ def measure(ex, q, segs, steps, warmup, inflight, world, barrier):
     return elapsed * 1000.0 / steps, sum(kernel_ms) / len(kernel_ms), result
 
 
-def algorithmic_bytes(ex, pm, q, segs, w, seg_ids, num_docs):
+def algorithmic_bytes(ex, pm, q, segs_by_dev, w, ids_by_dev, num_docs):
     """SURVEY.md 8(d) algorithmic bytes of the workload (tools/bytemodel.py: from the segments' dict ids and the
     reference's filter tree, the same figure whatever strategy the kernels pick), plus `bytes_read_model`: what this
     build's kernels read by their own stats pass (streamed tiles + 32-B sectors of their gathers + dictionaries +
@@ -102,23 +108,33 @@ def algorithmic_bytes(ex, pm, q, segs, w, seg_ids, num_docs):
 
     from tools.bytemodel import output_bytes, workload_bytes
 
+    segs = segs_by_dev[0]
     pm.collect_stats = True
     r = ex.execute(q, segs)
     st = ex.last_stats
     pm.collect_stats = False
+    all_segs = [s for ss in segs_by_dev for s in ss]
     ngroups = len(r.group_rows or []) if r is not None else 1  # ranks != 0 return no rows
     dict_bytes = 0
     for c in sorted(set(a.column for a in q.aggregations if a.column)):
         width = {0: 4, 1: 8, 2: 4, 3: 8}.get(segs[0].column(c).data_type, 4)
-        full = sum(s.column(c).cardinality * width for s in segs)
+        full = sum(s.column(c).cardinality * width for s in all_segs)
         dict_bytes += min(full, 32 * st.num_docs_scanned)
     out_bytes = output_bytes(ngroups, len(q.aggregations))
-    bitmap_bytes = inverted_bytes_read(q, segs)
+    bitmap_bytes = inverted_bytes_read(q, all_segs)
     read = st.dense_bytes + st.sparse_sector_bytes + dict_bytes + bitmap_bytes + out_bytes
     read_parts = {"dense_stream": st.dense_bytes, "sparse_sectors": st.sparse_sector_bytes,
                   "dictionaries": dict_bytes, "inverted_bitmaps": bitmap_bytes, "output": out_bytes}
-    algo, parts, matched = workload_bytes(w, q, segs, num_docs, seg_ids, torch.device("cuda", torch.cuda.current_device()),
-                                          ngroups=ngroups)
+    algo, parts, matched = 0, {}, 0
+    here = torch.cuda.current_device()
+    for ss, ids in zip(segs_by_dev, ids_by_dev):  # (node mode: every device's segments, on that device)
+        dev = ss[0].ctx.device if len(segs_by_dev) > 1 else here
+        torch.cuda.set_device(dev)
+        a, pp, m = workload_bytes(w, q, ss, num_docs, ids, torch.device("cuda", dev), ngroups=ngroups)
+        algo, matched = algo + a, matched + m
+        for k, v in pp.items():
+            parts[k] = parts.get(k, 0) + v
+    torch.cuda.set_device(here)
     if matched != st.num_docs_scanned:  # the model regenerates the ids: it must see the docs the GPU matched
         raise RuntimeError(f"byte model matched {matched} docs, the GPU {st.num_docs_scanned}")
     return algo, st, parts, read, read_parts
@@ -144,9 +160,51 @@ KERNEL_NAMES = {0: "query_kernel (ring)", 1: "query_kernel_direct", 2: "query_ke
                 6: "query_kernel_cand", 7: "part_scan_kernel + part_reduce_kernel"}
 
 
-def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier):
-    """Generate the workload's segments in HBM, measure it, time the CPU baseline beside it; returns the fields
-    of one result (the headline line or an entry of `workloads`)."""
+class NodeExecutor:
+    """bench.py's executor interface (submit / collect / execute / last_stats) over pinot_amd.node.GpuNode: one
+    process drives every device of the node and the partial tables merge over RCCL inside libpinotgpu
+    (pgpu_node_query_topk).  A node query launches every device and merges in one call, so submit runs it and
+    collect hands back its result."""
+
+    def __init__(self, node, segs_by_device):
+        self.node = node
+        self.segs_by_device = segs_by_device
+        self.last_stats = None
+
+    def execute(self, q, _segs=None):
+        res = self.node.execute(q, self.segs_by_device)
+        self.last_stats = res.stats
+        return res
+
+    def submit(self, q, _segs=None):
+        return self.execute(q)
+
+    def collect(self, res):
+        return res
+
+
+class _Planners:
+    """pm.collect_stats fanned out to every device's plan maker (node mode)."""
+
+    def __init__(self, planners):
+        object.__setattr__(self, "_pms", planners)
+
+    def __setattr__(self, name, value):
+        for pm in self._pms:
+            setattr(pm, name, value)
+
+
+def kernel_label(ex, opts) -> str:
+    name = KERNEL_NAMES.get(getattr(ex.last_stats, "kernel_variant", -1), "query_kernel")
+    if opts.get("exact_filter_stats"):
+        name += " + andfsm_tile_kernel + andfsm_segment_kernel (or leafbits_kernel)"
+    return name
+
+
+def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seconds, log, barrier, node=None):
+    """Generate the workload's segments in HBM, measure it, time the CPU baseline beside it; returns the full
+    record of one result (the compact line is built from it by compact_record).  `node` (a GpuNode) drives its
+    devices from this process; the segments are then sharded over the node's devices as over ranks."""
     import torch
     from pinot_amd.combine import DistributedExecutor
     from pinot_amd.plan import GpuPlanMaker
@@ -155,49 +213,79 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
 
     w = WORKLOADS[name]
     nseg = segments or w.segments
-    seg_ids = list(range(rank * nseg, (rank + 1) * nseg))
+    ndev = len(node.contexts) if node is not None else 1
+    shards = list(range(ndev)) if node is not None else [rank]
     t0 = time.time()
-    segs = build_segments_gpu(ctx, w, seg_ids, args.docs)
-    torch.cuda.synchronize()
+    segs_by_dev, ids_by_dev = [], []
+    for i, shard in enumerate(shards):
+        dctx = node.contexts[i] if node is not None else ctx
+        if node is not None:
+            torch.cuda.set_device(dctx.device)
+        ids = list(range(shard * nseg, (shard + 1) * nseg))
+        segs_by_dev.append(build_segments_gpu(dctx, w, ids, args.docs))
+        ids_by_dev.append(ids)
+        torch.cuda.synchronize()
+    if node is not None:
+        torch.cuda.set_device(node.contexts[0].device)
+    segs, seg_ids = segs_by_dev[0], ids_by_dev[0]
     gen_s = time.time() - t0
-    log(f"{name}: generated {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
+    log(f"{name}: generated {ndev} x {len(segs)} segments x {args.docs} docs in {gen_s:.1f}s")
     hbm = resident_bytes(ctx, segs, nseg * args.docs)
     log(f"{name}: resident {hbm['resident_bytes_per_gpu'] / 1e9:.2f} GB per GPU, {hbm['bytes_per_row']:.2f} B/row "
         f"({hbm['forward_index_bytes_per_row']:.2f} forward index, {hbm['derived_bytes_per_row']:.2f} derived)")
     opts = dict(w.options)
     q = parse_sql(w.sql)
-    pm = GpuPlanMaker(ctx, **plan_options(opts))
-    ex = DistributedExecutor(pm)
+    if node is not None:
+        for pm_ in node.planners:
+            for k, v in plan_options(opts).items():
+                setattr(pm_, k, v)
+        pm = _Planners(node.planners)
+        ex = NodeExecutor(node, segs_by_dev)
+    else:
+        pm = GpuPlanMaker(ctx, **plan_options(opts))
+        ex = DistributedExecutor(pm)
     try:
-        algo_bytes, st, breakdown, read_bytes, read_breakdown = algorithmic_bytes(ex, pm, q, segs, w, seg_ids,
-                                                                                  args.docs)
+        algo_bytes, st, breakdown, read_bytes, read_breakdown = algorithmic_bytes(ex, pm, q, segs_by_dev, w,
+                                                                                  ids_by_dev, args.docs)
         log(f"{name}: stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, "
             f"{read_bytes / 1e9:.3f} GB read by the kernels, {st.kernel_ms:.3f} ms")
-        ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight, world, barrier)
+        ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight if node is None else 1,
+                                                     world, barrier)
         rows_per_gpu = nseg * args.docs
-        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-        log(f"{name}: timed: {ms_per_step:.3f} ms/step, kernel {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s")
+        # per GPU: this rank's (or, in node mode, the average device's) algorithmic bytes over the span of the
+        # kernels of one query on its stream (the slowest device's in node mode)
+        achieved = algo_bytes / ndev / (avg_kernel_ms * 1e-3) / 1e9
+        log(f"{name}: timed: {ms_per_step:.3f} ms/step, kernels {avg_kernel_ms:.3f} ms, {achieved:.0f} GB/s per GPU")
         cpu = check = None
         if rank == 0 and not args.no_cpu_baseline:
             cpu, check = cpu_baseline(ctx, w, q, opts, args, cpu_seconds, segs)
         traffic, traffic_src = _pmc_traffic(name)
         return {
-            "value": rows_per_gpu * world / (ms_per_step * 1e-3),
+            "value": rows_per_gpu * world * ndev / (ms_per_step * 1e-3),
             "ms_per_step": ms_per_step,
             "steps": steps,
+            "n_gpus": world * ndev,
             "config": {"workload": name, "description": w.description, "query": w.sql,
                        "segments_per_gpu": nseg, "docs_per_segment": args.docs, "rows_per_gpu": rows_per_gpu,
-                       "total_rows": rows_per_gpu * world, "queries_in_flight": max(1, args.inflight),
-                       "parallelism": f"segments sharded over {world} GPU(s); partial tables merged over RCCL"},
+                       "total_rows": rows_per_gpu * world * ndev,
+                       "queries_in_flight": max(1, args.inflight) if node is None else 1,
+                       "parallelism": (f"segments sharded over {ndev} GPU(s) of one process; partial tables merged "
+                                       "over RCCL inside libpinotgpu (pgpu_node_query_topk)") if node is not None else
+                                      (f"segments sharded over {world} GPU(s), one process each; partial tables "
+                                       "merged over RCCL (torch.distributed)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": KERNEL_NAMES.get(getattr(ex.last_stats, "kernel_variant", -1), "query_kernel"),
-                         "algorithmic_bytes_per_launch": algo_bytes,
-                         "kernel_ms_avg": avg_kernel_ms, "bytes_breakdown": breakdown,
+                         "kernel": kernel_label(ex, opts),
+                         "algorithmic_bytes_per_launch": algo_bytes / ndev,
+                         "kernel_ms_avg": avg_kernel_ms,
+                         "kernel_ms_definition": "HIP events on the query stream around every kernel that reads "
+                                                 "the segments (leaf bitmaps, query kernel, group-by phases, "
+                                                 "filter-statistic kernels)",
+                         "bytes_breakdown": breakdown,
                          "bytes_definition": "SURVEY 8(d) workload bytes (tools/bytemodel.py), strategy-independent",
                          "bytes_read_model": read_bytes, "bytes_read_breakdown": read_breakdown},
             "cpu_baseline": cpu,
-            "result": {"matched_docs_per_gpu": st.num_docs_scanned,
+            "result": {"matched_docs_per_gpu": st.num_docs_scanned // ndev,
                        "groups": (len(result.group_rows) if result and result.group_rows is not None else None),
                        "rows": [list(r) for r in (result.rows[:3] if result else [])]},
             "parity_check": check,
@@ -205,8 +293,9 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
             "setup_s": round(gen_s, 1),
         }
     finally:
-        for s in segs:
-            s.release()
+        for ss in segs_by_dev:
+            for s in ss:
+                s.release()
 
 
 # Secondary workloads measured after the headline in the default run (BASELINE.json configs 2-4 and the SURVEY 8(d)
@@ -216,14 +305,125 @@ SECONDARY = [("range_in", 10, 2, 0, 3.0), ("groupby1m", 5, 1, 0, 3.0), ("bitmap5
              ("adanalytics_8b", 5, 1, 0, 2.0)]
 
 
-def main():
-    args = parse_args()
+METRIC = "rows/sec for filtered GROUP BY SUM at 1/8 GPUs + achieved HBM GB/s vs peak"
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "kernel", "kernel_ms_avg",
+                 "algorithmic_bytes_per_launch")
+LINE_LIMIT = 6000  # the driver keeps the last 8000 characters of stdout: the line must fit well inside them
+
+
+def compact_cpu(cpu):
+    if not cpu:
+        return None
+    out = {k: cpu[k] for k in ("value", "unit", "cores", "kind") if k in cpu}
+    out["sample"] = cpu.get("sample_short", "")
+    if cpu.get("all_cores"):
+        out["all_cores"] = {"value": cpu["all_cores"]["value"], "cores": cpu["all_cores"]["cores"]}
+    return out
+
+
+def compact_workload(rec):
+    """name -> {ms_per_step, kernel_ms, frac, traffic_ratio, parity_ok, cpu_rows_s} of one secondary workload."""
+    if "error" in rec:
+        return {"error": rec["error"][:160]}
+    rl = rec["roofline"]
+    algo = rl.get("algorithmic_bytes_per_launch") or 0
+    chk = rec.get("parity_check")
+    return {"ms_per_step": round(rec["ms_per_step"], 4), "kernel_ms": round(rl["kernel_ms_avg"], 4),
+            "frac": round(rl["frac"], 4),
+            "traffic_ratio": round(rl["traffic"] / algo, 3) if rl.get("traffic") and algo else None,
+            "parity_ok": None if chk is None else bool(chk.get("ok")),
+            "cpu_rows_s": (rec.get("cpu_baseline") or {}).get("value")}
+
+
+def compact_line(head, workloads, args, n_gpus):
+    """The ONE stdout JSON line: the headline with roofline and cpu_baseline, the secondary workloads as a compact
+    map; the full records go to --full-out."""
+    chk = head.get("parity_check")
+    cfg = head["config"]
+    line = {
+        "metric": METRIC,
+        "value": head["value"],
+        "unit": "rows/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded dict ids generated in HBM)",
+        "config": {"workload": cfg["workload"], "segments_per_gpu": cfg["segments_per_gpu"],
+                   "docs_per_segment": cfg["docs_per_segment"], "total_rows": cfg["total_rows"],
+                   "queries_in_flight": cfg["queries_in_flight"],
+                   "parallelism": ("node" if args.node else "dp") + str(n_gpus)},
+        "roofline": {k: head["roofline"].get(k) for k in ROOFLINE_KEYS},
+        "cpu_baseline": compact_cpu(head.get("cpu_baseline")),
+        "parity_ok": None if chk is None else bool(chk.get("ok")),
+        "matched_docs_per_gpu": head["result"]["matched_docs_per_gpu"],
+        "full_records": args.full_out,
+    }
+    if workloads:
+        line["workloads"] = {k: compact_workload(v) for k, v in workloads.items()}
+    return line
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` started without a launcher: one child process per GPU with the torch.distributed
+    environment a launcher would set (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), started
+    before this process touches the GPU (device_count() does not initialise it); rank 0 prints the line.  Returns
+    the worst child exit status; fewer than N visible devices is an error."""
+    import subprocess
+    import torch
+
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {have} GPU(s) are visible", file=sys.stderr, flush=True)
+        return 2
+    port = free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:  # a failed rank leaves the others blocked in a collective: stop exactly our children
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return rc
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.node:
+        return spawn_ranks(args)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    log = (lambda *a: print(f"[bench rank {rank}]", *a, file=sys.stderr, flush=True))
+    if world > 1 and args.gpus != world:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} ranks")
     local %= max(1, torch.cuda.device_count())  # > 1 rank per GPU only in the gloo rehearsal
     if world > 1:
         torch.cuda.set_device(local)
@@ -233,21 +433,33 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()  # the ranks the process group actually formed
     torch.cuda.set_device(local)
 
     from pinot_amd.segment import GpuContext
 
-    log = (lambda *a: print(f"[bench rank {rank}]", *a, file=sys.stderr, flush=True))
-    ctx = GpuContext(local)
+    node = None
+    if args.node:
+        if world > 1:
+            raise SystemExit("--node drives every GPU from one process: start it without a launcher")
+        from pinot_amd.node import GpuNode
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log(f"--gpus {args.gpus} but {have} GPU(s) are visible")
+            return 2
+        node = GpuNode(list(range(args.gpus)))
+        ctx = node.contexts[0]
+    else:
+        ctx = GpuContext(local)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     head = run_workload(args.workload, ctx, args, world, rank, args.steps, args.warmup, args.segments,
-                        args.cpu_seconds, log, barrier)
+                        args.cpu_seconds, log, barrier, node=node)
     workloads = {}
-    if args.secondary and world == 1 and args.workload == "adanalytics":
+    if args.secondary and world == 1 and node is None and args.workload == "adanalytics":
         for name, steps, warmup, nseg, cpu_s in SECONDARY:
             try:
                 workloads[name] = run_workload(name, ctx, args, world, rank, steps, warmup, nseg, cpu_s, log, barrier)
@@ -255,33 +467,26 @@ def main():
                 log(f"{name}: failed: {e!r}")
                 workloads[name] = {"error": repr(e)}
     if rank == 0:
-        line = {
-            "metric": "rows/sec for filtered GROUP BY SUM at 1/8 GPUs + achieved HBM GB/s vs peak",
-            "value": head["value"],
-            "unit": "rows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": head["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int64",
-            "data": "synthetic (seeded dict ids generated in HBM; dictionaries per BASELINE.md section 3)",
-            "config": head["config"],
-            "roofline": head["roofline"],
-            "cpu_baseline": head["cpu_baseline"],
-            "result": head["result"],
-            "parity_check": head["parity_check"],
-            "hbm": head["hbm"],
-            "setup_s": head["setup_s"],
-        }
-        if workloads:
-            line["workloads"] = workloads
-        print(json.dumps(line, default=float), flush=True)
-    ctx.close()
+        full = {"headline": head, "workloads": workloads}
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(args.full_out)), exist_ok=True)
+            with open(args.full_out, "w") as f:
+                json.dump(full, f, default=float, indent=1)
+        except OSError as e:
+            log(f"full records not written: {e!r}")
+        line = compact_line(head, workloads, args, head["n_gpus"])
+        text = json.dumps(line, default=float, separators=(",", ":"))
+        if len(text) > LINE_LIMIT:  # never let the line outgrow the driver's stdout tail
+            line.pop("workloads", None)
+            text = json.dumps(line, default=float, separators=(",", ":"))
+        print(text, flush=True)
+    if node is not None:
+        node.close()
+    else:
+        ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def _pmc_traffic(workload):
@@ -476,6 +681,8 @@ def c_baseline(w, q, args, seconds):
     all_value, all_runs, all_total = timed(all_cb, cores, len(segs), max(1.0, seconds / 2))
     skew = "" if all(c.dist == "uniform" for c in w.columns) else ", Zipf keys from the same CDF as the GPU's"
     return ({"value": value, "unit": "rows/s", "cores": threads, "kind": "port",
+             "sample_short": f"{runs} run(s) x {nseg} seg x {args.docs} docs, oracle/pinot_cpu.c, {threads} threads "
+                             f"(Pinot default), nproc={nproc}",
             "sample": f"{runs} run(s) over {nseg} segment(s) x {args.docs} docs of the same workload{skew}, "
                       f"oracle/pinot_cpu.c ({filt}, 10k-doc blocks, double SUM), "
                       f"{threads} thread(s) = Pinot default min(#segments, min(10, nproc/2)), nproc={nproc}",
@@ -485,4 +692,4 @@ def c_baseline(w, q, args, seconds):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -431,7 +431,7 @@ typedef struct {
   int64_t num_segments_matched;          /* segments with at least one matching doc (CombineOperatorUtils.java:64-67) */
   int64_t sparse_sector_bytes;           /* PGPU_Q_STATS: 32-B sectors touched by sparse reads * 32 */
   int64_t dense_bytes;                   /* forward-index bytes streamed in dense (staged) mode */
-  double kernel_ms;                      /* main query kernel time (HIP events on the query stream) */
+  double kernel_ms;                      /* every kernel reading the segments: leaf bitmaps, query kernel, group-by phases, filter-statistic kernels (HIP events on the query stream) */
   int64_t filter_stats_exact;            /* 1: num_entries_scanned_in_filter is the reference's figure */
   int64_t num_groups_limit_reached;      /* 1: a segment met >= num_groups_limit distinct group keys
                                             (AggregationGroupByOrderByOperator.java:111) */

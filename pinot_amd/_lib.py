@@ -17,6 +17,7 @@ SYNTH_LIB_PATH = os.path.join(_HERE, "libpinotgpu_synth.so")
 
 # ---- constants (mirror include/pinot_gpu.h) ------------------------------------------------------------------
 PGPU_OK = 0
+PGPU_MAX_SECTIONS = 17  # include/pinot_gpu.h: count + 16 value sections
 PGPU_E_INVALID = -1
 PGPU_E_HIP = -2
 PGPU_E_UNSUPPORTED = -3

@@ -282,14 +282,30 @@ class DistributedExecutor:
         """True on every rank iff it is true on every rank (cache hits must be collective decisions)."""
         return self._allreduce_i64([1 if flag else 0], "min")[0] == 1
 
+    def _agree_hits(self, query: QueryContext, segments: Sequence[GpuSegment]) -> Tuple[bool, bool, bool]:
+        """The three agreement caches' hits (global dictionaries, docs, table layout) decided together in ONE
+        collective: a query whose agreements are all cached pays one small all-reduce before its launch."""
+        mine = [query.group_by == [] or self._globals.get(self._globals_key(query, segments)) is not None,
+                self._docs.get(self._seg_key(segments)) is not None,
+                self._split.get(self._split_key(query, segments)) is not None]
+        got = self._allreduce_i64([int(bool(x)) for x in mine], "min")
+        return tuple(bool(x) for x in got)
+
     @staticmethod
     def _seg_key(segments: Sequence[GpuSegment]) -> tuple:
         return tuple(s.uid for s in segments)
 
-    def _global_dicts(self, query: QueryContext, segments: Sequence[GpuSegment]):
-        key = (tuple(query.group_by), self._seg_key(segments))
+    def _globals_key(self, query, segments):
+        return (tuple(query.group_by), self._seg_key(segments))
+
+    def _split_key(self, query, segments):
+        return (tuple((a.function, a.column) for a in query.aggregations), tuple(query.group_by),
+                self._seg_key(segments))
+
+    def _global_dicts(self, query: QueryContext, segments: Sequence[GpuSegment], agreed: Optional[bool] = None):
+        key = self._globals_key(query, segments)
         hit = self._globals.get(key)
-        if not self._agree(hit is not None):
+        if not (self._agree(hit is not None) if agreed is None else agreed):
             hit = None
         if hit is None:
             check_group_columns(query, segments)
@@ -303,27 +319,27 @@ class DistributedExecutor:
             self._globals[key] = hit
         return hit[0]
 
-    def _reduce_docs(self, segments: Sequence[GpuSegment]) -> int:
+    def _reduce_docs(self, segments: Sequence[GpuSegment], agreed: Optional[bool] = None) -> int:
         """Docs over all ranks (the bound of integer SUM cells after the reduce)."""
         key = self._seg_key(segments)
         hit = self._docs.get(key)
-        if not self._agree(hit is not None):
+        if not (self._agree(hit is not None) if agreed is None else agreed):
             hit = None
         if hit is None:
             hit = (self._allreduce_i64([sum(s.num_docs for s in segments)])[0], tuple(segments))
             self._docs[key] = hit
         return hit[0]
 
-    def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int):
+    def _layout_flags(self, query: QueryContext, segments: Sequence[GpuSegment], reduce_docs: int,
+                      agreed: Optional[bool] = None):
         """(flags, sum_layout) that give every rank the same table layout: PGPU_Q_SUM_SPLIT when any rank's
         integer-SUM bound needs the split sections, PGPU_Q_HASH when any rank's key space takes the hash group-by,
         and per aggregation the fixed-point window of a floating SUM spanning every rank's own (pgpu_sum_layout_agree
         over the ranks: the highest top, the finest exponent; PGPU_SUM_EXP_F64 anywhere makes every rank keep
         float64 sections)."""
-        key = (tuple((a.function, a.column) for a in query.aggregations), tuple(query.group_by),
-               self._seg_key(segments))
+        key = self._split_key(query, segments)
         hit = self._split.get(key)
-        if not self._agree(hit is not None):
+        if not (self._agree(hit is not None) if agreed is None else agreed):
             hit = None
         if hit is None:
             L = self._local_layout(query, segments, 0, reduce_docs)
@@ -439,9 +455,10 @@ class DistributedExecutor:
         import torch
         if not segments:
             raise ValueError("every rank needs at least one segment")
-        globals_ = self._global_dicts(query, segments) if query.group_by else []
-        reduce_docs = self._reduce_docs(segments)
-        flags, sum_layout = self._layout_flags(query, segments, reduce_docs)
+        hit_g, hit_d, hit_s = self._agree_hits(query, segments)
+        globals_ = self._global_dicts(query, segments, hit_g) if query.group_by else []
+        reduce_docs = self._reduce_docs(segments, hit_d)
+        flags, sum_layout = self._layout_flags(query, segments, reduce_docs, hit_s)
         non_scan = self.pm.non_scan_segments(query, segments)
         scan = [s for s, ns in zip(segments, non_scan) if not ns]
         # the layout is the same on every rank: group cardinalities are global, the split-SUM choice and the
@@ -502,21 +519,24 @@ class DistributedExecutor:
                 status, err = _WAIT_GROUPS_LIMIT, e
             except _lib.PinotGpuError as e:
                 status, err = _WAIT_FAILED, e
-        worst = self._allreduce_i64([status], "max")[0]
-        if worst != _WAIT_OK:
-            self._tables.setdefault(int(p.table.numel()), []).append(p.table)
-            if worst == _WAIT_FAILED:
-                raise err if status == _WAIT_FAILED else _lib.PinotGpuError(
-                    _lib.PGPU_E_INVALID, "the query failed on another rank")
-            return self._collect_first_seen(p)
-        self._fold_non_scan(p, stats)
+        if status == _WAIT_OK:
+            self._fold_non_scan(p, stats)
         query, L, table = p.query, p.layout, p.table
         scan_docs = stats["num_docs_scanned"] - sum(s.num_docs for s in p.non_scan)
         local = [stats["num_docs_scanned"], stats["num_entries_scanned_in_filter"],
                  scan_docs * len(query.projected_columns), stats["num_total_docs"], p.num_segments,
                  stats["num_segments_matched"], stats["sparse_sector_bytes"], stats["dense_bytes"],
                  int(bool(stats["num_groups_limit_reached"])), 0 if stats.get("filter_stats_exact", 1) else 1]
-        sums = self._allreduce_i64(local)
+        # the ranks' wait outcomes ride in the same all-reduce as the statistics (counts of ranks per outcome)
+        red = self._allreduce_i64([int(status == _WAIT_GROUPS_LIMIT), int(status == _WAIT_FAILED)] + local)
+        worst = _WAIT_FAILED if red[1] else (_WAIT_GROUPS_LIMIT if red[0] else _WAIT_OK)
+        if worst != _WAIT_OK:
+            self._tables.setdefault(int(p.table.numel()), []).append(p.table)
+            if worst == _WAIT_FAILED:
+                raise err if status == _WAIT_FAILED else _lib.PinotGpuError(
+                    _lib.PGPU_E_INVALID, "the query failed on another rank")
+            return self._collect_first_seen(p)
+        sums = red[2:]
         tot = dict(zip(STAT_FIELDS, sums))
         st = ExecutionStats(kernel_ms=stats["kernel_ms"], filter_stats_exact=sums[-1] == 0,  # this rank's kernel
                             num_groups_limit_reached=sums[-2] > 0, **tot)

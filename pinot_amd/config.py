@@ -144,6 +144,29 @@ class GpuExecutorConfig:
         if self.derived_budget_bytes >= 0:
             ctx.set_derived_budget(self.derived_budget_bytes)
 
+    def open_context(self, device: int):
+        """The GPU context of one device with this configuration's derived-copy budget applied (the server's one
+        place of context creation; a budget set later governs later seals only)."""
+        from .segment import GpuContext
+        ctx = GpuContext(device)
+        self.apply_budget(ctx)
+        return ctx
+
+    def upload(self, ctx, data, columns: Optional[Sequence[str]] = None):
+        """A segment made HBM-resident under this configuration's residency policy: seal builds the bit-sliced
+        copy and value planes only for the columns the table names (derived_flags)."""
+        from .segment import GpuSegment
+        names = list(columns) if columns is not None else list(data.columns)
+        return GpuSegment(ctx, data, columns, derived=self.derived_flags(names))
+
+    def plan_maker(self, ctx):
+        """The GpuPlanMaker of a context with this configuration's query options."""
+        from .plan import GpuPlanMaker
+        return GpuPlanMaker(ctx, num_groups_limit=self.num_groups_limit,
+                            max_init_group_holder_capacity=self.max_init_group_holder_capacity,
+                            exact_filter_stats=self.exact_filter_stats, timeout_ms=self.timeout_ms,
+                            gpu_topk=self.topk, min_server_group_trim_size=self.min_server_group_trim_size)
+
     def device_ids(self, num_visible: int) -> List[int]:
         return parse_devices(self.devices, num_visible)
 

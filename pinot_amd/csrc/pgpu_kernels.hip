@@ -3623,6 +3623,26 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_cand(DevPara
       const int c = __popc(x);
       const int tot = sgpr(wave_sum_i32(c));
       if (tot == 0) continue;
+      if (tot > PGPU_CQ_CAP) {  // more than a queue's worth in these 2,048 docs: two halves of <= 1,024 each
+        for (int h = 0; h < 2; ++h) {
+          const bool mine = (lane >> 5) == h;
+          const int ch = mine ? c : 0;
+          const int th = sgpr(wave_sum_i32(ch));
+          if (qn + th > PGPU_CQ_CAP) {
+            flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+            qn = 0;
+          }
+          int at = qn + wave_excl_scan(ch);
+          uint32_t y = mine ? x : 0u;
+          while (y) {
+            const int bit = __ffs(y) - 1;
+            y &= y - 1u;
+            cv.queue[at++] = (uint16_t)((w0 + lane) * 32 + bit);
+          }
+          qn += th;
+        }
+        continue;
+      }
       if (qn + tot > PGPU_CQ_CAP) {
         flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
         qn = 0;

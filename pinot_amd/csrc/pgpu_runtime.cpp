@@ -318,7 +318,9 @@ struct pgpu_context {
   // HBM held by derived copies (bit-sliced forward indexes, value planes) of this context's segments, and the budget
   // they are built under (pgpu_context_set_derived_budget; default half of the device's memory)
   std::atomic<uint64_t> derived_bytes{0};
-  uint64_t derived_budget = UINT64_MAX;
+  // (atomic: a budget set from one thread may meet another thread's seal; a new budget governs later seals only --
+  // copies already built are kept until their segment is released)
+  std::atomic<uint64_t> derived_budget{UINT64_MAX};
   ~pgpu_context() {
     pool.clear();
     if (qstream) (void)hipStreamDestroy(qstream);
@@ -1092,7 +1094,7 @@ namespace {
 bool reserve_derived(pgpu_context* ctx, uint64_t bytes) {
   uint64_t cur = ctx->derived_bytes.load();
   do {
-    if (cur + bytes > ctx->derived_budget) return false;
+    if (cur + bytes > ctx->derived_budget.load()) return false;
   } while (!ctx->derived_bytes.compare_exchange_weak(cur, cur + bytes));
   return true;
 }
@@ -1335,7 +1337,7 @@ int pgpu_context_set_derived_budget(pgpu_context* ctx, uint64_t bytes) {
 int pgpu_context_derived_bytes(pgpu_context* ctx, uint64_t* out_used, uint64_t* out_budget) {
   if (!ctx || !out_used || !out_budget) return fail(PGPU_E_INVALID, "null argument");
   *out_used = ctx->derived_bytes.load();
-  *out_budget = ctx->derived_budget;
+  *out_budget = ctx->derived_budget.load();
   return PGPU_OK;
 }
 
@@ -3036,7 +3038,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       // every BITS leaf an inverted one: read the containers per (segment, container key) unit into LDS instead of
       // expanding them into HBM bitmaps first (query_kernel_rkey)
       const bool no_rkey = getenv("PGPU_NO_RKEY") && atoi(getenv("PGPU_NO_RKEY")) != 0;  // per plan (tests)
-      bool rk = !no_rkey && !pk.invx.empty();
+      // (not under the exact-statistics replay: leafbits_kernel reads the inverted leaves as expanded bitmaps)
+      bool rk = !no_rkey && !pk.invx.empty() && pk.leaf_words == 0;
       int maxbits = 0, units = 0;
       for (DevSeg& ds : pk.segs) {
         ds.unit_begin = units;
@@ -3566,6 +3569,14 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     e = p.pscan ? pgpu_launch_part_scan(p, grid, dyn, st)
                 : (p.direct ? pgpu_launch_query_direct(p, grid, dyn, st) : pgpu_launch_query(p, grid, dyn, st));
   if (e == hipSuccess && p.mode == PGPU_MODE_PART) e = pgpu_launch_part_reduce(p, grid, st);
+  // the reference's filter statistic (andfsm maps or leaf bitmaps for the host replay) is part of the query's
+  // kernels: ev0 .. ev1 spans every kernel that reads the segments, so kernel_ms prices the whole step's reads
+  if (e == hipSuccess && pk.fsm) {
+    void* h_ent_dev = nullptr;
+    e = ws->h_fsment.device_ptr(&h_ent_dev);
+    if (e == hipSuccess) e = pgpu_launch_andfsm(p, pk.fsm_s2, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
+  }
+  if (e == hipSuccess && pk.leaf_words > 0) e = pgpu_launch_leafbits(p, st);
   if (e == hipSuccess) e = hipEventRecord(ws->ev1, st);
   // statistics, numSegmentsMatched flags and a small table into pinned host memory: one launch
   if (e == hipSuccess) {
@@ -3584,15 +3595,8 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     }
     if (e == hipSuccess) e = hipMemcpyAsync((char*)ws->h_stats.p + 8 * PGPU_NSTATS, ws->hflag.p, 4, hipMemcpyDeviceToHost, st);
   }
-  if (e == hipSuccess && pk.fsm) {
-    void* h_ent_dev = nullptr;
-    e = ws->h_fsment.device_ptr(&h_ent_dev);
-    if (e == hipSuccess) e = pgpu_launch_andfsm(p, pk.fsm_s2, (uint32_t*)ws->fsmfn.p, (int64_t*)h_ent_dev, st);
-  }
-  if (e == hipSuccess && pk.leaf_words > 0) {
-    e = pgpu_launch_leafbits(p, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(ws->h_leafbits.p, ws->leafbits.p, 4ull * pk.leaf_words, hipMemcpyDeviceToHost, st);
-  }
+  if (e == hipSuccess && pk.leaf_words > 0)
+    e = hipMemcpyAsync(ws->h_leafbits.p, ws->leafbits.p, 4ull * pk.leaf_words, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && eager) {
     const int crc = enqueue_compact(ctx, ws, &L, dev_table, st, eager_order);
     if (crc) return bail(crc);

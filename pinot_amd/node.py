@@ -83,17 +83,29 @@ class GpuNode:
         order = None
         if pm0.gpu_topk and pm0.min_server_group_trim_size > 0:
             order = topk_spec(query, [len(g) for g in globs], table_capacity(query.limit, pm0.min_server_group_trim_size))
-        cap = int(min(max(L0.num_keys * len(descs), 1), 1 << 26))
-        kw = 2  # enough for either key width
-        keys = np.empty(cap * kw, dtype=np.int64)
-        cells = np.empty((cap, 64), dtype=np.int64)
+        # result rows: a dense table's G keys (merged onto one key space); a hash table's keys are disjoint per
+        # owner device, at most every device's capacity; the ORDER BY trim keeps k per trimming device plus ties
+        # (a tie-heavy result that overflows reports its size and is run again with room for it)
+        ndev = len(descs)
+        cap = int(L0.num_keys) * (ndev if L0.key_kind == _lib.PGPU_KEYS_HASH else 1)
+        if order is not None:
+            cap = min(cap, 2 * ndev * int(order.k))
+        cap = max(cap, 1)
         n = C.c_uint64()
         st = QueryStats()
         L = TableLayout()
-        _lib.check(self._lib.pgpu_node_query_topk(self.handle, arr, C.byref(order) if order is not None else None,
-                                                  keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                                  cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
-                                                  C.byref(st), C.byref(L)))
+        for attempt in range(2):
+            keys = np.empty(cap * 2, dtype=np.int64)  # two key words at most
+            cells = np.empty((cap, _lib.PGPU_MAX_SECTIONS), dtype=np.int64)  # the agreed layout's sections fit
+            rc = self._lib.pgpu_node_query_topk(self.handle, arr, C.byref(order) if order is not None else None,
+                                                keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                                cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
+                                                C.byref(st), C.byref(L))
+            if rc != _lib.PGPU_OK and attempt == 0 and n.value > cap:
+                cap = int(n.value)
+                continue
+            _lib.check(rc)
+            break
         kw = key_words_out(L)
         ng = n.value
         k = keys[: ng * kw].reshape(ng, kw) if kw > 1 else keys[:ng]

@@ -188,3 +188,30 @@ def test_cand_sorted_leading_leaf(gpu_ctx, monkeypatch):
         monkeypatch.setenv("PGPU_NO_CAND", "1")
         _check(_run(gpu_ctx, segs, sql), ref)
         monkeypatch.delenv("PGPU_NO_CAND")
+
+
+@pytest.mark.parametrize("sql", ["SELECT COUNT(*), SUM(m), MAX(x) FROM t WHERE a IN (77, 88) AND d < 90",
+                                 "SELECT g, COUNT(*), SUM(m) FROM t WHERE a IN (77, 88) GROUP BY g",
+                                 "SELECT COUNT(*), SUM(m) FROM t WHERE a = 88"])
+def test_cand_chunk_above_queue_capacity(gpu_ctx, monkeypatch, sql):
+    """More than a candidate queue's 1,024 entries inside one 2,048-doc piece of a container: a run of 2,000 docs
+    of id 77 (1,760 of them in the tile at doc 10,240) and a bitmap container of id 88 whose first 2,048 docs hold
+    1,900 set bits.  The image is enumerated in queue-sized halves; results equal the oracle's and the tile sweep's."""
+    segs = []
+    rng = np.random.default_rng(21)
+    for i in range(2):
+        n = 200_003
+        a = rng.integers(0, 40_000, n)
+        a[10_000:12_000] = 77
+        a[65_536:65_536 + 1_900] = 88
+        a[65_536 + 2_048 + rng.choice(60_000, 4_000, replace=False)] = 88
+        cols = {"a": (_lib.PGPU_INT, a), "d": (_lib.PGPU_INT, rng.integers(0, 100, n)),
+                "g": (_lib.PGPU_INT, rng.integers(0, 50, n)), "m": (_lib.PGPU_INT, rng.integers(-1000, 100_000, n)),
+                "x": (_lib.PGPU_DOUBLE, rng.normal(0, 1e3, n))}
+        segs.append(build_segment(f"bigchunk{i}", cols, inverted=["a"], sorted_columns=[]))
+    ref = engine.execute(parse_sql(sql), segs, iterator_stats=True)
+    res = _run(gpu_ctx, segs, sql)
+    assert res.stats.kernel_variant == _lib.PGPU_KV_CAND
+    _check(res, ref)
+    monkeypatch.setenv("PGPU_NO_CAND", "1")
+    _check(_run(gpu_ctx, segs, sql), ref)

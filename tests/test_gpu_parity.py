@@ -11,6 +11,7 @@ import pytest
 
 from oracle import engine
 from oracle.segment_writer import build_segment
+from pinot_amd import _lib
 from pinot_amd._lib import PGPU_DOUBLE, PGPU_FLOAT, PGPU_INT, PGPU_LONG, PGPU_STRING, UnsupportedPlanError
 from pinot_amd.plan import GpuPlanMaker
 from pinot_amd.query import parse_sql
@@ -344,6 +345,31 @@ def test_index_only_programs_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n,
         for g in gs:
             g.release()
     _assert_same(res, _oracle(q, segs))
+
+
+@pytest.mark.parametrize("qi", [0, 1, 2])
+def test_index_only_programs_exact_filter_stats(gpu_ctx, qi):
+    """Index-only programs with the reference's numEntriesScannedInFilter requested: the replay reads the inverted
+    leaves as expanded bitmaps, so the container-keyed kernel (which expands nothing) must not be chosen; the
+    statistic and the results equal the oracle's iterator figures.  Without the request the same programs take
+    query_kernel_rkey."""
+    rng = np.random.default_rng(4100 + qi)
+    segs = [_index_segment(rng, 70_001 + 2048 * i, f"ipx{i}") for i in range(2)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql(RPROG_QUERIES[qi])
+        plain = _gpu(gpu_ctx, q, gs)
+        exact = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+    finally:
+        for g in gs:
+            g.release()
+    ref = _oracle(q, segs)
+    assert plain.stats.kernel_variant == _lib.PGPU_KV_RKEY
+    assert exact.stats.kernel_variant != _lib.PGPU_KV_RKEY
+    assert exact.stats.filter_stats_exact
+    _assert_same(plain, ref)
+    _assert_same(exact, ref)
+    assert exact.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
 
 
 @pytest.mark.parametrize("n", [2048, 70_001])

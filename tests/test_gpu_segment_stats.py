@@ -161,3 +161,43 @@ def test_derived_copies_follow_the_residency_policy(gpu_ctx):
             seg.release()
     finally:
         gpu_ctx.set_derived_budget(budget0)
+
+
+def test_executor_config_applies_the_residency_policy(gpu_ctx):
+    """GpuExecutorConfig is where a server applies its keys: upload() passes the table's derived-copy columns to
+    seal, apply_budget() the byte budget (a budget of 0 builds no derived copy), plan_maker() the query options."""
+    import numpy as np
+    from oracle import engine
+    from oracle.segment_writer import build_segment
+    from pinot_amd import _lib
+    from pinot_amd.config import GpuExecutorConfig
+    from pinot_amd.query import parse_sql
+    from tests.helpers import close
+    rng = np.random.default_rng(23)
+    n = 200_000
+    data = build_segment("cfg", {"f": (_lib.PGPU_INT, rng.integers(0, 1000, n).astype(np.int32)),
+                                 "m": (_lib.PGPU_INT, rng.integers(0, 1 << 16, n).astype(np.int32))},
+                         sorted_columns=())
+    cfg = GpuExecutorConfig.from_properties({"pinot.server.query.executor.gpu.sliced.columns": "f",
+                                             "pinot.server.query.executor.gpu.value.planes.columns": "m"})
+    seg = cfg.upload(gpu_ctx, data)
+    try:
+        b = seg.device_bytes_by_kind()
+        assert 0 < b["sliced"] < b["forward"] and b["value_planes"] > 0
+        q = parse_sql("SELECT COUNT(*), SUM(m) FROM t WHERE f < 300")
+        res = cfg.plan_maker(gpu_ctx).execute(q, [seg])
+        assert all(close(x, y) for x, y in zip(res.aggregation_result, engine.execute(q, [data]).aggregation_result))
+    finally:
+        seg.release()
+    _, budget = gpu_ctx.derived_bytes()
+    zero = GpuExecutorConfig.from_properties({"pinot.server.query.executor.gpu.derived.budget.bytes": "0"})
+    try:
+        zero.apply_budget(gpu_ctx)
+        seg = zero.upload(gpu_ctx, data)
+        try:
+            b = seg.device_bytes_by_kind()
+            assert b["sliced"] == 0 and b["value_planes"] == 0
+        finally:
+            seg.release()
+    finally:
+        gpu_ctx.set_derived_budget(budget)
