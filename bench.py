@@ -157,14 +157,14 @@ def resident_bytes(ctx, segs, rows):
 # pgpu_query_stats.kernel_variant -> the query kernel the runtime chose (and the kernels timed beside it)
 KERNEL_NAMES = {0: "query_kernel (ring)", 1: "query_kernel_direct", 2: "query_kernel_rdirect", 3: "query_kernel_rstream",
                 4: "query_kernel_rprog + invexp_kernel", 5: "query_kernel_rkey + rkey_ctab_kernel",
-                6: "query_kernel_cand", 7: "part_scan_kernel + part_reduce_kernel"}
+                6: "query_kernel_cand", 7: "part_scan_kernel + part_reduce_kernel",
+                8: "query_kernel_rfsm + andfsm_segment_kernel"}
 
 
 class NodeExecutor:
     """bench.py's executor interface (submit / collect / execute / last_stats) over pinot_amd.node.GpuNode: one
     process drives every device of the node and the partial tables merge over RCCL inside libpinotgpu
-    (pgpu_node_query_topk).  A node query launches every device and merges in one call, so submit runs it and
-    collect hands back its result."""
+    (pgpu_node_submit / pgpu_node_collect: several node queries in flight, like the per-GPU path's)."""
 
     def __init__(self, node, segs_by_device):
         self.node = node
@@ -177,9 +177,11 @@ class NodeExecutor:
         return res
 
     def submit(self, q, _segs=None):
-        return self.execute(q)
+        return self.node.submit(q, self.segs_by_device)
 
-    def collect(self, res):
+    def collect(self, pending):
+        res = self.node.collect(pending)
+        self.last_stats = res.stats
         return res
 
 
@@ -195,8 +197,9 @@ class _Planners:
 
 
 def kernel_label(ex, opts) -> str:
-    name = KERNEL_NAMES.get(getattr(ex.last_stats, "kernel_variant", -1), "query_kernel")
-    if opts.get("exact_filter_stats"):
+    variant = getattr(ex.last_stats, "kernel_variant", -1)
+    name = KERNEL_NAMES.get(variant, "query_kernel")
+    if opts.get("exact_filter_stats") and variant != 8:
         name += " + andfsm_tile_kernel + andfsm_segment_kernel (or leafbits_kernel)"
     return name
 
@@ -249,8 +252,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
                                                                                   ids_by_dev, args.docs)
         log(f"{name}: stats pass: {st.num_docs_scanned} matched, {algo_bytes / 1e9:.3f} GB algorithmic, "
             f"{read_bytes / 1e9:.3f} GB read by the kernels, {st.kernel_ms:.3f} ms")
-        ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight if node is None else 1,
-                                                     world, barrier)
+        ms_per_step, avg_kernel_ms, result = measure(ex, q, segs, steps, warmup, args.inflight, world, barrier)
         rows_per_gpu = nseg * args.docs
         # per GPU: this rank's (or, in node mode, the average device's) algorithmic bytes over the span of the
         # kernels of one query on its stream (the slowest device's in node mode)
@@ -268,7 +270,7 @@ def run_workload(name, ctx, args, world, rank, steps, warmup, segments, cpu_seco
             "config": {"workload": name, "description": w.description, "query": w.sql,
                        "segments_per_gpu": nseg, "docs_per_segment": args.docs, "rows_per_gpu": rows_per_gpu,
                        "total_rows": rows_per_gpu * world * ndev,
-                       "queries_in_flight": max(1, args.inflight) if node is None else 1,
+                       "queries_in_flight": max(1, args.inflight),
                        "parallelism": (f"segments sharded over {ndev} GPU(s) of one process; partial tables merged "
                                        "over RCCL inside libpinotgpu (pgpu_node_query_topk)") if node is not None else
                                       (f"segments sharded over {world} GPU(s), one process each; partial tables "

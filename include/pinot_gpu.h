@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PGPU_ABI_VERSION 11
+#define PGPU_ABI_VERSION 12
 
 /* ---- status codes ---------------------------------------------------------------------------------------- */
 #define PGPU_OK 0
@@ -445,6 +445,7 @@ typedef struct {
 #define PGPU_KV_RKEY 5       /* index-only program over Roaring containers read into LDS per container key */
 #define PGPU_KV_CAND 6       /* candidates from a sparse leading inverted leaf's containers */
 #define PGPU_KV_PSCAN 7      /* partitioned group-by, phase-1 scan + phase-2 reduce */
+#define PGPU_KV_RFSM 8       /* two bit-sliced leaves in VGPRs with the exact filter statistic's tile maps */
 
 /* Enqueue the query on `stream` (hipStream_t; NULL = the context's own stream) and leave the partial table in
  * caller-provided device memory `dev_table` (table_bytes >= pgpu_table_bytes(layout)).  Does not synchronize.
@@ -606,6 +607,17 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
 int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_topk* order,
                          int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups,
                          pgpu_query_stats* out_stats, pgpu_table_layout* out_layout);
+/* The same in two steps, so that several node queries can be in flight (the host plans and merges query i while
+ * the devices run query i + 1): pgpu_node_submit agrees the table layout and launches every device into a table set
+ * of the query's own; pgpu_node_collect waits for the devices, merges (on per-device merge streams, so a merge
+ * never queues behind later queries' kernels), compacts or trims, and releases the query (also on failure).
+ * Collect node queries in the order they were submitted.  Replaces the same combine as pgpu_node_query
+ * (BaseCombineOperator.java:79-227: the query's segments run while earlier results merge). */
+typedef struct pgpu_node_pending pgpu_node_pending;
+int pgpu_node_submit(pgpu_node* node, const pgpu_query_desc* const* descs, pgpu_node_pending** out_query);
+int pgpu_node_collect(pgpu_node_pending* query, const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells,
+                      uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
+                      pgpu_table_layout* out_layout);
 /* The partition arithmetic both multi-GPU combines share (host only, no device needed): the key slice
  * [first, first + count) of a dense table of num_keys keys that rank `rank` of `world` owns after the
  * reduce-scatter (slices of ceil(num_keys / world) keys, the last one shorter), and the rank owning a hash-table

@@ -43,7 +43,7 @@ PGPU_SUM_EXP_F64 = 32767  # pgpu_table_layout.agg_sum_exp of a float64 SUM secti
 PGPU_SUM_EXP_ZERO = -32767  # ... of a fixed-point SUM over a column holding only zeros
 PGPU_MAX_FIXED_PARTS = 6  # widest fixed-point window (21-bit parts) of a floating SUM
 PGPU_FIXED_TOL_BITS = 40
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class PinotGpuError(RuntimeError):
@@ -113,8 +113,8 @@ class SegmentBytes(C.Structure):
 
 
 # pgpu_query_stats.kernel_variant
-PGPU_KV_RING, PGPU_KV_DIRECT, PGPU_KV_RDIRECT, PGPU_KV_RSTREAM, PGPU_KV_RPROG, PGPU_KV_RKEY, PGPU_KV_CAND, PGPU_KV_PSCAN = \
-    range(8)
+PGPU_KV_RING, PGPU_KV_DIRECT, PGPU_KV_RDIRECT, PGPU_KV_RSTREAM, PGPU_KV_RPROG, PGPU_KV_RKEY, PGPU_KV_CAND, PGPU_KV_PSCAN, \
+    PGPU_KV_RFSM = range(9)
 
 # derived copies seal may build per column (pgpu_segment_set_derived)
 PGPU_DERIVE_SLICED, PGPU_DERIVE_VALUE_PLANES, PGPU_DERIVE_ALL = 1, 2, 3
@@ -217,6 +217,9 @@ SIGNATURES = [
     ("pgpu_node_query_topk", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(TopK), C.POINTER(C.c_int64),
                                        C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats),
                                        C.POINTER(TableLayout)]),
+    ("pgpu_node_submit", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(_P)]),
+    ("pgpu_node_collect", C.c_int, [_P, C.POINTER(TopK), C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
+                                    C.POINTER(C.c_uint64), C.POINTER(QueryStats), C.POINTER(TableLayout)]),
     ("pgpu_slice_of", None, [C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("pgpu_key_owner", C.c_int32, [C.POINTER(C.c_int64), C.c_int32, C.c_int32]),
     ("pgpu_filter_entries_scanned", C.c_int, [C.POINTER(FilterNode), C.c_int32, C.POINTER(C.POINTER(C.c_uint32)),

@@ -24,6 +24,7 @@ ranks before the collective runs, so no rank can skip or reorder one.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -250,6 +251,17 @@ class DistributedExecutor:
         self.dist = dist.is_available() and dist.is_initialized()
         self.rank = dist.get_rank(group) if self.dist else 0
         self.world = dist.get_world_size(group) if self.dist else 1
+        # the control plane -- cache agreements, wait outcomes, statistics, layout votes: a few int64s per query --
+        # runs over a gloo (host) group of the same ranks, so those collectives neither wait for a CU behind the
+        # next in-flight query kernel nor synchronise a device stream; the tables themselves go over RCCL
+        self.ctrl, self.ctrl_device = group, None
+        if self.dist and self.world > 1:
+            if dist.get_backend(group) == "gloo":
+                self.ctrl_device = torch.device("cpu")
+            elif not os.environ.get("PGPU_CONTROL_ON_DEVICE"):
+                ranks = None if group is None else dist.get_process_group_ranks(group)
+                self.ctrl = dist.new_group(ranks=ranks, backend="gloo")
+                self.ctrl_device = torch.device("cpu")
         if device is None:
             device = torch.device("cuda", plan_maker.ctx.device)
         self.device = device
@@ -273,9 +285,10 @@ class DistributedExecutor:
     def _allreduce_i64(self, vals: Sequence[int], op: str = "sum") -> List[int]:
         import torch
         import torch.distributed as dist
-        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=self.device)
+        dev = self.ctrl_device if self.ctrl_device is not None else self.device
+        t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
-                               "min": dist.ReduceOp.MIN}[op], group=self.group)
+                               "min": dist.ReduceOp.MIN}[op], group=self.ctrl)
         return [int(x) for x in t.cpu().tolist()]
 
     def _agree(self, flag: bool) -> bool:

@@ -436,6 +436,7 @@ struct DevParams {
   const struct DevContainer* rk_ctab;  // query_kernel_rkey: container record per (leaf, id, key) (rkey_ctab_kernel)
   const uint32_t* cand_ct;        // query_kernel_cand: per unit {segment, its container's index in InvLeafX::ct
                                   // (~0u: a sorted leaf's doc range), first doc, last doc}
+  uint32_t* fsm_fn;               // query_kernel_rfsm (direct == 8): per-tile transducer maps for andfsm_segment_kernel
   uint64_t gstride64[PGPU_MAX_GCOLS];  // HASH: mixed-radix stride of group column g within its key word
   DevAgg aggs[PGPU_MAX_AGGS];
   int32_t gcols[PGPU_MAX_GCOLS];
@@ -447,6 +448,7 @@ static_assert(sizeof(DevParams) <= 4096, "DevParams is a kernel argument");
 #define PGPU_FLAG_STATS 1
 #define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)
 #define PGPU_FLAG_NT 4        // direct kernel: tile DMAs with the non-temporal policy (default; PGPU_DIRECT_NT=0 off)
+#define PGPU_FLAG_NOHOT 8     // partitioned group-by phase 2: no register accumulation of hot keys (PGPU_NO_HOTKEYS=1)
 #define PGPU_NPROF 12
 // loader phases
 #define PGPU_P_L_TOTAL 0

@@ -2829,6 +2829,243 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rdirect(DevP
 }
 
 // ================================================================================================================
+// EXACT FILTER STATISTICS IN THE REGISTER STREAM (p.direct == 8).  With the reference's numEntriesScannedInFilter
+// requested and every segment's filter an AND of two bit-sliced scan leaves (config 5's shape), the count needs each
+// leaf's match word at every doc (AndDocIdIterator.java:40-67 leap-frogs SVScanDocIdIterator.java:57-71 over both
+// leaves), so both leaves' planes are streamed in full anyway.  This kernel streams them once -- RD tiles ahead in a
+// register ring, as query_kernel_rdirect does -- and from the same words (1) ANDs the leaves and aggregates the
+// matched docs through the candidate queue (no residual program left to run) and (2) writes the tile's transducer
+// map for andfsm_segment_kernel (the andfsm encoding), replacing query_kernel_rdirect + andfsm_tile_kernel, which
+// read the first leaf twice.
+// ================================================================================================================
+#ifndef PGPU_ANDFSM_WORDS
+#define PGPU_ANDFSM_WORDS 8  // per tile: next-state bits (2 per start state), then H per start state
+#endif
+struct RfIssue {  // the issue cursor's segment: both leaves' bit-sliced columns
+  const uint32_t* s0;
+  const uint32_t* s1;
+  int b0, b1;
+};
+FI void rf_load_issue(const DevParams& p, int seg, RfIssue& is) {
+  const DevSeg* sg = p.segs + seg;
+  const DevColumn* cols = p.cols + cld(&sg->col_begin);
+  const int lb = cld(&sg->leaf_begin);
+  const int c0 = cld(&p.instrs[cld(p.pool, lb)].col), c1 = cld(&p.instrs[cld(p.pool, lb + 1)].col);
+  is.s0 = (const uint32_t*)cld(&cols[c0].sliced);
+  is.b0 = cld(&cols[c0].bits);
+  is.s1 = (const uint32_t*)cld(&cols[c1].sliced);
+  is.b1 = cld(&cols[c1].bits);
+}
+template <int P>
+FI void rf_load(const uint32_t* sl, int bits, int tile_in_seg, uint32_t (&x)[P]) {
+  const uint32_t* src = sl + (size_t)tile_in_seg * bits * 64 + lane_id();
+#pragma unroll
+  for (int k = 0; k < P; ++k) x[k] = k < bits ? __builtin_nontemporal_load(src + 64 * k) : 0u;
+}
+// A scan leaf on its register planes (planes past the column's width are 0): a dict-id range, an id mask or <= 4 ids
+// (the shapes andfsm's fsm_sliced_ok admits), then negated for exclusive predicates.
+template <int P>
+FI uint32_t rf_leaf(const uint32_t (&x)[P], const DevInstr& in) {
+  uint32_t m;
+  if (in.pred == PRED_RANGE) {
+    m = rd_lt(x, (uint32_t)in.hi) & ~rd_lt(x, (uint32_t)in.lo);
+  } else if (in.pred == PRED_MASK) {
+    m = 0;
+    for (uint64_t mk = ((uint64_t)(uint32_t)in.hi << 32) | (uint32_t)in.lo; mk; mk &= mk - 1) {
+      const uint32_t id = (uint32_t)__builtin_ctzll(mk);
+      m |= rd_lt(x, id + 1u) & ~rd_lt(x, id);
+    }
+  } else {
+    m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < in.n) m |= rd_lt(x, in.ids[j] + 1u) & ~rd_lt(x, in.ids[j]);
+  }
+  return in.negate ? ~m : m;
+}
+// The tile's map of the two-iterator leap-frog: state s = the iterator scanning; per lane over its 32 docs, then
+// composed across lanes in doc order; lane 0 writes {next states, hand-offs per start state} (andfsm's encoding,
+// states 2 and 3 the identity).
+FI void rf_tile_map(uint32_t m0, uint32_t m1, uint32_t* fn_tile) {
+  const int lane = lane_id();
+  uint32_t nxt = (2u << 4) | (3u << 6), h[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int s0 = 0; s0 < 2; ++s0) {
+    int st = s0;
+    uint32_t hh = 0;
+    int pos = 0;
+    while (pos < 32) {
+      const uint32_t w = (st ? m1 : m0) >> pos;
+      if (!w) break;
+      const int d = pos + __builtin_ctz(w);
+      ++hh;  // the other iterator advances to d (one entry)
+      st = (((st ? m0 : m1) >> d) & 1u) ? 0 : 1 - st;  // both match: a result, iterator 0 leads again
+      pos = d + 1;
+    }
+    nxt |= (uint32_t)st << (2 * s0);
+    h[s0] = hh;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t rn = (uint32_t)__shfl_down((int)nxt, o, 64);
+    uint32_t rh[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rh[s] = (uint32_t)__shfl_down((int)h[s], o, 64);
+    if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
+      uint32_t nn = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int mid = (int)((nxt >> (2 * s)) & 3u);
+        nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
+        h[s] += mid == 0 ? rh[0] : mid == 1 ? rh[1] : mid == 2 ? rh[2] : rh[3];
+      }
+      nxt = nn;
+    }
+  }
+  if (lane == 0) {
+    fn_tile[0] = nxt;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) fn_tile[1 + s] = h[s];
+  }
+}
+
+template <int MODE, int P0, int P1>
+FI Stats rfsm_consumer(const DevParams& p, const Lds& L, int cidx, int t0, int ntiles, Prof& pf) {
+  constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH;
+  const int64_t t_start = now(pf);
+  const int lane = lane_id();
+  Cons cv;
+  {
+    unsigned char* base = L.cons + (size_t)cidx * p.cons_bytes;
+    cv.masks = (uint32_t*)base;
+    cv.queue = (uint16_t*)(base + p.mask_rows * 256);
+    cv.klist = (int32_t*)(base + p.mask_rows * 256);
+    cv.vlist = cv.klist + PGPU_AGG_LIST;
+    cv.acc = (int64_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0));
+    cv.qtiles = (int32_t*)(base + p.mask_rows * 256 + PGPU_CONS_LIST_BYTES_OF(0) + PGPU_CONS_ACC_BYTES);
+  }
+  if (MODE == PGPU_MODE_AGG && lane < PGPU_MAX_AGGS) cv.acc[lane] = lane < p.nagg ? sec_identity(p.aggs[lane].op) : 0;
+  wave_sync();
+  int64_t matched = 0, scanned = 0, sector_bytes = 0, dense_bytes = 0;
+  uint32_t lane_matched = 0;
+  LaneAcc la;
+#pragma unroll
+  for (int k = 0; k < NREG_ACC; ++k) la.v[k] = k < p.nagg ? sec_identity(p.aggs[k].op) : 0;
+  int qn = 0, qt = 0;
+  SegState ss;
+  int cseg = -1;
+  DevInstr in0, in1;
+  if (cidx < ntiles) {
+    const int own = (ntiles - cidx + NW - 1) / NW;  // this wave's tiles: cidx, cidx + NW, ...
+    Cursor ci = cursor_at(p, t0 + cidx), cur = ci;
+    RfIssue is;
+    rf_load_issue(p, ci.seg, is);
+    uint32_t x0[RD][P0], x1[RD][P1];
+#pragma unroll
+    for (int s = 0; s < RD; ++s) {
+      if (s < own) {
+        if (s > 0 && cursor_advance(p, ci, NW)) rf_load_issue(p, ci.seg, is);
+        rf_load<P0>(is.s0, is.b0, ci.tile_in_seg, x0[s]);
+        rf_load<P1>(is.s1, is.b1, ci.tile_in_seg, x1[s]);
+      }
+    }
+    int poll = p.cancel_poll;
+    bool stop = false;
+    for (int k0 = 0; k0 < own && !stop; k0 += RD) {
+#pragma unroll
+      for (int s = 0; s < RD; ++s) {
+        const int k = k0 + s;
+        if (k >= own || stop) break;
+        if (--poll == 0) {
+          poll = p.cancel_poll;
+          if (query_cancelled(p)) {
+            stop = true;
+            break;
+          }
+        }
+        if (k > 0) cursor_advance(p, cur, NW);
+        if (qn && (qn >= PGPU_CQ_FLUSH || qt >= PGPU_CQ_TILES || cur.seg != cseg)) {
+          flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+          qn = qt = 0;
+        }
+        if (cur.seg != cseg) {
+          cseg = cur.seg;
+          load_seg(p, cseg, ss);
+          ss.rprog_len = 0;  // both leaves are evaluated here: the queue carries results, not candidates
+          const int lb = cld(&ss.sg->leaf_begin);
+          in0 = cld(p.instrs + cld(p.pool, lb));
+          in1 = cld(p.instrs + cld(p.pool, lb + 1));
+        }
+        const int64_t tf = now(pf);
+        const int doc0 = cur.tile_in_seg * WT;
+        uint32_t valid;
+        {
+          const int ndocs = min(WT, ss.num_docs - doc0);
+          const int rem = ndocs - 32 * lane;
+          valid = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
+          if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += ((int64_t)ndocs * (in0.bits + in1.bits) + 7) / 8;
+        }
+        const uint32_t m0 = rf_leaf<P0>(x0[s], in0) & valid, m1 = rf_leaf<P1>(x1[s], in1) & valid;
+        // refill this register slot with the tile RD ahead (its loads overlap this tile's map and aggregation)
+        if (k + RD < own) {
+          if (cursor_advance(p, ci, NW)) rf_load_issue(p, ci.seg, is);
+          rf_load<P0>(is.s0, is.b0, ci.tile_in_seg, x0[s]);
+          rf_load<P1>(is.s1, is.b1, ci.tile_in_seg, x1[s]);
+        }
+        rf_tile_map(m0, m1, p.fsm_fn + (size_t)(t0 + cidx + k * NW) * PGPU_ANDFSM_WORDS);
+        PROF_ADD(pf, PGPU_P_C_FILTER, tf);
+        const int64_t ta = now(pf);
+        direct_candidates<MODE, NW>(p, L, cv, la, ss, cur.tile_in_seg, m0 & m1, qn, qt, lane_matched, matched,
+                                    scanned, sector_bytes, dense_bytes, pf);
+        PROF_ADD(pf, PGPU_P_C_AGG, ta);
+      }
+    }
+    if (qn && !stop) flush_queue<MODE, NW>(p, L, cv, la, ss, qn, matched, scanned, sector_bytes, dense_bytes, pf);
+  }
+  {
+    const int64_t lm = wave_sum_i64((int64_t)lane_matched);
+    if (lane == 0) matched += lm;
+  }
+  PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
+  if (MODE == PGPU_MODE_AGG) {
+#pragma unroll
+    for (int a = 0; a < NREG_ACC; ++a)
+      if (a < p.nagg && p.aggs[a].fn != PGPU_AGG_COUNT) acc_commit(cv, a, p.aggs[a].op, la.v[a]);
+  }
+  Stats st;
+  st.matched = matched;
+  st.scanned = 0;  // (the reference's count comes from the tile maps: andfsm_segment_kernel)
+  st.sector_bytes = sector_bytes;
+  st.dense_bytes = dense_bytes;
+  return st;
+}
+
+template <int MODE, int P0, int P1>
+__global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rfsm(DevParams p) {
+  constexpr int NT = PGPU_DIRECT_THREADS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Lds L = carve_direct(dyn_smem, p);
+  if (MODE == PGPU_MODE_LDS) {
+    const int n = p.nsec * (int)p.G;
+    for (int i = threadIdx.x; i < n; i += NT) L.ltab[i] = sec_identity(p.sec_op[i / (int)p.G]);
+  }
+  __syncthreads();
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int lb = (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+  const int t0 = (int)(((int64_t)p.total_tiles * lb) / nb);
+  const int t1 = (int)(((int64_t)p.total_tiles * (lb + 1)) / nb);
+  Prof pf;
+#ifdef PGPU_PROFILE_BUILD
+  pf.on = (p.flags & PGPU_FLAG_PROFILE) != 0;
+#pragma unroll
+  for (int k = 0; k < PGPU_NPROF; ++k) pf.t[k] = 0;
+#endif
+  const Stats st = rfsm_consumer<MODE, P0, P1>(p, L, wave, t0, t1 - t0, pf);
+  direct_epilogue<MODE>(p, L, st, wave, lane, pf);
+}
+
+// ================================================================================================================
 // REGISTER STREAMING (p.direct == 3, aggregation-only mode): every segment's filter is an AND of two bit-sliced fast
 // leaves -- one of <= 16 bits ("wide"), one of <= PN bits ("narrow") -- and every aggregation is answered from one
 // column's value planes (PGPU_AM_SLICED, no residual program).  All three plane sets of a tile stream into VGPRs
@@ -3397,7 +3634,6 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
     const int64_t tf = now(pf);
     __syncthreads();
     if (threadIdx.x == 0) rk_stop = query_cancelled(p) ? 1 : 0;
-    for (int i = threadIdx.x; i < nbits * 2048; i += NT) img[i] = 0u;
     if (threadIdx.x < npairs) {
       int j = 0, k = threadIdx.x;
       while (j + 1 < nbits && k >= nid[j]) k -= nid[j++];
@@ -3406,32 +3642,72 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
     }
     __syncthreads();
     if (rk_stop) break;
+    // Pass 1: each leaf's image = the OR of its bitmap containers, built in registers (thread t owns words t + NT*m)
+    // and stored once -- no clearing pass and no LDS atomics; every container word load of the leaf is issued
+    // before the first OR, so the loads overlap instead of paying one HBM round trip each.
+    constexpr int WPT = 2048 / NT;  // image words per thread
+    for (int t2 = 0, j = 0; j < nbits; ++j) {
+      uint32_t acc[WPT];
+#pragma unroll
+      for (int m = 0; m < WPT; ++m) acc[m] = 0u;
+      const uint8_t* data = (const uint8_t*)cld(&p.invx[cld(&ss.sg->inv_leaf[j])].data);
+      for (int e = t2 + nid[j]; t2 < e; ++t2) {
+        const DevContainer rc = recs[t2];
+        if (sgpr(rc.type) != PGPU_CT_BITMAP || sgpr(rc.card) == 0) continue;
+        const uint32_t* bm = (const uint32_t*)(data + sgpr(rc.offset));
+        uint32_t v[WPT];
+#pragma unroll
+        for (int m = 0; m < WPT; ++m) v[m] = gld(bm, threadIdx.x + NT * m);
+#pragma unroll
+        for (int m = 0; m < WPT; ++m) acc[m] |= v[m];
+      }
+#pragma unroll
+      for (int m = 0; m < WPT; ++m) img[j * 2048 + threadIdx.x + NT * m] = acc[m];
+    }
+    __syncthreads();
+    // Pass 2: array values and runs set with LDS atomics, their 16-bit values loaded AB at a time per thread first
     for (int t2 = 0, j = 0, left = nbits > 0 ? nid[0] : 0; t2 < npairs; ++t2) {
       while (left == 0) left = nid[++j];
       --left;
       const DevContainer rc = recs[t2];
       const uint32_t type = sgpr(rc.type), card = sgpr(rc.card), offset = sgpr(rc.offset);
-      if (card == 0) continue;  // no container of this id under this key
+      if (card == 0 || type == PGPU_CT_BITMAP) continue;  // (no container of this id under this key / pass 1)
       uint32_t* w = img + j * 2048;
       const uint8_t* data = (const uint8_t*)cld(&p.invx[cld(&ss.sg->inv_leaf[j])].data);
-      if (type == PGPU_CT_BITMAP) {
-        const uint32_t* bm = (const uint32_t*)(data + offset);
-        for (int i = threadIdx.x; i < 2048; i += NT) atomicOr(&w[i], gld(bm, i));
-      } else if (type == PGPU_CT_RUN) {
+      constexpr int AB = 8;
+      if (type == PGPU_CT_RUN) {
         const uint16_t* r = (const uint16_t*)(data + offset);
-        for (uint32_t q = threadIdx.x; q < card; q += NT) {
-          const uint32_t s0 = gld(r, 2 * q), e0 = s0 + gld(r, 2 * q + 1);  // inclusive
-          const uint32_t a = s0 >> 5, z = e0 >> 5;
-          for (uint32_t x = a; x <= z; ++x) {
-            const uint32_t lo = x == a ? (s0 & 31) : 0u, hi = x == z ? (e0 & 31) : 31u;
-            atomicOr(&w[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+        for (uint32_t q0 = 0; q0 < card; q0 += NT * AB) {
+          uint32_t st[AB], ln[AB];
+#pragma unroll
+          for (int b = 0; b < AB; ++b) {
+            const uint32_t q = q0 + threadIdx.x + NT * b;
+            st[b] = q < card ? gld(r, 2 * q) : 1u;
+            ln[b] = q < card ? gld(r, 2 * q + 1) : 0u;
+          }
+#pragma unroll
+          for (int b = 0; b < AB; ++b) {
+            if (q0 + threadIdx.x + NT * b >= card) continue;
+            const uint32_t s0 = st[b], e0 = s0 + ln[b];  // inclusive
+            const uint32_t a = s0 >> 5, z = e0 >> 5;
+            for (uint32_t x = a; x <= z; ++x) {
+              const uint32_t lo = x == a ? (s0 & 31) : 0u, hi = x == z ? (e0 & 31) : 31u;
+              atomicOr(&w[x], (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo));
+            }
           }
         }
       } else {
         const uint16_t* v = (const uint16_t*)(data + offset);
-        for (uint32_t q = threadIdx.x; q < card; q += NT) {
-          const uint32_t x = gld(v, q);
-          atomicOr(&w[x >> 5], 1u << (x & 31));
+        for (uint32_t q0 = 0; q0 < card; q0 += NT * AB) {
+          uint32_t x[AB];
+#pragma unroll
+          for (int b = 0; b < AB; ++b) {
+            const uint32_t q = q0 + threadIdx.x + NT * b;
+            x[b] = q < card ? gld(v, q) : 0xFFFFFFFFu;
+          }
+#pragma unroll
+          for (int b = 0; b < AB; ++b)
+            if (x[b] != 0xFFFFFFFFu) atomicOr(&w[x[b] >> 5], 1u << (x[b] & 31));
         }
       }
     }
@@ -4406,6 +4682,68 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
     const int idbits = p.rec_idbits;
     const uint32_t idmask = (1u << idbits) - 1u;
     constexpr int R = 16;
+    bool need_sum = false;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) need_sum |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
+    // Skewed keys: a partition heavy enough to be split over several workgroups (part_plan_kernel) holds a few keys
+    // that dominate it (Zipf(1.1): the top key alone is ~11 % of all rows), and same-address LDS atomics serialize
+    // within a wave instruction.  The workgroup finds its HK hottest keys from a sample of its own records and
+    // accumulates them in registers per lane; the LDS atomics never see them.  Partitions that are not split (even
+    // keys) skip all of it.
+    constexpr int HK = 4;
+    uint32_t hk[HK];
+#pragma unroll
+    for (int h = 0; h < HK; ++h) hk[h] = 0xFFFFFFFFu;
+    const bool hot_on = split && NS > 0 && !(p.flags & PGPU_FLAG_NOHOT);
+    if (hot_on) {
+      {  // histogram of up to 512 records per wave (the first ones of its walk) in cnt[]
+        RegionWalk sw(p, q, pj, pns, nwg, wave, nwaves);
+        uint32_t taken = 0;
+        while (taken < 512 && sw.next()) {
+          const uint32_t n2 = min(sw.n, 512u - taken);
+          for (uint32_t i = lane; i < n2; i += 64) atomicAdd(&cnt[gld(p.recs, sw.base + i) >> idbits], 1u);
+          taken += n2;
+        }
+      }
+      __syncthreads();
+      uint64_t* scratch = (uint64_t*)(base + soff[0]);  // (section 1's cells: cleared again below)
+      for (int h = 0; h < HK; ++h) {
+        uint64_t b = 0;  // (count << 32 | key): the largest count wins
+        for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) b = max(b, ((uint64_t)cnt[i] << 32) | i);
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint64_t x = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(b >> 32), o, 64) << 32) |
+                             (uint32_t)__shfl_xor((int)(uint32_t)b, o, 64);
+          b = max(b, x);
+        }
+        if (lane == 0) scratch[wave] = b;
+        __syncthreads();
+        uint64_t best = 0;
+        for (int w = 0; w < nwaves; ++w) best = max(best, scratch[w]);
+        // a hot key: >= 1/64 of the sample (8 of 512 records per wave on average)
+        const uint64_t total = (uint64_t)nwaves * 512u;
+        hk[h] = (best >> 32) * 64u >= total ? (uint32_t)best : 0xFFFFFFFFu;
+        __syncthreads();
+        if (threadIdx.x == 0 && hk[h] != 0xFFFFFFFFu) cnt[hk[h]] = 0u;
+        __syncthreads();
+      }
+      for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) cnt[i] = 0u;
+      for (int w = threadIdx.x; w < nwaves; w += blockDim.x) scratch[w] = 0;
+      __syncthreads();
+    }
+    uint32_t hc[HK];
+    int64_t hs[HK];                 // the SUM (one value column: every SUM section sums the same values)
+    uint32_t hm[HK][NS > 0 ? NS : 1];  // MIN / MAX dict ids per section
+#pragma unroll
+    for (int h = 0; h < HK; ++h) {
+      hc[h] = 0u;
+      hs[h] = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) hm[h][s] = op[s] == PGPU_RED_MIN_I64 ? 0xFFFFFFFFu : 0u;
+    }
+    // the walk over this workgroup's records, R records per lane in flight (8 with the hot keys' registers live)
+    auto walk = [&](auto rc, auto hot) {
+    constexpr int R = decltype(rc)::value;
+    constexpr bool HOT = decltype(hot)::value;
     RegionWalk rwk(p, q, pj, pns, nwg, wave, nwaves);
     while (rwk.next()) {
       if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
@@ -4413,6 +4751,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       const size_t rb = rwk.base;
       for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
         uint32_t k[R], id[R];
+        int32_t val[R];
         bool ok[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -4421,6 +4760,27 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
           const uint32_t v = gld(p.recs, rb + (ok[r] ? i : n - 1));
           k[r] = v >> idbits;
           id[r] = v & idmask;
+        }
+        if (need_sum) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) val[r] = (int32_t)for_value(fimg, fnblk, fbits, id[r]);
+        }
+        if constexpr (HOT) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int h = 0; h < HK; ++h) {
+              const bool is = ok[r] && k[r] == hk[h];
+              hc[h] += is ? 1u : 0u;
+              if (need_sum) hs[h] += is ? (int64_t)val[r] : 0;
+#pragma unroll
+              for (int s = 0; s < NS; ++s) {
+                if (op[s] == PGPU_RED_MIN_I64) hm[h][s] = is ? min(hm[h][s], id[r]) : hm[h][s];
+                else if (op[s] == PGPU_RED_MAX_I64) hm[h][s] = is ? max(hm[h][s], id[r]) : hm[h][s];
+              }
+              ok[r] = ok[r] && !is;
+            }
+          }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -4432,7 +4792,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               if (!ok[r]) continue;
-              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)for_value(fimg, fnblk, fbits, id[r]));
+              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)val[r]);
             }
           } else {
             uint32_t* sec = (uint32_t*)(base + soff[s]);
@@ -4441,6 +4801,36 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
               if (!ok[r]) continue;
               if (op[s] == PGPU_RED_MIN_I64) atomicMin(&sec[k[r]], id[r]);
               else atomicMax(&sec[k[r]], id[r]);
+            }
+          }
+        }
+      }
+    }
+    };
+    if (hot_on) walk(std::integral_constant<int, 8>{}, std::true_type{});
+    else walk(std::integral_constant<int, R>{}, std::false_type{});
+    if (hot_on) {  // the hot keys' register partials: one LDS update per key and wave
+#pragma unroll
+      for (int h = 0; h < HK; ++h) {
+        if (hk[h] == 0xFFFFFFFFu) continue;
+        const int c = wave_sum_i32((int)hc[h]);
+        if (c == 0) continue;
+        if (lane == 0) atomicAdd(&cnt[hk[h]], (uint32_t)c);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
+            const int64_t t = wave_sum_i64(hs[h]);
+            if (lane == 0) atomicAdd((unsigned long long*)(base + soff[s]) + hk[h], (unsigned long long)t);
+          } else {
+            uint32_t t = hm[h][s];
+            for (int o = 32; o > 0; o >>= 1) {
+              const uint32_t x = (uint32_t)__shfl_xor((int)t, o, 64);
+              t = op[s] == PGPU_RED_MIN_I64 ? min(t, x) : max(t, x);
+            }
+            uint32_t* sec = (uint32_t*)(base + soff[s]);
+            if (lane == 0) {
+              if (op[s] == PGPU_RED_MIN_I64) atomicMin(&sec[hk[h]], t);
+              else atomicMax(&sec[hk[h]], t);
             }
           }
         }
@@ -5226,6 +5616,22 @@ static hipError_t rk_attr(size_t lds_bytes) {
   else if (p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rprog<2, 20>), g, b, dyn_smem, st, p);
   else hipLaunchKernelGGL((query_kernel_rprog<2, 24>), g, b, dyn_smem, st, p);
 }
+// (fused exact statistics: rd_planes = the first leaf's planes held (12 / 16), rs_vplanes = the second's (20 / 24))
+template <int M>
+[[maybe_unused]] static void rf_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
+  const dim3 g(grid), b(PGPU_DIRECT_THREADS);
+  if (p.rd_planes <= 12 && p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rfsm<M, 12, 20>), g, b, dyn_smem, st, p);
+  else hipLaunchKernelGGL((query_kernel_rfsm<M, 16, 24>), g, b, dyn_smem, st, p);
+}
+template <int M>
+[[maybe_unused]] static hipError_t rf_attrs(size_t lds_bytes) {
+  hipError_t e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 12, 20>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 16, 24>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_bytes);
+  return e;
+}
 [[maybe_unused]] static void rs_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
   if (p.rd_planes <= 4 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rstream<4, 16>), g, b, dyn_smem, st, p);
@@ -5252,6 +5658,9 @@ static hipError_t rk_attr(size_t lds_bytes) {
         else rp_launch(p, grid, dyn_smem, st);                                                                  \
       } else                                                                                                    \
         return hipErrorInvalidValue;                                                                            \
+    } else if (p.direct == 8) {                                                                                 \
+      if constexpr (M != PGPU_MODE_PART) rf_launch<M>(p, grid, dyn_smem, st);                                   \
+      else return hipErrorInvalidValue;                                                                         \
     } else if (p.direct == 2) {                                                                                 \
       if (p.rd_pfx) rd_launch<M, PGPU_PFX_PLANES>(p, grid, dyn_smem, st);                                       \
       else rd_launch<M, 0>(p, grid, dyn_smem, st);                                                              \
@@ -5272,6 +5681,8 @@ static hipError_t rk_attr(size_t lds_bytes) {
       if (e == hipSuccess)                                                                                      \
         e = hipFuncSetAttribute((const void*)query_kernel_cand<M>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                 (int)lds_bytes);                                                                \
+    if constexpr (M != PGPU_MODE_PART)                                                                          \
+      if (e == hipSuccess) e = rf_attrs<M>(lds_bytes);                                                          \
     if (e == hipSuccess) e = rd_attrs<M, 0>(lds_bytes);                                                         \
     if (e == hipSuccess) e = rd_attrs<M, PGPU_PFX_PLANES>(lds_bytes);                                           \
     if constexpr (M == PGPU_MODE_AGG)                                                                           \
@@ -5716,7 +6127,7 @@ hipError_t pgpu_launch_leafbits(const DevParams& p, hipStream_t st) {
 
 hipError_t pgpu_launch_andfsm(const DevParams& p, bool s2, uint32_t* fn, int64_t* out, hipStream_t st) {
   if (p.nseg <= 0) return hipSuccess;
-  if (p.total_tiles > 0) {  // ~8 workgroups per CU, each wave over a contiguous run of tiles
+  if (p.total_tiles > 0 && p.direct != 8) {  // (query_kernel_rfsm has written the tile maps)  // ~8 workgroups per CU, each wave over a contiguous run of tiles
     const dim3 g(std::min(2048, (p.total_tiles + 3) / 4));
     if (s2) hipLaunchKernelGGL(andfsm_tile_kernel<true>, g, dim3(256), 0, st, p, fn);
     else hipLaunchKernelGGL(andfsm_tile_kernel<false>, g, dim3(256), 0, st, p, fn);

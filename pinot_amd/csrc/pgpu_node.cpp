@@ -124,13 +124,25 @@ struct DevBuf {
 struct pgpu_node {
   std::vector<int> devices;
   std::vector<pgpu_context*> ctxs;
-  std::vector<hipStream_t> streams;
+  std::vector<hipStream_t> streams;   // query kernels
+  std::vector<hipStream_t> mstreams;  // merges (collectives, compaction) of a query whose kernels are done, so they
+                                      // do not queue behind the kernels of queries submitted after it
   std::vector<ncclComm_t> comms;
-  std::vector<DevBuf> tables;
   // per device scratch of the merges: the slice copy (dense) / compacted rows, routing, send and receive buffers and
   // the merged table (hash)
   std::vector<DevBuf> slice, rkeys, rcells, route, send, recv, merged;
-  std::mutex mu;  // one node query at a time (the tables are node-owned)
+  // partial-table sets (one table per device) of the queries in flight, reused
+  std::vector<std::vector<DevBuf>> free_tables;
+  std::mutex mu;  // submit and collect are serialised (the merge scratch is node-owned)
+};
+
+// A node query in flight: every device's launch and the table set it writes.
+struct pgpu_node_pending {
+  pgpu_node* node = nullptr;
+  std::vector<pgpu_query*> qq;
+  std::vector<pgpu_table_layout> L;
+  std::vector<DevBuf> tables;
+  int32_t num_group_columns = 0;
 };
 
 namespace {
@@ -138,7 +150,7 @@ namespace {
 int sync_all(pgpu_node* nd, const char* what) {
   for (size_t i = 0; i < nd->devices.size(); ++i) {
     (void)hipSetDevice(nd->devices[i]);
-    const hipError_t e = hipStreamSynchronize(nd->streams[i]);
+    const hipError_t e = hipStreamSynchronize(nd->mstreams[i]);
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "%s: %s", what, hipGetErrorString(e));
   }
   return PGPU_OK;
@@ -148,7 +160,7 @@ int nccl_type(int op) { return op == PGPU_RED_SUM_F64 ? ncclFloat64 : ncclInt64;
 int nccl_op(int op) { return op == PGPU_RED_MIN_I64 ? ncclMin : (op == PGPU_RED_MAX_I64 ? ncclMax : ncclSum); }
 
 // Whole dense tables reduced onto device 0: one grouped ncclReduce per run of same-op sections.
-int reduce_dense(pgpu_node* nd, const pgpu_table_layout& L) {
+int reduce_dense(pgpu_node* nd, std::vector<DevBuf>& tables, const pgpu_table_layout& L) {
   const size_t G = L.num_keys;
   ncclResult_t r = g_rccl.GroupStart();
   for (size_t i = 0; i < nd->devices.size() && r == 0; ++i) {
@@ -157,10 +169,10 @@ int reduce_dense(pgpu_node* nd, const pgpu_table_layout& L) {
       int e = s + 1;
       while (e < L.num_sections && L.section_op[e] == L.section_op[s]) ++e;
       const int op = L.section_op[s];
-      const char* src = (const char*)nd->tables[i].p + 8 * G * (size_t)s;
-      char* dst = (char*)nd->tables[0].p + 8 * G * (size_t)s;  // significant on the root only
+      const char* src = (const char*)tables[i].p + 8 * G * (size_t)s;
+      char* dst = (char*)tables[0].p + 8 * G * (size_t)s;  // significant on the root only
       r = g_rccl.Reduce(src, i == 0 ? dst : (void*)src, G * (size_t)(e - s), nccl_type(op), nccl_op(op), 0,
-                        nd->comms[i], nd->streams[i]);
+                        nd->comms[i], nd->mstreams[i]);
       s = e;
     }
   }
@@ -172,7 +184,7 @@ int reduce_dense(pgpu_node* nd, const pgpu_table_layout& L) {
 // Reduce-scatter of dense tables: device d ends up owning the final cells of keys [first, first + count) of
 // pgpu_slice_of (in place in its own table).  One grouped ncclReduce per section and owner slice (an uneven G
 // needs no padding).
-int reduce_slices(pgpu_node* nd, const pgpu_table_layout& L) {
+int reduce_slices(pgpu_node* nd, std::vector<DevBuf>& tables, const pgpu_table_layout& L) {
   const size_t G = L.num_keys;
   const int n = (int)nd->devices.size();
   ncclResult_t r = g_rccl.GroupStart();
@@ -182,9 +194,9 @@ int reduce_slices(pgpu_node* nd, const pgpu_table_layout& L) {
         uint64_t first = 0, count = 0;
         pgpu_slice_of(G, n, d, &first, &count);
         if (!count) continue;
-        char* p = (char*)nd->tables[i].p + 8 * (G * (size_t)s + first);
+        char* p = (char*)tables[i].p + 8 * (G * (size_t)s + first);
         r = g_rccl.Reduce(p, p, count, nccl_type(L.section_op[s]), nccl_op(L.section_op[s]), d, nd->comms[i],
-                          nd->streams[i]);
+                          nd->mstreams[i]);
       }
   const ncclResult_t r2 = g_rccl.GroupEnd();
   if (r != 0 || r2 != 0) return nfail(PGPU_E_HIP, "ncclReduce (scatter): %s", g_rccl.str(r ? r : r2));
@@ -228,7 +240,8 @@ int append_rows(pgpu_context* ctx, const pgpu_table_layout& L, const void* table
 }
 
 // Hash tables: every device's rows to the owners of their keys, merged there, trimmed there.
-int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgpu_topk* order, Out& out) {
+int merge_hash(pgpu_node* nd, std::vector<DevBuf>& tables, const std::vector<pgpu_table_layout>& L,
+               const pgpu_topk* order, Out& out) {
   const int n = (int)nd->devices.size();
   const int kw = L[0].key_words == 2 ? 2 : 1, nsec = L[0].num_sections, width = kw + nsec;
   std::vector<uint64_t> rows(n, 0);
@@ -239,7 +252,7 @@ int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgp
     if (e == hipSuccess) e = nd->rkeys[i].ensure(8 * G * kw + 16);
     if (e == hipSuccess) e = nd->rcells[i].ensure(8 * G * nsec + 16);
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node rows: %s", hipGetErrorString(e));
-    int rc = pgpu_compact_to_device(nd->ctxs[i], &L[i], nd->tables[i].p, nd->streams[i], (int64_t*)nd->rkeys[i].p,
+    int rc = pgpu_compact_to_device(nd->ctxs[i], &L[i], tables[i].p, nd->mstreams[i], (int64_t*)nd->rkeys[i].p,
                                     (int64_t*)nd->rcells[i].p, G, &rows[i]);
     if (rc) return rc;
     // route scratch: owner byte per row, then counts and cursors (n each)
@@ -248,12 +261,12 @@ int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgp
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node route: %s", hipGetErrorString(e));
     uint8_t* owner = (uint8_t*)nd->route[i].p;
     uint32_t* counts = (uint32_t*)((char*)nd->route[i].p + ((rows[i] + 15) & ~15ull));
-    e = hipMemsetAsync(counts, 0, 4 * (size_t)n, nd->streams[i]);
+    e = hipMemsetAsync(counts, 0, 4 * (size_t)n, nd->mstreams[i]);
     if (e == hipSuccess && rows[i])
       e = pgpu_launch_node_route((const int64_t*)nd->rkeys[i].p, nullptr, rows[i], kw, nsec, n, owner, counts,
-                                 nullptr, nullptr, false, nd->streams[i]);
-    if (e == hipSuccess) e = hipMemcpyAsync(cnt[i].data(), counts, 4 * (size_t)n, hipMemcpyDeviceToHost, nd->streams[i]);
-    if (e == hipSuccess) e = hipStreamSynchronize(nd->streams[i]);
+                                 nullptr, nullptr, false, nd->mstreams[i]);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt[i].data(), counts, 4 * (size_t)n, hipMemcpyDeviceToHost, nd->mstreams[i]);
+    if (e == hipSuccess) e = hipStreamSynchronize(nd->mstreams[i]);
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node owners: %s", hipGetErrorString(e));
   }
   for (int i = 0; i < n; ++i) {  // rows grouped by owner in the send buffer
@@ -266,11 +279,11 @@ int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgp
     (void)hipSetDevice(nd->devices[i]);
     uint8_t* owner = (uint8_t*)nd->route[i].p;
     uint32_t* cursor = (uint32_t*)((char*)nd->route[i].p + ((rows[i] + 15) & ~15ull)) + n;
-    hipError_t e = hipMemcpyAsync(cursor, off[i].data(), 4 * (size_t)n, hipMemcpyHostToDevice, nd->streams[i]);
+    hipError_t e = hipMemcpyAsync(cursor, off[i].data(), 4 * (size_t)n, hipMemcpyHostToDevice, nd->mstreams[i]);
     if (e == hipSuccess)
       e = pgpu_launch_node_route((const int64_t*)nd->rkeys[i].p, (const int64_t*)nd->rcells[i].p, rows[i], kw, nsec,
-                                 n, owner, nullptr, cursor, (int64_t*)nd->send[i].p, true, nd->streams[i]);
-    if (e == hipSuccess) e = hipStreamSynchronize(nd->streams[i]);  // (the cursors' host copy is a stack array)
+                                 n, owner, nullptr, cursor, (int64_t*)nd->send[i].p, true, nd->mstreams[i]);
+    if (e == hipSuccess) e = hipStreamSynchronize(nd->mstreams[i]);  // (the cursors' host copy is a stack array)
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node scatter: %s", hipGetErrorString(e));
   }
   std::vector<uint64_t> incoming(n, 0);
@@ -285,7 +298,7 @@ int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgp
       (void)hipSetDevice(nd->devices[i]);
       e = hipMemcpyPeerAsync((char*)nd->recv[o].p + 8 * at * width, nd->devices[o],
                              (const char*)nd->send[i].p + 8 * (size_t)off[i][o] * width, nd->devices[i],
-                             8 * (size_t)cnt[i][o] * width, nd->streams[i]);
+                             8 * (size_t)cnt[i][o] * width, nd->mstreams[i]);
       if (e != hipSuccess) return nfail(PGPU_E_HIP, "node peer copy: %s", hipGetErrorString(e));
       at += cnt[i][o];
     }
@@ -301,14 +314,14 @@ int merge_hash(pgpu_node* nd, const std::vector<pgpu_table_layout>& L, const pgp
     hipError_t e = nd->merged[o].ensure(8 * P * (size_t)(nsec + 2) + 16);
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node merged table: %s", hipGetErrorString(e));
     int32_t* hflag = (int32_t*)((char*)nd->merged[o].p + 8 * P * (size_t)(nsec + 2));
-    e = hipMemsetAsync(hflag, 0, 4, nd->streams[o]);
+    e = hipMemsetAsync(hflag, 0, 4, nd->mstreams[o]);
     if (e == hipSuccess)
       e = pgpu_launch_node_merge((const int64_t*)nd->recv[o].p, incoming[o], kw, nsec, (int64_t*)nd->merged[o].p, P,
-                                 ops, hflag, nd->streams[o]);
+                                 ops, hflag, nd->mstreams[o]);
     if (e != hipSuccess) return nfail(PGPU_E_HIP, "node merge: %s", hipGetErrorString(e));
     pgpu_table_layout Lo = L[0];
     Lo.num_keys = P;
-    rc = append_rows(nd->ctxs[o], Lo, nd->merged[o].p, nd->streams[o], order, 0, out);
+    rc = append_rows(nd->ctxs[o], Lo, nd->merged[o].p, nd->mstreams[o], order, 0, out);
     if (rc) return rc;
   }
   return PGPU_OK;
@@ -337,12 +350,16 @@ int pgpu_node_init(const int32_t* device_ordinals, int32_t num_devices, pgpu_nod
     nd->ctxs.push_back(ctx);
     hipStream_t st = nullptr;
     (void)hipSetDevice(device_ordinals[i]);
-    const hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e != hipSuccess) return bail(nfail(PGPU_E_HIP, "node stream: %s", hipGetErrorString(e)));
     nd->streams.push_back(st);
+    hipStream_t ms = nullptr;
+    e = hipStreamCreateWithFlags(&ms, hipStreamNonBlocking);
+    if (e != hipSuccess) return bail(nfail(PGPU_E_HIP, "node merge stream: %s", hipGetErrorString(e)));
+    nd->mstreams.push_back(ms);
     DevBuf b;
     b.device = device_ordinals[i];
-    for (auto* v : {&nd->tables, &nd->slice, &nd->rkeys, &nd->rcells, &nd->route, &nd->send, &nd->recv, &nd->merged})
+    for (auto* v : {&nd->slice, &nd->rkeys, &nd->rcells, &nd->route, &nd->send, &nd->recv, &nd->merged})
       v->push_back(b);
   }
   nd->comms.assign(num_devices, nullptr);
@@ -366,15 +383,20 @@ int pgpu_node_shutdown(pgpu_node* node) {
   if (!node) return PGPU_OK;
   for (ncclComm_t c : node->comms)
     if (c) (void)g_rccl.CommDestroy(c);
-  for (auto* v : {&node->tables, &node->slice, &node->rkeys, &node->rcells, &node->route, &node->send, &node->recv,
-                  &node->merged})
+  for (auto* v : {&node->slice, &node->rkeys, &node->rcells, &node->route, &node->send, &node->recv, &node->merged})
     for (DevBuf& b : *v) {
+      (void)hipSetDevice(b.device);
+      if (b.p) (void)hipFree(b.p);
+    }
+  for (auto& set : node->free_tables)
+    for (DevBuf& b : set) {
       (void)hipSetDevice(b.device);
       if (b.p) (void)hipFree(b.p);
     }
   for (size_t i = 0; i < node->streams.size(); ++i) {
     (void)hipSetDevice(node->devices[i]);
     (void)hipStreamDestroy(node->streams[i]);
+    if (i < node->mstreams.size()) (void)hipStreamDestroy(node->mstreams[i]);
   }
   for (pgpu_context* c : node->ctxs) pgpu_shutdown(c);
   delete node;
@@ -403,8 +425,14 @@ int pgpu_node_query(pgpu_node* node, const pgpu_query_desc* const* descs, int64_
 int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_topk* order,
                          int64_t* out_keys, int64_t* out_cells, uint64_t capacity, uint64_t* out_num_groups,
                          pgpu_query_stats* out_stats, pgpu_table_layout* out_layout) {
-  if (!node || !descs || !out_num_groups) return nfail(PGPU_E_INVALID, "null argument");
-  if (order && order->k == 0) order = nullptr;
+  pgpu_node_pending* nq = nullptr;
+  const int rc = pgpu_node_submit(node, descs, &nq);
+  if (rc) return rc;
+  return pgpu_node_collect(nq, order, out_keys, out_cells, capacity, out_num_groups, out_stats, out_layout);
+}
+
+int pgpu_node_submit(pgpu_node* node, const pgpu_query_desc* const* descs, pgpu_node_pending** out_query) {
+  if (!node || !descs || !out_query) return nfail(PGPU_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(node->mu);
   const size_t n = node->devices.size();
   // one table layout on every device: the docs of the whole node bound the integer sums, and a split or hash
@@ -449,23 +477,60 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
                       !memcmp(L[i].agg_sum_parts, L[0].agg_sum_parts, sizeof(L[0].agg_sum_parts));
     if (!same) return nfail(PGPU_E_INVALID, "device %zu's table layout differs from device 0's", i);
   }
-  // launch every device, then wait for all
-  std::vector<pgpu_query*> qq(n, nullptr);
+  auto* nq = new pgpu_node_pending();
+  nq->node = node;
+  nq->L = L;
+  nq->num_group_columns = qs[0].num_group_columns;
+  if (!node->free_tables.empty()) {
+    nq->tables = std::move(node->free_tables.back());
+    node->free_tables.pop_back();
+  } else {
+    nq->tables.resize(n);
+    for (size_t i = 0; i < n; ++i) nq->tables[i].device = node->devices[i];
+  }
+  nq->qq.assign(n, nullptr);
+  // launch every device (each query's kernels on the device's query stream; pgpu_node_collect waits for them)
   int rc = PGPU_OK;
   for (size_t i = 0; i < n && rc == PGPU_OK; ++i) {
     const uint64_t bytes = pgpu_table_bytes(&L[i]);
-    const hipError_t e = node->tables[i].ensure(bytes);
+    const hipError_t e = nq->tables[i].ensure(bytes);
     if (e != hipSuccess) rc = nfail(PGPU_E_HIP, "node table on device %d: %s", node->devices[i], hipGetErrorString(e));
-    else rc = pgpu_query_launch(node->ctxs[i], &qs[i], node->streams[i], node->tables[i].p, bytes, &qq[i]);
+    else rc = pgpu_query_launch(node->ctxs[i], &qs[i], node->streams[i], nq->tables[i].p, bytes, &nq->qq[i]);
   }
+  if (rc) {
+    for (pgpu_query* q : nq->qq)
+      if (q) {
+        (void)pgpu_query_wait(q, nullptr);
+        pgpu_query_release(q);
+      }
+    node->free_tables.push_back(std::move(nq->tables));
+    delete nq;
+    return rc;
+  }
+  *out_query = nq;
+  return PGPU_OK;
+}
+
+int pgpu_node_collect(pgpu_node_pending* nq, const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells,
+                      uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
+                      pgpu_table_layout* out_layout) {
+  if (!nq || !out_num_groups) return nfail(PGPU_E_INVALID, "null argument");
+  if (order && order->k == 0) order = nullptr;
+  pgpu_node* node = nq->node;
+  std::lock_guard<std::mutex> lk(node->mu);
+  const size_t n = node->devices.size();
+  std::vector<pgpu_table_layout>& L = nq->L;
+  const bool hash = L[0].key_kind == PGPU_KEYS_HASH;
+  int rc = PGPU_OK;
   pgpu_query_stats tot{};
   tot.filter_stats_exact = 1;
   for (size_t i = 0; i < n; ++i) {
-    if (!qq[i]) continue;
+    if (!nq->qq[i]) continue;
     pgpu_query_stats st{};
-    const int w = pgpu_query_wait(qq[i], &st);
+    const int w = pgpu_query_wait(nq->qq[i], &st);
     if (rc == PGPU_OK && w != PGPU_OK) rc = w;
-    pgpu_query_release(qq[i]);
+    pgpu_query_release(nq->qq[i]);
+    nq->qq[i] = nullptr;
     tot.num_docs_scanned += st.num_docs_scanned;
     tot.num_entries_scanned_in_filter += st.num_entries_scanned_in_filter;
     tot.num_total_docs += st.num_total_docs;
@@ -477,24 +542,33 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
     tot.kernel_variant = std::max(tot.kernel_variant, st.kernel_variant);
     tot.filter_stats_exact &= st.filter_stats_exact;
   }
-  if (rc) return rc;
+  auto done = [&](int r) {
+    node->free_tables.push_back(std::move(nq->tables));
+    delete nq;
+    return r;
+  };
+  if (rc) return done(rc);
   if (out_stats) *out_stats = tot;
   if (out_layout) *out_layout = L[0];
   const int okw = L[0].key_kind == PGPU_KEYS_HASH && L[0].key_words == 2 ? 2 : 1;
   Out out{out_keys, out_cells, capacity, 0, okw, L[0].num_sections};
+  std::vector<DevBuf>& tables = nq->tables;
   if (!hash) {
     const uint64_t G = L[0].num_keys;
     // PGPU_NODE_SCATTER_MIN (bytes; read per query, tests lower it to run the reduce-scatter on small tables)
     const char* sm = getenv("PGPU_NODE_SCATTER_MIN");
     const int64_t scatter_min = sm ? atoll(sm) : (int64_t)1 << 20;
-    const bool scatter = qs[0].num_group_columns > 0 && (int64_t)(8 * G * (uint64_t)L[0].num_sections) >= scatter_min;
+    const bool scatter = nq->num_group_columns > 0 && (int64_t)(8 * G * (uint64_t)L[0].num_sections) >= scatter_min;
     if (!scatter) {
-      rc = reduce_dense(node, L[0]);
-      if (rc) return rc;
-      rc = append_rows(node->ctxs[0], L[0], node->tables[0].p, node->streams[0], order, 0, out);
+      // (one device: its table is the result -- PGPU_NODE_FORCE_RCCL=1, read per query, still reduces: tests)
+      const char* fr = getenv("PGPU_NODE_FORCE_RCCL");
+      if (n > 1 || (fr && atoi(fr) != 0)) rc = reduce_dense(node, tables, L[0]);
+      if (rc) return done(rc);
+      (void)hipSetDevice(node->devices[0]);
+      rc = append_rows(node->ctxs[0], L[0], tables[0].p, node->mstreams[0], order, 0, out);
     } else {
-      rc = reduce_slices(node, L[0]);
-      if (rc) return rc;
+      rc = reduce_slices(node, tables, L[0]);
+      if (rc) return done(rc);
       for (size_t d = 0; d < n && rc == PGPU_OK; ++d) {  // every device trims its own slice
         uint64_t first = 0, count = 0;
         pgpu_slice_of(G, (int32_t)n, (int32_t)d, &first, &count);
@@ -502,23 +576,23 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
         (void)hipSetDevice(node->devices[d]);
         hipError_t e = node->slice[d].ensure(8 * count * (size_t)L[0].num_sections + 16);
         if (e == hipSuccess)
-          e = hipMemcpy2DAsync(node->slice[d].p, 8 * count, (const char*)node->tables[d].p + 8 * first, 8 * G, 8 * count,
-                               (size_t)L[0].num_sections, hipMemcpyDeviceToDevice, node->streams[d]);
-        if (e != hipSuccess) return nfail(PGPU_E_HIP, "node slice: %s", hipGetErrorString(e));
+          e = hipMemcpy2DAsync(node->slice[d].p, 8 * count, (const char*)tables[d].p + 8 * first, 8 * G, 8 * count,
+                               (size_t)L[0].num_sections, hipMemcpyDeviceToDevice, node->mstreams[d]);
+        if (e != hipSuccess) return done(nfail(PGPU_E_HIP, "node slice: %s", hipGetErrorString(e)));
         pgpu_table_layout Ls = L[0];
         Ls.num_keys = count;
-        rc = append_rows(node->ctxs[d], Ls, node->slice[d].p, node->streams[d], order, (int64_t)first, out);
+        rc = append_rows(node->ctxs[d], Ls, node->slice[d].p, node->mstreams[d], order, (int64_t)first, out);
       }
     }
   } else {
-    rc = merge_hash(node, L, order, out);
+    rc = merge_hash(node, tables, L, order, out);
   }
-  if (rc) return rc;
+  if (rc) return done(rc);
   *out_num_groups = out.n;
   if (out.overflow)
-    return nfail(PGPU_E_INVALID, "%llu result rows exceed capacity %llu", (unsigned long long)out.n,
-                 (unsigned long long)capacity);
-  return PGPU_OK;
+    return done(nfail(PGPU_E_INVALID, "%llu result rows exceed capacity %llu", (unsigned long long)out.n,
+                      (unsigned long long)capacity));
+  return done(PGPU_OK);
 }
 
 }  // extern "C"

@@ -2632,6 +2632,10 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   // restores the default policy
   static const bool direct_nt = !(getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) == 0);
   if (direct_nt) p.flags |= PGPU_FLAG_NT;
+  {
+    const bool no_hot = getenv("PGPU_NO_HOTKEYS") && atoi(getenv("PGPU_NO_HOTKEYS")) != 0;  // per query (tests)
+    if (no_hot) p.flags |= PGPU_FLAG_NOHOT;
+  }
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
   uint64_t stride64 = 1;
@@ -3166,6 +3170,33 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       for (DevSeg& ds : pk.segs) ds.cand_leaf = -1;
     }
   }
+  // the reference's numEntriesScannedInFilter fused into the register stream (query_kernel_rfsm): on the
+  // register-direct path with every segment an AND of two bit-sliced leaves (andfsm's two-leaf build), both leaves'
+  // planes are streamed once for the query and the tile maps together (PGPU_NO_RFSM=1, read per plan: tests)
+  if (p.direct == 2 && pk.fsm && pk.fsm_s2 && p.mode != PGPU_MODE_PART &&
+      !(getenv("PGPU_NO_RFSM") && atoi(getenv("PGPU_NO_RFSM")) != 0)) {
+    int b0 = 1, b1 = 1;
+    for (const DevSeg& ds : pk.segs)
+      if (ds.ntiles && ds.leaf_len == 2) {
+        b0 = std::max(b0, (int)pk.instrs[pk.pool[ds.leaf_begin]].bits);
+        b1 = std::max(b1, (int)pk.instrs[pk.pool[ds.leaf_begin + 1]].bits);
+      }
+    const size_t rdyn = (size_t)4 * p.cons_bytes + align16(p.ltab_bytes) + 16;
+    if (b0 <= 16 && b1 <= 24 && rdyn <= PGPU_LDS_LIMIT) {
+      const bool small = b0 <= 12 && b1 <= 20;
+      // 142-167 VGPRs: three waves per SIMD; the aggregation-only mode's 183-199: two
+      const int per_cu = (int)std::min<size_t>(p.mode == PGPU_MODE_AGG ? 2 : 3, PGPU_LDS_LIMIT / rdyn);
+      int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
+      if (g >= 8) g &= ~7;
+      p.direct = 8;
+      p.rd_planes = small ? 12 : 16;
+      p.rs_vplanes = small ? 20 : 24;
+      p.rd_pfx = 0;
+      p.dslots = 0;
+      grid = std::max(1, g);
+      dyn = rdyn;
+    }
+  }
   // sliced aggregation runs in the self-loading kernels only (query_kernel_direct, and query_kernel_rstream with the
   // value planes in VGPRs): elsewhere its segments gather per candidate (their staged aggregation planes are then
   // only extra DMA, never read)
@@ -3445,10 +3476,12 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "container table: %s", hipGetErrorString(e)));
     p.rk_ctab = (const DevContainer*)ws->rkctab.p;
   }
+  p.fsm_fn = nullptr;
   if (pk.fsm) {
     e = ws->fsmfn.ensure(32ull * std::max(1, p.total_tiles), ctx->mpool, st);
     if (e == hipSuccess) e = ws->h_fsment.ensure(8ull * std::max(1, p.nseg));
     if (e != hipSuccess) return bail(fail(PGPU_E_HIP, "filter-statistics maps: %s", hipGetErrorString(e)));
+    p.fsm_fn = (uint32_t*)ws->fsmfn.p;
   }
   if (pk.leaf_words > 0) {
     e = ws->leafbits.ensure(4ull * pk.leaf_words, ctx->mpool, st);

@@ -44,6 +44,7 @@ class GpuNode:
             _lib.check(self._lib.pgpu_node_context(h, i, C.byref(ch)))
             self.contexts.append(GpuContext(d, _handle=ch))
         self.planners = [GpuPlanMaker(c, **plan_options) for c in self.contexts]
+        self._globs = {}  # (group columns, segment uids) -> node-global group dictionaries (set on every planner)
 
     def close(self) -> None:
         if self.handle:
@@ -60,52 +61,71 @@ class GpuNode:
 
     def execute(self, query: QueryContext, segments_by_device: Sequence[Sequence[GpuSegment]]) -> QueryResult:
         """One query over every device's segments, merged inside the library."""
+        if has_mv_aggregations(query):  # *MV aggregations over row columns (pinot_amd/mv.py)
+            check_group_columns(query, [s for segs in segments_by_device for s in segs])
+            low, parts = mv_lower(query)
+            return mv_raise(query, parts, self.execute(low, segments_by_device))
+        return self.collect(self.submit(query, segments_by_device))
+
+    def submit(self, query: QueryContext, segments_by_device: Sequence[Sequence[GpuSegment]]) -> "_NodePending":
+        """Plan the query for every device and launch them (pgpu_node_submit); several may be in flight, collected
+        in submission order."""
         if len(segments_by_device) != len(self.contexts):
             raise ValueError("one segment list per device")
         everything = [s for segs in segments_by_device for s in segs]
         check_group_columns(query, everything)
-        if has_mv_aggregations(query):  # *MV aggregations over row columns (pinot_amd/mv.py)
-            low, parts = mv_lower(query)
-            return mv_raise(query, parts, self.execute(low, segments_by_device))
-        globs = [union_dictionary(g, everything) for g in query.group_by]
+        if has_mv_aggregations(query):
+            raise ValueError("*MV aggregations: use execute()")
+        gkey = (tuple(query.group_by), tuple(s.uid for s in everything))
+        globs = self._globs.get(gkey)
+        if globs is None:  # node-global group dictionaries, set on every device (cached for the segment set)
+            globs = [union_dictionary(g, everything) for g in query.group_by]
+            for pm, segs in zip(self.planners, segments_by_device):
+                for g, glob in zip(query.group_by, globs):
+                    pm.set_global_dictionary(g, segs, glob)
+            if len(self._globs) >= 16:  # (bounded: the oldest segment set's entry goes)
+                self._globs.pop(next(iter(self._globs)))
+            self._globs[gkey] = globs
         keep, descs = [], []
         for pm, segs in zip(self.planners, segments_by_device):
-            for g, glob in zip(query.group_by, globs):
-                pm.set_global_dictionary(g, segs, glob)
             desc, k, _ = pm.build_desc(query, segs)
             keep.append((desc, k))
             descs.append(desc)
         arr = (C.POINTER(QueryDesc) * len(descs))(*[C.pointer(d) for d in descs])
         L0 = self.planners[0].layout(descs[0])
+        h = C.c_void_p()
+        _lib.check(self._lib.pgpu_node_submit(self.handle, arr, C.byref(h)))
+        return _NodePending(query, globs, keep, arr, L0, h, len(everything), segments_by_device)
+
+    def collect(self, p: "_NodePending", min_cap: int = 0) -> QueryResult:
+        """Wait for a submitted node query, merge and compact / trim it (pgpu_node_collect), finish on the host."""
+        query, globs, L0 = p.query, p.globs, p.layout
         # the server's ORDER BY ... LIMIT trim (IndexedTable.finish): every device keeps its best rows of the
-        # groups it owns after the merge (pgpu_node_query_topk)
+        # groups it owns after the merge
         pm0 = self.planners[0]
         order = None
         if pm0.gpu_topk and pm0.min_server_group_trim_size > 0:
             order = topk_spec(query, [len(g) for g in globs], table_capacity(query.limit, pm0.min_server_group_trim_size))
         # result rows: a dense table's G keys (merged onto one key space); a hash table's keys are disjoint per
         # owner device, at most every device's capacity; the ORDER BY trim keeps k per trimming device plus ties
-        # (a tie-heavy result that overflows reports its size and is run again with room for it)
-        ndev = len(descs)
+        ndev = len(self.contexts)
         cap = int(L0.num_keys) * (ndev if L0.key_kind == _lib.PGPU_KEYS_HASH else 1)
         if order is not None:
             cap = min(cap, 2 * ndev * int(order.k))
-        cap = max(cap, 1)
+        cap = max(cap, 1, min_cap)
         n = C.c_uint64()
         st = QueryStats()
         L = TableLayout()
-        for attempt in range(2):
-            keys = np.empty(cap * 2, dtype=np.int64)  # two key words at most
-            cells = np.empty((cap, _lib.PGPU_MAX_SECTIONS), dtype=np.int64)  # the agreed layout's sections fit
-            rc = self._lib.pgpu_node_query_topk(self.handle, arr, C.byref(order) if order is not None else None,
-                                                keys.ctypes.data_as(C.POINTER(C.c_int64)),
-                                                cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n),
-                                                C.byref(st), C.byref(L))
-            if rc != _lib.PGPU_OK and attempt == 0 and n.value > cap:
-                cap = int(n.value)
-                continue
-            _lib.check(rc)
-            break
+        keys = np.empty(cap * 2, dtype=np.int64)  # two key words at most
+        cells = np.empty((cap, _lib.PGPU_MAX_SECTIONS), dtype=np.int64)  # the agreed layout's sections fit
+        h, p.handle = p.handle, None
+        rc = self._lib.pgpu_node_collect(h, C.byref(order) if order is not None else None,
+                                         keys.ctypes.data_as(C.POINTER(C.c_int64)),
+                                         cells.ctypes.data_as(C.POINTER(C.c_int64)), cap, C.byref(n), C.byref(st),
+                                         C.byref(L))
+        if rc != _lib.PGPU_OK and n.value > cap and not min_cap:  # (a tie-heavy trim past the estimate: again, with room)
+            return self.collect(self.submit(query, p.segments_by_device), min_cap=int(n.value))
+        _lib.check(rc)
         kw = key_words_out(L)
         ng = n.value
         k = keys[: ng * kw].reshape(ng, kw) if kw > 1 else keys[:ng]
@@ -113,9 +133,18 @@ class GpuNode:
         stats = ExecutionStats(num_docs_scanned=st.num_docs_scanned,
                                num_entries_scanned_in_filter=st.num_entries_scanned_in_filter,
                                num_entries_scanned_post_filter=st.num_docs_scanned * len(query.projected_columns),
-                               num_total_docs=st.num_total_docs, num_segments_processed=len(everything),
+                               num_total_docs=st.num_total_docs, num_segments_processed=p.num_segments,
                                num_segments_matched=st.num_segments_matched,
                                num_groups_limit_reached=bool(st.num_groups_limit_reached),
                                kernel_ms=st.kernel_ms, sparse_sector_bytes=st.sparse_sector_bytes,
-                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact))
+                               dense_bytes=st.dense_bytes, filter_stats_exact=bool(st.filter_stats_exact),
+                               kernel_variant=st.kernel_variant)
         return finish(query, GroupTable.sorted(k, c, L), globs, stats)
+
+
+class _NodePending:
+    """A submitted node query: its descriptors (kept alive until collect) and the handle."""
+
+    def __init__(self, query, globs, keep, arr, layout, handle, num_segments, segments_by_device):
+        self.query, self.globs, self.keep, self.arr, self.layout = query, globs, keep, arr, layout
+        self.handle, self.num_segments, self.segments_by_device = handle, num_segments, segments_by_device

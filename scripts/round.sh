@@ -9,7 +9,9 @@ cd "$R"
 timeout -k 10 ${TEST_LIMIT:-700} python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 rc=$?
 echo "tests rc=$rc"; tail -3 "$OUT/gpu_tests.log"
-if [ $rc -ne 0 ] && [ $rc -ne 5 ]; then exit $rc; fi
+# assertion failures (1) still let the bench run; a fault, abort, time limit or pytest error ends the call
+if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then exit $rc; fi
+TRC=$rc
 if [ "${BENCH:-1}" = "1" ]; then
   timeout -k 10 600 python -u bench.py --full-out "$OUT/bench_full.json" ${BENCH_ARGS:-} > "$OUT/bench.out" 2> "$OUT/bench.err"
   rc=$?
@@ -22,4 +24,4 @@ if [ "${NODE:-0}" = "1" ]; then
   echo "node rc=$rc"; tail -c 400 "$OUT/node.out"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/node.err"; exit $rc; fi
 fi
-echo done
+echo "done (tests rc=$TRC)"

@@ -140,3 +140,28 @@ def test_node_topk_one_device(monkeypatch, scatter, flags):
         finally:
             for g in gs:
                 g.release()
+
+
+@pytest.mark.parametrize("rccl", [False, True], ids=["direct", "rccl"])
+def test_node_queries_in_flight(monkeypatch, rccl):
+    """pgpu_node_submit / pgpu_node_collect: three node queries in flight (each in its own table set, merged on the
+    merge streams), collected in order -- the same results as one at a time and as the oracle; with
+    PGPU_NODE_FORCE_RCCL=1 the one-device clique still reduces through ncclReduce."""
+    from pinot_amd.node import GpuNode
+    if rccl:
+        monkeypatch.setenv("PGPU_NODE_FORCE_RCCL", "1")
+    segs = _segments(400)
+    with GpuNode([0], min_server_group_trim_size=20) as node:
+        gs = [GpuSegment(node.contexts[0], s) for s in segs]
+        try:
+            qs = [parse_sql(sql) for sql in QUERIES]
+            pending = [node.submit(q, [gs]) for q in qs]
+            got = [node.collect(p) for p in pending]
+            for q, res in zip(qs, got):
+                _check(res, engine.execute(q, segs))
+            again = [node.execute(q, [gs]) for q in qs]
+            for a, b in zip(got, again):
+                assert a.rows == b.rows
+        finally:
+            for g in gs:
+                g.release()

@@ -213,6 +213,68 @@ def test_random_segments_vs_oracle(gpu_ctx, n, qi):
             g.release()
 
 
+# ANDs of exactly two scan leaves: on the register-direct path the exact statistic is fused into the query's own
+# register stream (query_kernel_rfsm: both leaves' planes read once, PGPU_NO_RFSM=1 keeps rdirect + andfsm)
+AND2_QUERIES = [
+    "SELECT COUNT(*) FROM t WHERE c < 1500 AND d > 20000",
+    "SELECT g, COUNT(*), SUM(m) FROM t WHERE c BETWEEN 10 AND 2000 AND d IN (100, 5000, 77777, 123) GROUP BY g",
+    "SELECT COUNT(*), SUM(m), MAX(f) FROM t WHERE b IN (3, 9, 30) AND d < 150000",
+    "SELECT b, SUM(m), MIN(f) FROM t WHERE g <> 9 AND c > 100 GROUP BY b ORDER BY SUM(m) DESC LIMIT 5",
+    "SELECT COUNT(*), AVG(m) FROM t WHERE f NOT IN (1, 2, 3) AND d BETWEEN 1000 AND 9000",
+]
+
+
+@pytest.mark.parametrize("n", [4097, 200_003])
+@pytest.mark.parametrize("qi", range(len(AND2_QUERIES)))
+def test_two_leaf_and_fused_exact_filter_stats(gpu_ctx, monkeypatch, n, qi):
+    rng = np.random.default_rng(900 + n + qi)
+    segs = [_random_segment(rng, n + 1000 * i, f"r2{i}") for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    q = parse_sql(AND2_QUERIES[qi])
+    try:
+        fused = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+        monkeypatch.setenv("PGPU_NO_RFSM", "1")
+        apart = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+    finally:
+        for g in gs:
+            g.release()
+    ref = _oracle(q, segs)
+    for res in (fused, apart):
+        assert res.stats.filter_stats_exact
+        assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
+        _assert_same(res, ref)
+    assert apart.stats.kernel_variant != _lib.PGPU_KV_RFSM
+    if fused.stats.kernel_variant == _lib.PGPU_KV_RFSM:
+        assert apart.stats.kernel_variant == _lib.PGPU_KV_RDIRECT
+
+
+def test_fused_exact_filter_stats_on_the_bench_shape(gpu_ctx, monkeypatch):
+    """Config 5's query (days RANGE AND accountId IN, GROUP BY days ORDER BY ... LIMIT) and its looser variant on the
+    workload's own segments: the fused kernel is the one chosen, and it agrees with the oracle's iterator count and
+    with rdirect + andfsm."""
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import WORKLOADS, build_segment_cpu
+    w = WORKLOADS["adanalytics_exact"]
+    segs = [build_segment_cpu(w, s, (1 << 18) + 333 * s, pack_fixed_bit) for s in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        for sql in (w.sql, w.sql.replace("accountId IN (123456789)", "accountId < 123456789")):
+            q = parse_sql(sql)
+            ref = _oracle(q, segs)
+            monkeypatch.delenv("PGPU_NO_RFSM", raising=False)
+            fused = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+            assert fused.stats.kernel_variant == _lib.PGPU_KV_RFSM
+            monkeypatch.setenv("PGPU_NO_RFSM", "1")
+            apart = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+            for res in (fused, apart):
+                assert res.stats.filter_stats_exact
+                assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
+                _assert_same(res, ref)
+    finally:
+        for g in gs:
+            g.release()
+
+
 # flat ANDs of 2-4 scan leaves: the reference leap-frogs AndDocIdIterator over the scan iterators; with
 # exact_filter_stats the GPU counts its entries with the andfsm transducer kernels (no leaf bitmaps, no host replay)
 AND_QUERIES = [
@@ -769,6 +831,38 @@ def test_partitioned_groupby_shared_dictionary(gpu_ctx, dist):
             _assert_same(res, ref)
             if "AVG" not in sql:
                 assert res.rows == ref.rows
+    finally:
+        for g in gs:
+            g.release()
+
+
+@pytest.mark.parametrize("hot", ["on", "off"])
+def test_partitioned_groupby_hot_keys_frame_of_reference(gpu_ctx, monkeypatch, hot):
+    """Config 4's phase-2 shape -- a 64K-value shared dictionary read through its frame-of-reference image in LDS --
+    under skewed keys: the split hot partition's workgroups accumulate their sampled hottest keys in registers
+    (PGPU_NO_HOTKEYS=1 turns that off).  Every group equals the oracle's, SUM / MAX / MIN / COUNT / AVG, bit-exact."""
+    if hot == "off":
+        monkeypatch.setenv("PGPU_NO_HOTKEYS", "1")
+    rng = np.random.default_rng(97)
+    # 64K distinct values over 2^20 (config 4's metric): the dictionary misses LDS, its frame-of-reference image fits
+    mvals = (np.sort(rng.choice(1 << 20, 65_536, replace=False)) - (1 << 19)).astype(np.int32)
+    segs = []
+    for i in range(3):
+        n = 600_001 + 4096 * i
+        # ~70 % of the rows on a few hundred Zipf keys in the first partition, the rest spread over 300K keys
+        k = np.where(rng.random(n) < 0.7, rng.zipf(1.1, n) % 4096, rng.integers(0, 300_000, n))
+        m = mvals[rng.integers(0, len(mvals), n)]
+        cols = {"k": (PGPU_INT, k.astype(np.int32)), "m": (PGPU_INT, m)}
+        segs.append(build_segment(f"hot{hot}{i}", cols, sorted_columns=()))
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        for sql in ("SELECT k, SUM(m), MAX(m), COUNT(*) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 50",
+                    "SELECT k, MIN(m), MAX(m), SUM(m), AVG(m) FROM t GROUP BY k ORDER BY MIN(m), k LIMIT 50"):
+            q = parse_sql(sql)
+            res = _gpu(gpu_ctx, q, gs, num_groups_limit=1_000_000, min_server_group_trim_size=-1)
+            ref = engine.execute(q, segs, num_groups_limit=1_000_000)
+            _assert_same(res, ref)
+            assert sorted(res.group_rows) == sorted(ref.group_rows)
     finally:
         for g in gs:
             g.release()
