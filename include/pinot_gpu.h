@@ -615,6 +615,10 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
  * (BaseCombineOperator.java:79-227: the query's segments run while earlier results merge). */
 typedef struct pgpu_node_pending pgpu_node_pending;
 int pgpu_node_submit(pgpu_node* node, const pgpu_query_desc* const* descs, pgpu_node_pending** out_query);
+/* ... with each device's filter as a pgpu_expr_node program (pgpu_query_submit_expr's form: planned per segment
+ * inside the library from the literals); exprs[i] == NULL keeps descs[i]'s own per-segment filter trees. */
+int pgpu_node_submit_expr(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_expr_node* const* exprs,
+                          const int32_t* num_nodes, pgpu_node_pending** out_query);
 int pgpu_node_collect(pgpu_node_pending* query, const pgpu_topk* order, int64_t* out_keys, int64_t* out_cells,
                       uint64_t capacity, uint64_t* out_num_groups, pgpu_query_stats* out_stats,
                       pgpu_table_layout* out_layout);

@@ -218,6 +218,8 @@ SIGNATURES = [
                                        C.POINTER(C.c_int64), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(QueryStats),
                                        C.POINTER(TableLayout)]),
     ("pgpu_node_submit", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(_P)]),
+    ("pgpu_node_submit_expr", C.c_int, [_P, C.POINTER(C.POINTER(QueryDesc)), C.POINTER(C.POINTER(ExprNode)),
+                                        C.POINTER(C.c_int32), C.POINTER(_P)]),
     ("pgpu_node_collect", C.c_int, [_P, C.POINTER(TopK), C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint64,
                                     C.POINTER(C.c_uint64), C.POINTER(QueryStats), C.POINTER(TableLayout)]),
     ("pgpu_slice_of", None, [C.c_uint64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

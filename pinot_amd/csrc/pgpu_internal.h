@@ -448,7 +448,6 @@ static_assert(sizeof(DevParams) <= 4096, "DevParams is a kernel argument");
 #define PGPU_FLAG_STATS 1
 #define PGPU_FLAG_PROFILE 2   // per-wave phase cycle counters into DevParams::prof (PGPU_PROFILE=1)
 #define PGPU_FLAG_NT 4        // direct kernel: tile DMAs with the non-temporal policy (default; PGPU_DIRECT_NT=0 off)
-#define PGPU_FLAG_NOHOT 8     // partitioned group-by phase 2: no register accumulation of hot keys (PGPU_NO_HOTKEYS=1)
 #define PGPU_NPROF 12
 // loader phases
 #define PGPU_P_L_TOTAL 0

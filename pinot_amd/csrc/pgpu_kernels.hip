@@ -4682,68 +4682,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
     const int idbits = p.rec_idbits;
     const uint32_t idmask = (1u << idbits) - 1u;
     constexpr int R = 16;
-    bool need_sum = false;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) need_sum |= op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64;
-    // Skewed keys: a partition heavy enough to be split over several workgroups (part_plan_kernel) holds a few keys
-    // that dominate it (Zipf(1.1): the top key alone is ~11 % of all rows), and same-address LDS atomics serialize
-    // within a wave instruction.  The workgroup finds its HK hottest keys from a sample of its own records and
-    // accumulates them in registers per lane; the LDS atomics never see them.  Partitions that are not split (even
-    // keys) skip all of it.
-    constexpr int HK = 4;
-    uint32_t hk[HK];
-#pragma unroll
-    for (int h = 0; h < HK; ++h) hk[h] = 0xFFFFFFFFu;
-    const bool hot_on = split && NS > 0 && !(p.flags & PGPU_FLAG_NOHOT);
-    if (hot_on) {
-      {  // histogram of up to 512 records per wave (the first ones of its walk) in cnt[]
-        RegionWalk sw(p, q, pj, pns, nwg, wave, nwaves);
-        uint32_t taken = 0;
-        while (taken < 512 && sw.next()) {
-          const uint32_t n2 = min(sw.n, 512u - taken);
-          for (uint32_t i = lane; i < n2; i += 64) atomicAdd(&cnt[gld(p.recs, sw.base + i) >> idbits], 1u);
-          taken += n2;
-        }
-      }
-      __syncthreads();
-      uint64_t* scratch = (uint64_t*)(base + soff[0]);  // (section 1's cells: cleared again below)
-      for (int h = 0; h < HK; ++h) {
-        uint64_t b = 0;  // (count << 32 | key): the largest count wins
-        for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) b = max(b, ((uint64_t)cnt[i] << 32) | i);
-        for (int o = 32; o > 0; o >>= 1) {
-          const uint64_t x = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(b >> 32), o, 64) << 32) |
-                             (uint32_t)__shfl_xor((int)(uint32_t)b, o, 64);
-          b = max(b, x);
-        }
-        if (lane == 0) scratch[wave] = b;
-        __syncthreads();
-        uint64_t best = 0;
-        for (int w = 0; w < nwaves; ++w) best = max(best, scratch[w]);
-        // a hot key: >= 1/64 of the sample (8 of 512 records per wave on average)
-        const uint64_t total = (uint64_t)nwaves * 512u;
-        hk[h] = (best >> 32) * 64u >= total ? (uint32_t)best : 0xFFFFFFFFu;
-        __syncthreads();
-        if (threadIdx.x == 0 && hk[h] != 0xFFFFFFFFu) cnt[hk[h]] = 0u;
-        __syncthreads();
-      }
-      for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) cnt[i] = 0u;
-      for (int w = threadIdx.x; w < nwaves; w += blockDim.x) scratch[w] = 0;
-      __syncthreads();
-    }
-    uint32_t hc[HK];
-    int64_t hs[HK];                 // the SUM (one value column: every SUM section sums the same values)
-    uint32_t hm[HK][NS > 0 ? NS : 1];  // MIN / MAX dict ids per section
-#pragma unroll
-    for (int h = 0; h < HK; ++h) {
-      hc[h] = 0u;
-      hs[h] = 0;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) hm[h][s] = op[s] == PGPU_RED_MIN_I64 ? 0xFFFFFFFFu : 0u;
-    }
-    // the walk over this workgroup's records, R records per lane in flight (8 with the hot keys' registers live)
-    auto walk = [&](auto rc, auto hot) {
-    constexpr int R = decltype(rc)::value;
-    constexpr bool HOT = decltype(hot)::value;
     RegionWalk rwk(p, q, pj, pns, nwg, wave, nwaves);
     while (rwk.next()) {
       if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
@@ -4751,7 +4689,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       const size_t rb = rwk.base;
       for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
         uint32_t k[R], id[R];
-        int32_t val[R];
         bool ok[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -4760,27 +4697,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
           const uint32_t v = gld(p.recs, rb + (ok[r] ? i : n - 1));
           k[r] = v >> idbits;
           id[r] = v & idmask;
-        }
-        if (need_sum) {
-#pragma unroll
-          for (int r = 0; r < R; ++r) val[r] = (int32_t)for_value(fimg, fnblk, fbits, id[r]);
-        }
-        if constexpr (HOT) {
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-#pragma unroll
-            for (int h = 0; h < HK; ++h) {
-              const bool is = ok[r] && k[r] == hk[h];
-              hc[h] += is ? 1u : 0u;
-              if (need_sum) hs[h] += is ? (int64_t)val[r] : 0;
-#pragma unroll
-              for (int s = 0; s < NS; ++s) {
-                if (op[s] == PGPU_RED_MIN_I64) hm[h][s] = is ? min(hm[h][s], id[r]) : hm[h][s];
-                else if (op[s] == PGPU_RED_MAX_I64) hm[h][s] = is ? max(hm[h][s], id[r]) : hm[h][s];
-              }
-              ok[r] = ok[r] && !is;
-            }
-          }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -4792,7 +4708,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               if (!ok[r]) continue;
-              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)val[r]);
+              atomicAdd(&sec[k[r]], (unsigned long long)(int64_t)(int32_t)for_value(fimg, fnblk, fbits, id[r]));
             }
           } else {
             uint32_t* sec = (uint32_t*)(base + soff[s]);
@@ -4801,36 +4717,6 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
               if (!ok[r]) continue;
               if (op[s] == PGPU_RED_MIN_I64) atomicMin(&sec[k[r]], id[r]);
               else atomicMax(&sec[k[r]], id[r]);
-            }
-          }
-        }
-      }
-    }
-    };
-    if (hot_on) walk(std::integral_constant<int, 8>{}, std::true_type{});
-    else walk(std::integral_constant<int, R>{}, std::false_type{});
-    if (hot_on) {  // the hot keys' register partials: one LDS update per key and wave
-#pragma unroll
-      for (int h = 0; h < HK; ++h) {
-        if (hk[h] == 0xFFFFFFFFu) continue;
-        const int c = wave_sum_i32((int)hc[h]);
-        if (c == 0) continue;
-        if (lane == 0) atomicAdd(&cnt[hk[h]], (uint32_t)c);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          if (op[s] == PGPU_RED_SUM_I64 || op[s] == PGPU_RED_SUM_F64) {
-            const int64_t t = wave_sum_i64(hs[h]);
-            if (lane == 0) atomicAdd((unsigned long long*)(base + soff[s]) + hk[h], (unsigned long long)t);
-          } else {
-            uint32_t t = hm[h][s];
-            for (int o = 32; o > 0; o >>= 1) {
-              const uint32_t x = (uint32_t)__shfl_xor((int)t, o, 64);
-              t = op[s] == PGPU_RED_MIN_I64 ? min(t, x) : max(t, x);
-            }
-            uint32_t* sec = (uint32_t*)(base + soff[s]);
-            if (lane == 0) {
-              if (op[s] == PGPU_RED_MIN_I64) atomicMin(&sec[hk[h]], t);
-              else atomicMax(&sec[hk[h]], t);
             }
           }
         }
@@ -5328,23 +5214,28 @@ __global__ __launch_bounds__(256, S2 ? 4 : 1) void andfsm_tile_kernel(DevParams 
 
 // One workgroup per segment: compose its tiles' maps in order and write numDocs + H (from state 0) -- the
 // reference's numEntriesScannedInFilter of the segment -- into pinned host memory.
-__global__ __launch_bounds__(256) void andfsm_segment_kernel(DevParams p, const uint32_t* fn, int64_t* out) {
-  __shared__ uint32_t s_n[256];
-  __shared__ uint64_t s_h[256][4];
+// (1024 threads: a 2^25-doc segment's 16,384 tile maps are 16 sequential compositions per thread, then a 10-level
+// tree -- 256 threads left a 64-long dependent chain of loads per thread, 44 us per query on config 5)
+#define FSM_SEG_THREADS 1024
+__global__ __launch_bounds__(FSM_SEG_THREADS) void andfsm_segment_kernel(DevParams p, const uint32_t* fn, int64_t* out) {
+  __shared__ uint32_t s_n[FSM_SEG_THREADS];
+  __shared__ uint64_t s_h[FSM_SEG_THREADS][4];
   const int seg = blockIdx.x, t = threadIdx.x;
   const int nt = cld(&p.segs[seg].ntiles), t0 = cld(&p.segs[seg].tile_begin);
-  const int per = (nt + 255) / 256;
+  const int per = (nt + FSM_SEG_THREADS - 1) / FSM_SEG_THREADS;
   uint32_t nxt = 0xE4u;  // identity: state s -> s
   uint64_t h[4] = {0, 0, 0, 0};
   for (int i = t * per; i < min(nt, (t + 1) * per); ++i) {
-    const uint32_t* f = fn + (size_t)(t0 + i) * PGPU_ANDFSM_WORDS;
-    const uint32_t rn = f[0];
+    const uint32_t* f = fn + (size_t)(t0 + i) * PGPU_ANDFSM_WORDS;  // (32-B records: both loads independent)
+    const u32x4 a = *(const u32x4*)f;
+    const uint32_t f4 = f[4];
+    const uint32_t rn = a.x, hv[4] = {a.y, a.z, a.w, f4};
     uint32_t nn = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int mid = (int)((nxt >> (2 * s)) & 3u);
       nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
-      h[s] += f[1 + mid];
+      h[s] += mid == 0 ? hv[0] : mid == 1 ? hv[1] : mid == 2 ? hv[2] : hv[3];
     }
     nxt = nn;
   }
@@ -5352,7 +5243,7 @@ __global__ __launch_bounds__(256) void andfsm_segment_kernel(DevParams p, const 
 #pragma unroll
   for (int s = 0; s < 4; ++s) s_h[t][s] = h[s];
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
+  for (int o = 1; o < FSM_SEG_THREADS; o <<= 1) {
     if ((t & (2 * o - 1)) == 0) {
       const uint32_t ln = s_n[t], rn = s_n[t + o];
       uint32_t nn = 0;
@@ -5616,17 +5507,21 @@ static hipError_t rk_attr(size_t lds_bytes) {
   else if (p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rprog<2, 20>), g, b, dyn_smem, st, p);
   else hipLaunchKernelGGL((query_kernel_rprog<2, 24>), g, b, dyn_smem, st, p);
 }
-// (fused exact statistics: rd_planes = the first leaf's planes held (12 / 16), rs_vplanes = the second's (20 / 24))
+// (fused exact statistics: rd_planes = the first leaf's planes held (10 / 12 / 16), rs_vplanes = the second's (20 / 24))
 template <int M>
 [[maybe_unused]] static void rf_launch(const DevParams& p, int grid, size_t dyn_smem, hipStream_t st) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
-  if (p.rd_planes <= 12 && p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rfsm<M, 12, 20>), g, b, dyn_smem, st, p);
+  if (p.rd_planes <= 10 && p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rfsm<M, 10, 20>), g, b, dyn_smem, st, p);
+  else if (p.rd_planes <= 12 && p.rs_vplanes <= 20) hipLaunchKernelGGL((query_kernel_rfsm<M, 12, 20>), g, b, dyn_smem, st, p);
   else hipLaunchKernelGGL((query_kernel_rfsm<M, 16, 24>), g, b, dyn_smem, st, p);
 }
 template <int M>
 [[maybe_unused]] static hipError_t rf_attrs(size_t lds_bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 12, 20>,
+  hipError_t e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 10, 20>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 12, 20>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_bytes);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)query_kernel_rfsm<M, 16, 24>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_bytes);
@@ -5652,15 +5547,15 @@ template <int M>
         hipLaunchKernelGGL((query_kernel_cand<M>), dim3(grid), dim3(PGPU_DIRECT_THREADS), dyn_smem, st, p);     \
       else                                                                                                      \
         return hipErrorInvalidValue;                                                                            \
+    } else if (p.direct == 8) {                                                                                 \
+      if constexpr (M != PGPU_MODE_PART) rf_launch<M>(p, grid, dyn_smem, st);                                   \
+      else return hipErrorInvalidValue;                                                                         \
     } else if (p.direct >= 3) {                                                                                 \
       if constexpr (M == PGPU_MODE_AGG) {                                                                       \
         if (p.direct == 3) rs_launch(p, grid, dyn_smem, st);                                                    \
         else rp_launch(p, grid, dyn_smem, st);                                                                  \
       } else                                                                                                    \
         return hipErrorInvalidValue;                                                                            \
-    } else if (p.direct == 8) {                                                                                 \
-      if constexpr (M != PGPU_MODE_PART) rf_launch<M>(p, grid, dyn_smem, st);                                   \
-      else return hipErrorInvalidValue;                                                                         \
     } else if (p.direct == 2) {                                                                                 \
       if (p.rd_pfx) rd_launch<M, PGPU_PFX_PLANES>(p, grid, dyn_smem, st);                                       \
       else rd_launch<M, 0>(p, grid, dyn_smem, st);                                                              \
@@ -6132,7 +6027,7 @@ hipError_t pgpu_launch_andfsm(const DevParams& p, bool s2, uint32_t* fn, int64_t
     if (s2) hipLaunchKernelGGL(andfsm_tile_kernel<true>, g, dim3(256), 0, st, p, fn);
     else hipLaunchKernelGGL(andfsm_tile_kernel<false>, g, dim3(256), 0, st, p, fn);
   }
-  hipLaunchKernelGGL(andfsm_segment_kernel, dim3(p.nseg), dim3(256), 0, st, p, (const uint32_t*)fn, out);
+  hipLaunchKernelGGL(andfsm_segment_kernel, dim3(p.nseg), dim3(FSM_SEG_THREADS), 0, st, p, (const uint32_t*)fn, out);
   return hipGetLastError();
 }
 

@@ -432,7 +432,13 @@ int pgpu_node_query_topk(pgpu_node* node, const pgpu_query_desc* const* descs, c
 }
 
 int pgpu_node_submit(pgpu_node* node, const pgpu_query_desc* const* descs, pgpu_node_pending** out_query) {
+  return pgpu_node_submit_expr(node, descs, nullptr, nullptr, out_query);
+}
+
+int pgpu_node_submit_expr(pgpu_node* node, const pgpu_query_desc* const* descs, const pgpu_expr_node* const* exprs,
+                          const int32_t* num_nodes, pgpu_node_pending** out_query) {
   if (!node || !descs || !out_query) return nfail(PGPU_E_INVALID, "null argument");
+  if (exprs && !num_nodes) return nfail(PGPU_E_INVALID, "filter expressions without their node counts");
   std::lock_guard<std::mutex> lk(node->mu);
   const size_t n = node->devices.size();
   // one table layout on every device: the docs of the whole node bound the integer sums, and a split or hash
@@ -495,6 +501,9 @@ int pgpu_node_submit(pgpu_node* node, const pgpu_query_desc* const* descs, pgpu_
     const uint64_t bytes = pgpu_table_bytes(&L[i]);
     const hipError_t e = nq->tables[i].ensure(bytes);
     if (e != hipSuccess) rc = nfail(PGPU_E_HIP, "node table on device %d: %s", node->devices[i], hipGetErrorString(e));
+    else if (exprs && exprs[i])  // the filter planned per segment inside the library from its literals
+      rc = pgpu_query_launch_expr(node->ctxs[i], &qs[i], exprs[i], num_nodes[i], node->streams[i], nq->tables[i].p,
+                                  bytes, &nq->qq[i]);
     else rc = pgpu_query_launch(node->ctxs[i], &qs[i], node->streams[i], nq->tables[i].p, bytes, &nq->qq[i]);
   }
   if (rc) {

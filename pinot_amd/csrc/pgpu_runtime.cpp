@@ -2632,10 +2632,6 @@ int pack_query(pgpu_context* ctx, const pgpu_query_desc* q, const pgpu_table_lay
   // restores the default policy
   static const bool direct_nt = !(getenv("PGPU_DIRECT_NT") && atoi(getenv("PGPU_DIRECT_NT")) == 0);
   if (direct_nt) p.flags |= PGPU_FLAG_NT;
-  {
-    const bool no_hot = getenv("PGPU_NO_HOTKEYS") && atoi(getenv("PGPU_NO_HOTKEYS")) != 0;  // per query (tests)
-    if (no_hot) p.flags |= PGPU_FLAG_NOHOT;
-  }
   for (int s = 0; s < L.num_sections; ++s) p.sec_op[s] = L.section_op[s];
   uint32_t stride = 1;
   uint64_t stride64 = 1;
@@ -3189,7 +3185,7 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
       int g = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, p.total_tiles / 16));
       if (g >= 8) g &= ~7;
       p.direct = 8;
-      p.rd_planes = small ? 12 : 16;
+      p.rd_planes = small ? (b0 <= 10 ? 10 : 12) : 16;
       p.rs_vplanes = small ? 20 : 24;
       p.rd_pfx = 0;
       p.dslots = 0;

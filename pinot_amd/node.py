@@ -86,15 +86,25 @@ class GpuNode:
             if len(self._globs) >= 16:  # (bounded: the oldest segment set's entry goes)
                 self._globs.pop(next(iter(self._globs)))
             self._globs[gkey] = globs
+        # numeric filters go to the library as expression programs (planned per segment in C++, as the
+        # one-process-per-GPU path's pgpu_query_launch_expr does); otherwise every segment's tree is planned here
+        exprs = [pm.filter_expr(query, segs) for pm, segs in zip(self.planners, segments_by_device)]
+        use_expr = all(e is not None for e in exprs)
         keep, descs = [], []
         for pm, segs in zip(self.planners, segments_by_device):
-            desc, k, _ = pm.build_desc(query, segs)
+            desc, k, _ = pm.build_desc(query, segs, plan_filters=not use_expr)
             keep.append((desc, k))
             descs.append(desc)
         arr = (C.POINTER(QueryDesc) * len(descs))(*[C.pointer(d) for d in descs])
         L0 = self.planners[0].layout(descs[0])
         h = C.c_void_p()
-        _lib.check(self._lib.pgpu_node_submit(self.handle, arr, C.byref(h)))
+        if use_expr:
+            earr = (C.POINTER(_lib.ExprNode) * len(exprs))(*[C.cast(e[0], C.POINTER(_lib.ExprNode)) for e in exprs])
+            narr = (C.c_int32 * len(exprs))(*[int(e[1]) for e in exprs])
+            keep.append((exprs, earr, narr))
+            _lib.check(self._lib.pgpu_node_submit_expr(self.handle, arr, earr, narr, C.byref(h)))
+        else:
+            _lib.check(self._lib.pgpu_node_submit(self.handle, arr, C.byref(h)))
         return _NodePending(query, globs, keep, arr, L0, h, len(everything), segments_by_device)
 
     def collect(self, p: "_NodePending", min_cap: int = 0) -> QueryResult:

@@ -17,9 +17,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the kernels inside the query's timed region (pgpu_runtime.cpp: HIP events ev0..ev1): leaf bitmaps, the query kernel
-# or the partitioned group-by's phases (its sampling and planning passes included)
+# or the partitioned group-by's phases (its sampling and planning passes included), the exact filter statistic's
 TIMED = ("rawpred_kernel", "mvpred_kernel", "invexp_kernel", "rkey_ctab_kernel", "progbits_kernel", "query_kernel", "part_scan_kernel",
-         "part_plan_kernel", "part_reduce_kernel")
+         "part_plan_kernel", "part_reduce_kernel", "andfsm_tile_kernel", "andfsm_segment_kernel", "leafbits_kernel")
 
 
 def _base(name: str) -> str:

@@ -151,7 +151,7 @@ def test_node_queries_in_flight(monkeypatch, rccl):
     if rccl:
         monkeypatch.setenv("PGPU_NODE_FORCE_RCCL", "1")
     segs = _segments(400)
-    with GpuNode([0], min_server_group_trim_size=20) as node:
+    with GpuNode([0]) as node:
         gs = [GpuSegment(node.contexts[0], s) for s in segs]
         try:
             qs = [parse_sql(sql) for sql in QUERIES]

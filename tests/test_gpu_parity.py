@@ -836,13 +836,10 @@ def test_partitioned_groupby_shared_dictionary(gpu_ctx, dist):
             g.release()
 
 
-@pytest.mark.parametrize("hot", ["on", "off"])
-def test_partitioned_groupby_hot_keys_frame_of_reference(gpu_ctx, monkeypatch, hot):
+def test_partitioned_groupby_skewed_frame_of_reference(gpu_ctx):
     """Config 4's phase-2 shape -- a 64K-value shared dictionary read through its frame-of-reference image in LDS --
-    under skewed keys: the split hot partition's workgroups accumulate their sampled hottest keys in registers
-    (PGPU_NO_HOTKEYS=1 turns that off).  Every group equals the oracle's, SUM / MAX / MIN / COUNT / AVG, bit-exact."""
-    if hot == "off":
-        monkeypatch.setenv("PGPU_NO_HOTKEYS", "1")
+    under skewed keys, whose hot partition is split over several phase-2 workgroups by record ranges.  Every group
+    equals the oracle's, SUM / MAX / MIN / COUNT / AVG, bit-exact."""
     rng = np.random.default_rng(97)
     # 64K distinct values over 2^20 (config 4's metric): the dictionary misses LDS, its frame-of-reference image fits
     mvals = (np.sort(rng.choice(1 << 20, 65_536, replace=False)) - (1 << 19)).astype(np.int32)
@@ -853,7 +850,7 @@ def test_partitioned_groupby_hot_keys_frame_of_reference(gpu_ctx, monkeypatch, h
         k = np.where(rng.random(n) < 0.7, rng.zipf(1.1, n) % 4096, rng.integers(0, 300_000, n))
         m = mvals[rng.integers(0, len(mvals), n)]
         cols = {"k": (PGPU_INT, k.astype(np.int32)), "m": (PGPU_INT, m)}
-        segs.append(build_segment(f"hot{hot}{i}", cols, sorted_columns=()))
+        segs.append(build_segment(f"skf{i}", cols, sorted_columns=()))
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
     try:
         for sql in ("SELECT k, SUM(m), MAX(m), COUNT(*) FROM t GROUP BY k ORDER BY SUM(m) DESC LIMIT 50",
