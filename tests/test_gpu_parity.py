@@ -863,3 +863,32 @@ def test_partitioned_groupby_skewed_frame_of_reference(gpu_ctx):
     finally:
         for g in gs:
             g.release()
+
+
+def test_prepared_submission_reuse(gpu_ctx):
+    """The same query object re-submitted over the same segments reuses its prepared descriptor (GpuPlanMaker's
+    prepared submissions): three in flight, identical results; an option change or a released segment re-plans."""
+    rng = np.random.default_rng(515)
+    segs = [_random_segment(rng, 50_000 + 100 * i, f"prep{i}") for i in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        q = parse_sql("SELECT b, COUNT(*), SUM(m) FROM t WHERE c < 1500 AND g > 5 GROUP BY b ORDER BY SUM(m) DESC LIMIT 5")
+        ref = _oracle(q, segs)
+        pm = GpuPlanMaker(gpu_ctx)
+        pending = [pm.submit(q, gs) for _ in range(3)]
+        assert len(pm._prepared) == 1
+        results = [pm.collect(p) for p in pending]
+        for r in results:
+            _assert_same(r, ref)
+            assert r.rows == results[0].rows
+        pm.exact_filter_stats = True
+        exact = pm.collect(pm.submit(q, gs))
+        assert len(pm._prepared) == 2 and exact.stats.filter_stats_exact
+        _assert_same(exact, ref)
+        gs[2].release()
+        assert not pm._prepared
+        gs = gs[:2]
+        _assert_same(pm.collect(pm.submit(q, gs)), _oracle(q, segs[:2]))
+    finally:
+        for g in gs:
+            g.release()
