@@ -432,6 +432,7 @@ struct DevParams {
   int32_t total_units;            // query_kernel_rkey: (segment, 65,536-doc container key) units; query_kernel_cand:
                                   // (segment, container) units
   int32_t rk_leaves;              // query_kernel_rkey: leaf images per LDS buffer (max BITS slots of a segment)
+  int32_t rk_ids;                 // query_kernel_rkey: stream the aggregated 16-bit columns' packed ids, gather values
   const struct InvLeafX* invx;    // query_kernel_rkey: the inverted leaves (containers read per unit)
   const struct DevContainer* rk_ctab;  // query_kernel_rkey: container record per (leaf, id, key) (rkey_ctab_kernel)
   const uint32_t* cand_ct;        // query_kernel_cand: per unit {segment, its container's index in InvLeafX::ct

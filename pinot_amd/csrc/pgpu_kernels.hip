@@ -392,6 +392,14 @@ FI void hbm_lane_words(const uint32_t* fwd, int tile_in_seg, uint32_t (&w)[B]) {
   for (int k = 0; k < B; ++k) w[k] = bswap32(src[k]);
 }
 
+// ... raw (big-endian as stored: a caller unpacks later), for loads issued ahead of their use
+template <int B>
+FI void hbm_lane_raw(const uint32_t* fwd, int tile_in_seg, uint32_t (&w)[B]) {
+  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
+#pragma unroll
+  for (int k = 0; k < B; ++k) w[k] = src[k];
+}
+
 template <int B>
 FI void decode_b(const uint32_t* region, const uint32_t* fwd, int tile_in_seg, uint32_t (&ids)[32]) {
   uint32_t w[B];
@@ -3535,7 +3543,27 @@ FI bool unit_next(const DevParams& p, UnitCursor& c, int wave, int* seg, int* ti
   }
   return false;
 }
-template <int NA, int NV>
+// IDS: the aggregated columns' packed 16-bit dict ids stream instead of their value planes (16 words per lane and
+// tile instead of vbits planes); the matched docs' ids go to the wave's LDS queue and their values are gathered from
+// the (L2-resident) dictionaries when it fills (sliced_flush) -- fewer bytes than the value planes when few docs match.
+// Every aggregation's column of an IDS launch is a 16-bit fixed-bit dictionary column (the runtime checks).
+// The lane's matched docs' ids (docs 2k, 2k + 1 are the MSB-first halves of big-endian word k) into q[at, ...).
+// The word is picked with constant register indices: a register array indexed by a doc number would live in
+// scratch, and walking all 16 words unrolled per aggregation costs ~100 VGPRs.
+FI uint32_t pick16(const uint32_t (&w)[16], uint32_t k) {
+  uint32_t x = 0;  // (an OR of masked words: a select tree gets folded back into an indexed scratch load)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x |= w[j] & (0u - (uint32_t)(k == (uint32_t)j));
+  return x;
+}
+FI void packed16_enqueue(const uint32_t (&w)[16], uint32_t mm, uint16_t* q, int at) {
+  for (uint32_t left = mm; left; left &= left - 1) {
+    const uint32_t i = (uint32_t)__builtin_ctz(left);
+    const uint32_t x = bswap32(pick16(w, i >> 1));
+    q[at++] = (uint16_t)((i & 1u) ? (x & 0xFFFFu) : (x >> 16));
+  }
+}
+template <int NA, int NV, bool IDS = false>
 __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevParams p) {
   constexpr int NW = PGPU_DIRECT_WAVES, RD = PGPU_RDIRECT_DEPTH, NT = PGPU_DIRECT_THREADS;
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
@@ -3589,8 +3617,13 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
     int sseg, stile;                                                                                         \
     if (unit_next(p, ci, wave, &sseg, &stile)) {                                                             \
       const DevColumn* pc = p.cols + cld(&p.segs[sseg].col_begin);                                           \
-      rs_load_planes(cld(&pc[vc0].vsliced), cld(&pc[vc0].vbits), stile, xv[S][0]);                          \
-      if constexpr (NA > 1) rs_load_planes(cld(&pc[vc1].vsliced), cld(&pc[vc1].vbits), stile, xv[S][NA - 1]); \
+      if constexpr (IDS) {                                                                                   \
+        hbm_lane_raw<NV>(cld(&pc[vc0].fwd), stile, xv[S][0]);                                               \
+        if constexpr (NA > 1) hbm_lane_raw<NV>(cld(&pc[vc1].fwd), stile, xv[S][NA - 1]);                     \
+      } else {                                                                                               \
+        rs_load_planes(cld(&pc[vc0].vsliced), cld(&pc[vc0].vbits), stile, xv[S][0]);                        \
+        if constexpr (NA > 1) rs_load_planes(cld(&pc[vc1].vsliced), cld(&pc[vc1].vbits), stile, xv[S][NA - 1]); \
+      }                                                                                                      \
       ++have;                                                                                                \
     }                                                                                                        \
   } while (0)
@@ -3602,9 +3635,14 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
   int64_t vmin0 = 0, vmin1 = 0, vbytes = 0;
   int nid[PGPU_PREBITS] = {0, 0, 0, 0}, npairs = 0;  // ids per leaf, (leaf, id) pairs of the segment
   int slot = 0;
+  int sn = 0;  // IDS: ids queued per aggregation (sliced_flush)
   for (int u = u0; u < u1; ++u) {
     const int seg = unit_segment(p, u);
     if (seg != cseg) {
+      if (IDS && sn) {  // the queued ids are the old segment's: gather them from its dictionaries first
+        sliced_flush(p, cv, la, ss, sn);
+        sn = 0;
+      }
       cseg = seg;
       load_seg(p, cseg, ss);
       T = cld(&ss.sg->ptt);
@@ -3618,7 +3656,7 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
       vmin1 = vc1 >= 0 ? cld(&ss.cols[vc1].vmin) : 0;
       vbytes = 0;
       for (int a = 0; a < p.nagg; ++a)
-        if (p.aggs[a].fn != PGPU_AGG_COUNT) vbytes += (int64_t)WT * (p.aggs[a].col == vc0 ? vb0 : vb1) / 8;
+        if (p.aggs[a].fn != PGPU_AGG_COUNT) vbytes += (int64_t)WT * (IDS ? 16 : (p.aggs[a].col == vc0 ? vb0 : vb1)) / 8;
       negm = 0;  // leaves of NOT IN / <> predicates: complemented within the segment
       npairs = 0;
       for (int j = 0; j < nbits; ++j) {
@@ -3753,8 +3791,35 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
       for (int s = 0; s < RD; ++s) {
         if (s != slot) continue;
         if (any) {
-          rs_fold<NV>(p, cv, la, xv[s][0], mm, vb0, vmin0, vc0);
-          if constexpr (NA > 1) rs_fold<NV>(p, cv, la, xv[s][NA - 1], mm, vb1, vmin1, vc1);
+          if constexpr (IDS) {
+            // the matched docs' ids into the queue, one sub-queue per aggregation (a tile with more matches than a
+            // sub-queue holds goes in quarters of 16 lanes), gathered when full
+            constexpr int cap = PGPU_CQ_CAP / 2;
+            const int nm_all = wave_sum_i32(__popc(mm));
+            const int parts = nm_all <= cap ? 1 : 4;
+            for (int part = 0; part < parts; ++part) {
+              const uint32_t mp = parts == 1 ? mm : ((lane >> 4) == part ? mm : 0u);
+              const int cnt = __popc(mp);
+              const int ex = wave_excl_scan(cnt);
+              const int nm = __builtin_amdgcn_readlane(ex + cnt, 63);
+              if (nm == 0) continue;
+              if (sn + nm > cap) {
+                sliced_flush(p, cv, la, ss, sn);
+                sn = 0;
+              }
+              int q = 0;
+              for (int a = 0; a < p.nagg; ++a) {
+                if (p.aggs[a].fn == PGPU_AGG_COUNT) continue;
+                uint16_t* qq = cv.queue + q++ * cap;
+                if (p.aggs[a].col == vc0) packed16_enqueue(xv[s][0], mp, qq, sn + ex);
+                else packed16_enqueue(xv[s][NA - 1], mp, qq, sn + ex);
+              }
+              sn += nm;
+            }
+          } else {
+            rs_fold<NV>(p, cv, la, xv[s][0], mm, vb0, vmin0, vc0);
+            if constexpr (NA > 1) rs_fold<NV>(p, cv, la, xv[s][NA - 1], mm, vb1, vmin1, vc1);
+          }
           if ((p.flags & PGPU_FLAG_STATS) && lane == 0) dense_bytes += vbytes;
         }
         --have;
@@ -3765,6 +3830,7 @@ __global__ __launch_bounds__(PGPU_DIRECT_THREADS) void query_kernel_rkey(DevPara
     }
   }
 #undef RK_ISSUE
+  if (IDS && sn && !rk_stop) sliced_flush(p, cv, la, ss, sn);
   {
     const int64_t lm = wave_sum_i64((int64_t)lane_matched);
     PROF_ADD(pf, PGPU_P_C_TOTAL, t_start);
@@ -4148,12 +4214,6 @@ FI void pscan_flush(const DevParams& p, uint32_t* ht, const uint32_t* ring,
 // bits and there is no filter -- the next step's tile words are loaded a step ahead, raw, into VGPRs (phase 1 runs
 // two waves per SIMD, bound by its LDS rings, so the registers are free), and the step's own HBM latency overlaps
 // the previous step's inserts, flush and barriers.
-template <int B>
-FI void hbm_lane_raw(const uint32_t* fwd, int tile_in_seg, uint32_t (&w)[B]) {
-  const GAS uint32_t* src = (const GAS uint32_t*)fwd + ((size_t)tile_in_seg * 64 + opaque_lane()) * B;
-#pragma unroll
-  for (int k = 0; k < B; ++k) w[k] = src[k];
-}
 template <bool COUNT, int KB = 0, int VB = 0>
 __global__ __launch_bounds__(PGPU_PSCAN_THREADS, 2) void part_scan_kernel(DevParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn_smem[];
@@ -5470,9 +5530,9 @@ static hipError_t rp_attr(size_t lds_bytes) {
   return hipFuncSetAttribute((const void*)query_kernel_rprog<NA, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds_bytes);
 }
-template <int NA, int NV>
+template <int NA, int NV, bool IDS = false>
 static hipError_t rk_attr(size_t lds_bytes) {
-  return hipFuncSetAttribute((const void*)query_kernel_rkey<NA, NV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  return hipFuncSetAttribute((const void*)query_kernel_rkey<NA, NV, IDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds_bytes);
 }
 [[maybe_unused]] static hipError_t rp_attrs(size_t lds_bytes) {
@@ -5482,6 +5542,8 @@ static hipError_t rk_attr(size_t lds_bytes) {
   if (e == hipSuccess) e = rk_attr<2, 16>(lds_bytes);
   if (e == hipSuccess) e = rk_attr<2, 20>(lds_bytes);
   if (e == hipSuccess) e = rk_attr<2, 24>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<1, 16, true>(lds_bytes);
+  if (e == hipSuccess) e = rk_attr<2, 16, true>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<1, 24>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 16>(lds_bytes);
   if (e == hipSuccess) e = rp_attr<2, 20>(lds_bytes);
@@ -5494,6 +5556,11 @@ static hipError_t rk_attr(size_t lds_bytes) {
   const dim3 g(grid), b(PGPU_DIRECT_THREADS);
   if (p.direct == 5) {  // the inverted leaves' containers read into LDS per unit (query_kernel_rkey)
     const dim3 kb(PGPU_DIRECT_THREADS);
+    if (p.rk_ids) {  // the aggregated columns' packed 16-bit ids, values gathered for the matched docs
+      if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rkey<1, 16, true>), g, kb, dyn_smem, st, p);
+      else hipLaunchKernelGGL((query_kernel_rkey<2, 16, true>), g, kb, dyn_smem, st, p);
+      return;
+    }
     if (p.rd_planes <= 1 && p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rkey<1, 16>), g, kb, dyn_smem, st, p);
     else if (p.rd_planes <= 1) hipLaunchKernelGGL((query_kernel_rkey<1, 24>), g, kb, dyn_smem, st, p);
     else if (p.rs_vplanes <= 16) hipLaunchKernelGGL((query_kernel_rkey<2, 16>), g, kb, dyn_smem, st, p);

@@ -3069,6 +3069,19 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
         p.direct = 5;
         p.total_units = units;
         p.rk_leaves = std::max(1, maxbits);
+        // the aggregated columns' packed 16-bit ids instead of their value planes, values gathered per matched doc
+        // (PGPU_RKEY_IDS, read per plan): every value column a 16-bit dictionary column, <= 2
+        // non-COUNT aggregations (one queue half each)
+        int nq = 0;
+        for (int a = 0; a < p.nagg; ++a) nq += p.aggs[a].fn != PGPU_AGG_COUNT;
+        bool ids = nq >= 1 && nq <= 2;
+        for (const DevSeg& ds : pk.segs)
+          for (int c = 0; c < nv && ids && ds.ntiles; ++c) {
+            const DevColumn& vc = pk.cols[ds.col_begin + vcols[c]];
+            ids = vc.kind == PGPU_COL_FIXED_BIT && vc.bits == 16 && vc.dict != nullptr && vc.fwd != nullptr;
+          }
+        const char* ev = getenv("PGPU_RKEY_IDS");
+        p.rk_ids = ids && ev && atoi(ev) != 0 ? 1 : 0;
         const int per_cu = (int)std::min<size_t>(nv > 1 && vbmax > 20 ? 2 : 3, PGPU_LDS_LIMIT / kdyn);
         int gk = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, std::max(1, units / 2));
         if (gk >= 8) gk &= ~7;

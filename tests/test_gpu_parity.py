@@ -892,3 +892,27 @@ def test_prepared_submission_reuse(gpu_ctx):
     finally:
         for g in gs:
             g.release()
+
+
+@pytest.mark.parametrize("ids", ["planes", "ids"])
+def test_container_keyed_kernel_value_sources(gpu_ctx, monkeypatch, ids):
+    """Config 3's query on the workload's own segments (ragged sizes) through query_kernel_rkey with either value
+    source: the metrics' value planes, or their packed 16-bit ids with the values gathered per matched doc
+    (PGPU_RKEY_IDS=1) -- SUM, MIN, MAX and AVG against the oracle."""
+    from oracle.segment_writer import pack_fixed_bit
+    from pinot_amd.synth import WORKLOADS, build_segment_cpu
+    monkeypatch.setenv("PGPU_RKEY_IDS", "1" if ids == "ids" else "0")
+    w = WORKLOADS["bitmap5"]
+    segs = [build_segment_cpu(w, s, (1 << 18) + 4099 * s, pack_fixed_bit) for s in range(3)]
+    gs = [GpuSegment(gpu_ctx, s) for s in segs]
+    try:
+        where = w.sql[w.sql.index(" WHERE "):]
+        for sql in (w.sql, "SELECT SUM(m1), MAX(m2)" + " FROM bitmap5" + where,
+                    "SELECT MIN(m1), AVG(m1)" + " FROM bitmap5" + where, "SELECT COUNT(*), SUM(m2) FROM bitmap5" + where):
+            q = parse_sql(sql)
+            res = _gpu(gpu_ctx, q, gs)
+            assert res.stats.kernel_variant == _lib.PGPU_KV_RKEY, sql
+            _assert_same(res, _oracle(q, segs))
+    finally:
+        for g in gs:
+            g.release()
