@@ -79,9 +79,13 @@ def main():
     cal_csv = os.path.join(src, "pmc_cal", "run_counter_collection.csv")
     if os.path.exists(cal_csv):
         cal_fetch, _ = per_launch(cal_csv)
-        b = bench_json(os.path.join(src, "pmc_cal.log"))
+        full = os.path.join(src, "pmc_cal.json")  # bench.py --full-out: the full records (the stdout line is compact)
+        if os.path.exists(full):
+            rl = json.load(open(full))["headline"]["roofline"]
+        else:
+            b = bench_json(os.path.join(src, "pmc_cal.log"))
+            rl = b["roofline"] if b else {}
         # the filter stream's known bytes: the kernel's read model (the byte model's full first-leaf stream)
-        rl = b["roofline"] if b else {}
         known = (rl.get("bytes_read_breakdown") or {}).get("dense_stream") or \
             (rl.get("bytes_breakdown") or {}).get("forward_full")
         if known:
