@@ -2809,6 +2809,29 @@ static int launch_impl(pgpu_context* ctx, const pgpu_query_desc* q, void* stream
   rc = pack_query(ctx, q, L, pk, p);
   host_timing().add(2, tp0, HostTiming::us());
   if (rc) return rc;
+  if (pk.leaf_words > 0 && !pk.legacy_range) {
+    // the reference's numEntriesScannedInFilter requested, but every segment's program is one whose GPU count IS
+    // the reference's (scans driven by next(): OR / NOT trees, index merges then applyAnd, a lone multi-value scan;
+    // pgpu_filter_count_is_reference): no leaf bitmaps, no copy to the host, no replay
+    bool all_ref = true;
+    for (int s = 0; s < q->num_segments && all_ref; ++s) {
+      const pgpu_segment_plan& sp = q->segments[s];
+      all_ref = pgpu_filter_count_is_reference(sp.filter, sp.num_filter_nodes);
+      int nmv = 0;
+      for (int i = 0; i < sp.num_filter_nodes && all_ref; ++i) {
+        const pgpu_filter_node& nd = sp.filter[i];
+        if (nd.op != PGPU_F_SCAN || nd.column < 0 || nd.column >= q->num_columns) continue;
+        const int32_t slot = sp.column_map[nd.column];
+        nmv += slot >= 0 && slot < (int32_t)sp.segment->cols.size() && sp.segment->cols[slot].kind == PGPU_COL_MV;
+      }
+      all_ref = all_ref && (nmv == 0 || sp.num_filter_nodes == 1);
+    }
+    const bool always_replay = getenv("PGPU_ALWAYS_REPLAY") && atoi(getenv("PGPU_ALWAYS_REPLAY")) != 0;  // (per plan: tests)
+    if (all_ref && !always_replay) {
+      pk.leaf_words = 0;
+      for (DevSeg& ds : pk.segs) ds.leaf_len = 0;
+    }
+  }
   HIP_TRY(hipSetDevice(ctx->device));
 
   // mode and LDS geometry: consumer areas, optional LDS group table, then as many ring slots as fit

@@ -410,11 +410,11 @@ def test_index_only_programs_value_planes_vs_oracle(gpu_ctx, monkeypatch, qi, n,
 
 
 @pytest.mark.parametrize("qi", [0, 1, 2])
-def test_index_only_programs_exact_filter_stats(gpu_ctx, qi):
-    """Index-only programs with the reference's numEntriesScannedInFilter requested: the replay reads the inverted
-    leaves as expanded bitmaps, so the container-keyed kernel (which expands nothing) must not be chosen; the
-    statistic and the results equal the oracle's iterator figures.  Without the request the same programs take
-    query_kernel_rkey."""
+def test_index_only_programs_exact_filter_stats(gpu_ctx, monkeypatch, qi):
+    """Index-only programs with the reference's numEntriesScannedInFilter requested.  Their GPU count is the
+    reference's (no scan leaf), so no replay runs and the container-keyed kernel is kept; forcing the leaf-bitmap
+    replay (PGPU_ALWAYS_REPLAY=1) reads the inverted leaves as expanded bitmaps, so the container-keyed kernel (which
+    expands nothing) must then not be chosen.  Both give the oracle's iterator figure."""
     rng = np.random.default_rng(4100 + qi)
     segs = [_index_segment(rng, 70_001 + 2048 * i, f"ipx{i}") for i in range(2)]
     gs = [GpuSegment(gpu_ctx, s) for s in segs]
@@ -422,16 +422,20 @@ def test_index_only_programs_exact_filter_stats(gpu_ctx, qi):
         q = parse_sql(RPROG_QUERIES[qi])
         plain = _gpu(gpu_ctx, q, gs)
         exact = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
+        monkeypatch.setenv("PGPU_ALWAYS_REPLAY", "1")
+        replay = _gpu(gpu_ctx, q, gs, exact_filter_stats=True)
     finally:
         for g in gs:
             g.release()
     ref = _oracle(q, segs)
     assert plain.stats.kernel_variant == _lib.PGPU_KV_RKEY
-    assert exact.stats.kernel_variant != _lib.PGPU_KV_RKEY
-    assert exact.stats.filter_stats_exact
-    _assert_same(plain, ref)
-    _assert_same(exact, ref)
-    assert exact.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
+    assert exact.stats.kernel_variant == _lib.PGPU_KV_RKEY
+    assert replay.stats.kernel_variant != _lib.PGPU_KV_RKEY
+    for res in (plain, exact, replay):
+        _assert_same(res, ref)
+    for res in (exact, replay):
+        assert res.stats.filter_stats_exact
+        assert res.stats.num_entries_scanned_in_filter == ref.num_entries_scanned_in_filter
 
 
 @pytest.mark.parametrize("n", [2048, 70_001])
