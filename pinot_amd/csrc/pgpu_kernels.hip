@@ -2913,27 +2913,24 @@ FI void rf_tile_map(uint32_t m0, uint32_t m1, uint32_t* fn_tile) {
     nxt |= (uint32_t)st << (2 * s0);
     h[s0] = hh;
   }
+  // (two live states: 2 and 3 stay the identity with no hand-offs, so only states 0 and 1 are composed)
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t rn = (uint32_t)__shfl_down((int)nxt, o, 64);
-    uint32_t rh[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) rh[s] = (uint32_t)__shfl_down((int)h[s], o, 64);
+    const uint32_t r0 = (uint32_t)__shfl_down((int)h[0], o, 64), r1 = (uint32_t)__shfl_down((int)h[1], o, 64);
     if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
-      uint32_t nn = 0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int mid = (int)((nxt >> (2 * s)) & 3u);
-        nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
-        h[s] += mid == 0 ? rh[0] : mid == 1 ? rh[1] : mid == 2 ? rh[2] : rh[3];
-      }
-      nxt = nn;
+      const uint32_t m0 = nxt & 3u, m1 = (nxt >> 2) & 3u;  // (each 0 or 1)
+      h[0] += m0 ? r1 : r0;
+      h[1] += m1 ? r1 : r0;
+      nxt = (nxt & 0xF0u) | ((rn >> (2 * m0)) & 3u) | (((rn >> (2 * m1)) & 3u) << 2);
     }
   }
   if (lane == 0) {
     fn_tile[0] = nxt;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) fn_tile[1 + s] = h[s];
+    fn_tile[1] = h[0];
+    fn_tile[2] = h[1];
+    fn_tile[3] = 0u;
+    fn_tile[4] = 0u;
   }
 }
 
@@ -5285,19 +5282,30 @@ __global__ __launch_bounds__(FSM_SEG_THREADS) void andfsm_segment_kernel(DevPara
   const int per = (nt + FSM_SEG_THREADS - 1) / FSM_SEG_THREADS;
   uint32_t nxt = 0xE4u;  // identity: state s -> s
   uint64_t h[4] = {0, 0, 0, 0};
-  for (int i = t * per; i < min(nt, (t + 1) * per); ++i) {
-    const uint32_t* f = fn + (size_t)(t0 + i) * PGPU_ANDFSM_WORDS;  // (32-B records: both loads independent)
-    const u32x4 a = *(const u32x4*)f;
-    const uint32_t f4 = f[4];
-    const uint32_t rn = a.x, hv[4] = {a.y, a.z, a.w, f4};
-    uint32_t nn = 0;
+  // eight maps loaded before the first is composed: the loads overlap instead of one round trip per map
+  const int i1 = min(nt, (t + 1) * per);
+  for (int i0 = t * per; i0 < i1; i0 += 8) {
+    u32x4 a[8];
+    uint32_t f4[8];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int mid = (int)((nxt >> (2 * s)) & 3u);
-      nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
-      h[s] += mid == 0 ? hv[0] : mid == 1 ? hv[1] : mid == 2 ? hv[2] : hv[3];
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t* f = fn + (size_t)(t0 + min(i0 + j, i1 - 1)) * PGPU_ANDFSM_WORDS;  // (32-B records)
+      a[j] = *(const u32x4*)f;
+      f4[j] = f[4];
     }
-    nxt = nn;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i0 + j >= i1) break;
+      const uint32_t rn = a[j].x;
+      uint32_t nn = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int mid = (int)((nxt >> (2 * s)) & 3u);
+        nn |= ((rn >> (2 * mid)) & 3u) << (2 * s);
+        h[s] += mid == 0 ? a[j].y : mid == 1 ? a[j].z : mid == 2 ? a[j].w : f4[j];
+      }
+      nxt = nn;
+    }
   }
   s_n[t] = nxt;
 #pragma unroll
