@@ -4637,6 +4637,10 @@ struct RegionWalk {
   const DevParams* p;
   uint32_t q;
   int nwg, wave, nwaves;
+  // all: every wave walks every piece and the caller deals each piece's chunks out across the waves.  A split
+  // partition's share is a few large pieces (Zipf(1.1): ~2 phase-1 regions of ~2.7 M records per workgroup), so
+  // dealing whole pieces to waves left 14 of 16 waves idle; an unsplit partition's are many small pieces, dealt whole.
+  bool all;
   uint64_t r0, r1;     // this workgroup's record range in the partition
   uint64_t run;        // records of the regions before the current chunk of 64
   int wb;              // current chunk's first region
@@ -4647,8 +4651,8 @@ struct RegionWalk {
   uint32_t n;          // out: records
   int visited;
   FI RegionWalk(const DevParams& pp, uint32_t qq, int j, int ns, int nw, int wv, int nwv)
-      : p(&pp), q(qq), nwg(nw), wave(wv), nwaves(nwv), run(0), wb(-64), todo(0), excl(0), cnt(0), base(0), n(0),
-        visited(0) {
+      : p(&pp), q(qq), nwg(nw), wave(wv), nwaves(nwv), all(ns > 1), run(0), wb(-64), todo(0), excl(0), cnt(0), base(0),
+        n(0), visited(0) {
     r0 = 0;
     r1 = ~0ull;
     if (ns > 1) {
@@ -4670,7 +4674,7 @@ struct RegionWalk {
              (uint64_t)(uint32_t)wave_excl_scan((int)(c & 0xFFFFu));
       run += (uint64_t)wave_sum_i64((int64_t)c);
       cnt = c;
-      const bool mine = w < nwg && w % nwaves == wave && excl < r1 && excl + c > r0;
+      const bool mine = w < nwg && (all || w % nwaves == wave) && excl < r1 && excl + c > r0;
       todo = __ballot(mine);
     }
     const int l = __builtin_ctzll(todo);
@@ -4744,7 +4748,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
       const uint32_t n = rwk.n;
       const size_t rb = rwk.base;
-      for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
+      for (uint32_t i0 = (rwk.all ? wave : 0) * R * 64; i0 < n; i0 += (rwk.all ? nwaves : 1) * R * 64) {
         uint32_t k[R], id[R];
         bool ok[R];
 #pragma unroll
@@ -4825,7 +4829,7 @@ __global__ __launch_bounds__(1024) void part_reduce_kernel(DevParams p, int nwg)
       if (rwk.visited % 8 == 0 && query_cancelled(p)) break;
       const uint32_t n = rwk.n;
       const size_t base = rwk.base;
-      for (uint32_t i0 = 0; i0 < n; i0 += R * 64) {
+      for (uint32_t i0 = (rwk.all ? wave : 0) * R * 64; i0 < n; i0 += (rwk.all ? nwaves : 1) * R * 64) {
         uint32_t k[R], raw[R], val[R];
         bool ok[R];
 #pragma unroll

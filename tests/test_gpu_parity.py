@@ -842,8 +842,9 @@ def test_partitioned_groupby_shared_dictionary(gpu_ctx, dist):
 
 def test_partitioned_groupby_skewed_frame_of_reference(gpu_ctx):
     """Config 4's phase-2 shape -- a 64K-value shared dictionary read through its frame-of-reference image in LDS --
-    under skewed keys, whose hot partition is split over several phase-2 workgroups by record ranges.  Every group
-    equals the oracle's, SUM / MAX / MIN / COUNT / AVG, bit-exact."""
+    under skewed keys, whose hot partition is split over several phase-2 workgroups by record ranges, each dealing
+    its pieces' chunks to all of its waves.  Every group equals the oracle's, SUM / MAX / MIN / COUNT / AVG,
+    bit-exact."""
     rng = np.random.default_rng(97)
     # 64K distinct values over 2^20 (config 4's metric): the dictionary misses LDS, its frame-of-reference image fits
     mvals = (np.sort(rng.choice(1 << 20, 65_536, replace=False)) - (1 << 19)).astype(np.int32)
