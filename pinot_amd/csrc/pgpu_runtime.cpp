@@ -3828,13 +3828,28 @@ int pgpu_query_wait(pgpu_query* qq, pgpu_query_stats* out_stats) {
   }
   if (qq->exact_filter) {
     // the reference's iterators replayed over the leaves' bitmaps (pgpu_iterstats.cpp)
+    // one segment per task on up to 16 host threads (segments replay independently, as the reference's
+    // per-segment operators run on its query executor's threads)
     const uint32_t* bits = (const uint32_t*)qq->ws->h_leafbits.p;
+    const size_t nr = qq->replay.size();
+    std::vector<int64_t> counts(nr, 0);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i = next++; i < nr; i = next++) {
+        const pgpu_query::FilterReplay& r = qq->replay[i];
+        std::vector<const uint32_t*> leaf(r.num_leaves);
+        for (int k = 0; k < r.num_leaves; ++k) leaf[k] = bits + r.bits_off + (int64_t)k * r.ntiles * 64;
+        counts[i] = reference_entries_scanned(r.nodes.data(), (int)r.nodes.size(), leaf.data(), r.num_leaves,
+                                              r.num_docs, r.leaf_off.empty() ? nullptr : r.leaf_off.data());
+      }
+    };
+    const size_t nthreads = std::min<size_t>({nr, 16, std::max(1u, std::thread::hardware_concurrency() / 2)});
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < nthreads; ++t) pool.emplace_back(work);
+    work();
+    for (std::thread& t : pool) t.join();
     int64_t total = 0;
-    for (const pgpu_query::FilterReplay& r : qq->replay) {
-      std::vector<const uint32_t*> leaf(r.num_leaves);
-      for (int k = 0; k < r.num_leaves; ++k) leaf[k] = bits + r.bits_off + (int64_t)k * r.ntiles * 64;
-      const int64_t c = reference_entries_scanned(r.nodes.data(), (int)r.nodes.size(), leaf.data(), r.num_leaves,
-                                                  r.num_docs, r.leaf_off.empty() ? nullptr : r.leaf_off.data());
+    for (int64_t c : counts) {
       if (c < 0) return fail(PGPU_E_INVALID, "filter program cannot be replayed for statistics");
       total += c;
     }
