@@ -39,7 +39,7 @@ def _is_timed(name: str) -> bool:
 def _is_main(name: str) -> bool:
     """One launch per query: the query kernel, or phase 1 proper of the partitioned group-by."""
     b = _base(name)
-    return b.startswith("query_kernel") or (b == "part_scan_kernel" and "<false>" in name)
+    return b.startswith("query_kernel") or (b == "part_scan_kernel" and "<false" in name)
 
 
 def per_launch(path):
@@ -69,7 +69,7 @@ def main():
     avg_ns, kname, calls, per_kernel = 0.0, None, 0, {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
         if _is_timed(r["Name"]):
-            per_kernel[_base(r["Name"]) + ("<false>" if "<false>" in r["Name"] else "<true>" if "<true>" in r["Name"] else "")] = {
+            per_kernel[_base(r["Name"]) + ("<false>" if "<false" in r["Name"] else "<true>" if "<true" in r["Name"] else "")] = {
                 "calls": int(r["Calls"]), "total_ns": float(r["TotalDurationNs"]), "avg_ns": float(r["AverageNs"])}
             avg_ns += float(r["TotalDurationNs"])
         if _is_main(r["Name"]):
